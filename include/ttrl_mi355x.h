@@ -1,0 +1,215 @@
+/*
+ * ttrl_mi355x.h — C ABI of the MI355X batched straight-highway simulator.
+ *
+ * This is the drop-in boundary for the reference's env.step() hot path
+ * (SURVEY.md §8(b)).  Every entry point works IN PLACE on caller-owned device
+ * buffers (plain pointers + sizes; no torch types), enqueues its kernels on the
+ * HIP stream passed as `stream` (hipStream_t, may be NULL = default stream), and
+ * returns 0 on success or a negative TTRL_E* code.  No entry point allocates,
+ * synchronises or keeps global state, so they are reentrant and graph-capturable.
+ *
+ * Reference interfaces replaced (file:line in ITCAAdvancedTeam/TopoTrafficRL):
+ *   ttrl_road_act            Road.act                      ttrl_env/road/road.py:461-464
+ *                            (IDMVehicle.act behavior.py:93-137, ControlledVehicle.act controller.py:89-133)
+ *   ttrl_road_step           Road.step(dt)                 ttrl_env/road/road.py:466-478
+ *                            (Vehicle.step kinematics.py:130-177, handle_collisions objects.py:91-137)
+ *   ttrl_meta_action         DiscreteMetaAction.act        ttrl_env/envs/common/action.py:259-260
+ *                            (MDPVehicle.act controller.py:295-315)
+ *   ttrl_simulate            AbstractEnv._simulate         ttrl_env/envs/common/abstract.py:252-282
+ *   ttrl_neighbours          Road.neighbour_vehicles       ttrl_env/road/road.py:480-513
+ *   ttrl_observe_kinematics  KinematicObservation.observe  ttrl_env/envs/common/observation.py:233-275
+ *                            (Road.close_objects_to road.py:418-447, Vehicle.to_dict kinematics.py:237-261)
+ *   ttrl_observe_grid        OccupancyGridObservation.observe observation.py:353-483
+ *   ttrl_reset_highway       scene init: Vehicle.create_random kinematics.py:50-104,
+ *                            IDMVehicle.__init__/randomize_behavior behavior.py:48-69
+ *   ttrl_rewards             reward/termination template  ttrl_env/envs/intersection_env.py:78-119
+ */
+#ifndef TTRL_MI355X_H
+#define TTRL_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TTRL_ABI_VERSION 1
+#define TTRL_MAX_LANES 16
+
+enum { TTRL_F32 = 0, TTRL_F64 = 1 };
+
+enum {
+  TTRL_OK = 0,
+  TTRL_E_ARG = -1,      /* bad argument (null pointer, size out of range, bad dtype) */
+  TTRL_E_LAUNCH = -2,   /* HIP launch / runtime error */
+  TTRL_E_UNSUPPORTED = -3
+};
+
+/* Vehicle kinds (the reference's class per row of road.vehicles). */
+enum { TTRL_ABSENT = 0, TTRL_MDP = 1, TTRL_IDM = 2 };
+
+/* DiscreteMetaAction.ACTIONS_ALL (action.py:204). */
+enum { TTRL_LANE_LEFT = 0, TTRL_IDLE = 1, TTRL_LANE_RIGHT = 2, TTRL_FASTER = 3, TTRL_SLOWER = 4 };
+
+/*
+ * One straight road "0"->"1" with n_lanes parallel StraightLanes in graph order
+ * (RoadNetwork.straight_road_network, road.py:291-321; StraightLane lane.py:159-213).
+ * Derived geometry (direction, length, heading) is computed on the host with
+ * the same float64 formulas as StraightLane.__init__ and passed in.
+ * Shared by every env of a batch.
+ */
+typedef struct ttrl_lane_table {
+  int32_t n_lanes;
+  int32_t _pad;
+  double start_x[TTRL_MAX_LANES], start_y[TTRL_MAX_LANES];
+  double dir_x[TTRL_MAX_LANES], dir_y[TTRL_MAX_LANES];   /* direction; lateral = (-dir_y, dir_x) */
+  double length[TTRL_MAX_LANES], width[TTRL_MAX_LANES];
+  double heading[TTRL_MAX_LANES], speed_limit[TTRL_MAX_LANES];
+  int32_t forbidden[TTRL_MAX_LANES];
+} ttrl_lane_table_t;
+
+/*
+ * Behaviour constants, explicit per run instead of the reference's mutable class
+ * attributes (IDMVehicle behavior.py:20-46, ControlledVehicle controller.py:24-33,
+ * Vehicle kinematics.py:21-29, RoadObject objects.py:62, MDPVehicle controller.py:259).
+ */
+typedef struct ttrl_params {
+  double acc_max;                 /* 6.0   ACC_MAX                       */
+  double comfort_acc_max;         /* 3.0   COMFORT_ACC_MAX               */
+  double comfort_acc_min;         /* -5.0  COMFORT_ACC_MIN               */
+  double distance_wanted;         /* 10.0  DISTANCE_WANTED               */
+  double time_wanted;             /* 1.5   TIME_WANTED                   */
+  double gap_denom;               /* 2*sqrt(-COMFORT_ACC_MAX*COMFORT_ACC_MIN) */
+  double politeness;              /* 0.0   POLITENESS                    */
+  double lane_change_min_acc_gain;/* 0.2                                 */
+  double lane_change_max_braking; /* 2.0   LANE_CHANGE_MAX_BRAKING_IMPOSED */
+  double lane_change_delay;       /* 1.0                                 */
+  double tau_pursuit;             /* 0.1   TAU_PURSUIT                   */
+  double kp_a;                    /* 1/0.6 KP_A                          */
+  double kp_heading;              /* 1/0.2 KP_HEADING                    */
+  double kp_lateral;              /* 1/0.6 KP_LATERAL                    */
+  double max_steering;            /* pi/3  MAX_STEERING_ANGLE            */
+  double length;                  /* 5.0   Vehicle.LENGTH                */
+  double width;                   /* 2.0   Vehicle.WIDTH                 */
+  double diagonal;                /* sqrt(LENGTH^2 + WIDTH^2)            */
+  double max_speed;               /* 40.0                                */
+  double min_speed;               /* -40.0                               */
+  double lane_vehicle_length;     /* 5.0   AbstractLane.VEHICLE_LENGTH   */
+  double target_speeds[8];        /* MDPVehicle target speeds (ego)      */
+  int32_t n_target_speeds;        /* 3                                   */
+  int32_t _pad;
+} ttrl_params_t;
+
+/*
+ * Batched vehicle state, struct-of-arrays, row-major [n_envs][n_veh].
+ * Real fields have dtype `dtype` (float or double); vehicle 0 of an env is the ego.
+ */
+typedef struct ttrl_state {
+  int32_t n_envs;
+  int32_t n_veh;
+  int32_t dtype;
+  int32_t _pad;
+  void *x, *y, *heading, *speed, *target_speed, *timer, *delta;
+  void *steer, *acc;              /* Vehicle.action {steering, acceleration}   */
+  void *impact_x, *impact_y;      /* Vehicle.impact, valid where has_impact    */
+  int32_t *lane, *target_lane;    /* lane ids on road ("0","1",id)             */
+  int32_t *speed_index;           /* MDPVehicle.speed_index (ego rows)         */
+  uint8_t *kind;                  /* TTRL_ABSENT / TTRL_MDP / TTRL_IDM         */
+  uint8_t *crashed, *has_impact, *lane_change; /* crashed, impact!=None, enable_lane_change */
+} ttrl_state_t;
+
+/* KinematicObservation config (observation.py:159-196).  Feature codes below. */
+enum {
+  TTRL_F_PRESENCE = 0, TTRL_F_X, TTRL_F_Y, TTRL_F_VX, TTRL_F_VY, TTRL_F_HEADING,
+  TTRL_F_COS_H, TTRL_F_SIN_H, TTRL_F_COS_D, TTRL_F_SIN_D, TTRL_F_LONG_OFF,
+  TTRL_F_LAT_OFF, TTRL_F_ANG_OFF, TTRL_F_ON_ROAD, TTRL_N_FEATURES
+};
+
+typedef struct ttrl_kin_cfg {
+  int32_t vehicles_count;         /* V rows                                     */
+  int32_t n_features;             /* F columns                                  */
+  int32_t features[TTRL_N_FEATURES];
+  int32_t absolute, normalize, clip, see_behind;
+  int32_t order_shuffled;         /* 0 sorted, 1 shuffled (Philox, seed+offset) */
+  int32_t _pad;
+  double range_lo[TTRL_N_FEATURES], range_hi[TTRL_N_FEATURES];
+  int32_t has_range[TTRL_N_FEATURES];
+  double perception_distance;     /* AbstractEnv.PERCEPTION_DISTANCE = 200      */
+  uint64_t shuffle_seed, shuffle_offset;
+} ttrl_kin_cfg_t;
+
+/* OccupancyGridObservation config (observation.py:285-326). */
+typedef struct ttrl_grid_cfg {
+  int32_t n_features;
+  int32_t features[TTRL_N_FEATURES];
+  int32_t shape_x, shape_y;       /* floor((max-min)/step)                      */
+  int32_t clip;
+  double grid_min_x, grid_min_y, step_x, step_y;
+  double range_lo[TTRL_N_FEATURES], range_hi[TTRL_N_FEATURES];
+  int32_t has_range[TTRL_N_FEATURES];
+  double lane_perception_distance;/* 100 (fill_road_layer_by_lanes)             */
+} ttrl_grid_cfg_t;
+
+/* Highway scene generator config. */
+typedef struct ttrl_reset_cfg {
+  int32_t n_vehicles;             /* vehicles actually spawned per env (<= n_veh) */
+  int32_t ego_lane;               /* 1                                          */
+  double ego_x, ego_speed;        /* 50, 25                                     */
+  double speed_lo, speed_hi;      /* 0.7*limit, 0.8*limit (host float64)        */
+  double spacing;                 /* 1                                          */
+  double density_factor;          /* exp(-5/40 * n_lanes) (host float64)        */
+  double delta_lo, delta_hi;      /* IDMVehicle.DELTA_RANGE                     */
+  int32_t lane_change;            /* enable_lane_change for IDM vehicles        */
+  int32_t _pad;
+} ttrl_reset_cfg_t;
+
+/* Reward / termination config (IntersectionEnv._agent_reward template). */
+typedef struct ttrl_reward_cfg {
+  double collision_reward, high_speed_reward, speed_lo, speed_hi;
+  int32_t normalize_reward, offroad_terminal;
+  double duration;                /* truncation time [s]                        */
+} ttrl_reward_cfg_t;
+
+int ttrl_abi_version(void);
+
+/* Ego meta-action (frame 0 of a policy step); actions [n_envs] int32. */
+int ttrl_meta_action(const ttrl_state_t* s, const ttrl_lane_table_t* road,
+                     const ttrl_params_t* p, const int32_t* actions, void* stream);
+/* One Road.act() over every env. */
+int ttrl_road_act(const ttrl_state_t* s, const ttrl_lane_table_t* road,
+                  const ttrl_params_t* p, void* stream);
+/* One Road.step(dt) over every env: kinematics + lane update + collisions. */
+int ttrl_road_step(const ttrl_state_t* s, const ttrl_lane_table_t* road,
+                   const ttrl_params_t* p, double dt, void* stream);
+/* Fused AbstractEnv._simulate: `frames` x (meta-action at frame 0 if actions
+ * != NULL, Road.act, Road.step(dt)) with the state resident on chip. */
+int ttrl_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road,
+                  const ttrl_params_t* p, const int32_t* actions, int32_t frames,
+                  double dt, void* stream);
+/* Road.neighbour_vehicles(v, lane) for every vehicle; query_lane [E*N] int32
+ * (-1 = the vehicle's own lane).  front/rear [E*N] int32 vehicle index or -1. */
+int ttrl_neighbours(const ttrl_state_t* s, const ttrl_lane_table_t* road,
+                    const int32_t* query_lane, int32_t* front, int32_t* rear, void* stream);
+/* Kinematics observation of the ego: out [E][V][F] float32, ids [E][V-1] int32 (-1 pad). */
+int ttrl_observe_kinematics(const ttrl_state_t* s, const ttrl_lane_table_t* road,
+                            const ttrl_params_t* p, const ttrl_kin_cfg_t* cfg,
+                            float* out, int32_t* ids, void* stream);
+/* Occupancy grid of the ego: out [E][F][shape_x][shape_y] float32. */
+int ttrl_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* road,
+                      const ttrl_params_t* p, const ttrl_grid_cfg_t* cfg,
+                      float* out, void* stream);
+/* Scene generation, bit-exact with numpy.random.Generator(PCG64) draws:
+ * pcg [E][4] uint64 = {state_hi, state_lo, inc_hi, inc_lo} per env (from
+ * SeedSequence on the host); writes all state rows (slots >= n_vehicles absent). */
+int ttrl_reset_highway(const ttrl_state_t* s, const ttrl_lane_table_t* road,
+                       const ttrl_params_t* p, const ttrl_reset_cfg_t* cfg,
+                       const uint64_t* pcg, void* stream);
+/* Per-env reward [E] float32, terminated/truncated [E] uint8, given time [E] float64. */
+int ttrl_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* road,
+                 const ttrl_reward_cfg_t* cfg, const double* time, float* reward,
+                 uint8_t* terminated, uint8_t* truncated, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TTRL_MI355X_H */

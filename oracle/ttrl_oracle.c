@@ -1,0 +1,658 @@
+/*
+ * ttrl_oracle.c — TEST INFRASTRUCTURE ONLY (parity checker, CPU baseline).
+ *
+ * A plain-C, float64, strictly sequential restatement of the reference's
+ * env.step() hot path (ITCAAdvancedTeam/TopoTrafficRL, ttrl_env).  Each function
+ * follows one reference function and cites it; loops run in the reference's
+ * list order so Gauss-Seidel reads (change_lane_policy) and last-writer
+ * collision impacts come out exactly as in Python.  Compiled with
+ * -ffp-contract=off so every + and * rounds like numpy float64.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline call this.
+ * The product path (topotrafficrl_amd) never links or loads it.
+ *
+ * Pinned against tests/golden/ (npz files), which oracle/gen_golden.py captures from
+ * the unmodified reference sim core.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/ttrl_mi355x.h"
+
+typedef struct {
+  int E, N;
+  double *x, *y, *h, *v, *ts, *timer, *delta, *steer, *acc, *ix, *iy;
+  int32_t *lane, *tgt, *sidx;
+  uint8_t *kind, *crashed, *hasimp, *lc;
+} S;
+
+static S view(const ttrl_state_t* s) {
+  S o;
+  o.E = s->n_envs; o.N = s->n_veh;
+  o.x = (double*)s->x; o.y = (double*)s->y; o.h = (double*)s->heading; o.v = (double*)s->speed;
+  o.ts = (double*)s->target_speed; o.timer = (double*)s->timer; o.delta = (double*)s->delta;
+  o.steer = (double*)s->steer; o.acc = (double*)s->acc; o.ix = (double*)s->impact_x; o.iy = (double*)s->impact_y;
+  o.lane = s->lane; o.tgt = s->target_lane; o.sidx = s->speed_index;
+  o.kind = s->kind; o.crashed = s->crashed; o.hasimp = s->has_impact; o.lc = s->lane_change;
+  return o;
+}
+
+static const double PI = 3.141592653589793;
+
+/* utils.py:48-54 */
+static double not_zero(double x) {
+  const double eps = 1e-2;
+  if (fabs(x) > eps) return x;
+  return x >= 0 ? eps : -eps;
+}
+/* numpy float64 remainder (sign of divisor) */
+static double pymod(double a, double b) {
+  double m = fmod(a, b);
+  if (m != 0.0) { if ((b < 0) != (m < 0)) m += b; }
+  else m = copysign(0.0, b);
+  return m;
+}
+/* utils.py:57-58 */
+static double wrap_to_pi(double x) { return pymod(x + PI, 2 * PI) - PI; }
+static double clipd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+/* utils.py:29-31 */
+static double lmap(double v, double x0, double x1, double y0, double y1) {
+  return y0 + (v - x0) * (y1 - y0) / (x1 - x0);
+}
+
+/* StraightLane.local_coordinates lane.py:209-213 (np.dot of 2-vectors) */
+static void local(const ttrl_lane_table_t* R, int l, double px, double py, double* s, double* r) {
+  double dx = px - R->start_x[l], dy = py - R->start_y[l];
+  *s = dx * R->dir_x[l] + dy * R->dir_y[l];
+  *r = dx * (-R->dir_y[l]) + dy * R->dir_x[l];
+}
+/* AbstractLane.on_lane lane.py:80-102 */
+static int on_lane(const ttrl_lane_table_t* R, const ttrl_params_t* P, int l, double s, double r, double margin) {
+  return fabs(r) <= R->width[l] / 2 + margin && -P->lane_vehicle_length <= s && s < R->length[l] + P->lane_vehicle_length;
+}
+/* AbstractLane.is_reachable_from lane.py:104-118 */
+static int reachable(const ttrl_lane_table_t* R, const ttrl_params_t* P, int l, double px, double py) {
+  if (R->forbidden[l]) return 0;
+  double s, r; local(R, l, px, py, &s, &r);
+  return fabs(r) <= 2 * R->width[l] && 0 <= s && s < R->length[l] + P->lane_vehicle_length;
+}
+/* RoadNetwork.get_closest_lane_index road.py:55-71 + distance_with_heading lane.py:132-147 */
+static int closest_lane(const ttrl_lane_table_t* R, double px, double py, double heading) {
+  int best = 0; double bd = 0;
+  for (int l = 0; l < R->n_lanes; ++l) {
+    double s, r; local(R, l, px, py, &s, &r);
+    double ang = fabs(wrap_to_pi(heading - R->heading[l]));
+    double a = s - R->length[l]; if (!(a > 0)) a = 0;   /* Python max(s - len, 0) */
+    double b = 0 - s; if (!(b > 0)) b = 0;
+    double d = fabs(r) + a + b + 1.0 * ang;
+    if (l == 0 || d < bd) { bd = d; best = l; }          /* np.argmin: first minimum */
+  }
+  return best;
+}
+
+/* RoadObject.lane_distance_to objects.py:182-197 (along `self`'s current lane) */
+static double lane_distance(const S* o, const ttrl_lane_table_t* R, int base, int self, int other) {
+  int l = o->lane[base + self];
+  double s1, r1, s0, r0;
+  local(R, l, o->x[base + other], o->y[base + other], &s1, &r1);
+  local(R, l, o->x[base + self], o->y[base + self], &s0, &r0);
+  return s1 - s0;
+}
+
+/* Road.neighbour_vehicles road.py:480-513 */
+static void neighbour(const S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base, int self, int l,
+                      int* front, int* rear) {
+  double s, r; local(R, l, o->x[base + self], o->y[base + self], &s, &r);
+  int hf = 0, hr = 0; double sf = 0, sr = 0; *front = *rear = -1;
+  for (int j = 0; j < o->N; ++j) {
+    if (j == self || o->kind[base + j] == TTRL_ABSENT) continue;
+    double sv, lv; local(R, l, o->x[base + j], o->y[base + j], &sv, &lv);
+    if (!on_lane(R, P, l, sv, lv, 1.0)) continue;
+    if (s <= sv && (!hf || sv <= sf)) { sf = sv; hf = 1; *front = j; }
+    if (sv < s && (!hr || sv > sr)) { sr = sv; hr = 1; *rear = j; }
+  }
+}
+
+/* IDMVehicle.desired_gap behavior.py:192-217 (projected=True) */
+static double desired_gap(const S* o, const ttrl_params_t* P, int base, int ego, int front) {
+  double eh = o->h[base + ego], fh = o->h[base + front], ev = o->v[base + ego], fv = o->v[base + front];
+  double ecx = cos(eh), esx = sin(eh);
+  double dvx = ev * ecx - fv * cos(fh), dvy = ev * esx - fv * sin(fh);
+  double dv = dvx * ecx + dvy * esx;
+  return P->distance_wanted + ev * P->time_wanted + ev * dv / P->gap_denom;
+}
+
+/* IDMVehicle.acceleration behavior.py:150-190; DELTA is the caller's (`selfd`). */
+static double idm_acc(const S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base, double selfd,
+                      int ego, int front) {
+  if (ego < 0) return 0;
+  double ts = o->ts[base + ego];
+  ts = clipd(ts, 0, R->speed_limit[o->lane[base + ego]]);
+  double v = o->v[base + ego]; if (!(v > 0)) v = (0 > v) ? 0 : v;  /* Python max(v, 0) */
+  double a = P->comfort_acc_max * (1 - pow(v / fabs(not_zero(ts)), selfd));
+  if (front >= 0) {
+    double d = lane_distance(o, R, base, ego, front);
+    double q = desired_gap(o, P, base, ego, front) / not_zero(d);
+    a -= P->comfort_acc_max * (q * q);
+  }
+  return a;
+}
+
+/* IDMVehicle.mobil behavior.py:265-324 (route None) */
+static int mobil(const S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base, int self, int l) {
+  double d = o->delta[base + self];
+  int np_, nf; neighbour(o, R, P, base, self, l, &np_, &nf);
+  double nfa = idm_acc(o, R, P, base, d, nf, np_);
+  double nfpa = idm_acc(o, R, P, base, d, nf, self);
+  if (nfpa < -P->lane_change_max_braking) return 0;
+  int op, of; neighbour(o, R, P, base, self, o->lane[base + self], &op, &of);
+  double spa = idm_acc(o, R, P, base, d, self, np_);
+  double sa = idm_acc(o, R, P, base, d, self, op);
+  double ofa = idm_acc(o, R, P, base, d, of, self);
+  double ofpa = idm_acc(o, R, P, base, d, of, op);
+  double jerk = spa - sa + P->politeness * (nfpa - nfa + ofpa - ofa);
+  if (jerk < P->lane_change_min_acc_gain) return 0;
+  return 1;
+}
+
+/* IDMVehicle.change_lane_policy behavior.py:219-263 */
+static void change_lane_policy(S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base, int self) {
+  int lane = o->lane[base + self], tgt = o->tgt[base + self];
+  if (lane != tgt) {
+    for (int j = 0; j < o->N; ++j) {
+      if (j == self || o->kind[base + j] == TTRL_ABSENT) continue;
+      if (o->lane[base + j] != tgt && o->tgt[base + j] == tgt) {
+        double d = lane_distance(o, R, base, self, j);
+        double ds = desired_gap(o, P, base, self, j);
+        if (0 < d && d < ds) { o->tgt[base + self] = lane; break; }
+      }
+    }
+    return;
+  }
+  if (!(P->lane_change_delay < o->timer[base + self])) return;   /* utils.do_every */
+  o->timer[base + self] = 0;
+  int cand[2], nc = 0;                                             /* RoadNetwork.side_lanes road.py:200-211 */
+  if (lane > 0) cand[nc++] = lane - 1;
+  if (lane < R->n_lanes - 1) cand[nc++] = lane + 1;
+  for (int k = 0; k < nc; ++k) {
+    if (!reachable(R, P, cand[k], o->x[base + self], o->y[base + self])) continue;
+    if (fabs(o->v[base + self]) < 1) continue;
+    if (mobil(o, R, P, base, self, cand[k])) o->tgt[base + self] = cand[k];
+  }
+}
+
+/* ControlledVehicle.steering_control controller.py:145-187 */
+static double steering_control(const S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base, int i, int l) {
+  double s, r; local(R, l, o->x[base + i], o->y[base + i], &s, &r);
+  double v = o->v[base + i];
+  double lane_future_heading = R->heading[l];                 /* heading_at(s + v*TAU_PURSUIT) */
+  double lat_cmd = -P->kp_lateral * r;
+  double hcmd = asin(clipd(lat_cmd / not_zero(v), -1, 1));
+  double href = lane_future_heading + clipd(hcmd, -PI / 4, PI / 4);
+  double hrate = P->kp_heading * wrap_to_pi(href - o->h[base + i]);
+  double slip = asin(clipd(P->length / 2 / not_zero(v) * hrate, -1, 1));
+  double st = atan(2 * tan(slip));
+  return clipd(st, -P->max_steering, P->max_steering);
+}
+
+/* IDMVehicle.act behavior.py:93-137 */
+static void idm_act(S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base, int i) {
+  if (o->crashed[base + i]) return;
+  /* follow_road (controller.py:135-143): single-segment road, next_lane is a no-op (road.py:129-130) */
+  if (o->lc[base + i]) change_lane_policy(o, R, P, base, i);
+  double st = steering_control(o, R, P, base, i, o->tgt[base + i]);
+  st = clipd(st, -P->max_steering, P->max_steering);
+  int f, r; neighbour(o, R, P, base, i, o->lane[base + i], &f, &r);
+  double d = o->delta[base + i];
+  double a = idm_acc(o, R, P, base, d, i, f);
+  if (o->lane[base + i] != o->tgt[base + i]) {
+    neighbour(o, R, P, base, i, o->tgt[base + i], &f, &r);
+    double a2 = idm_acc(o, R, P, base, d, i, f);
+    if (a2 < a) a = a2;                                        /* Python min(a, a2) */
+  }
+  o->acc[base + i] = clipd(a, -P->acc_max, P->acc_max);
+  o->steer[base + i] = st;
+}
+
+/* ControlledVehicle.act controller.py:89-133 with action in {None, LANE_LEFT, LANE_RIGHT, IDLE} */
+static void controlled_act(S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base, int i, int action) {
+  if (action == TTRL_LANE_RIGHT || action == TTRL_LANE_LEFT) {
+    int id = o->tgt[base + i] + (action == TTRL_LANE_RIGHT ? 1 : -1);
+    if (id < 0) id = 0;
+    if (id > R->n_lanes - 1) id = R->n_lanes - 1;
+    if (reachable(R, P, id, o->x[base + i], o->y[base + i])) o->tgt[base + i] = id;
+  }
+  double st = steering_control(o, R, P, base, i, o->tgt[base + i]);
+  double a = P->kp_a * (o->ts[base + i] - o->v[base + i]);
+  o->steer[base + i] = clipd(st, -P->max_steering, P->max_steering);
+  o->acc[base + i] = a;
+}
+
+/* MDPVehicle.speed_to_index controller.py:326-344 (np.round = half-to-even) */
+static int speed_to_index(const ttrl_params_t* P, double v) {
+  int n = P->n_target_speeds;
+  double x = (v - P->target_speeds[0]) / (P->target_speeds[n - 1] - P->target_speeds[0]);
+  return (int)clipd(nearbyint(x * (n - 1)), 0, n - 1);
+}
+
+/* MDPVehicle.act controller.py:295-315 */
+static void mdp_act(S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base, int i, int action) {
+  if (action == TTRL_FASTER || action == TTRL_SLOWER) {
+    int si = speed_to_index(P, o->v[base + i]) + (action == TTRL_FASTER ? 1 : -1);
+    if (si < 0) si = 0;
+    if (si > P->n_target_speeds - 1) si = P->n_target_speeds - 1;
+    o->sidx[base + i] = si;
+    o->ts[base + i] = P->target_speeds[si];
+    controlled_act(o, R, P, base, i, -1);
+    return;
+  }
+  controlled_act(o, R, P, base, i, action);
+}
+
+/* Vehicle.step kinematics.py:130-153 (+ clip_actions :155-168, on_state_update :170-177) */
+static void vehicle_step(S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base, int i, double dt) {
+  int k = base + i;
+  if (o->kind[k] == TTRL_IDM) o->timer[k] += dt;                   /* IDMVehicle.step behavior.py:147 */
+  if (o->crashed[k]) { o->steer[k] = 0; o->acc[k] = -1.0 * o->v[k]; }
+  if (o->v[k] > P->max_speed) { double c = 1.0 * (P->max_speed - o->v[k]); if (c < o->acc[k]) o->acc[k] = c; }
+  else if (o->v[k] < P->min_speed) { double c = 1.0 * (P->min_speed - o->v[k]); if (c > o->acc[k]) o->acc[k] = c; }
+  double beta = atan(1.0 / 2 * tan(o->steer[k]));
+  double vx = o->v[k] * cos(o->h[k] + beta), vy = o->v[k] * sin(o->h[k] + beta);
+  o->x[k] += vx * dt; o->y[k] += vy * dt;
+  if (o->hasimp[k]) { o->x[k] += o->ix[k]; o->y[k] += o->iy[k]; o->crashed[k] = 1; o->hasimp[k] = 0; }
+  o->h[k] += o->v[k] * sin(beta) / (P->length / 2) * dt;
+  o->v[k] += o->acc[k] * dt;
+  o->lane[k] = closest_lane(R, o->x[k], o->y[k], o->h[k]);
+}
+
+/* RoadObject.polygon objects.py:168-180 (closed: 5 points) */
+static void polygon(const ttrl_params_t* P, double px, double py, double h, double pts[5][2]) {
+  const double L = P->length, W = P->width;
+  double c = cos(h), s = sin(h);
+  double lx[4] = {-L / 2, -L / 2, +L / 2, +L / 2}, ly[4] = {-W / 2, +W / 2, +W / 2, -W / 2};
+  for (int k = 0; k < 4; ++k) {
+    pts[k][0] = c * lx[k] + (-s) * ly[k] + px;
+    pts[k][1] = s * lx[k] + c * ly[k] + py;
+  }
+  pts[4][0] = pts[0][0]; pts[4][1] = pts[0][1];
+}
+static void project(double pts[5][2], double nx, double ny, double* mn, double* mx) {
+  for (int k = 0; k < 5; ++k) {
+    double p = pts[k][0] * nx + pts[k][1] * ny;
+    if (k == 0 || p < *mn) *mn = p;
+    if (k == 0 || p > *mx) *mx = p;
+  }
+}
+static double interval_distance(double mina, double maxa, double minb, double maxb) {
+  return mina < minb ? minb - maxa : mina - maxb;                /* utils.py:186-191 */
+}
+/* utils.are_polygons_intersecting utils.py:194-239 */
+static void sat(double a[5][2], double b[5][2], double dax, double day, double dbx, double dby,
+                int* inter, int* will, double* tx, double* ty) {
+  int it = 1, wi = 1; double mind = INFINITY, axx = 0, axy = 0;
+  double (*polys[2])[2] = {a, b};
+  for (int pi = 0; pi < 2; ++pi) {
+    double (*pg)[2] = polys[pi];
+    for (int e = 0; e < 4; ++e) {
+      double nx = -pg[e + 1][1] + pg[e][1], ny = pg[e + 1][0] - pg[e][0];
+      double nn = sqrt(nx * nx + ny * ny);
+      nx /= nn; ny /= nn;
+      double mina = 0, maxa = 0, minb = 0, maxb = 0;
+      project(a, nx, ny, &mina, &maxa);
+      project(b, nx, ny, &minb, &maxb);
+      if (interval_distance(mina, maxa, minb, maxb) > 0) it = 0;
+      double vp = nx * (dax - dbx) + ny * (day - dby);
+      if (vp < 0) mina += vp; else maxa += vp;
+      double dist = interval_distance(mina, maxa, minb, maxb);
+      if (dist > 0) wi = 0;
+      if (!it && !wi) break;
+      if (fabs(dist) < mind) {
+        mind = fabs(dist);
+        double cax = (((a[0][0] + a[1][0]) + a[2][0]) + a[3][0]) / 4, cay = (((a[0][1] + a[1][1]) + a[2][1]) + a[3][1]) / 4;
+        double cbx = (((b[0][0] + b[1][0]) + b[2][0]) + b[3][0]) / 4, cby = (((b[0][1] + b[1][1]) + b[2][1]) + b[3][1]) / 4;
+        double dx = cax - cbx, dy = cay - cby;
+        if (dx * nx + dy * ny > 0) { axx = nx; axy = ny; } else { axx = -nx; axy = -ny; }
+      }
+    }
+  }
+  *inter = it; *will = wi;
+  *tx = wi ? mind * axx : 0; *ty = wi ? mind * axy : 0;
+}
+
+/* RoadObject.handle_collisions objects.py:91-137 for a vehicle pair i<j */
+static void handle_collisions(S* o, const ttrl_params_t* P, int base, int i, int j, double dt) {
+  int a = base + i, b = base + j;
+  double dx = o->x[b] - o->x[a], dy = o->y[b] - o->y[a];
+  if (sqrt(dx * dx + dy * dy) > (P->diagonal + P->diagonal) / 2 + o->v[a] * dt) return;
+  double pa[5][2], pb[5][2];
+  polygon(P, o->x[a], o->y[a], o->h[a], pa);
+  polygon(P, o->x[b], o->y[b], o->h[b], pb);
+  double ca = cos(o->h[a]), sa = sin(o->h[a]), cb = cos(o->h[b]), sb = sin(o->h[b]);
+  double dax = o->v[a] * ca * dt, day = o->v[a] * sa * dt, dbx = o->v[b] * cb * dt, dby = o->v[b] * sb * dt;
+  int inter, will; double tx, ty;
+  sat(pa, pb, dax, day, dbx, dby, &inter, &will, &tx, &ty);
+  if (will) {
+    o->ix[a] = tx / 2; o->iy[a] = ty / 2; o->hasimp[a] = 1;
+    o->ix[b] = -tx / 2; o->iy[b] = -ty / 2; o->hasimp[b] = 1;
+  }
+  if (inter) { o->crashed[a] = 1; o->crashed[b] = 1; }
+}
+
+static int check(const ttrl_state_t* s) {
+  if (!s || s->dtype != TTRL_F64 || s->n_envs < 0 || s->n_veh <= 0) return TTRL_E_ARG;
+  return 0;
+}
+
+int oracle_meta_action(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                       const int32_t* actions, void* stream) {
+  (void)stream; if (check(s)) return TTRL_E_ARG;
+  S o = view(s);
+  for (int e = 0; e < o.E; ++e) {
+    int base = e * o.N;
+    if (o.kind[base] != TTRL_MDP) continue;
+    int a = actions[e];
+    if (a < 0 || a > 4) return TTRL_E_ARG;
+    mdp_act(&o, R, P, base, 0, a);
+  }
+  return 0;
+}
+
+/* Road.act road.py:461-464 */
+int oracle_road_act(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P, void* stream) {
+  (void)stream; if (check(s)) return TTRL_E_ARG;
+  S o = view(s);
+  for (int e = 0; e < o.E; ++e) {
+    int base = e * o.N;
+    for (int i = 0; i < o.N; ++i) {
+      if (o.kind[base + i] == TTRL_MDP) controlled_act(&o, R, P, base, i, -1);
+      else if (o.kind[base + i] == TTRL_IDM) idm_act(&o, R, P, base, i);
+    }
+  }
+  return 0;
+}
+
+/* Road.step road.py:466-478 */
+int oracle_road_step(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P, double dt, void* stream) {
+  (void)stream; if (check(s)) return TTRL_E_ARG;
+  S o = view(s);
+  for (int e = 0; e < o.E; ++e) {
+    int base = e * o.N;
+    for (int i = 0; i < o.N; ++i)
+      if (o.kind[base + i] != TTRL_ABSENT) vehicle_step(&o, R, P, base, i, dt);
+    for (int i = 0; i < o.N; ++i) {
+      if (o.kind[base + i] == TTRL_ABSENT) continue;
+      for (int j = i + 1; j < o.N; ++j)
+        if (o.kind[base + j] != TTRL_ABSENT) handle_collisions(&o, P, base, i, j, dt);
+    }
+  }
+  return 0;
+}
+
+/* AbstractEnv._simulate abstract.py:252-282 */
+int oracle_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                    const int32_t* actions, int32_t frames, double dt, void* stream) {
+  if (check(s)) return TTRL_E_ARG;
+  for (int f = 0; f < frames; ++f) {
+    int rc;
+    if (f == 0 && actions && (rc = oracle_meta_action(s, R, P, actions, stream))) return rc;
+    if ((rc = oracle_road_act(s, R, P, stream))) return rc;
+    if ((rc = oracle_road_step(s, R, P, dt, stream))) return rc;
+  }
+  return 0;
+}
+
+int oracle_neighbours(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                      const int32_t* query_lane, int32_t* front, int32_t* rear) {
+  if (check(s)) return TTRL_E_ARG;
+  S o = view(s);
+  for (int e = 0; e < o.E; ++e)
+    for (int i = 0; i < o.N; ++i) {
+      int k = e * o.N + i, f = -1, r = -1;
+      if (o.kind[k] != TTRL_ABSENT) {
+        int l = query_lane && query_lane[k] >= 0 ? query_lane[k] : o.lane[k];
+        neighbour(&o, R, P, e * o.N, i, l, &f, &r);
+      }
+      front[k] = f; rear[k] = r;
+    }
+  return 0;
+}
+
+/* ---------------------------------------------------------------- observations */
+/* Vehicle.to_dict kinematics.py:237-261 (route None => cos_d = sin_d = 0) */
+static double feature(const S* o, const ttrl_lane_table_t* R, int k, int f) {
+  double c = cos(o->h[k]), sn = sin(o->h[k]);
+  switch (f) {
+    case TTRL_F_PRESENCE: return 1;
+    case TTRL_F_X: return o->x[k];
+    case TTRL_F_Y: return o->y[k];
+    case TTRL_F_VX: return o->v[k] * c;
+    case TTRL_F_VY: return o->v[k] * sn;
+    case TTRL_F_HEADING: return o->h[k];
+    case TTRL_F_COS_H: return c;
+    case TTRL_F_SIN_H: return sn;
+    case TTRL_F_COS_D: case TTRL_F_SIN_D: return 0;
+    case TTRL_F_LONG_OFF: case TTRL_F_LAT_OFF: case TTRL_F_ANG_OFF: {
+      double s, r; local(R, o->lane[k], o->x[k], o->y[k], &s, &r);
+      if (f == TTRL_F_LONG_OFF) return s;
+      if (f == TTRL_F_LAT_OFF) return r;
+      return wrap_to_pi(o->h[k] - R->heading[o->lane[k]]);
+    }
+  }
+  return 0;
+}
+
+/* KinematicObservation.observe observation.py:233-275, order sorted/shuffled(ids only) */
+int oracle_observe_kinematics(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                              const ttrl_kin_cfg_t* cfg, float* out, int32_t* ids) {
+  (void)P; if (check(s)) return TTRL_E_ARG;
+  S o = view(s);
+  const int V = cfg->vehicles_count, F = cfg->n_features;
+  int* cand = (int*)malloc(sizeof(int) * o.N);
+  double* key = (double*)malloc(sizeof(double) * o.N);
+  for (int e = 0; e < o.E; ++e) {
+    int base = e * o.N, ego = base;
+    float* ob = out + (size_t)e * V * F;
+    int nc = 0;
+    for (int j = 0; j < o.N; ++j) {              /* Road.close_objects_to road.py:427-433 */
+      int k = base + j;
+      if (j == 0 || o.kind[k] == TTRL_ABSENT) continue;
+      double dx = o.x[k] - o.x[ego], dy = o.y[k] - o.y[ego];
+      if (!(sqrt(dx * dx + dy * dy) < cfg->perception_distance)) continue;
+      double ld = lane_distance(&o, R, base, 0, j);
+      if (!cfg->see_behind && !(-2 * P->length < ld)) continue;
+      cand[nc] = j; key[nc] = fabs(ld); nc++;
+    }
+    /* stable insertion sort by |lane distance| (sorted(), road.py:444) */
+    if (!cfg->order_shuffled)
+      for (int a = 1; a < nc; ++a) {
+        int cj = cand[a]; double ck = key[a]; int b = a - 1;
+        while (b >= 0 && key[b] > ck) { cand[b + 1] = cand[b]; key[b + 1] = key[b]; b--; }
+        cand[b + 1] = cj; key[b + 1] = ck;
+      }
+    if (nc > V - 1) nc = V - 1;
+    for (int r = 0; r < V; ++r)
+      for (int c = 0; c < F; ++c) {
+        double val = 0;
+        if (r == 0 || r <= nc) {
+          int k = r == 0 ? ego : base + cand[r - 1];
+          int f = cfg->features[c];
+          val = feature(&o, R, k, f);
+          if (r > 0 && !cfg->absolute && (f == TTRL_F_X || f == TTRL_F_Y || f == TTRL_F_VX || f == TTRL_F_VY))
+            val -= feature(&o, R, ego, f);
+          if (cfg->normalize && cfg->has_range[f]) {
+            val = lmap(val, cfg->range_lo[f], cfg->range_hi[f], -1, 1);
+            if (cfg->clip) val = clipd(val, -1, 1);
+          }
+        }
+        ob[r * F + c] = (float)val;
+      }
+    if (ids)
+      for (int r = 0; r < V - 1; ++r) ids[e * (V - 1) + r] = r < nc ? cand[r] : -1;
+  }
+  free(cand); free(key);
+  return 0;
+}
+
+/* OccupancyGridObservation.observe observation.py:353-434 (+ fill_road_layer_by_lanes :453-483) */
+int oracle_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                        const ttrl_grid_cfg_t* cfg, float* out) {
+  (void)P; if (check(s)) return TTRL_E_ARG;
+  S o = view(s);
+  const int F = cfg->n_features, W = cfg->shape_x, H = cfg->shape_y;
+  double* grid = (double*)malloc(sizeof(double) * F * W * H);
+  for (int e = 0; e < o.E; ++e) {
+    int base = e * o.N, ego = base;
+    for (int q = 0; q < F * W * H; ++q) grid[q] = NAN;
+    for (int c = 0; c < F; ++c) {
+      int f = cfg->features[c];
+      if (f == TTRL_F_ON_ROAD) {
+        double spacing = cfg->step_x < cfg->step_y ? cfg->step_x : cfg->step_y;
+        for (int l = 0; l < R->n_lanes; ++l) {
+          double origin, rr; local(R, l, o.x[ego], o.y[ego], &origin, &rr);
+          double start = origin - cfg->lane_perception_distance, stop = origin + cfg->lane_perception_distance;
+          long n = (long)ceil((stop - start) / spacing);           /* np.arange length */
+          double d1 = (start + spacing) - start;                    /* numpy fill: delta = buf[1]-buf[0] */
+          for (long i = 0; i < n; ++i) {
+            double wp = i == 0 ? start : (i == 1 ? start + spacing : start + i * d1);
+            wp = clipd(wp, 0, R->length[l]);
+            double px = R->start_x[l] + wp * R->dir_x[l] + 0 * (-R->dir_y[l]);
+            double py = R->start_y[l] + wp * R->dir_y[l] + 0 * R->dir_x[l];
+            px -= o.x[ego]; py -= o.y[ego];
+            long cx = (long)floor((px - cfg->grid_min_x) / cfg->step_x);
+            long cy = (long)floor((py - cfg->grid_min_y) / cfg->step_y);
+            if (0 <= cx && cx < W && 0 <= cy && cy < H) grid[(c * W + cx) * H + cy] = 1;
+          }
+        }
+        continue;
+      }
+      for (int j = o.N - 1; j >= 0; --j) {        /* df[::-1].iterrows(): lowest index wins */
+        int k = base + j;
+        if (o.kind[k] == TTRL_ABSENT) continue;
+        double x = o.x[k] - o.x[ego], y = o.y[k] - o.y[ego];
+        double val = feature(&o, R, k, f);
+        if (f == TTRL_F_X || f == TTRL_F_Y || f == TTRL_F_VX || f == TTRL_F_VY) val -= feature(&o, R, ego, f);
+        if (cfg->has_range[f]) val = lmap(val, cfg->range_lo[f], cfg->range_hi[f], -1, 1);
+        if (cfg->has_range[TTRL_F_X]) {
+          x = lmap(x, cfg->range_lo[TTRL_F_X], cfg->range_hi[TTRL_F_X], -1, 1);
+          x = lmap(x, -1, 1, cfg->range_lo[TTRL_F_X], cfg->range_hi[TTRL_F_X]);
+        }
+        if (cfg->has_range[TTRL_F_Y]) {
+          y = lmap(y, cfg->range_lo[TTRL_F_Y], cfg->range_hi[TTRL_F_Y], -1, 1);
+          y = lmap(y, -1, 1, cfg->range_lo[TTRL_F_Y], cfg->range_hi[TTRL_F_Y]);
+        }
+        long cx = (long)floor((x - cfg->grid_min_x) / cfg->step_x);
+        long cy = (long)floor((y - cfg->grid_min_y) / cfg->step_y);
+        if (0 <= cx && cx < W && 0 <= cy && cy < H) grid[(c * W + cx) * H + cy] = val;
+      }
+    }
+    float* ob = out + (size_t)e * F * W * H;
+    for (int q = 0; q < F * W * H; ++q) {
+      double g = grid[q];
+      if (cfg->clip && g == g) g = clipd(g, -1, 1);
+      ob[q] = (float)(g == g ? g : 0.0);
+    }
+  }
+  free(grid);
+  return 0;
+}
+
+/* ---------------------------------------------------------------- scene generation */
+/* numpy PCG64 (pcg_setseq_128_xsl_rr_64): step, then output of the new state. */
+typedef struct { unsigned __int128 st, inc; int has32; uint32_t u32; } pcg_t;
+static const unsigned __int128 PCG_MULT =
+    ((unsigned __int128)0x2360ED051FC65DA4ULL << 64) | 0x4385DF649FCCF645ULL;
+static uint64_t pcg_next64(pcg_t* g) {
+  g->st = g->st * PCG_MULT + g->inc;
+  uint64_t hi = (uint64_t)(g->st >> 64), lo = (uint64_t)g->st;
+  uint64_t x = hi ^ lo; unsigned rot = (unsigned)(hi >> 58);
+  return (x >> rot) | (x << ((64 - rot) & 63));
+}
+static uint32_t pcg_next32(pcg_t* g) {
+  if (g->has32) { g->has32 = 0; return g->u32; }
+  uint64_t n = pcg_next64(g); g->has32 = 1; g->u32 = (uint32_t)(n >> 32); return (uint32_t)n;
+}
+static double pcg_double(pcg_t* g) { return (double)(pcg_next64(g) >> 11) * (1.0 / 9007199254740992.0); }
+/* Generator.integers(0, n) for 1 < n <= 2^32 (buffered Lemire, numpy distributions.c) */
+static uint32_t pcg_bounded(pcg_t* g, uint32_t n) {
+  if (n <= 1) return 0;
+  uint32_t rng = n - 1; uint64_t rexcl = (uint64_t)rng + 1;
+  uint64_t m = (uint64_t)pcg_next32(g) * rexcl;
+  uint32_t left = (uint32_t)m;
+  if (left < rexcl) {
+    uint32_t thr = (uint32_t)((0xFFFFFFFFULL - rng) % rexcl);
+    while (left < thr) { m = (uint64_t)pcg_next32(g) * rexcl; left = (uint32_t)m; }
+  }
+  return (uint32_t)(m >> 32);
+}
+static double pcg_uniform(pcg_t* g, double lo, double hi) { return lo + (hi - lo) * pcg_double(g); }
+
+/* highway scene, SURVEY.md §3.C: ego MDPVehicle then create_random + randomize_behavior */
+int oracle_reset_highway(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                         const ttrl_reset_cfg_t* cfg, const uint64_t* pcg) {
+  if (check(s) || cfg->n_vehicles > s->n_veh || cfg->n_vehicles < 1) return TTRL_E_ARG;
+  S o = view(s);
+  for (int e = 0; e < o.E; ++e) {
+    int base = e * o.N;
+    pcg_t g;
+    g.st = ((unsigned __int128)pcg[4 * e] << 64) | pcg[4 * e + 1];
+    g.inc = ((unsigned __int128)pcg[4 * e + 2] << 64) | pcg[4 * e + 3];
+    g.has32 = 0; g.u32 = 0;
+    for (int i = 0; i < o.N; ++i) {
+      int k = base + i;
+      o.kind[k] = TTRL_ABSENT; o.crashed[k] = 0; o.hasimp[k] = 0; o.lc[k] = 0;
+      o.x[k] = o.y[k] = o.h[k] = o.v[k] = o.ts[k] = o.timer[k] = o.steer[k] = o.acc[k] = 0;
+      o.ix[k] = o.iy[k] = 0; o.delta[k] = 4.0; o.lane[k] = o.tgt[k] = 0; o.sidx[k] = -1;
+    }
+    /* ego: MDPVehicle(road, lane.position(x, 0), lane.heading_at(x), speed) */
+    int l = cfg->ego_lane;
+    double ex = R->start_x[l] + cfg->ego_x * R->dir_x[l] + 0.0 * (-R->dir_y[l]);
+    double ey = R->start_y[l] + cfg->ego_x * R->dir_y[l] + 0.0 * R->dir_x[l];
+    o.kind[base] = TTRL_MDP; o.x[base] = ex; o.y[base] = ey; o.h[base] = R->heading[l]; o.v[base] = cfg->ego_speed;
+    o.lane[base] = o.tgt[base] = closest_lane(R, ex, ey, R->heading[l]);
+    o.sidx[base] = speed_to_index(P, cfg->ego_speed);
+    o.ts[base] = P->target_speeds[o.sidx[base]];
+    for (int i = 1; i < cfg->n_vehicles; ++i) {
+      int k = base + i;
+      int lid = (int)pcg_bounded(&g, (uint32_t)R->n_lanes);          /* choice(len(lanes)) */
+      double sp = pcg_uniform(&g, cfg->speed_lo, cfg->speed_hi);
+      double offset = cfg->spacing * (12 + 1.0 * sp) * cfg->density_factor;
+      double x0 = 0; int have = 0;
+      for (int j = 0; j < i; ++j) {
+        double sj, rj; local(R, lid, o.x[base + j], o.y[base + j], &sj, &rj);
+        if (!have || sj > x0) { x0 = sj; have = 1; }
+      }
+      x0 += offset * pcg_uniform(&g, 0.9, 1.1);
+      o.kind[k] = TTRL_IDM; o.lc[k] = (uint8_t)cfg->lane_change;
+      o.x[k] = R->start_x[lid] + x0 * R->dir_x[lid] + 0.0 * (-R->dir_y[lid]);
+      o.y[k] = R->start_y[lid] + x0 * R->dir_y[lid] + 0.0 * R->dir_x[lid];
+      o.h[k] = R->heading[lid]; o.v[k] = sp; o.ts[k] = sp;
+      o.lane[k] = o.tgt[k] = closest_lane(R, o.x[k], o.y[k], o.h[k]);
+      o.timer[k] = pymod((o.x[k] + o.y[k]) * PI, P->lane_change_delay);
+      o.delta[k] = pcg_uniform(&g, cfg->delta_lo, cfg->delta_hi);
+    }
+  }
+  return 0;
+}
+
+/* IntersectionEnv._agent_reward / _is_terminated / _is_truncated template (intersection_env.py:78-119) */
+int oracle_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_reward_cfg_t* cfg,
+                   const double* time, float* reward, uint8_t* terminated, uint8_t* truncated) {
+  if (check(s)) return TTRL_E_ARG;
+  S o = view(s);
+  ttrl_params_t dummy; memset(&dummy, 0, sizeof dummy); dummy.lane_vehicle_length = 5.0;
+  for (int e = 0; e < o.E; ++e) {
+    int k = e * o.N;
+    double hs = clipd(lmap(o.v[k], cfg->speed_lo, cfg->speed_hi, 0, 1), 0, 1);
+    double sr, rr; local(R, o.lane[k], o.x[k], o.y[k], &sr, &rr);
+    int onroad = on_lane(R, &dummy, o.lane[k], sr, rr, 0.0);
+    double r = cfg->collision_reward * (double)o.crashed[k] + cfg->high_speed_reward * hs;
+    r *= (double)onroad;
+    if (cfg->normalize_reward) r = lmap(r, cfg->collision_reward, cfg->high_speed_reward, 0, 1);
+    reward[e] = (float)r;
+    terminated[e] = (uint8_t)(o.crashed[k] || (cfg->offroad_terminal && !onroad));
+    truncated[e] = (uint8_t)(time[e] >= cfg->duration);
+  }
+  return 0;
+}

@@ -1,0 +1,272 @@
+"""ctypes mirror of include/ttrl_mi355x.h and the host-side builders of its structs.
+
+The derived lane geometry and behaviour constants are computed here with the
+same float64 expressions the reference evaluates (StraightLane.__init__
+lane.py:162-194, IDMVehicle/ControlledVehicle class constants behavior.py:20-46,
+controller.py:24-33), so the kernels receive bit-identical constants.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+MAX_LANES = 16
+N_FEATURES = 14
+F32, F64 = 0, 1
+ABSENT, MDP, IDM = 0, 1, 2
+LANE_LEFT, IDLE, LANE_RIGHT, FASTER, SLOWER = 0, 1, 2, 3, 4
+ACTIONS_ALL = {0: "LANE_LEFT", 1: "IDLE", 2: "LANE_RIGHT", 3: "FASTER", 4: "SLOWER"}  # action.py:204
+
+FEATURES = ["presence", "x", "y", "vx", "vy", "heading", "cos_h", "sin_h", "cos_d", "sin_d",
+            "long_off", "lat_off", "ang_off", "on_road"]
+FEATURE_CODE = {f: i for i, f in enumerate(FEATURES)}
+
+REAL_FIELDS = ["x", "y", "heading", "speed", "target_speed", "timer", "delta",
+               "steer", "acc", "impact_x", "impact_y"]
+I32_FIELDS = ["lane", "target_lane", "speed_index"]
+U8_FIELDS = ["kind", "crashed", "has_impact", "lane_change"]
+ALL_FIELDS = REAL_FIELDS + I32_FIELDS + U8_FIELDS
+
+ERRORS = {-1: "TTRL_E_ARG (bad argument)", -2: "TTRL_E_LAUNCH (HIP error)", -3: "TTRL_E_UNSUPPORTED"}
+
+
+class LaneTable(C.Structure):
+    _fields_ = [("n_lanes", C.c_int32), ("_pad", C.c_int32),
+                ("start_x", C.c_double * MAX_LANES), ("start_y", C.c_double * MAX_LANES),
+                ("dir_x", C.c_double * MAX_LANES), ("dir_y", C.c_double * MAX_LANES),
+                ("length", C.c_double * MAX_LANES), ("width", C.c_double * MAX_LANES),
+                ("heading", C.c_double * MAX_LANES), ("speed_limit", C.c_double * MAX_LANES),
+                ("forbidden", C.c_int32 * MAX_LANES)]
+
+
+class Params(C.Structure):
+    _fields_ = [(n, C.c_double) for n in (
+        "acc_max", "comfort_acc_max", "comfort_acc_min", "distance_wanted", "time_wanted",
+        "gap_denom", "politeness", "lane_change_min_acc_gain", "lane_change_max_braking",
+        "lane_change_delay", "tau_pursuit", "kp_a", "kp_heading", "kp_lateral", "max_steering",
+        "length", "width", "diagonal", "max_speed", "min_speed", "lane_vehicle_length")] + [
+        ("target_speeds", C.c_double * 8), ("n_target_speeds", C.c_int32), ("_pad", C.c_int32)]
+
+
+class State(C.Structure):
+    _fields_ = ([("n_envs", C.c_int32), ("n_veh", C.c_int32), ("dtype", C.c_int32), ("_pad", C.c_int32)]
+                + [(n, C.c_void_p) for n in ALL_FIELDS])
+
+
+class KinCfg(C.Structure):
+    _fields_ = [("vehicles_count", C.c_int32), ("n_features", C.c_int32),
+                ("features", C.c_int32 * N_FEATURES),
+                ("absolute", C.c_int32), ("normalize", C.c_int32), ("clip", C.c_int32),
+                ("see_behind", C.c_int32), ("order_shuffled", C.c_int32), ("_pad", C.c_int32),
+                ("range_lo", C.c_double * N_FEATURES), ("range_hi", C.c_double * N_FEATURES),
+                ("has_range", C.c_int32 * N_FEATURES), ("perception_distance", C.c_double),
+                ("shuffle_seed", C.c_uint64), ("shuffle_offset", C.c_uint64)]
+
+
+class GridCfg(C.Structure):
+    _fields_ = [("n_features", C.c_int32), ("features", C.c_int32 * N_FEATURES),
+                ("shape_x", C.c_int32), ("shape_y", C.c_int32), ("clip", C.c_int32),
+                ("grid_min_x", C.c_double), ("grid_min_y", C.c_double),
+                ("step_x", C.c_double), ("step_y", C.c_double),
+                ("range_lo", C.c_double * N_FEATURES), ("range_hi", C.c_double * N_FEATURES),
+                ("has_range", C.c_int32 * N_FEATURES), ("lane_perception_distance", C.c_double)]
+
+
+class ResetCfg(C.Structure):
+    _fields_ = [("n_vehicles", C.c_int32), ("ego_lane", C.c_int32),
+                ("ego_x", C.c_double), ("ego_speed", C.c_double),
+                ("speed_lo", C.c_double), ("speed_hi", C.c_double), ("spacing", C.c_double),
+                ("density_factor", C.c_double), ("delta_lo", C.c_double), ("delta_hi", C.c_double),
+                ("lane_change", C.c_int32), ("_pad", C.c_int32)]
+
+
+class RewardCfg(C.Structure):
+    _fields_ = [("collision_reward", C.c_double), ("high_speed_reward", C.c_double),
+                ("speed_lo", C.c_double), ("speed_hi", C.c_double),
+                ("normalize_reward", C.c_int32), ("offroad_terminal", C.c_int32),
+                ("duration", C.c_double)]
+
+
+# ----------------------------------------------------------------------------- builders
+def straight_lane_table(lanes: int = 4, start: float = 0.0, length: float = 10000.0, angle: float = 0.0,
+                        speed_limit: float = 30.0, width: float = 4.0, forbidden=None) -> LaneTable:
+    """RoadNetwork.straight_road_network (road.py:291-321) + StraightLane.__init__ (lane.py:162-194)."""
+    if not 1 <= lanes <= MAX_LANES:
+        raise ValueError(f"lanes must be in [1, {MAX_LANES}]")
+    t = LaneTable()
+    t.n_lanes = lanes
+    rot = np.array([[np.cos(angle), np.sin(angle)], [-np.sin(angle), np.cos(angle)]])
+    for i in range(lanes):
+        o = rot @ np.array([start, i * 4.0])      # StraightLane.DEFAULT_WIDTH spacing
+        e = rot @ np.array([start + length, i * 4.0])
+        ln = np.linalg.norm(e - o)
+        d = (e - o) / ln
+        t.start_x[i], t.start_y[i] = float(o[0]), float(o[1])
+        t.dir_x[i], t.dir_y[i] = float(d[0]), float(d[1])
+        t.length[i] = float(ln)
+        t.width[i] = float(width)
+        t.heading[i] = float(np.arctan2(e[1] - o[1], e[0] - o[0]))
+        t.speed_limit[i] = float(speed_limit)
+        t.forbidden[i] = int(bool(forbidden[i])) if forbidden is not None else 0
+    return t
+
+
+def lane_table_from_arrays(table: np.ndarray) -> LaneTable:
+    """[L, 6] rows (start_x, start_y, end_x, end_y, width, speed_limit), as dumped by gen_golden."""
+    t = LaneTable()
+    t.n_lanes = len(table)
+    for i, (sx, sy, ex, ey, w, lim) in enumerate(np.asarray(table, dtype=np.float64)):
+        s, e = np.array([sx, sy]), np.array([ex, ey])
+        ln = np.linalg.norm(e - s)
+        d = (e - s) / ln
+        t.start_x[i], t.start_y[i], t.dir_x[i], t.dir_y[i] = sx, sy, d[0], d[1]
+        t.length[i], t.width[i], t.speed_limit[i] = ln, w, lim
+        t.heading[i] = np.arctan2(e[1] - s[1], e[0] - s[0])
+    return t
+
+
+def default_params(target_speeds=None, **overrides) -> Params:
+    """Reference class constants (behavior.py:20-46, controller.py:24-33, kinematics.py:21-29)."""
+    p = Params()
+    p.acc_max = 6.0
+    p.comfort_acc_max = 3.0
+    p.comfort_acc_min = -5.0
+    p.distance_wanted = 5.0 + 5.0
+    p.time_wanted = 1.5
+    p.politeness = 0.0
+    p.lane_change_min_acc_gain = 0.2
+    p.lane_change_max_braking = 2.0
+    p.lane_change_delay = 1.0
+    tau_heading = 0.2
+    p.tau_pursuit = 0.5 * tau_heading
+    p.kp_a = 1 / 0.6
+    p.kp_heading = 1 / tau_heading
+    p.kp_lateral = 1 / 0.6
+    p.max_steering = np.pi / 3
+    p.length = 5.0
+    p.width = 2.0
+    p.max_speed = 40.0
+    p.min_speed = -40.0
+    p.lane_vehicle_length = 5.0
+    for k, v in overrides.items():
+        if not hasattr(p, k):
+            raise KeyError(k)
+        setattr(p, k, v)
+    p.gap_denom = float(2 * np.sqrt(-p.comfort_acc_max * p.comfort_acc_min))
+    p.diagonal = float(np.sqrt(p.length ** 2 + p.width ** 2))
+    ts = np.linspace(20, 30, 3) if target_speeds is None else np.asarray(target_speeds, dtype=np.float64)
+    if not 1 <= len(ts) <= 8:
+        raise ValueError("1..8 target speeds supported")
+    for i, v in enumerate(ts):
+        p.target_speeds[i] = float(v)
+    p.n_target_speeds = len(ts)
+    return p
+
+
+def _ranges(cfg_ranges, code_arrays):
+    lo, hi, has = code_arrays
+    for name, (a, b) in (cfg_ranges or {}).items():
+        if name in FEATURE_CODE:
+            c = FEATURE_CODE[name]
+            lo[c], hi[c], has[c] = float(a), float(b), 1
+
+
+def kin_cfg(features=("presence", "x", "y", "vx", "vy"), vehicles_count=5, features_range=None,
+            absolute=False, order="sorted", normalize=True, clip=True, see_behind=False,
+            lanes_on_road=4, perception_distance=200.0, shuffle_seed=0, shuffle_offset=0,
+            observe_intentions=False, include_obstacles=True, **_ignored) -> KinCfg:
+    """KinematicObservation.__init__ (observation.py:159-196); default ranges observation.py:213-225."""
+    if order not in ("sorted", "shuffled"):
+        raise ValueError(f"unknown order {order!r}")
+    c = KinCfg()
+    c.vehicles_count = int(vehicles_count)
+    c.n_features = len(features)
+    if not 1 <= c.n_features <= N_FEATURES or c.vehicles_count < 1:
+        raise ValueError("bad Kinematics observation shape")
+    for i, f in enumerate(features):
+        if f not in FEATURE_CODE or f == "on_road":
+            raise ValueError(f"unsupported Kinematics feature {f!r}")
+        c.features[i] = FEATURE_CODE[f]
+    c.absolute, c.normalize, c.clip, c.see_behind = int(absolute), int(normalize), int(clip), int(see_behind)
+    c.order_shuffled = int(order == "shuffled")
+    if not features_range:
+        features_range = {"x": [-5.0 * 40.0, 5.0 * 40.0], "y": [-4 * lanes_on_road, 4 * lanes_on_road],
+                          "vx": [-2 * 40.0, 2 * 40.0], "vy": [-2 * 40.0, 2 * 40.0]}
+    _ranges(features_range, (c.range_lo, c.range_hi, c.has_range))
+    c.perception_distance = float(perception_distance)
+    c.shuffle_seed, c.shuffle_offset = int(shuffle_seed), int(shuffle_offset)
+    return c
+
+
+def grid_cfg(features=("presence", "vx", "vy", "on_road"), grid_size=((-27.5, 27.5), (-27.5, 27.5)),
+             grid_step=(5, 5), features_range=None, absolute=False, align_to_vehicle_axes=False,
+             clip=True, as_image=False, **_ignored) -> GridCfg:
+    """OccupancyGridObservation.__init__ (observation.py:285-326); default ranges :343-347."""
+    if absolute:
+        raise NotImplementedError("OccupancyGrid absolute=True (observation.py:357-358)")
+    if align_to_vehicle_axes or as_image:
+        raise NotImplementedError("align_to_vehicle_axes / as_image are not on the hot path")
+    g = GridCfg()
+    g.n_features = len(features)
+    for i, f in enumerate(features):
+        if f not in FEATURE_CODE:
+            raise ValueError(f"unsupported OccupancyGrid feature {f!r}")
+        g.features[i] = FEATURE_CODE[f]
+    size = np.array(grid_size, dtype=np.float64)
+    step = np.array(grid_step, dtype=np.float64)
+    shape = np.asarray(np.floor((size[:, 1] - size[:, 0]) / step), dtype=np.uint8)
+    g.shape_x, g.shape_y = int(shape[0]), int(shape[1])
+    g.grid_min_x, g.grid_min_y = float(size[0, 0]), float(size[1, 0])
+    g.step_x, g.step_y = float(step[0]), float(step[1])
+    g.clip = int(clip)
+    if not features_range:
+        features_range = {"vx": [-2 * 40.0, 2 * 40.0], "vy": [-2 * 40.0, 2 * 40.0]}
+    _ranges(features_range, (g.range_lo, g.range_hi, g.has_range))
+    g.lane_perception_distance = 100.0
+    return g
+
+
+def reset_cfg(n_vehicles, lanes: LaneTable, ego_lane=1, ego_x=50.0, ego_speed=25.0, spacing=1.0,
+              lane_change=True) -> ResetCfg:
+    """Highway scene parameters, float64 constants as create_random evaluates them."""
+    r = ResetCfg()
+    r.n_vehicles = int(n_vehicles)
+    r.ego_lane = int(ego_lane)
+    r.ego_x, r.ego_speed = float(ego_x), float(ego_speed)
+    lim = lanes.speed_limit[0]
+    r.speed_lo, r.speed_hi = float(0.7 * lim), float(0.8 * lim)
+    r.spacing = float(spacing)
+    r.density_factor = float(np.exp(-5 / 40 * lanes.n_lanes))
+    r.delta_lo, r.delta_hi = 3.5, 4.5
+    r.lane_change = int(lane_change)
+    return r
+
+
+def reward_cfg(collision_reward=-1.0, high_speed_reward=0.4, reward_speed_range=(20.0, 30.0),
+               normalize_reward=False, offroad_terminal=False, duration=40.0) -> RewardCfg:
+    c = RewardCfg()
+    c.collision_reward, c.high_speed_reward = float(collision_reward), float(high_speed_reward)
+    c.speed_lo, c.speed_hi = float(reward_speed_range[0]), float(reward_speed_range[1])
+    c.normalize_reward, c.offroad_terminal = int(normalize_reward), int(offroad_terminal)
+    c.duration = float(duration)
+    return c
+
+
+def pcg64_states(seeds) -> np.ndarray:
+    """Initial numpy PCG64 state per env, [E, 4] uint64 {state_hi, state_lo, inc_hi, inc_lo}.
+    np.random.default_rng(seed) == Generator(PCG64(SeedSequence(seed)))."""
+    out = np.zeros((len(seeds), 4), dtype=np.uint64)
+    m = (1 << 64) - 1
+    for i, s in enumerate(seeds):
+        st = np.random.PCG64(int(s)).state["state"]
+        out[i] = [(st["state"] >> 64) & m, st["state"] & m, (st["inc"] >> 64) & m, st["inc"] & m]
+    return out
+
+
+def state_struct(ptrs: dict, n_envs: int, n_veh: int, dtype: int) -> State:
+    s = State()
+    s.n_envs, s.n_veh, s.dtype = int(n_envs), int(n_veh), int(dtype)
+    for f in ALL_FIELDS:
+        setattr(s, f, ptrs[f])
+    return s
