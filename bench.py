@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Benchmark of the batched env.step() hot path (BASELINE.json north star).
+
+A "step" is one batched env.step(): the fused 15-frame AbstractEnv._simulate
+(meta-action + 15 x {Road.act, Road.step}) of every env on the GPU, then the
+Kinematics observation and the rewards.  value = vehicle-steps/s over ALL ranks,
+where one vehicle-step = one vehicle through one simulation frame.
+
+Default workload (config 4, per GPU): 4096 envs x 64 vehicles, Kinematics 15x7
+(env.json ranges, absolute=false, sorted), synthetic straight 4-lane highway,
+random-seeded scenes and uniformly random ego actions (pre-drawn on the device).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype f64|f32] [--config 2|3|4|5]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+KIN15 = {"type": "Kinematics", "vehicles_count": 15,
+         "features": ["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"],
+         "features_range": {"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]},
+         "absolute": False, "order": "sorted"}
+GRID7 = {"type": "OccupancyGrid", "features": ["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"],
+         "features_range": {"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]},
+         "grid_size": [[-32, 32], [-32, 32]], "grid_step": [2, 2], "absolute": False}
+CONFIGS = {
+    2: dict(num_envs=4096, vehicles=32, obs=KIN15, name="4096 envs x 32 vehicles, Kinematics 15x7"),
+    3: dict(num_envs=4096, vehicles=128, obs=GRID7, name="4096 envs x 128 vehicles, OccupancyGrid 7x32x32"),
+    4: dict(num_envs=4096, vehicles=64, obs=KIN15, name="4096 envs x 64 vehicles per GPU, Kinematics 15x7"),
+    5: dict(num_envs=8192, vehicles=64, obs=KIN15, name="8192 envs x 64 vehicles, EgoAttention-2h policy in the loop"),
+}
+
+
+def state_bytes(dtype: str) -> tuple[int, int]:
+    """Algorithmic HBM bytes per vehicle for one fused launch: (read, written).
+    read: 11 real fields + lane, target_lane, speed_index (i32) + kind, crashed, has_impact, lane_change (u8)
+    written: 10 real fields (all but delta) + 3 x i32 + crashed, has_impact (u8)."""
+    r = 8 if dtype == "f64" else 4
+    return 11 * r + 3 * 4 + 4, 10 * r + 3 * 4 + 2
+
+
+def cpu_baseline(vehicles: int, obs_cfg: dict, seconds_target: float = 10.0) -> dict:
+    """The float64 C restatement (oracle/) on host cores, bounded sample of the same workload."""
+    from oracle.oracle import HostState, Oracle
+    from topotrafficrl_amd import _abi
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    lanes = _abi.straight_lane_table(4)
+    o = Oracle(lanes, _abi.default_params())
+    kin = _abi.kin_cfg(**{k: v for k, v in obs_cfg.items() if k != "type"}) if obs_cfg["type"] == "Kinematics" else None
+    grid = _abi.grid_cfg(**{k: v for k, v in obs_cfg.items() if k != "type"}) if kin is None else None
+    E = 64 * threads
+    h = HostState(E, vehicles)
+    o.reset_highway(h, _abi.reset_cfg(vehicles, lanes), list(range(E)))
+    rng = np.random.default_rng(0)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        o.simulate(h, rng.integers(0, 5, size=E).astype(np.int32), 15, 1 / 15)
+        if kin is not None:
+            o.observe_kinematics(h, kin)
+        else:
+            o.observe_grid(h, grid)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds_target or steps >= 40:
+            break
+    return {"value": E * vehicles * 15 * steps / el, "unit": "vehicle-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{E} envs x {vehicles} vehicles x {steps} env.step (15 frames + obs), float64 C restatement "
+                      f"of the reference loop order (oracle/ttrl_oracle.c), OpenMP over envs, {el:.1f} s"}
+
+
+def read_pmc(dtype: str, cfg_id: int) -> dict | None:
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        return d.get(f"config{cfg_id}_{dtype}")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--config", type=int, default=4, choices=[2, 3, 4, 5])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from topotrafficrl_amd.envs import VecHighwayEnv
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    C = CONFIGS[args.config]
+    E, N = C["num_envs"], C["vehicles"]
+    env = VecHighwayEnv({"num_envs": E, "vehicles_count": N, "observation": C["obs"], "device": str(dev),
+                         "dtype": args.dtype, "env_id_offset": rank * E})
+    policy = None
+    if args.config == 5:
+        from topotrafficrl_amd.agent import EgoAttentionPolicy
+        policy = EgoAttentionPolicy(device=dev, seed=0)
+    obs, _ = env.reset(seed=12345)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    acts = torch.randint(0, 5, (args.warmup + args.steps, E), device=dev, generator=g, dtype=torch.int64)
+
+    def one_step(t):
+        nonlocal obs
+        a = policy.act(obs, t) if policy is not None else acts[t]
+        obs, rew, term, trunc, info = env.step(a)
+
+    for t in range(args.warmup):
+        one_step(t)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    road = env.road
+    orig_sim = road.simulate
+    k_iter = iter(ev)
+
+    def timed_sim(*a, **kw):  # HIP events bracket the fused simulate kernel on its stream
+        s, e = next(k_iter)
+        s.record(stream)
+        orig_sim(*a, **kw)
+        e.record(stream)
+
+    road.simulate = timed_sim
+    t0 = time.perf_counter()
+    for t in range(args.warmup, args.warmup + args.steps):
+        one_step(t)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    road.simulate = orig_sim
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    veh_steps = world * E * N * 15 * args.steps
+    value = veh_steps / elapsed
+    rd, wr = state_bytes(args.dtype)
+    alg_bytes = E * N * (rd + wr)  # per fused simulate launch
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    pmc = read_pmc(args.dtype, args.config)
+    out = {
+        "metric": "vehicle-steps/sec at 4096 envs×64 vehicles; 1/2/4/8 GPUs; HBM GB/s achieved",
+        "value": value,
+        "unit": "vehicle-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic",
+        "config": {"workload": C["name"], "envs_per_gpu": E, "vehicles_per_env": N, "frames_per_step": 15,
+                   "observation": C["obs"]["type"], "parallelism": f"env-sharded x{world}, no collective on the step"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
+                     "kernel": "simulate_kernel (fused 15-frame Road.act+Road.step)",
+                     "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
+                     "alg_bytes_per_vehicle_step": (rd + wr) / 15.0},
+        "env_steps_per_s": world * E * args.steps / elapsed,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(N, C["obs"] if C["obs"]["type"] == "Kinematics" else GRID7,
+                                           args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

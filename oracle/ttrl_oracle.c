@@ -349,12 +349,12 @@ int oracle_meta_action(const ttrl_state_t* s, const ttrl_lane_table_t* R, const 
                        const int32_t* actions, void* stream) {
   (void)stream; if (check(s)) return TTRL_E_ARG;
   S o = view(s);
+  for (int e = 0; e < o.E; ++e)
+    if (actions[e] < 0 || actions[e] > 4) return TTRL_E_ARG;
   for (int e = 0; e < o.E; ++e) {
     int base = e * o.N;
     if (o.kind[base] != TTRL_MDP) continue;
-    int a = actions[e];
-    if (a < 0 || a > 4) return TTRL_E_ARG;
-    mdp_act(&o, R, P, base, 0, a);
+    mdp_act(&o, R, P, base, 0, actions[e]);
   }
   return 0;
 }
@@ -363,6 +363,7 @@ int oracle_meta_action(const ttrl_state_t* s, const ttrl_lane_table_t* R, const 
 int oracle_road_act(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P, void* stream) {
   (void)stream; if (check(s)) return TTRL_E_ARG;
   S o = view(s);
+#pragma omp parallel for schedule(static)
   for (int e = 0; e < o.E; ++e) {
     int base = e * o.N;
     for (int i = 0; i < o.N; ++i) {
@@ -377,6 +378,7 @@ int oracle_road_act(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttr
 int oracle_road_step(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P, double dt, void* stream) {
   (void)stream; if (check(s)) return TTRL_E_ARG;
   S o = view(s);
+#pragma omp parallel for schedule(static)
   for (int e = 0; e < o.E; ++e) {
     int base = e * o.N;
     for (int i = 0; i < o.N; ++i)
@@ -449,8 +451,11 @@ int oracle_observe_kinematics(const ttrl_state_t* s, const ttrl_lane_table_t* R,
   (void)P; if (check(s)) return TTRL_E_ARG;
   S o = view(s);
   const int V = cfg->vehicles_count, F = cfg->n_features;
+#pragma omp parallel
+  {
   int* cand = (int*)malloc(sizeof(int) * o.N);
   double* key = (double*)malloc(sizeof(double) * o.N);
+#pragma omp for schedule(static)
   for (int e = 0; e < o.E; ++e) {
     int base = e * o.N, ego = base;
     float* ob = out + (size_t)e * V * F;
@@ -492,6 +497,7 @@ int oracle_observe_kinematics(const ttrl_state_t* s, const ttrl_lane_table_t* R,
       for (int r = 0; r < V - 1; ++r) ids[e * (V - 1) + r] = r < nc ? cand[r] : -1;
   }
   free(cand); free(key);
+  }
   return 0;
 }
 
@@ -501,7 +507,10 @@ int oracle_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* R, const
   (void)P; if (check(s)) return TTRL_E_ARG;
   S o = view(s);
   const int F = cfg->n_features, W = cfg->shape_x, H = cfg->shape_y;
+#pragma omp parallel
+  {
   double* grid = (double*)malloc(sizeof(double) * F * W * H);
+#pragma omp for schedule(static)
   for (int e = 0; e < o.E; ++e) {
     int base = e * o.N, ego = base;
     for (int q = 0; q < F * W * H; ++q) grid[q] = NAN;
@@ -555,6 +564,7 @@ int oracle_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* R, const
     }
   }
   free(grid);
+  }
   return 0;
 }
 
@@ -593,6 +603,7 @@ int oracle_reset_highway(const ttrl_state_t* s, const ttrl_lane_table_t* R, cons
                          const ttrl_reset_cfg_t* cfg, const uint64_t* pcg) {
   if (check(s) || cfg->n_vehicles > s->n_veh || cfg->n_vehicles < 1) return TTRL_E_ARG;
   S o = view(s);
+#pragma omp parallel for schedule(static)
   for (int e = 0; e < o.E; ++e) {
     int base = e * o.N;
     pcg_t g;
