@@ -1,0 +1,89 @@
+"""Build (here) and time (on the GPU) compile-time variants of the fused kernel, interleaved in one process.
+
+  python tools/variants.py build          # cross-compile variants into tools/_variants/
+  python tools/variants.py run [f64 f32]  # on the GPU box
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+OUT = os.path.join(ROOT, "tools", "_variants")
+VARIANTS = {
+    "w0": [],
+    "w2": ["-DTTRL_SIM_WAVES=2"],
+    "w3": ["-DTTRL_SIM_WAVES=3"],
+    "w4": ["-DTTRL_SIM_WAVES=4"],
+    "w2_ni": ["-DTTRL_SIM_WAVES=2", "-DTTRL_SAT_NOINLINE"],
+    "w3_ni": ["-DTTRL_SIM_WAVES=3", "-DTTRL_SAT_NOINLINE"],
+    "w4_ni": ["-DTTRL_SIM_WAVES=4", "-DTTRL_SAT_NOINLINE"],
+}
+for arg in os.environ.get("EXTRA_VARIANTS", "").split(";"):
+    if arg.strip():
+        name, flags = arg.split("=", 1)
+        VARIANTS[name] = flags.split()
+
+
+def build():
+    os.makedirs(OUT, exist_ok=True)
+    src = os.path.join(ROOT, "topotrafficrl_amd", "csrc", "ttrl_mi355x.hip")
+    procs = []
+    for name, flags in VARIANTS.items():
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
+               "-shared", "-I", os.path.join(ROOT, "include"), *flags, "-o", os.path.join(OUT, f"lib_{name}.so"), src]
+        procs.append(subprocess.Popen(cmd))
+    for p in procs:
+        assert p.wait() == 0
+
+
+def run(dtypes, E=4096, N=64, rounds=7):
+    import numpy as np
+    import torch
+    from topotrafficrl_amd import _abi, _lib
+    from topotrafficrl_amd.envs import reset_highway
+    from topotrafficrl_amd.road import RoadNetwork
+    from topotrafficrl_amd.state import BatchState
+    dev = torch.device("cuda:0")
+    net = RoadNetwork.straight_road_network(4)
+    P = _abi.default_params()
+    libs = {}
+    for name in VARIANTS:
+        lib = _lib.load(os.path.join(OUT, f"lib_{name}.so"))
+        lib.ttrl_simulate.argtypes = [C.c_void_p] * 4 + [C.c_int32, C.c_double, C.c_void_p]
+        libs[name] = lib
+    for dtype in dtypes:
+        base = BatchState(E, N, device=dev, dtype=dtype)
+        reset_highway(base, net, P, _abi.reset_cfg(N, net.table), list(range(E)))
+        torch.cuda.synchronize()
+        ref = None
+        work = base.clone()
+        acts = torch.randint(0, 5, (E,), device=dev, dtype=torch.int32, generator=torch.Generator(device=dev).manual_seed(0))
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        times = {k: [] for k in VARIANTS}
+        for r in range(rounds):
+            for name, lib in libs.items():
+                work.copy_(base)
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                rc = lib.ttrl_simulate(C.byref(work.struct()), C.byref(net.table), C.byref(P), acts.data_ptr(), 15,
+                                       1 / 15, stream)
+                e.record()
+                torch.cuda.synchronize()
+                assert rc == 0
+                times[name].append(s.elapsed_time(e))
+                out = work["x"].cpu().numpy()
+                if ref is None:
+                    ref = out
+                assert np.array_equal(out, ref), f"variant {name} changed the result"
+        print(f"[{dtype}] E={E} N={N} fused 15-frame launch, median of {rounds - 1} rounds")
+        for k, v in times.items():
+            print(f"  {k:10s} {np.median(v[1:]):8.3f} ms  min {np.min(v[1:]):8.3f}")
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "build":
+        build()
+    else:
+        run(sys.argv[2:] or ["f64", "f32"])

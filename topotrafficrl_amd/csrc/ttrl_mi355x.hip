@@ -20,6 +20,7 @@
 namespace {
 
 constexpr int LMAX = TTRL_MAX_LANES;
+constexpr float FAR = 1e30f;  // x of absent slots in the LDS view: never within a collision window
 
 template <typename T> struct K;
 template <> struct K<double> {
@@ -41,6 +42,7 @@ template <typename T> __device__ __forceinline__ T not_zero(T x) {
 }
 // numpy float remainder (result has the divisor's sign)
 template <typename T> __device__ __forceinline__ T pymod(T a, T b) {
+  if (a >= T(0) && a < b) return a;  // fmod(a, b) == a exactly; skips the generic fmod
   T m = fmod(a, b);
   if (m != T(0)) { if ((b < T(0)) != (m < T(0))) m += b; }
   else m = copysign(T(0), b);
@@ -100,10 +102,19 @@ __device__ __forceinline__ int speed_to_index(const ttrl_params_t& P, T v) {
   return (int)clip(rint(x * T(n - 1)), T(0), T(n - 1));
 }
 
+#ifndef TTRL_SIM_WAVES
+#define TTRL_SIM_WAVES 0   // min waves/SIMD for the fused kernel; 0 = tuned default (f64: 2, f32: 4)
+#endif
+#ifdef TTRL_SAT_NOINLINE
+#define TTRL_SAT_ATTR __noinline__
+#else
+#define TTRL_SAT_ATTR
+#endif
+
 // utils.are_polygons_intersecting utils.py:194-239 on the closed 5-point rectangles of
 // RoadObject.polygon objects.py:168-180.  a = lower-index vehicle (the reference's self).
 template <typename T>
-__device__ void sat_pair(const ttrl_params_t& P, T ax, T ay, T ac, T as, T av, T bx, T by, T bc, T bs, T bv,
+__device__ TTRL_SAT_ATTR void sat_pair(const ttrl_params_t& P, T ax, T ay, T ac, T as, T av, T bx, T by, T bc, T bs, T bv,
                          T dt, bool& inter, bool& will, T& tx, T& ty) {
   const T hl = T(P.length) / T(2), hw = T(P.width) / T(2);
   const T lx[4] = {-hl, -hl, +hl, +hl}, ly[4] = {-hw, +hw, +hw, -hw};
@@ -163,30 +174,36 @@ __device__ void sat_pair(const ttrl_params_t& P, T ax, T ay, T ac, T as, T av, T
 }
 
 // ---------------------------------------------------------------------------------
+// Per-lane candidate list entry: (longitudinal coordinate on the lane, vehicle slot).
+template <typename T> struct LEnt;
+template <> struct __attribute__((aligned(16))) LEnt<double> { double s; int idx; int pad; };
+template <> struct __attribute__((aligned(8))) LEnt<float> { float s; int idx; };
+
 // LDS "road view" of one workgroup (EPW envs x NS slots).
 template <typename T> struct View {
   LaneT<T>* lanes;   // [LMAX]
   T *x, *y, *v, *ch, *sh, *ts;  // [EPW*NS]
-  T* proj;           // [n_lanes][EPW][NSP] masked lane projection (NaN off-lane / absent)
+  LEnt<T>* ent;      // [n_lanes][EPW][NS+1] vehicles on each lane (AbstractLane.on_lane margin 1), slot order
+  int* cnt;          // [EPW][LMAX+1] list lengths; [LMAX] = longest list of the env
+  int* wcnt;         // [LMAX][4] per-wave list lengths (NS > 64)
   int8_t *lane, *tgt;            // [EPW*NS] lane (-1 absent), target (old, for the act phase)
   unsigned long long* bal;       // [2][8] cross-wave ballots (NS > 64)
+  T* red;                        // [8] cross-wave reduction scratch
 };
 
-template <typename T>
-__device__ __forceinline__ size_t view_bytes(int EPW, int NS, int n_lanes) {
-  const int NSP = NS + 1;
-  size_t b = sizeof(LaneT<T>) * LMAX;
-  b += sizeof(T) * (6 * EPW * NS + (size_t)n_lanes * EPW * NSP);
+inline __host__ __device__ size_t view_bytes_t(size_t t, size_t lane_sz, size_t ent_sz, int EPW, int NS, int n_lanes) {
+  size_t b = lane_sz * LMAX + t * (6 * EPW * NS);
+  b = (b + 15) & ~(size_t)15;
+  b += ent_sz * (size_t)n_lanes * EPW * (NS + 1);
+  b += sizeof(int) * (EPW * (LMAX + 1) + LMAX * 4);
   b += 2 * EPW * NS;
   b = (b + 15) & ~(size_t)15;
-  b += 16 * sizeof(unsigned long long);
-  return b;
+  return b + 16 * sizeof(unsigned long long) + 8 * t;
 }
 
 template <typename T>
 __device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lanes) {
   View<T> V;
-  const int NSP = NS + 1;
   char* p = smem;
   V.lanes = (LaneT<T>*)p; p += sizeof(LaneT<T>) * LMAX;
   V.x = (T*)p; p += sizeof(T) * EPW * NS;
@@ -195,20 +212,22 @@ __device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lane
   V.ch = (T*)p; p += sizeof(T) * EPW * NS;
   V.sh = (T*)p; p += sizeof(T) * EPW * NS;
   V.ts = (T*)p; p += sizeof(T) * EPW * NS;
-  V.proj = (T*)p; p += sizeof(T) * (size_t)n_lanes * EPW * NSP;
+  p = (char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
+  V.ent = (LEnt<T>*)p; p += sizeof(LEnt<T>) * (size_t)n_lanes * EPW * (NS + 1);
+  V.cnt = (int*)p; p += sizeof(int) * EPW * (LMAX + 1);
+  V.wcnt = (int*)p; p += sizeof(int) * LMAX * 4;
   V.lane = (int8_t*)p; p += EPW * NS;
   V.tgt = (int8_t*)p; p += EPW * NS;
   p = (char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
-  V.bal = (unsigned long long*)p;
+  V.bal = (unsigned long long*)p; p += 16 * sizeof(unsigned long long);
+  V.red = (T*)p;
   return V;
 }
 
 size_t host_view_bytes(int dtype, int EPW, int NS, int n_lanes) {
-  const size_t t = dtype == TTRL_F64 ? 8 : 4;
-  const size_t lane_sz = dtype == TTRL_F64 ? sizeof(LaneT<double>) : sizeof(LaneT<float>);
-  size_t b = lane_sz * LMAX + t * (6 * EPW * NS + (size_t)n_lanes * EPW * (NS + 1)) + 2 * EPW * NS;
-  b = (b + 15) & ~(size_t)15;
-  return b + 16 * sizeof(unsigned long long);
+  return dtype == TTRL_F64
+             ? view_bytes_t(8, sizeof(LaneT<double>), sizeof(LEnt<double>), EPW, NS, n_lanes)
+             : view_bytes_t(4, sizeof(LaneT<float>), sizeof(LEnt<float>), EPW, NS, n_lanes);
 }
 
 template <typename T>
@@ -220,6 +239,25 @@ __device__ __forceinline__ void stage_lanes(View<T>& V, const ttrl_lane_table_t&
     L.forb = R.forbidden[tid]; L._pad = 0;
     V.lanes[tid] = L;
   }
+}
+
+// Max over the NS slots of an env (all threads of the workgroup must call it).
+template <typename T, int NS, int EPW>
+__device__ __forceinline__ T env_max(T v, const View<T>& V, int tid) {
+  constexpr int W = NS < 64 ? NS : 64;
+#pragma unroll
+  for (int off = 1; off < W; off <<= 1) {
+    const T o = __shfl_xor(v, off);
+    v = v > o ? v : o;
+  }
+  if constexpr (NS > 64) {
+    __syncthreads();
+    if ((tid & 63) == 0) V.red[tid >> 6] = v;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < NS / 64; ++w) v = v > V.red[w] ? v : V.red[w];
+  }
+  return v;
 }
 
 // Per-thread vehicle registers.
@@ -272,31 +310,88 @@ __device__ __forceinline__ void store_veh(const Veh<T>& a, const ttrl_state_t& s
   s.has_impact[k] = a.hasimp ? 1 : 0;
 }
 
-// Lane projections of one vehicle onto every lane: fills the masked LDS projection rows
-// (AbstractLane.on_lane margin=1, lane.py:80-102) and returns the closest lane index
-// (RoadNetwork.get_closest_lane_index road.py:55-71, distance_with_heading lane.py:132-147).
-template <typename T>
-__device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t& P, int nl, int EPW, int NS,
-                                           int le, int i, bool present, T x, T y, T h, bool want_closest) {
-  const int NSP = NS + 1;
+// Lane projections of one vehicle onto every lane.  Builds, per lane, the compacted list
+// of the env's vehicles that are on it (AbstractLane.on_lane margin=1, lane.py:80-102) in
+// slot order (ballot + popcount prefix), so neighbour scans visit only real candidates in
+// the reference's list order; returns the closest lane (RoadNetwork.get_closest_lane_index
+// road.py:55-71, distance_with_heading lane.py:132-147).  All threads must call it.
+template <typename T, int NS, int EPW>
+__device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t& P, int nl, int tid, int le, int i,
+                                           bool present, T x, T y, T h, bool want_closest) {
+  constexpr int NSP = NS + 1;
   const T vl = T(P.lane_vehicle_length);
-  int best = 0;
+  int best = 0, mx = 0;
   T bd = T(0), ang = T(0), prev_hd = T(0);
-  for (int l = 0; l < nl; ++l) {
-    const LaneT<T> L = V.lanes[l];
-    T s, r;
-    lane_local(L, x, y, s, r);
-    const bool on = present && fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl;
-    V.proj[((size_t)l * EPW + le) * NSP + i] = on ? s : K<T>::nan();
-    if (want_closest) {
-      if (l == 0 || L.hd != prev_hd) ang = fabs(wrap_to_pi(h - L.hd));
-      prev_hd = L.hd;
-      T a = s - L.len; if (!(a > T(0))) a = T(0);
-      T b = T(0) - s; if (!(b > T(0))) b = T(0);
-      const T d = fabs(r) + a + b + T(1) * ang;
-      if (l == 0 || d < bd) { bd = d; best = l; }
+  int* cnt = V.cnt + le * (LMAX + 1);
+  if constexpr (NS <= 64) {
+    const int sh = (tid & 63) / NS * NS;
+    const unsigned long long seg = NS == 64 ? ~0ull : ((1ull << NS) - 1);
+    for (int l = 0; l < nl; ++l) {
+      const LaneT<T> L = V.lanes[l];
+      T s, r;
+      lane_local(L, x, y, s, r);
+      const bool on = present && fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl;
+      const unsigned long long m = (__ballot(on) >> sh) & seg;
+      if (on) {
+        LEnt<T> e{};
+        e.s = s; e.idx = i;
+        V.ent[((size_t)l * EPW + le) * NSP + __popcll(m & ((1ull << i) - 1))] = e;
+      }
+      const int c = __popcll(m);
+      mx = c > mx ? c : mx;
+      if (i == 0) cnt[l] = c;
+      if (want_closest) {
+        if (l == 0 || L.hd != prev_hd) ang = fabs(wrap_to_pi(h - L.hd));
+        prev_hd = L.hd;
+        T a = s - L.len; if (!(a > T(0))) a = T(0);
+        T b = T(0) - s; if (!(b > T(0))) b = T(0);
+        const T d = fabs(r) + a + b + T(1) * ang;
+        if (l == 0 || d < bd) { bd = d; best = l; }
+      }
+    }
+  } else {
+    constexpr int W = NS / 64;
+    const int wave = tid >> 6, lane = tid & 63;
+    for (int l = 0; l < nl; ++l) {
+      const LaneT<T> L = V.lanes[l];
+      T s, r;
+      lane_local(L, x, y, s, r);
+      const bool on = present && fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl;
+      const unsigned long long b = __ballot(on);
+      if (lane == 0) V.wcnt[l * 4 + wave] = __popcll(b);
+    }
+    __syncthreads();
+    for (int l = 0; l < nl; ++l) {
+      const LaneT<T> L = V.lanes[l];
+      T s, r;
+      lane_local(L, x, y, s, r);
+      const bool on = present && fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl;
+      const unsigned long long b = __ballot(on);
+      int off = 0, c = 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const int wc = V.wcnt[l * 4 + w];
+        off += w < wave ? wc : 0;
+        c += wc;
+      }
+      if (on) {
+        LEnt<T> e{};
+        e.s = s; e.idx = i;
+        V.ent[(size_t)l * NSP + off + __popcll(b & ((1ull << lane) - 1))] = e;
+      }
+      mx = c > mx ? c : mx;
+      if (i == 0) cnt[l] = c;
+      if (want_closest) {
+        if (l == 0 || L.hd != prev_hd) ang = fabs(wrap_to_pi(h - L.hd));
+        prev_hd = L.hd;
+        T a = s - L.len; if (!(a > T(0))) a = T(0);
+        T bb = T(0) - s; if (!(bb > T(0))) bb = T(0);
+        const T d = fabs(r) + a + bb + T(1) * ang;
+        if (l == 0 || d < bd) { bd = d; best = l; }
+      }
     }
   }
+  if (i == 0) cnt[LMAX] = mx;
   return best;
 }
 
@@ -337,41 +432,55 @@ __device__ __forceinline__ T idm_acc(const View<T>& V, const ttrl_params_t& P, i
   return a;
 }
 
-// One pass over the env's slots answering up to 3 Road.neighbour_vehicles queries per
-// thread (road.py:480-513): front = min s_v >= s (ties: later index), rear = max s_v < s
-// (ties: earlier index).  Off-lane / absent candidates are NaN in the LDS rows.
-template <typename T, int NQ>
-__device__ __forceinline__ void scan_neighbours(const View<T>& V, int EPW, int NS, int le, int N, int self,
-                                                const int (&ql)[NQ], const T (&s)[NQ], int (&f)[NQ], int (&r)[NQ]) {
-  const int NSP = NS + 1;
+// One pass answering up to 3 Road.neighbour_vehicles queries per thread (road.py:480-513)
+// over the compacted per-lane candidate lists: front = min s_v >= s (ties: later slot),
+// rear = max s_v < s (ties: earlier slot), visiting candidates in slot (= list) order.
+template <typename T, int NQ, int NS, int EPW>
+__device__ __forceinline__ void scan_neighbours(const View<T>& V, int le, int self, const int (&ql)[NQ],
+                                                const T (&s)[NQ], int (&f)[NQ], int (&r)[NQ]) {
+  constexpr int NSP = NS + 1;
+  const int* cnt = V.cnt + le * (LMAX + 1);
+  const int mx = cnt[LMAX];
   T sf[NQ], sr[NQ];
-  const T* row[NQ];
+  int n[NQ];
+  const LEnt<T>* row[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     sf[q] = K<T>::inf(); sr[q] = -K<T>::inf(); f[q] = -1; r[q] = -1;
-    row[q] = V.proj + ((size_t)(ql[q] < 0 ? 0 : ql[q]) * EPW + le) * NSP;
+    const int l = ql[q] < 0 ? 0 : ql[q];
+    row[q] = V.ent + ((size_t)l * EPW + le) * NSP;
+    n[q] = ql[q] < 0 ? 0 : cnt[l];
   }
-  for (int j = 0; j < N; ++j) {
-    const bool other = j != self;
+  constexpr int U = NQ == 1 ? 4 : 2;
+  for (int k0 = 0; k0 < mx; k0 += U) {
+    LEnt<T> e[NQ][U];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const T sv = row[q][j];
-      if (other && s[q] <= sv && sv <= sf[q]) { sf[q] = sv; f[q] = j; }
-      if (other && sv < s[q] && sv > sr[q]) { sr[q] = sv; r[q] = j; }
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int u = 0; u < U; ++u) e[q][u] = row[q][k0 + u];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const T sv = e[q][u].s;
+        const bool ok = k0 + u < n[q] && e[q][u].idx != self;
+        if (ok && s[q] <= sv && sv <= sf[q]) { sf[q] = sv; f[q] = e[q][u].idx; }
+        if (ok && sv < s[q] && sv > sr[q]) { sr[q] = sv; r[q] = e[q][u].idx; }
+      }
     }
   }
-#pragma unroll
-  for (int q = 0; q < NQ; ++q)
-    if (ql[q] < 0) { f[q] = -1; r[q] = -1; }
 }
 
 enum { MODE_META = 1, MODE_ACT = 2, MODE_STEP = 4 };
+// Diagnostic ablation bits (ttrl_diag_simulate only; results are then NOT the reference's).
+enum { A_NO_COLL = 1, A_NO_MOBIL = 2, A_NO_ABORT = 4, A_NO_SCAN = 8, A_NO_STEER = 16, A_NO_KIN = 32,
+       A_NO_LANE = 64, A_NO_IDM = 128 };
 
 // Fused frame loop.  EPW envs per workgroup, NS slots per env, blockDim = EPW*NS.
 template <typename T, int NS, int EPW>
-__global__ void __launch_bounds__(NS* EPW)
+__global__ void __launch_bounds__(NS* EPW, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES : (sizeof(T) == 8 ? 2 : 4))
 simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int32_t* __restrict__ actions,
-                int frames, double dt_d, int mode) {
+                int frames, double dt_d, int mode, int ablate) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = NS * EPW;
   constexpr int WAVES = NT / 64 > 0 ? NT / 64 : 1;
@@ -392,9 +501,9 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   a.ch = cos(a.h); a.sh = sin(a.h);
   const T dt = T(dt_d);
   __syncthreads();  // lane table staged
-  project_all(V, P, nl, EPW, NS, le, i, present, a.x, a.y, a.h, false);
-  V.x[eb + i] = a.x; V.y[eb + i] = a.y; V.v[eb + i] = a.v; V.ch[eb + i] = a.ch; V.sh[eb + i] = a.sh;
-  V.ts[eb + i] = a.ts;
+  project_all<T, NS, EPW>(V, P, nl, tid, le, i, present, a.x, a.y, a.h, false);
+  V.x[eb + i] = present ? a.x : T(FAR); V.y[eb + i] = a.y; V.v[eb + i] = a.v; V.ch[eb + i] = a.ch;
+  V.sh[eb + i] = a.sh; V.ts[eb + i] = a.ts;
   V.lane[eb + i] = (int8_t)(present ? a.lane : -1);
   V.tgt[eb + i] = (int8_t)(present ? a.tgt : -1);
 
@@ -427,7 +536,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       const bool changing = idm && a.lane != a.tgt;
       const bool abort_cand = changing && a.lc;
       bool fire = false;
-      if (idm && a.lc && !changing && T(P.lane_change_delay) < a.timer) {  // utils.do_every
+      if (idm && a.lc && !changing && T(P.lane_change_delay) < a.timer && !(ablate & A_NO_MOBIL)) {  // utils.do_every
         fire = true;
         a.timer = T(0);
       }
@@ -446,20 +555,22 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         lane_local(V.lanes[ql[q] < 0 ? 0 : ql[q]], a.x, a.y, s3[q], rr);
       }
       int f3[3], r3[3];
-      if (__any(ql[1] >= 0 || ql[2] >= 0)) {
-        scan_neighbours<T, 3>(V, EPW, NS, le, N, i, ql, s3, f3, r3);
+      if (ablate & A_NO_SCAN) {
+        f3[0] = f3[1] = f3[2] = r3[0] = r3[1] = r3[2] = -1;
+      } else if (__any(ql[1] >= 0 || ql[2] >= 0)) {
+        scan_neighbours<T, 3, NS, EPW>(V, le, i, ql, s3, f3, r3);
       } else {
         int ql1[1] = {ql[0]};
         T s1[1] = {s3[0]};
         int f1[1], r1[1];
-        scan_neighbours<T, 1>(V, EPW, NS, le, N, i, ql1, s1, f1, r1);
+        scan_neighbours<T, 1, NS, EPW>(V, le, i, ql1, s1, f1, r1);
         f3[0] = f1[0]; r3[0] = r1[0]; f3[1] = f3[2] = r3[1] = r3[2] = -1;
       }
 
       // MOBIL (IDMVehicle.mobil behavior.py:265-324, route None); DELTA is ours.
       int tgt_new = a.tgt;
       T a_free = T(0);
-      if (idm) a_free = idm_free(P, a.v, a.ts, V.lanes[a.lane].lim, a.delta);
+      if (idm && !(ablate & A_NO_IDM)) a_free = idm_free(P, a.v, a.ts, V.lanes[a.lane].lim, a.delta);
       if (fire) {
 #pragma unroll
         for (int side = 1; side <= 2; ++side) {
@@ -490,7 +601,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       // Lane-change abort in list order (behavior.py:229-244): vehicle i aborts if some
       // v != i with v.lane != T_i and v.target == T_i (v's target as of its own turn:
       // final for v < i, previous for v > i) is 0 < d(i->v) < d*(i, v).
-      {
+      if (!(ablate & A_NO_ABORT)) {
         auto contributes = [&](int ii) -> bool {
           if (!present || ii == i) return false;
           const int Ti = V.tgt[eb + ii];
@@ -548,7 +659,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
 
       // steering + IDM longitudinal (behavior.py:109-135); ego: ControlledVehicle.act (controller.py:126-133)
       if (idm) {
-        a.steer = steering_control(V.lanes[tgt_new], P, a.x, a.y, a.h, a.v);
+        a.steer = (ablate & A_NO_STEER) ? T(0) : steering_control(V.lanes[tgt_new], P, a.x, a.y, a.h, a.v);
         T acc = a_free;
         if (f3[0] >= 0) acc -= idm_interact(V, P, eb, i, f3[0]);
         if (a.lane != tgt_new) {
@@ -574,6 +685,9 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         if (a.v > T(P.max_speed)) { const T c = T(1) * (T(P.max_speed) - a.v); if (c < a.acc) a.acc = c; }
         else if (a.v < T(P.min_speed)) { const T c = T(1) * (T(P.min_speed) - a.v); if (c > a.acc) a.acc = c; }
         // kinematic bicycle, Vehicle.step kinematics.py:140-153
+        if (ablate & A_NO_KIN) {
+          a.x += a.v * a.ch * dt; a.y += a.v * a.sh * dt; a.v += a.acc * dt;
+        } else {
         const T beta = atan(T(1) / T(2) * tan(a.steer));
         const T vx = a.v * cos(a.h + beta), vy = a.v * sin(a.h + beta);
         a.x += vx * dt; a.y += vy * dt;
@@ -581,40 +695,62 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         a.h += a.v * sin(beta) / (T(P.length) / T(2)) * dt;
         a.v += a.acc * dt;
         a.ch = cos(a.h); a.sh = sin(a.h);
+        }
       }
       __syncthreads();  // act-phase readers of the old view are done
-      const int cl = project_all(V, P, nl, EPW, NS, le, i, present, a.x, a.y, a.h, true);
-      if (present) a.lane = cl;  // on_state_update kinematics.py:170-177
-      V.x[eb + i] = a.x; V.y[eb + i] = a.y; V.v[eb + i] = a.v; V.ch[eb + i] = a.ch; V.sh[eb + i] = a.sh;
-      V.ts[eb + i] = a.ts;
+      const int cl = project_all<T, NS, EPW>(V, P, nl, tid, le, i, present, a.x, a.y, a.h, !(ablate & A_NO_LANE));
+      if (present && !(ablate & A_NO_LANE)) a.lane = cl;  // on_state_update kinematics.py:170-177
+      V.x[eb + i] = present ? a.x : T(FAR); V.y[eb + i] = a.y; V.v[eb + i] = a.v; V.ch[eb + i] = a.ch;
+      V.sh[eb + i] = a.sh; V.ts[eb + i] = a.ts;
       V.lane[eb + i] = (int8_t)(present ? a.lane : -1);
       V.tgt[eb + i] = (int8_t)(present ? a.tgt : -1);
       __syncthreads();
 
-      // collisions for all pairs (road.py:474-476, objects.py:91-137), impact: last writer
-      if (present) {
+      // collisions for all pairs (road.py:474-476, objects.py:91-137), impact: last writer.
+      // Pass 1 (pipelined LDS loads): 1-D prefilter |dx| <= R, with R >= every pair's
+      // threshold (diag + v*dt, v <= env max), so no pair the reference tests is dropped.
+      // Pass 2: the reference's exact norm test and SAT on the candidates, in index order.
+      const T vmax = env_max<T, NS, EPW>(present ? fabs(a.v) : T(0), V, tid);
+      if (present && !(ablate & A_NO_COLL)) {
         const T thr0 = (T(P.diagonal) + T(P.diagonal)) / T(2);
+        const T R = thr0 + vmax * dt + T(1);
         bool crash = a.crashed, has_gt = false, has_lt = false;
         T gx = T(0), gy = T(0), lx = T(0), ly = T(0);
-        for (int j = 0; j < N; ++j) {
-          if (j == i || V.lane[eb + j] < 0) continue;
-          const T xj = V.x[eb + j], yj = V.y[eb + j], vj = V.v[eb + j];
-          const bool lo = i < j;  // this vehicle is the reference's `self`
-          const T dx = lo ? xj - a.x : a.x - xj, dy = lo ? yj - a.y : a.y - yj;
-          const T thr = thr0 + (lo ? a.v : vj) * dt;
-          const T d2 = dx * dx + dy * dy;
-          if (d2 > (thr + T(1)) * (thr + T(1))) continue;  // far: skip the exact test
-          if (sqrt(d2) > thr) continue;                     // objects.py:123-133 exact
-          bool inter, will;
-          T tx, ty;
-          const T cj = V.ch[eb + j], sj = V.sh[eb + j];
-          if (lo) sat_pair(P, a.x, a.y, a.ch, a.sh, a.v, xj, yj, cj, sj, vj, dt, inter, will, tx, ty);
-          else sat_pair(P, xj, yj, cj, sj, vj, a.x, a.y, a.ch, a.sh, a.v, dt, inter, will, tx, ty);
-          if (will) {
-            if (lo) { has_gt = true; gx = tx / T(2); gy = ty / T(2); }
-            else { has_lt = true; lx = -tx / T(2); ly = -ty / T(2); }
+        constexpr int CH = NS < 64 ? NS : 64;
+#pragma unroll
+        for (int c0 = 0; c0 < NS; c0 += CH) {
+          unsigned long long m = 0;
+#pragma unroll
+          for (int j1 = 0; j1 < CH; j1 += 8) {
+            T xs[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) xs[u] = V.x[eb + c0 + j1 + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+              if (!(fabs(xs[u] - a.x) > R)) m |= 1ull << (j1 + u);
           }
-          if (inter) crash = true;
+          if (i >= c0 && i < c0 + CH) m &= ~(1ull << (i - c0));
+          while (m) {
+            const int j = c0 + __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const T xj = V.x[eb + j], yj = V.y[eb + j], vj = V.v[eb + j];
+            const bool lo = i < j;  // this vehicle is the reference's `self`
+            const T dx = lo ? xj - a.x : a.x - xj, dy = lo ? yj - a.y : a.y - yj;
+            const T thr = thr0 + (lo ? a.v : vj) * dt;
+            const T d2 = dx * dx + dy * dy;
+            if (d2 > (thr + T(1)) * (thr + T(1))) continue;  // far: skip the exact test
+            if (sqrt(d2) > thr) continue;                     // objects.py:123-133 exact
+            bool inter, will;
+            T tx, ty;
+            const T cj = V.ch[eb + j], sj = V.sh[eb + j];
+            if (lo) sat_pair(P, a.x, a.y, a.ch, a.sh, a.v, xj, yj, cj, sj, vj, dt, inter, will, tx, ty);
+            else sat_pair(P, xj, yj, cj, sj, vj, a.x, a.y, a.ch, a.sh, a.v, dt, inter, will, tx, ty);
+            if (will) {
+              if (lo) { has_gt = true; gx = tx / T(2); gy = ty / T(2); }
+              else { has_lt = true; lx = -tx / T(2); ly = -ty / T(2); }
+            }
+            if (inter) crash = true;
+          }
         }
         a.crashed = crash;
         if (has_gt) { a.hasimp = true; a.ix = gx; a.iy = gy; }
@@ -649,14 +785,14 @@ neighbours_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const i
     if (l < 0 || l >= nl) l = 0;
   }
   __syncthreads();
-  project_all(V, P, nl, EPW, NS, le, i, present, x, y, T(0), false);
+  project_all<T, NS, EPW>(V, P, nl, tid, le, i, present, x, y, T(0), false);
   __syncthreads();
   int ql[1] = {present ? l : -1};
   T s[1];
   T rr;
   lane_local(V.lanes[l], x, y, s[0], rr);
   int f[1], r[1];
-  scan_neighbours<T, 1>(V, EPW, NS, le, N, i, ql, s, f, r);
+  scan_neighbours<T, 1, NS, EPW>(V, le, i, ql, s, f, r);
   if (slot) { front[k] = f[0]; rear[k] = r[0]; }
 }
 
@@ -1073,34 +1209,34 @@ int launch_status() { return hipGetLastError() == hipSuccess ? TTRL_OK : TTRL_E_
 
 template <typename T, int NS, int EPW>
 int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const int32_t* actions,
-               int frames, double dt, int mode, hipStream_t stream) {
+               int frames, double dt, int mode, int ablate, hipStream_t stream) {
   const int blocks = (s.n_envs + EPW - 1) / EPW;
   if (blocks == 0) return TTRL_OK;
   const size_t lds = host_view_bytes(sizeof(T) == 8 ? TTRL_F64 : TTRL_F32, EPW, NS, R.n_lanes);
   hipLaunchKernelGGL((simulate_kernel<T, NS, EPW>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, P, actions,
-                     frames, dt, mode);
+                     frames, dt, mode, ablate);
   return launch_status();
 }
 
 template <typename T>
 int dispatch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const int32_t* actions,
-                 int frames, double dt, int mode, hipStream_t stream) {
+                 int frames, double dt, int mode, int ablate, hipStream_t stream) {
   switch (slots_for(s.n_veh)) {
-    case 32: return launch_sim<T, 32, 2>(s, R, P, actions, frames, dt, mode, stream);
-    case 64: return launch_sim<T, 64, 1>(s, R, P, actions, frames, dt, mode, stream);
-    case 128: return launch_sim<T, 128, 1>(s, R, P, actions, frames, dt, mode, stream);
-    default: return launch_sim<T, 256, 1>(s, R, P, actions, frames, dt, mode, stream);
+    case 32: return launch_sim<T, 32, 2>(s, R, P, actions, frames, dt, mode, ablate, stream);
+    case 64: return launch_sim<T, 64, 1>(s, R, P, actions, frames, dt, mode, ablate, stream);
+    case 128: return launch_sim<T, 128, 1>(s, R, P, actions, frames, dt, mode, ablate, stream);
+    default: return launch_sim<T, 256, 1>(s, R, P, actions, frames, dt, mode, ablate, stream);
   }
 }
 
 int run_sim(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P, const int32_t* actions,
-            int frames, double dt, int mode, void* stream) {
+            int frames, double dt, int mode, void* stream, int ablate = 0) {
   int rc = check_state(s, R);
   if (rc) return rc;
   if (!P || frames < 0 || P->n_target_speeds < 1 || P->n_target_speeds > 8) return TTRL_E_ARG;
   hipStream_t st = (hipStream_t)stream;
-  return s->dtype == TTRL_F64 ? dispatch_sim<double>(*s, *R, *P, actions, frames, dt, mode, st)
-                              : dispatch_sim<float>(*s, *R, *P, actions, frames, dt, mode, st);
+  return s->dtype == TTRL_F64 ? dispatch_sim<double>(*s, *R, *P, actions, frames, dt, mode, ablate, st)
+                              : dispatch_sim<float>(*s, *R, *P, actions, frames, dt, mode, ablate, st);
 }
 
 template <typename T, int NS, int EPW>
@@ -1169,6 +1305,12 @@ int ttrl_road_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const t
 int ttrl_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                   const int32_t* actions, int32_t frames, double dt, void* stream) {
   return run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream);
+}
+
+/* Diagnostic only (not in include/): the fused loop with phases ablated, for profiling. */
+int ttrl_diag_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                       const int32_t* actions, int32_t frames, double dt, int32_t ablate, void* stream) {
+  return run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream, ablate);
 }
 
 int ttrl_neighbours(const ttrl_state_t* s, const ttrl_lane_table_t* road, const int32_t* query_lane,
