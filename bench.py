@@ -106,9 +106,8 @@ def main():
     import torch.distributed as dist
     from topotrafficrl_amd.envs import VecHighwayEnv
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from topotrafficrl_amd import sharding
+    rank, local, world = sharding.world()
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
@@ -118,8 +117,9 @@ def main():
 
     C = CONFIGS[args.config]
     E, N = C["num_envs"], C["vehicles"]
+    offset, _ = sharding.weak_shard(E, rank)  # weak scaling: E envs per GPU, global ids [rank*E, (rank+1)*E)
     env = VecHighwayEnv({"num_envs": E, "vehicles_count": N, "observation": C["obs"], "device": str(dev),
-                         "dtype": args.dtype, "env_id_offset": rank * E})
+                         "dtype": args.dtype, "env_id_offset": offset})
     policy = None
     if args.config == 5:
         from topotrafficrl_amd.agent import EgoAttentionPolicy
@@ -163,10 +163,7 @@ def main():
     elapsed = time.perf_counter() - t0
     road.simulate = orig_sim
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
-    if world > 1:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = sharding.max_over_ranks(elapsed, device=dev)
 
     veh_steps = world * E * N * 15 * args.steps
     value = veh_steps / elapsed

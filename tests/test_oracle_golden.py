@@ -1,0 +1,119 @@
+"""The float64 oracle (oracle/ttrl_oracle.c) against golden vectors captured from the
+unmodified reference (oracle/gen_golden.py).  CPU only.
+
+Pinned here: Road.act/Road.step per frame (positions/speeds/headings to 1e-12, every
+discrete field exact), the fused 15-frame policy step, Road.neighbour_vehicles,
+Kinematics (5x5 default, 15x7 env.json) and OccupancyGrid (7x32x32 dense, 4x11x11 on_road)
+observations bit-identical, and the numpy-PCG64 scene generator bit-identical.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_files, load_golden
+from oracle.oracle import HostState, Oracle
+from topotrafficrl_amd import _abi
+
+P = _abi.default_params()
+KD = _abi.kin_cfg()
+K15 = _abi.kin_cfg(features=["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"], vehicles_count=15,
+                   features_range={"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]})
+G7 = _abi.grid_cfg(features=["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"],
+                   features_range={"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]},
+                   grid_size=[[-32, 32], [-32, 32]], grid_step=[2, 2])
+GR = _abi.grid_cfg()
+CONT = ["x", "y", "heading", "speed", "timer", "target_speed", "steer", "acc"]
+DISC = ["lane", "target_lane", "crashed", "has_impact", "speed_index"]
+IDS = lambda p: p.split("/")[-1][:-4]  # noqa: E731
+
+
+def check(h: HostState, g: HostState, tol: float):
+    for k in CONT:
+        err = np.max(np.abs(h[k] - g[k]) / (1 + np.abs(g[k])))
+        assert err <= tol, (k, err)
+    imp = g["has_impact"].astype(bool)
+    for k in ("impact_x", "impact_y"):
+        assert np.max(np.abs(h[k][imp] - g[k][imp]), initial=0.0) <= tol, k
+    for k in DISC:
+        assert np.array_equal(h[k], g[k]), k
+
+
+@pytest.fixture(scope="module")
+def cases():
+    return {IDS(p): load_golden(p) for p in golden_files()}
+
+
+@pytest.mark.parametrize("name", [IDS(p) for p in golden_files()])
+def test_every_frame(name, cases):
+    d = cases[name]
+    o = Oracle(_abi.lane_table_from_arrays(d["lane_table"]), P)
+    for f in range(d["x"].shape[0] - 1):
+        h = HostState.from_golden(d, f)
+        if f % 15 == 0:
+            o.meta_action(h, [int(d["actions"][f // 15])])
+        o.road_act(h)
+        check(h, HostState.from_golden(d, f, prefix="act_"), 1e-12)
+        o.road_step(h)
+        check(h, HostState.from_golden(d, f + 1), 1e-12)
+
+
+@pytest.mark.parametrize("name", [IDS(p) for p in golden_files()])
+def test_policy_step_rollout(name, cases):
+    d = cases[name]
+    o = Oracle(_abi.lane_table_from_arrays(d["lane_table"]), P)
+    h = HostState.from_golden(d, 0)
+    for p in range(int(d["meta"][2])):
+        o.simulate(h, [int(d["actions"][p])], 15, 1 / 15)
+        check(h, HostState.from_golden(d, 15 * (p + 1)), 1e-10)
+
+
+@pytest.mark.parametrize("name", [IDS(p) for p in golden_files()])
+def test_neighbour_vehicles(name, cases):
+    d = cases[name]
+    o = Oracle(_abi.lane_table_from_arrays(d["lane_table"]), P)
+    for f in range(d["x"].shape[0] - 1):
+        h = HostState.from_golden(d, f, prefix="act_")
+        fr, rr = o.neighbours(h)
+        assert np.array_equal(fr[0], d["nbr"][f][0]) and np.array_equal(rr[0], d["nbr"][f][1])
+        fr, rr = o.neighbours(h, h["target_lane"])
+        assert np.array_equal(fr[0], d["nbr"][f][2]) and np.array_equal(rr[0], d["nbr"][f][3])
+
+
+@pytest.mark.parametrize("name", [IDS(p) for p in golden_files()])
+def test_observations(name, cases):
+    d = cases[name]
+    o = Oracle(_abi.lane_table_from_arrays(d["lane_table"]), P)
+    for p in range(int(d["meta"][2]) + 1):
+        h = HostState.from_golden(d, 15 * p)
+        obs, ids = o.observe_kinematics(h, KD)
+        assert np.array_equal(obs[0], d["kin5"][p]) and np.array_equal(ids[0], d["kin5_ids"][p])
+        obs, ids = o.observe_kinematics(h, K15)
+        assert np.array_equal(obs[0], d["kin15"][p]) and np.array_equal(ids[0], d["kin15_ids"][p])
+        assert np.array_equal(o.observe_grid(h, G7)[0], d["grid7"][p])
+        assert np.array_equal(o.observe_grid(h, GR)[0], d["grid_onroad"][p])
+
+
+@pytest.mark.parametrize("name", [IDS(p) for p in golden_files("highway_*")])
+def test_scene_generation_matches_reference_rng(name, cases):
+    d = cases[name]
+    n, seed = int(d["meta"][0]), int(d["meta"][1])
+    lanes = _abi.lane_table_from_arrays(d["lane_table"])
+    o = Oracle(lanes, P)
+    h = HostState(1, n)
+    o.reset_highway(h, _abi.reset_cfg(n, lanes), [seed])
+    g = HostState.from_golden(d, 0)
+    for k in ["x", "y", "heading", "speed", "target_speed", "timer", "delta"]:
+        assert np.array_equal(h[k], g[k]), k
+    for k in ["lane", "target_lane", "kind", "speed_index", "lane_change"]:
+        assert np.array_equal(h[k], g[k]), k
+
+
+def test_golden_covers_the_hard_cases(cases):
+    """The fixtures must exercise MOBIL lane changes, aborts, impacts and crashes."""
+    changes = aborts = impacts = crashes = 0
+    for d in cases.values():
+        before, after, lane = d["target_lane"][:-1], d["act_target_lane"], d["lane"][:-1]
+        changes += int(np.sum((after != before) & (after != lane)))
+        aborts += int(np.sum((after != before) & (after == lane)))
+        impacts += int(np.isfinite(d["impact_x"]).sum())
+        crashes += int(d["crashed"][-1].sum())
+    assert changes > 50 and aborts > 0 and impacts > 100 and crashes > 50, (changes, aborts, impacts, crashes)
