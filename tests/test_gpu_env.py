@@ -1,0 +1,99 @@
+"""The batched env API on the GPU (VecHighwayEnv.reset/step, obs/reward/termination,
+policy in the loop) against the float64 oracle driven through the same calls."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.oracle import HostState, Oracle
+from topotrafficrl_amd import _abi
+from topotrafficrl_amd.agent import EgoAttentionPolicy
+from topotrafficrl_amd.envs import VecHighwayEnv
+from topotrafficrl_amd.trainer import BatchedDQNAgent, BatchedEvaluation
+
+pytestmark = pytest.mark.gpu
+
+KIN15 = {"type": "Kinematics", "vehicles_count": 15, "features": ["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"],
+         "features_range": {"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]},
+         "absolute": False, "order": "sorted"}
+
+
+def make(E=16, N=40, obs=None, dtype="f64", **kw):
+    cfg = {"num_envs": E, "vehicles_count": N, "observation": obs or KIN15, "device": "cuda:0", "dtype": dtype}
+    cfg.update(kw)
+    return VecHighwayEnv(cfg)
+
+
+def test_env_step_matches_oracle(hip_device):
+    E, N = 16, 40
+    env = make(E, N)
+    obs, info = env.reset(seed=77)
+    lanes = env.network.table
+    o = Oracle(lanes, env.params)
+    h = HostState(E, N)
+    o.reset_highway(h, env.reset_cfg, [77 + e for e in range(E)])
+    kin = _abi.kin_cfg(**{k: v for k, v in KIN15.items() if k != "type"})
+    ref_obs, _ = o.observe_kinematics(h, kin)
+    assert np.array_equal(obs.cpu().numpy(), ref_obs)
+    rng = np.random.default_rng(3)
+    for t in range(1, 6):
+        a = rng.integers(0, 5, size=E)
+        obs, rew, term, trunc, info = env.step(torch.from_numpy(a))
+        o.simulate(h, a.astype(np.int32), 15, 1 / 15)
+        ref_obs, _ = o.observe_kinematics(h, kin)
+        ref_r, ref_term, ref_trunc = o.rewards(h, env.reward_cfg, float(t))
+        assert np.max(np.abs(obs.cpu().numpy() - ref_obs)) < 1e-6
+        assert np.allclose(rew.cpu().numpy(), ref_r, atol=1e-6)
+        assert np.array_equal(term.cpu().numpy(), ref_term) and np.array_equal(trunc.cpu().numpy(), ref_trunc)
+        assert np.allclose(info["speed"].cpu().numpy(), h["speed"][:, 0])
+
+
+def test_truncation_and_auto_reset(hip_device):
+    env = make(8, 20, duration=3, auto_reset=True)
+    env.reset(seed=1)
+    for t in range(3):
+        _, _, term, trunc, _ = env.step(torch.ones(8, dtype=torch.int64))
+    assert bool(trunc.all())
+    assert float(env.time.max()) == 0.0  # every env was truncated at t=3 and auto-reset
+
+
+def test_sharded_envs_equal_one_big_batch(hip_device):
+    """env_id_offset sharding: two shards == one batch of the same global envs."""
+    big = make(8, 30)
+    big.reset(seed=5)
+    a = make(4, 30, env_id_offset=0)
+    b = make(4, 30, env_id_offset=4)
+    a.reset(seed=5)
+    b.reset(seed=5)
+    acts = torch.tensor([0, 1, 2, 3, 4, 1, 3, 2])
+    o1, *_ = big.step(acts)
+    oa, *_ = a.step(acts[:4])
+    ob, *_ = b.step(acts[4:])
+    assert torch.equal(o1, torch.cat([oa, ob]))
+    for k in ("x", "lane", "crashed"):
+        assert torch.equal(big.state[k], torch.cat([a.state[k], b.state[k]]))
+
+
+def test_policy_in_the_loop(hip_device):
+    env = make(32, 64)
+    pol = EgoAttentionPolicy(hip_device, seed=0)
+    obs, _ = env.reset(seed=9)
+    for t in range(3):
+        act = pol.act(obs, t)
+        assert act.shape == (32,) and act.device.type == "cuda"
+        obs, rew, term, trunc, info = env.step(act)
+    assert torch.isfinite(obs).all()
+    ev = BatchedEvaluation(env, BatchedDQNAgent(hip_device), num_episodes=1, sim_seed=0, max_steps=3)
+    ev.run_episodes()
+    assert ev.last_stats["episode/length"] == 3
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_occupancy_grid_env(dtype, hip_device):
+    grid = {"type": "OccupancyGrid", "features": ["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"],
+            "features_range": {"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]},
+            "grid_size": [[-32, 32], [-32, 32]], "grid_step": [2, 2]}
+    env = make(8, 128, obs=grid, dtype=dtype)
+    obs, _ = env.reset(seed=2)
+    assert obs.shape == (8, 7, 32, 32)
+    obs, *_ = env.step(torch.ones(8, dtype=torch.int64))
+    assert float(obs[:, 0].sum()) >= 8  # the ego occupies the centre cell of every env

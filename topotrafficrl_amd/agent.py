@@ -1,0 +1,133 @@
+"""Policy in the loop (BASELINE config 5): the ttrl_agent DQN ego-attention network,
+batched over every env of the simulator and fed the Kinematics observation in place.
+
+Restates ttrl_agent/agents/common/models.py — MultiLayerPerceptron (:50-76),
+EgoAttention (:157-194), EgoAttentionNetwork (:237-312), attention (:370-388) — and the
+acting side of the DQN agent: AbstractDQNAgent.act (deep_q_network/abstract.py:65-83)
+with EpsilonGreedy exploration (exploration/epsilon_greedy.py:7-57; schedule from
+scripts/configs/IntersectionEnv/agents/DQNAgent/baseline.json:12-17).  The forward is a
+dense contraction (7->64->64 embeddings, 2-head attention over 15 entities, 64->64->64->n
+head): it runs as torch GEMMs on the same HIP stream as the simulator (hipBLASLt/MFMA),
+no host round trip between env.step and the next action.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+from torch.nn import functional as F
+
+EGO_ATTENTION_2H = {  # configs/IntersectionEnv/agents/DQNAgent/ego_attention.json + ego_attention_2h.json
+    "type": "EgoAttentionNetwork",
+    "presence_feature_idx": 0,
+    "embedding_layer": {"type": "MultiLayerPerceptron", "layers": [64, 64], "reshape": False, "in": 7},
+    "others_embedding_layer": {"type": "MultiLayerPerceptron", "layers": [64, 64], "reshape": False, "in": 7},
+    "self_attention_layer": None,
+    "attention_layer": {"type": "EgoAttention", "feature_size": 64, "heads": 2},
+    "output_layer": {"type": "MultiLayerPerceptron", "layers": [64, 64], "reshape": False},
+}
+
+
+class MultiLayerPerceptron(nn.Module):
+    def __init__(self, inp: int, layers, out: int | None = None, reshape: bool = False):
+        super().__init__()
+        sizes = [inp] + list(layers)
+        self.layers = nn.ModuleList([nn.Linear(sizes[i], sizes[i + 1]) for i in range(len(sizes) - 1)])
+        self.predict = nn.Linear(sizes[-1], out) if out else None
+        self.reshape = reshape
+
+    def forward(self, x):
+        if self.reshape:
+            x = x.reshape(x.shape[0], -1)
+        for layer in self.layers:
+            x = F.relu(layer(x))
+        return self.predict(x) if self.predict is not None else x
+
+
+class EgoAttention(nn.Module):
+    def __init__(self, feature_size: int = 64, heads: int = 2):
+        super().__init__()
+        self.f, self.h = feature_size, heads
+        self.dph = feature_size // heads
+        self.value_all = nn.Linear(feature_size, feature_size, bias=False)
+        self.key_all = nn.Linear(feature_size, feature_size, bias=False)
+        self.query_ego = nn.Linear(feature_size, feature_size, bias=False)
+        self.attention_combine = nn.Linear(feature_size, feature_size, bias=False)
+
+    def forward(self, ego, others, mask=None):
+        b, n = others.shape[0], others.shape[1] + 1
+        x = torch.cat((ego.view(b, 1, self.f), others), dim=1)
+        k = self.key_all(x).view(b, n, self.h, self.dph).permute(0, 2, 1, 3)
+        v = self.value_all(x).view(b, n, self.h, self.dph).permute(0, 2, 1, 3)
+        q = self.query_ego(ego).view(b, 1, self.h, self.dph).permute(0, 2, 1, 3)
+        scores = torch.matmul(q, k.transpose(-2, -1)) / math.sqrt(self.dph)
+        if mask is not None:
+            scores = scores.masked_fill(mask.view(b, 1, 1, n).repeat(1, self.h, 1, 1), -1e9)
+        p = F.softmax(scores, dim=-1)
+        out = torch.matmul(p, v)
+        return (self.attention_combine(out.reshape(b, self.f)) + ego.squeeze(1)) / 2, p
+
+
+class EgoAttentionNetwork(nn.Module):
+    def __init__(self, n_actions: int = 5, config: dict | None = None):
+        super().__init__()
+        c = config or EGO_ATTENTION_2H
+        e, o, a, h = c["embedding_layer"], c["others_embedding_layer"], c["attention_layer"], c["output_layer"]
+        self.presence_idx = c.get("presence_feature_idx", 0)
+        self.ego_embedding = MultiLayerPerceptron(e["in"], e["layers"])
+        self.others_embedding = MultiLayerPerceptron(o["in"], o["layers"])
+        self.attention_layer = EgoAttention(a["feature_size"], a["heads"])
+        self.output_layer = MultiLayerPerceptron(a["feature_size"], h["layers"], out=n_actions)
+
+    def reset(self, generator: torch.Generator | None = None):
+        """BaseModule._init_weights (models.py:24-33): Xavier-uniform weights, zero biases."""
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                bound = math.sqrt(6.0 / (m.in_features + m.out_features))
+                with torch.no_grad():
+                    m.weight.uniform_(-bound, bound, generator=generator)
+                    if m.bias is not None:
+                        m.bias.zero_()
+        return self
+
+    def forward(self, x):
+        ego, others = x[:, 0:1, :], x[:, 1:, :]
+        mask = x[:, :, self.presence_idx:self.presence_idx + 1] < 0.5
+        att, _ = self.attention_layer(self.ego_embedding(ego), self.others_embedding(others), mask)
+        return self.output_layer(att)
+
+
+class EgoAttentionPolicy:
+    """Batched DQN acting: Q = value_net(obs[E, V, F]); epsilon-greedy on the device."""
+
+    def __init__(self, device, n_actions: int = 5, seed: int = 0, tau: float = 15000.0, temperature: float = 1.0,
+                 final_temperature: float = 0.05):
+        self.device = torch.device(device)
+        g = torch.Generator(device="cpu")
+        g.manual_seed(seed)
+        self.value_net = EgoAttentionNetwork(n_actions).reset(g).to(self.device).eval()
+        self.n_actions = n_actions
+        self.tau, self.t0, self.t1 = tau, temperature, final_temperature
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed + 1)
+        self.time = 0
+
+    def epsilon(self, t: int) -> float:
+        """EpsilonGreedy.update (epsilon_greedy.py:37-48)."""
+        return self.t1 + (self.t0 - self.t1) * math.exp(-t / self.tau)
+
+    @torch.no_grad()
+    def q_values(self, obs: torch.Tensor) -> torch.Tensor:
+        return self.value_net(obs)
+
+    @torch.no_grad()
+    def act(self, obs: torch.Tensor, t: int | None = None) -> torch.Tensor:
+        t = self.time if t is None else t
+        self.time = t + 1
+        q = self.value_net(obs)
+        greedy = q.argmax(dim=1)
+        e = obs.shape[0]
+        u = torch.rand(e, device=self.device, generator=self.gen)
+        rnd = torch.randint(0, self.n_actions, (e,), device=self.device, generator=self.gen)
+        return torch.where(u < self.epsilon(t), rnd, greedy)
