@@ -1,0 +1,21 @@
+#!/bin/bash
+# Run ON the GPU box (gpurun): kernel-trace stats + separate PMC passes for the bench workload.
+# Outputs under gpurun_out/prof_$TAG; summarise with tools/profile_summary.py.
+set -e
+TAG=${TAG:-r01}
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+for DT in f64 f32; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o trace_$DT -- \
+    python3 bench.py --steps 20 --warmup 3 --dtype $DT --no-cpu-baseline > $OUT/bench_trace_$DT.json 2> $OUT/trace_$DT.err
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT -o fetch_$DT -- \
+    python3 bench.py --steps 5 --warmup 1 --dtype $DT --no-cpu-baseline > /dev/null 2> $OUT/fetch_$DT.err
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT -o write_$DT -- \
+    python3 bench.py --steps 5 --warmup 1 --dtype $DT --no-cpu-baseline > /dev/null 2> $OUT/write_$DT.err
+  timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --output-format csv -d $OUT -o sq_$DT -- \
+    python3 bench.py --steps 5 --warmup 1 --dtype $DT --no-cpu-baseline > /dev/null 2> $OUT/sq_$DT.err
+  timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d $OUT -o grbm_$DT -- \
+    python3 bench.py --steps 5 --warmup 1 --dtype $DT --no-cpu-baseline > /dev/null 2> $OUT/grbm_$DT.err
+done
+echo profile done

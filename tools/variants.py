@@ -13,10 +13,10 @@ sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "_variants")
 VARIANTS = {
     "w0": [],
+    "w1": ["-DTTRL_SIM_WAVES=1"],
     "w2": ["-DTTRL_SIM_WAVES=2"],
     "w3": ["-DTTRL_SIM_WAVES=3"],
     "w4": ["-DTTRL_SIM_WAVES=4"],
-    "w2_ni": ["-DTTRL_SIM_WAVES=2", "-DTTRL_SAT_NOINLINE"],
     "w3_ni": ["-DTTRL_SIM_WAVES=3", "-DTTRL_SAT_NOINLINE"],
     "w4_ni": ["-DTTRL_SIM_WAVES=4", "-DTTRL_SAT_NOINLINE"],
 }

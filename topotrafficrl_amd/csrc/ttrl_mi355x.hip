@@ -19,6 +19,23 @@
 
 namespace {
 
+// Transcendentals.  The float64 ocml expansions (Payne-Hanek reduction, extra-precision
+// log/exp) are register-hungry; inlined at every call site they force spills of the
+// resident vehicle state.  Out of line, the fused kernel fits its register budget with no
+// scratch; the call overhead is paid ~10 times per vehicle-frame.
+__device__ __noinline__ double t_sin(double x) { return ::sin(x); }
+__device__ __noinline__ double t_cos(double x) { return ::cos(x); }
+__device__ __noinline__ double t_tan(double x) { return ::tan(x); }
+__device__ __noinline__ double t_atan(double x) { return ::atan(x); }
+__device__ __noinline__ double t_asin(double x) { return ::asin(x); }
+__device__ __noinline__ double t_pow(double x, double y) { return ::pow(x, y); }
+__device__ __forceinline__ float t_sin(float x) { return ::sinf(x); }
+__device__ __forceinline__ float t_cos(float x) { return ::cosf(x); }
+__device__ __forceinline__ float t_tan(float x) { return ::tanf(x); }
+__device__ __forceinline__ float t_atan(float x) { return ::atanf(x); }
+__device__ __forceinline__ float t_asin(float x) { return ::asinf(x); }
+__device__ __forceinline__ float t_pow(float x, float y) { return ::powf(x, y); }
+
 constexpr int LMAX = TTRL_MAX_LANES;
 constexpr float FAR = 1e30f;  // x of absent slots in the LDS view: never within a collision window
 
@@ -86,11 +103,11 @@ __device__ __forceinline__ T steering_control(const LaneT<T>& L, const ttrl_para
   lane_local(L, x, y, s, r);
   const T lfh = L.hd;  // heading_at(s + v * TAU_PURSUIT) of a straight lane
   const T lat_cmd = -T(P.kp_lateral) * r;
-  const T hcmd = asin(clip(lat_cmd / not_zero(v), T(-1), T(1)));
+  const T hcmd = t_asin(clip(lat_cmd / not_zero(v), T(-1), T(1)));
   const T href = lfh + clip(hcmd, -Tpi<T>() / T(4), Tpi<T>() / T(4));
   const T hrate = T(P.kp_heading) * wrap_to_pi(href - h);
-  const T slip = asin(clip(T(P.length) / T(2) / not_zero(v) * hrate, T(-1), T(1)));
-  const T st = atan(T(2) * tan(slip));
+  const T slip = t_asin(clip(T(P.length) / T(2) / not_zero(v) * hrate, T(-1), T(1)));
+  const T st = t_atan(T(2) * t_tan(slip));
   return clip(st, -T(P.max_steering), T(P.max_steering));
 }
 
@@ -103,7 +120,7 @@ __device__ __forceinline__ int speed_to_index(const ttrl_params_t& P, T v) {
 }
 
 #ifndef TTRL_SIM_WAVES
-#define TTRL_SIM_WAVES 0   // min waves/SIMD for the fused kernel; 0 = tuned default (f64: 2, f32: 4)
+#define TTRL_SIM_WAVES 0   // min waves/SIMD for the fused kernel; 0 = tuned default (4)
 #endif
 #ifdef TTRL_SAT_NOINLINE
 #define TTRL_SAT_ATTR __noinline__
@@ -401,7 +418,7 @@ __device__ __forceinline__ T idm_free(const ttrl_params_t& P, T v, T ts, T lim, 
   ts = clip(ts, T(0), lim);
   T vv = v;
   if (!(vv > T(0))) vv = (T(0) > vv) ? T(0) : vv;
-  return T(P.comfort_acc_max) * (T(1) - pow(vv / fabs(not_zero(ts)), delta));
+  return T(P.comfort_acc_max) * (T(1) - t_pow(vv / fabs(not_zero(ts)), delta));
 }
 
 // IDM interaction term  COMFORT_ACC_MAX * (desired_gap(e, f) / not_zero(d))^2 (behavior.py:185-189,
@@ -478,7 +495,7 @@ enum { A_NO_COLL = 1, A_NO_MOBIL = 2, A_NO_ABORT = 4, A_NO_SCAN = 8, A_NO_STEER 
 
 // Fused frame loop.  EPW envs per workgroup, NS slots per env, blockDim = EPW*NS.
 template <typename T, int NS, int EPW>
-__global__ void __launch_bounds__(NS* EPW, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES : (sizeof(T) == 8 ? 2 : 4))
+__global__ void __launch_bounds__(NS* EPW, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES : 4)
 simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int32_t* __restrict__ actions,
                 int frames, double dt_d, int mode, int ablate) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -498,7 +515,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   if (slot) load_veh(a, st, k);
   else { a = Veh<T>{}; a.kind = TTRL_ABSENT; a.lane = -1; a.tgt = -1; }
   const bool present = slot && a.kind != TTRL_ABSENT;
-  a.ch = cos(a.h); a.sh = sin(a.h);
+  a.ch = t_cos(a.h); a.sh = t_sin(a.h);
   const T dt = T(dt_d);
   __syncthreads();  // lane table staged
   project_all<T, NS, EPW>(V, P, nl, tid, le, i, present, a.x, a.y, a.h, false);
@@ -688,13 +705,13 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         if (ablate & A_NO_KIN) {
           a.x += a.v * a.ch * dt; a.y += a.v * a.sh * dt; a.v += a.acc * dt;
         } else {
-        const T beta = atan(T(1) / T(2) * tan(a.steer));
-        const T vx = a.v * cos(a.h + beta), vy = a.v * sin(a.h + beta);
+        const T beta = t_atan(T(1) / T(2) * t_tan(a.steer));
+        const T vx = a.v * t_cos(a.h + beta), vy = a.v * t_sin(a.h + beta);
         a.x += vx * dt; a.y += vy * dt;
         if (a.hasimp) { a.x += a.ix; a.y += a.iy; a.crashed = true; a.hasimp = false; }
-        a.h += a.v * sin(beta) / (T(P.length) / T(2)) * dt;
+        a.h += a.v * t_sin(beta) / (T(P.length) / T(2)) * dt;
         a.v += a.acc * dt;
-        a.ch = cos(a.h); a.sh = sin(a.h);
+        a.ch = t_cos(a.h); a.sh = t_sin(a.h);
         }
       }
       __syncthreads();  // act-phase readers of the old view are done
@@ -918,9 +935,9 @@ kinematics_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttr
   if (!env_ok) return;
   float* ob = out + (size_t)env * V * F;
   auto slot_of = [&](int q) { return cfg.order_shuffled && V - 1 <= 64 ? 1 + s_perm[le][q] : 1 + q; };
-  const T ec = cos(eh), es = sin(eh);
+  const T ec = t_cos(eh), es = t_sin(eh);
   auto emit = [&](int row, T px, T py, T phd, T pv, int pl, bool rel) {
-    const T c = cos(phd), s = sin(phd);
+    const T c = t_cos(phd), s = t_sin(phd);
     for (int cidx = 0; cidx < F; ++cidx) {
       const int f = cfg.features[cidx];
       T val = feature(s_lanes[pl], f, px, py, phd, pv, c, s);
@@ -982,7 +999,7 @@ grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid
     L.len = T(R.length[ln]); L.w = T(R.width[ln]); L.hd = T(R.heading[ln]); L.lim = T(R.speed_limit[ln]); L.forb = 0;
     EL.sx = T(R.start_x[elane]); EL.sy = T(R.start_y[elane]); EL.dx = T(R.dir_x[elane]); EL.dy = T(R.dir_y[elane]);
     EL.len = T(R.length[elane]); EL.w = T(R.width[elane]); EL.hd = T(R.heading[elane]); EL.lim = T(0); EL.forb = 0;
-    const T c = cos(h), s = sin(h), ec = cos(eh), es = sin(eh);
+    const T c = t_cos(h), s = t_sin(h), ec = t_cos(eh), es = t_sin(eh);
     T rx = x - ex, ry = y - ey;
     for (int ci = 0; ci < F; ++ci) {
       const int f = cfg.features[ci];
