@@ -60,7 +60,7 @@ def cpu_baseline(vehicles: int, obs_cfg: dict, seconds_target: float = 10.0) -> 
     o = Oracle(lanes, _abi.default_params())
     kin = _abi.kin_cfg(**{k: v for k, v in obs_cfg.items() if k != "type"}) if obs_cfg["type"] == "Kinematics" else None
     grid = _abi.grid_cfg(**{k: v for k, v in obs_cfg.items() if k != "type"}) if kin is None else None
-    E = 64 * threads
+    E = 4096  # the same batch as the GPU workload
     h = HostState(E, vehicles)
     o.reset_highway(h, _abi.reset_cfg(vehicles, lanes), list(range(E)))
     rng = np.random.default_rng(0)
@@ -73,7 +73,7 @@ def cpu_baseline(vehicles: int, obs_cfg: dict, seconds_target: float = 10.0) -> 
             o.observe_grid(h, grid)
         steps += 1
         el = time.perf_counter() - t0
-        if el >= seconds_target or steps >= 40:
+        if el >= seconds_target or steps >= 200:
             break
     return {"value": E * vehicles * 15 * steps / el, "unit": "vehicle-steps/s", "cores": threads, "kind": "port",
             "sample": f"{E} envs x {vehicles} vehicles x {steps} env.step (15 frames + obs), float64 C restatement "

@@ -12,13 +12,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "_variants")
 VARIANTS = {
-    "w0": [],
-    "w1": ["-DTTRL_SIM_WAVES=1"],
     "w2": ["-DTTRL_SIM_WAVES=2"],
     "w3": ["-DTTRL_SIM_WAVES=3"],
     "w4": ["-DTTRL_SIM_WAVES=4"],
-    "w3_ni": ["-DTTRL_SIM_WAVES=3", "-DTTRL_SAT_NOINLINE"],
     "w4_ni": ["-DTTRL_SIM_WAVES=4", "-DTTRL_SAT_NOINLINE"],
+    "w5": ["-DTTRL_SIM_WAVES=5"],
+    "w6": ["-DTTRL_SIM_WAVES=6"],
+    "w6_ni": ["-DTTRL_SIM_WAVES=6", "-DTTRL_SAT_NOINLINE"],
 }
 for arg in os.environ.get("EXTRA_VARIANTS", "").split(";"):
     if arg.strip():

@@ -199,7 +199,10 @@ template <> struct __attribute__((aligned(8))) LEnt<float> { float s; int idx; }
 // LDS "road view" of one workgroup (EPW envs x NS slots).
 template <typename T> struct View {
   LaneT<T>* lanes;   // [LMAX]
-  T *x, *y, *v, *ch, *sh, *ts;  // [EPW*NS]
+  T *x, *y, *v, *ch, *sh, *ts;  // [EPW*NS] shared road view (read by other vehicles)
+  T *h, *timer, *delta, *steer, *acc, *ix, *iy;  // [EPW*NS] per-vehicle state resident in LDS
+  uint8_t *kind, *flags;         // [EPW*NS] flags: 1 crashed, 2 has_impact, 4 enable_lane_change
+  int8_t* sidx;                  // [EPW*NS] MDPVehicle.speed_index
   LEnt<T>* ent;      // [n_lanes][EPW][NS+1] vehicles on each lane (AbstractLane.on_lane margin 1), slot order
   int* cnt;          // [EPW][LMAX+1] list lengths; [LMAX] = longest list of the env
   int* wcnt;         // [LMAX][4] per-wave list lengths (NS > 64)
@@ -209,7 +212,7 @@ template <typename T> struct View {
 };
 
 inline __host__ __device__ size_t view_bytes_t(size_t t, size_t lane_sz, size_t ent_sz, int EPW, int NS, int n_lanes) {
-  size_t b = lane_sz * LMAX + t * (6 * EPW * NS);
+  size_t b = lane_sz * n_lanes + t * (13 * EPW * NS) + 3 * EPW * NS;
   b = (b + 15) & ~(size_t)15;
   b += ent_sz * (size_t)n_lanes * EPW * (NS + 1);
   b += sizeof(int) * (EPW * (LMAX + 1) + LMAX * 4);
@@ -222,13 +225,23 @@ template <typename T>
 __device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lanes) {
   View<T> V;
   char* p = smem;
-  V.lanes = (LaneT<T>*)p; p += sizeof(LaneT<T>) * LMAX;
+  V.lanes = (LaneT<T>*)p; p += sizeof(LaneT<T>) * n_lanes;
   V.x = (T*)p; p += sizeof(T) * EPW * NS;
   V.y = (T*)p; p += sizeof(T) * EPW * NS;
   V.v = (T*)p; p += sizeof(T) * EPW * NS;
   V.ch = (T*)p; p += sizeof(T) * EPW * NS;
   V.sh = (T*)p; p += sizeof(T) * EPW * NS;
   V.ts = (T*)p; p += sizeof(T) * EPW * NS;
+  V.h = (T*)p; p += sizeof(T) * EPW * NS;
+  V.timer = (T*)p; p += sizeof(T) * EPW * NS;
+  V.delta = (T*)p; p += sizeof(T) * EPW * NS;
+  V.steer = (T*)p; p += sizeof(T) * EPW * NS;
+  V.acc = (T*)p; p += sizeof(T) * EPW * NS;
+  V.ix = (T*)p; p += sizeof(T) * EPW * NS;
+  V.iy = (T*)p; p += sizeof(T) * EPW * NS;
+  V.kind = (uint8_t*)p; p += EPW * NS;
+  V.flags = (uint8_t*)p; p += EPW * NS;
+  V.sidx = (int8_t*)p; p += EPW * NS;
   p = (char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
   V.ent = (LEnt<T>*)p; p += sizeof(LEnt<T>) * (size_t)n_lanes * EPW * (NS + 1);
   V.cnt = (int*)p; p += sizeof(int) * EPW * (LMAX + 1);
@@ -493,7 +506,12 @@ enum { MODE_META = 1, MODE_ACT = 2, MODE_STEP = 4 };
 enum { A_NO_COLL = 1, A_NO_MOBIL = 2, A_NO_ABORT = 4, A_NO_SCAN = 8, A_NO_STEER = 16, A_NO_KIN = 32,
        A_NO_LANE = 64, A_NO_IDM = 128 };
 
-// Fused frame loop.  EPW envs per workgroup, NS slots per env, blockDim = EPW*NS.
+enum { FL_CRASHED = 1, FL_IMPACT = 2, FL_LC = 4 };
+
+// Fused frame loop.  EPW envs per workgroup, NS slots per env, blockDim = EPW*NS.  The whole
+// vehicle state of the workgroup's envs is resident in LDS for the launch (HBM is read once
+// and written once); each phase loads the few fields it needs into registers, so no state is
+// live across phases and the kernel runs at high occupancy without spilling.
 template <typename T, int NS, int EPW>
 __global__ void __launch_bounds__(NS* EPW, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES : 4)
 simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int32_t* __restrict__ actions,
@@ -507,69 +525,86 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   const int env = blockIdx.x * EPW + le;
   const bool slot = env < st.n_envs && i < N;
   const size_t k = (size_t)env * N + i;
-  const int eb = le * NS;  // env base in the LDS view
+  const int me = le * NS + i;  // this vehicle's LDS slot
+  const int eb = le * NS;      // env base in the LDS view
   View<T> V = carve<T>(smem, EPW, NS, nl);
   stage_lanes(V, R, tid);
-
-  Veh<T> a;
-  if (slot) load_veh(a, st, k);
-  else { a = Veh<T>{}; a.kind = TTRL_ABSENT; a.lane = -1; a.tgt = -1; }
-  const bool present = slot && a.kind != TTRL_ABSENT;
-  a.ch = t_cos(a.h); a.sh = t_sin(a.h);
   const T dt = T(dt_d);
-  __syncthreads();  // lane table staged
-  project_all<T, NS, EPW>(V, P, nl, tid, le, i, present, a.x, a.y, a.h, false);
-  V.x[eb + i] = present ? a.x : T(FAR); V.y[eb + i] = a.y; V.v[eb + i] = a.v; V.ch[eb + i] = a.ch;
-  V.sh[eb + i] = a.sh; V.ts[eb + i] = a.ts;
-  V.lane[eb + i] = (int8_t)(present ? a.lane : -1);
-  V.tgt[eb + i] = (int8_t)(present ? a.tgt : -1);
+
+  bool present;
+  {  // HBM -> LDS, once per launch (coalesced SoA rows)
+    Veh<T> a;
+    if (slot) load_veh(a, st, k);
+    else { a = Veh<T>{}; a.kind = TTRL_ABSENT; a.lane = -1; a.tgt = -1; }
+    present = slot && a.kind != TTRL_ABSENT;
+    V.x[me] = present ? a.x : T(FAR); V.y[me] = a.y; V.v[me] = a.v; V.ts[me] = a.ts;
+    V.ch[me] = t_cos(a.h); V.sh[me] = t_sin(a.h);
+    V.h[me] = a.h; V.timer[me] = a.timer; V.delta[me] = a.delta; V.steer[me] = a.steer; V.acc[me] = a.acc;
+    V.ix[me] = a.ix; V.iy[me] = a.iy;
+    V.kind[me] = (uint8_t)(present ? a.kind : TTRL_ABSENT);
+    V.flags[me] = (uint8_t)((a.crashed ? FL_CRASHED : 0) | (a.hasimp ? FL_IMPACT : 0) | (a.lc ? FL_LC : 0));
+    V.sidx[me] = (int8_t)a.sidx;
+    V.lane[me] = (int8_t)(present ? a.lane : -1);
+    V.tgt[me] = (int8_t)(present ? a.tgt : -1);
+  }
+  __syncthreads();  // lane table + view staged
+  project_all<T, NS, EPW>(V, P, nl, tid, le, i, present, V.x[me], V.y[me], T(0), false);
+  const int kind = V.kind[me];
 
   for (int frame = 0; frame < frames; ++frame) {
     // ---------------- ego meta-action (DiscreteMetaAction.act, action.py:259-260) ----
-    if ((mode & MODE_META) && frame == 0 && actions && present && a.kind == TTRL_MDP && env < st.n_envs) {
+    if ((mode & MODE_META) && frame == 0 && actions && present && kind == TTRL_MDP) {
       const int act = actions[env];
+      const T x = V.x[me], y = V.y[me], h = V.h[me], v = V.v[me];
+      T ts = V.ts[me];
+      int tgt = V.tgt[me];
       if (act == TTRL_FASTER || act == TTRL_SLOWER) {  // MDPVehicle.act controller.py:304-315
-        int si = speed_to_index(P, a.v) + (act == TTRL_FASTER ? 1 : -1);
+        int si = speed_to_index(P, v) + (act == TTRL_FASTER ? 1 : -1);
         si = si < 0 ? 0 : (si > P.n_target_speeds - 1 ? P.n_target_speeds - 1 : si);
-        a.sidx = si;
-        a.ts = T(P.target_speeds[si]);
+        V.sidx[me] = (int8_t)si;
+        ts = T(P.target_speeds[si]);
       } else if (act == TTRL_LANE_LEFT || act == TTRL_LANE_RIGHT) {  // controller.py:103-124
-        int id = a.tgt + (act == TTRL_LANE_RIGHT ? 1 : -1);
+        int id = tgt + (act == TTRL_LANE_RIGHT ? 1 : -1);
         id = id < 0 ? 0 : (id > nl - 1 ? nl - 1 : id);
-        if (reachable(V.lanes[id], T(P.lane_vehicle_length), a.x, a.y)) a.tgt = id;
+        if (reachable(V.lanes[id], T(P.lane_vehicle_length), x, y)) tgt = id;
       }
       // ControlledVehicle.act low-level control (controller.py:126-133); Road.act recomputes
       // the same values this frame, the standalone ttrl_meta_action returns them.
-      a.steer = steering_control(V.lanes[a.tgt], P, a.x, a.y, a.h, a.v);
-      a.acc = T(P.kp_a) * (a.ts - a.v);
-      V.ts[eb + i] = a.ts;
-      V.tgt[eb + i] = (int8_t)a.tgt;
+      V.steer[me] = steering_control(V.lanes[tgt], P, x, y, h, v);
+      V.acc[me] = T(P.kp_a) * (ts - v);
+      V.ts[me] = ts;
+      V.tgt[me] = (int8_t)tgt;
     }
     __syncthreads();
 
     // ---------------- Road.act (road.py:461-464) ----------------
+    int tgt_new = V.tgt[me];
     if (mode & MODE_ACT) {
-      const bool idm = present && a.kind == TTRL_IDM && !a.crashed;
-      const bool changing = idm && a.lane != a.tgt;
-      const bool abort_cand = changing && a.lc;
+      const int lane = V.lane[me], tgt = V.tgt[me];
+      const int fl = V.flags[me];
+      const bool idm = present && kind == TTRL_IDM && !(fl & FL_CRASHED);
+      const bool lc = (fl & FL_LC) != 0;
+      const bool changing = idm && lane != tgt;
+      const bool abort_cand = changing && lc;
+      const T x = V.x[me], y = V.y[me], v = V.v[me];
       bool fire = false;
-      if (idm && a.lc && !changing && T(P.lane_change_delay) < a.timer && !(ablate & A_NO_MOBIL)) {  // utils.do_every
-        fire = true;
-        a.timer = T(0);
+      if (idm && lc && !changing && T(P.lane_change_delay) < V.timer[me] && !(ablate & A_NO_MOBIL)) {
+        fire = true;  // utils.do_every
+        V.timer[me] = T(0);
       }
       // side lanes (RoadNetwork.side_lanes road.py:200-211), gated as behavior.py:252-260
       int left = -1, right = -1;
       if (fire) {
-        const bool moving = !(fabs(a.v) < T(1));
-        if (a.lane > 0 && moving && reachable(V.lanes[a.lane - 1], T(P.lane_vehicle_length), a.x, a.y)) left = a.lane - 1;
-        if (a.lane < nl - 1 && moving && reachable(V.lanes[a.lane + 1], T(P.lane_vehicle_length), a.x, a.y)) right = a.lane + 1;
+        const bool moving = !(fabs(v) < T(1));
+        if (lane > 0 && moving && reachable(V.lanes[lane - 1], T(P.lane_vehicle_length), x, y)) left = lane - 1;
+        if (lane < nl - 1 && moving && reachable(V.lanes[lane + 1], T(P.lane_vehicle_length), x, y)) right = lane + 1;
       }
-      int ql[3] = {idm ? a.lane : -1, changing ? a.tgt : left, right};
+      int ql[3] = {idm ? lane : -1, changing ? tgt : left, right};
       T s3[3];
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         T rr;
-        lane_local(V.lanes[ql[q] < 0 ? 0 : ql[q]], a.x, a.y, s3[q], rr);
+        lane_local(V.lanes[ql[q] < 0 ? 0 : ql[q]], x, y, s3[q], rr);
       }
       int f3[3], r3[3];
       if (ablate & A_NO_SCAN) {
@@ -585,9 +620,9 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       }
 
       // MOBIL (IDMVehicle.mobil behavior.py:265-324, route None); DELTA is ours.
-      int tgt_new = a.tgt;
       T a_free = T(0);
-      if (idm && !(ablate & A_NO_IDM)) a_free = idm_free(P, a.v, a.ts, V.lanes[a.lane].lim, a.delta);
+      const T delta = V.delta[me];
+      if (idm && !(ablate & A_NO_IDM)) a_free = idm_free(P, v, V.ts[me], V.lanes[lane].lim, delta);
       if (fire) {
 #pragma unroll
         for (int side = 1; side <= 2; ++side) {
@@ -595,7 +630,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
           const int np_ = f3[side], nf = r3[side];
           const int op = f3[0], of = r3[0];
           T nfpa = T(0);
-          if (nf >= 0) nfpa = idm_free(P, V.v[eb + nf], V.ts[eb + nf], V.lanes[V.lane[eb + nf]].lim, a.delta)
+          if (nf >= 0) nfpa = idm_free(P, V.v[eb + nf], V.ts[eb + nf], V.lanes[V.lane[eb + nf]].lim, delta)
                                - idm_interact(V, P, eb, nf, i);
           if (nfpa < -T(P.lane_change_max_braking)) continue;
           T spa = a_free, sa = a_free;
@@ -603,9 +638,9 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
           if (op >= 0) sa -= idm_interact(V, P, eb, i, op);
           T jerk;
           if (P.politeness != 0.0) {
-            const T nfa = idm_acc(V, P, eb, nf, np_, a.delta);
-            const T ofa = idm_acc(V, P, eb, of, i, a.delta);
-            const T ofpa = idm_acc(V, P, eb, of, op, a.delta);
+            const T nfa = idm_acc(V, P, eb, nf, np_, delta);
+            const T ofa = idm_acc(V, P, eb, of, i, delta);
+            const T ofpa = idm_acc(V, P, eb, of, op, delta);
             jerk = spa - sa + T(P.politeness) * (nfpa - nfa + ofpa - ofa);
           } else {
             jerk = spa - sa + T(P.politeness) * T(0);
@@ -622,15 +657,15 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         auto contributes = [&](int ii) -> bool {
           if (!present || ii == i) return false;
           const int Ti = V.tgt[eb + ii];
-          const int tv = i < ii ? tgt_new : a.tgt;
-          if (!(a.lane != Ti && tv == Ti)) return false;
+          const int tv = i < ii ? tgt_new : tgt;
+          if (!(lane != Ti && tv == Ti)) return false;
           const LaneT<T> L = V.lanes[V.lane[eb + ii]];
           T s1, r1, s0, r0;
-          lane_local(L, a.x, a.y, s1, r1);
+          lane_local(L, x, y, s1, r1);
           lane_local(L, V.x[eb + ii], V.y[eb + ii], s0, r0);
           const T d = s1 - s0;
           const T ev = V.v[eb + ii], ec = V.ch[eb + ii], es = V.sh[eb + ii];
-          const T dvx = ev * ec - a.v * a.ch, dvy = ev * es - a.v * a.sh;
+          const T dvx = ev * ec - v * V.ch[me], dvy = ev * es - v * V.sh[me];
           const T dv = dvx * ec + dvy * es;
           const T ds = T(P.distance_wanted) + ev * T(P.time_wanted) + ev * dv / T(P.gap_denom);
           return T(0) < d && d < ds;
@@ -643,7 +678,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             const int ii = mine ? __ffsll((long long)mine) - 1 : -1;
             const bool c = ii >= 0 && contributes(ii);
             const unsigned long long cb = (__ballot(c) >> sh) & seg;
-            if (ii >= 0 && cb != 0 && i == ii) tgt_new = a.lane;
+            if (ii >= 0 && cb != 0 && i == ii) tgt_new = lane;
             if (mine) mine &= mine - 1;
           }
         } else {
@@ -667,7 +702,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
               bool any = false;
 #pragma unroll
               for (int w2 = 0; w2 < WAVES; ++w2) any |= V.bal[8 + par * 4 + w2] != 0;
-              if (any && i == ii) tgt_new = a.lane;
+              if (any && i == ii) tgt_new = lane;
               par ^= 1;
             }
           }
@@ -676,62 +711,66 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
 
       // steering + IDM longitudinal (behavior.py:109-135); ego: ControlledVehicle.act (controller.py:126-133)
       if (idm) {
-        a.steer = (ablate & A_NO_STEER) ? T(0) : steering_control(V.lanes[tgt_new], P, a.x, a.y, a.h, a.v);
+        V.steer[me] = (ablate & A_NO_STEER) ? T(0) : steering_control(V.lanes[tgt_new], P, x, y, V.h[me], v);
         T acc = a_free;
         if (f3[0] >= 0) acc -= idm_interact(V, P, eb, i, f3[0]);
-        if (a.lane != tgt_new) {
-          const int ft = tgt_new == a.tgt ? f3[1] : (tgt_new == ql[1] ? f3[1] : f3[2]);
+        if (lane != tgt_new) {
+          const int ft = tgt_new == tgt ? f3[1] : (tgt_new == ql[1] ? f3[1] : f3[2]);
           T a2 = a_free;
           if (ft >= 0) a2 -= idm_interact(V, P, eb, i, ft);
           if (a2 < acc) acc = a2;
         }
-        a.acc = clip(acc, -T(P.acc_max), T(P.acc_max));
-        a.tgt = tgt_new;
-      } else if (present && a.kind == TTRL_MDP) {
-        a.steer = steering_control(V.lanes[a.tgt], P, a.x, a.y, a.h, a.v);
-        a.acc = T(P.kp_a) * (a.ts - a.v);
+        V.acc[me] = clip(acc, -T(P.acc_max), T(P.acc_max));
+      } else if (present && kind == TTRL_MDP) {
+        V.steer[me] = steering_control(V.lanes[tgt], P, x, y, V.h[me], v);
+        V.acc[me] = T(P.kp_a) * (V.ts[me] - v);
       }
     }
 
+    __syncthreads();  // act-phase readers of the old view are done
+    if (mode & MODE_ACT) V.tgt[me] = (int8_t)(present ? tgt_new : -1);
+
     // ---------------- Road.step(dt) (road.py:466-478) ----------------
     if (mode & MODE_STEP) {
+      T x = V.x[me], y = V.y[me], h = V.h[me];
       if (present) {
-        if (a.kind == TTRL_IDM) a.timer += dt;  // IDMVehicle.step behavior.py:147
+        T v = V.v[me], steer = V.steer[me], acc = V.acc[me];
+        int fl = V.flags[me];
+        if (kind == TTRL_IDM) V.timer[me] += dt;  // IDMVehicle.step behavior.py:147
         // Vehicle.clip_actions kinematics.py:155-168
-        if (a.crashed) { a.steer = T(0); a.acc = T(-1) * a.v; }
-        if (a.v > T(P.max_speed)) { const T c = T(1) * (T(P.max_speed) - a.v); if (c < a.acc) a.acc = c; }
-        else if (a.v < T(P.min_speed)) { const T c = T(1) * (T(P.min_speed) - a.v); if (c > a.acc) a.acc = c; }
+        if (fl & FL_CRASHED) { steer = T(0); acc = T(-1) * v; }
+        if (v > T(P.max_speed)) { const T c = T(1) * (T(P.max_speed) - v); if (c < acc) acc = c; }
+        else if (v < T(P.min_speed)) { const T c = T(1) * (T(P.min_speed) - v); if (c > acc) acc = c; }
+        V.steer[me] = steer;
+        V.acc[me] = acc;
         // kinematic bicycle, Vehicle.step kinematics.py:140-153
         if (ablate & A_NO_KIN) {
-          a.x += a.v * a.ch * dt; a.y += a.v * a.sh * dt; a.v += a.acc * dt;
+          x += v * V.ch[me] * dt; y += v * V.sh[me] * dt; v += acc * dt;
         } else {
-        const T beta = t_atan(T(1) / T(2) * t_tan(a.steer));
-        const T vx = a.v * t_cos(a.h + beta), vy = a.v * t_sin(a.h + beta);
-        a.x += vx * dt; a.y += vy * dt;
-        if (a.hasimp) { a.x += a.ix; a.y += a.iy; a.crashed = true; a.hasimp = false; }
-        a.h += a.v * t_sin(beta) / (T(P.length) / T(2)) * dt;
-        a.v += a.acc * dt;
-        a.ch = t_cos(a.h); a.sh = t_sin(a.h);
+          const T beta = t_atan(T(1) / T(2) * t_tan(steer));
+          const T vx = v * t_cos(h + beta), vy = v * t_sin(h + beta);
+          x += vx * dt; y += vy * dt;
+          if (fl & FL_IMPACT) { x += V.ix[me]; y += V.iy[me]; fl = (fl | FL_CRASHED) & ~FL_IMPACT; }
+          h += v * t_sin(beta) / (T(P.length) / T(2)) * dt;
+          v += acc * dt;
+          V.ch[me] = t_cos(h); V.sh[me] = t_sin(h);
         }
+        V.flags[me] = (uint8_t)fl;
+        V.x[me] = x; V.y[me] = y; V.h[me] = h; V.v[me] = v;
       }
-      __syncthreads();  // act-phase readers of the old view are done
-      const int cl = project_all<T, NS, EPW>(V, P, nl, tid, le, i, present, a.x, a.y, a.h, !(ablate & A_NO_LANE));
-      if (present && !(ablate & A_NO_LANE)) a.lane = cl;  // on_state_update kinematics.py:170-177
-      V.x[eb + i] = present ? a.x : T(FAR); V.y[eb + i] = a.y; V.v[eb + i] = a.v; V.ch[eb + i] = a.ch;
-      V.sh[eb + i] = a.sh; V.ts[eb + i] = a.ts;
-      V.lane[eb + i] = (int8_t)(present ? a.lane : -1);
-      V.tgt[eb + i] = (int8_t)(present ? a.tgt : -1);
+      const int cl = project_all<T, NS, EPW>(V, P, nl, tid, le, i, present, x, y, h, !(ablate & A_NO_LANE));
+      if (present && !(ablate & A_NO_LANE)) V.lane[me] = (int8_t)cl;  // on_state_update kinematics.py:170-177
       __syncthreads();
 
       // collisions for all pairs (road.py:474-476, objects.py:91-137), impact: last writer.
       // Pass 1 (pipelined LDS loads): 1-D prefilter |dx| <= R, with R >= every pair's
       // threshold (diag + v*dt, v <= env max), so no pair the reference tests is dropped.
       // Pass 2: the reference's exact norm test and SAT on the candidates, in index order.
-      const T vmax = env_max<T, NS, EPW>(present ? fabs(a.v) : T(0), V, tid);
+      const T vmax = env_max<T, NS, EPW>(present ? fabs(V.v[me]) : T(0), V, tid);
       if (present && !(ablate & A_NO_COLL)) {
         const T thr0 = (T(P.diagonal) + T(P.diagonal)) / T(2);
-        const T R = thr0 + vmax * dt + T(1);
-        bool crash = a.crashed, has_gt = false, has_lt = false;
+        const T Rw = thr0 + vmax * dt + T(1);
+        bool has_gt = false, has_lt = false, crash = false;
         T gx = T(0), gy = T(0), lx = T(0), ly = T(0);
         constexpr int CH = NS < 64 ? NS : 64;
 #pragma unroll
@@ -744,24 +783,25 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             for (int u = 0; u < 8; ++u) xs[u] = V.x[eb + c0 + j1 + u];
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-              if (!(fabs(xs[u] - a.x) > R)) m |= 1ull << (j1 + u);
+              if (!(fabs(xs[u] - x) > Rw)) m |= 1ull << (j1 + u);
           }
           if (i >= c0 && i < c0 + CH) m &= ~(1ull << (i - c0));
           while (m) {
             const int j = c0 + __ffsll((long long)m) - 1;
             m &= m - 1;
+            const T xi = V.x[me], yi = V.y[me], vi = V.v[me];
             const T xj = V.x[eb + j], yj = V.y[eb + j], vj = V.v[eb + j];
             const bool lo = i < j;  // this vehicle is the reference's `self`
-            const T dx = lo ? xj - a.x : a.x - xj, dy = lo ? yj - a.y : a.y - yj;
-            const T thr = thr0 + (lo ? a.v : vj) * dt;
+            const T dx = lo ? xj - xi : xi - xj, dy = lo ? yj - yi : yi - yj;
+            const T thr = thr0 + (lo ? vi : vj) * dt;
             const T d2 = dx * dx + dy * dy;
             if (d2 > (thr + T(1)) * (thr + T(1))) continue;  // far: skip the exact test
             if (sqrt(d2) > thr) continue;                     // objects.py:123-133 exact
             bool inter, will;
             T tx, ty;
-            const T cj = V.ch[eb + j], sj = V.sh[eb + j];
-            if (lo) sat_pair(P, a.x, a.y, a.ch, a.sh, a.v, xj, yj, cj, sj, vj, dt, inter, will, tx, ty);
-            else sat_pair(P, xj, yj, cj, sj, vj, a.x, a.y, a.ch, a.sh, a.v, dt, inter, will, tx, ty);
+            const T ci = V.ch[me], si = V.sh[me], cj = V.ch[eb + j], sj = V.sh[eb + j];
+            if (lo) sat_pair(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt, inter, will, tx, ty);
+            else sat_pair(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt, inter, will, tx, ty);
             if (will) {
               if (lo) { has_gt = true; gx = tx / T(2); gy = ty / T(2); }
               else { has_lt = true; lx = -tx / T(2); ly = -ty / T(2); }
@@ -769,13 +809,27 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             if (inter) crash = true;
           }
         }
-        a.crashed = crash;
-        if (has_gt) { a.hasimp = true; a.ix = gx; a.iy = gy; }
-        else if (has_lt) { a.hasimp = true; a.ix = lx; a.iy = ly; }
+        int fl = V.flags[me];
+        if (crash) fl |= FL_CRASHED;
+        if (has_gt) { fl |= FL_IMPACT; V.ix[me] = gx; V.iy[me] = gy; }
+        else if (has_lt) { fl |= FL_IMPACT; V.ix[me] = lx; V.iy[me] = ly; }
+        V.flags[me] = (uint8_t)fl;
       }
     }
   }
-  if (slot) store_veh(a, st, k);
+  __syncthreads();
+  if (slot) {  // LDS -> HBM, once per launch
+    Veh<T> a;
+    a.x = V.x[me]; a.y = V.y[me]; a.h = V.h[me]; a.v = V.v[me]; a.ts = V.ts[me]; a.timer = V.timer[me];
+    a.steer = V.steer[me]; a.acc = V.acc[me]; a.ix = V.ix[me]; a.iy = V.iy[me];
+    a.lane = V.lane[me]; a.tgt = V.tgt[me]; a.sidx = V.sidx[me];
+    const int fl = V.flags[me];
+    a.crashed = (fl & FL_CRASHED) != 0; a.hasimp = (fl & FL_IMPACT) != 0;
+    if (!present) {  // absent rows pass through untouched
+      a.x = ((const T*)st.x)[k]; a.lane = st.lane[k]; a.tgt = st.target_lane[k];
+    }
+    store_veh(a, st, k);
+  }
 }
 
 // Road.neighbour_vehicles for an explicit query lane per vehicle (road.py:480-513).
