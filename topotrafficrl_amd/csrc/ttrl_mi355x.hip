@@ -120,7 +120,7 @@ __device__ __forceinline__ int speed_to_index(const ttrl_params_t& P, T v) {
 }
 
 #ifndef TTRL_SIM_WAVES
-#define TTRL_SIM_WAVES 0   // min waves/SIMD for the fused kernel; 0 = tuned default (4)
+#define TTRL_SIM_WAVES 0   // min waves/SIMD for the fused kernel; 0 = tuned default (f64: 2, f32: 4)
 #endif
 #ifdef TTRL_SAT_NOINLINE
 #define TTRL_SAT_ATTR __noinline__
@@ -190,11 +190,24 @@ __device__ TTRL_SAT_ATTR void sat_pair(const ttrl_params_t& P, T ax, T ay, T ac,
   ty = wi ? mind * axy : T(0);
 }
 
+// Out-of-line copy for the rare overflow sweep (keeps the hot path's register budget).
+template <typename T>
+__device__ __noinline__ void sat_pair_ool(const ttrl_params_t& P, T ax, T ay, T ac, T as, T av, T bx, T by, T bc,
+                                          T bs, T bv, T dt, bool& inter, bool& will, T& tx, T& ty) {
+  sat_pair(P, ax, ay, ac, as, av, bx, by, bc, bs, bv, dt, inter, will, tx, ty);
+}
+
 // ---------------------------------------------------------------------------------
-// Per-lane candidate list entry: (longitudinal coordinate on the lane, vehicle slot).
-template <typename T> struct LEnt;
-template <> struct __attribute__((aligned(16))) LEnt<double> { double s; int idx; int pad; };
-template <> struct __attribute__((aligned(8))) LEnt<float> { float s; int idx; };
+// Per-lane candidate lists: for every lane, the longitudinal coordinates of the env's
+// vehicles that are on it (keys) and their slots (idx), in slot order; each vehicle also
+// records its own position in the lists it belongs to (mypos, -1 if not on the lane).
+
+// A close pair (i < j) queued for the SAT test, and its result.
+template <typename T> struct PairRec {
+  T tx, ty;
+  short i, j;
+  int res;  // bit0 intersecting, bit1 will_intersect
+};
 
 // LDS "road view" of one workgroup (EPW envs x NS slots).
 template <typename T> struct View {
@@ -203,22 +216,29 @@ template <typename T> struct View {
   T *h, *timer, *delta, *steer, *acc, *ix, *iy;  // [EPW*NS] per-vehicle state resident in LDS
   uint8_t *kind, *flags;         // [EPW*NS] flags: 1 crashed, 2 has_impact, 4 enable_lane_change
   int8_t* sidx;                  // [EPW*NS] MDPVehicle.speed_index
-  LEnt<T>* ent;      // [n_lanes][EPW][NS+1] vehicles on each lane (AbstractLane.on_lane margin 1), slot order
+  T* key;            // [n_lanes][EPW][NS+1] s of the vehicles on each lane (AbstractLane.on_lane margin 1)
+  uint8_t* idx;      // [n_lanes][EPW][NS+1] their slots, slot order
+  short* mypos;      // [n_lanes][EPW*NS] each vehicle's position in the list, -1 if not on the lane
   int* cnt;          // [EPW][LMAX+1] list lengths; [LMAX] = longest list of the env
   int* wcnt;         // [LMAX][4] per-wave list lengths (NS > 64)
   int8_t *lane, *tgt;            // [EPW*NS] lane (-1 absent), target (old, for the act phase)
   unsigned long long* bal;       // [2][8] cross-wave ballots (NS > 64)
   T* red;                        // [8] cross-wave reduction scratch
+  PairRec<T>* pq;                // [EPW][NS] close vehicle pairs of the frame (collision queue)
+  int* pq_n;                     // [EPW] queue lengths (> NS: overflow)
 };
 
-inline __host__ __device__ size_t view_bytes_t(size_t t, size_t lane_sz, size_t ent_sz, int EPW, int NS, int n_lanes) {
+inline __host__ __device__ size_t view_bytes_t(size_t t, size_t lane_sz, int EPW, int NS, int n_lanes) {
   size_t b = lane_sz * n_lanes + t * (13 * EPW * NS) + 3 * EPW * NS;
   b = (b + 15) & ~(size_t)15;
-  b += ent_sz * (size_t)n_lanes * EPW * (NS + 1);
+  b += (t + 1) * (size_t)n_lanes * EPW * (NS + 1) + 2 * (size_t)n_lanes * EPW * NS;
+  b = (b + 15) & ~(size_t)15;
   b += sizeof(int) * (EPW * (LMAX + 1) + LMAX * 4);
   b += 2 * EPW * NS;
   b = (b + 15) & ~(size_t)15;
-  return b + 16 * sizeof(unsigned long long) + 8 * t;
+  b += 16 * sizeof(unsigned long long) + 8 * t;
+  b = (b + 15) & ~(size_t)15;
+  return b + (2 * t + 8) * EPW * NS + 4 * EPW + 16;
 }
 
 template <typename T>
@@ -243,21 +263,27 @@ __device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lane
   V.flags = (uint8_t*)p; p += EPW * NS;
   V.sidx = (int8_t*)p; p += EPW * NS;
   p = (char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
-  V.ent = (LEnt<T>*)p; p += sizeof(LEnt<T>) * (size_t)n_lanes * EPW * (NS + 1);
+  V.key = (T*)p; p += sizeof(T) * (size_t)n_lanes * EPW * (NS + 1);
+  V.mypos = (short*)p; p += sizeof(short) * (size_t)n_lanes * EPW * NS;
+  V.idx = (uint8_t*)p; p += (size_t)n_lanes * EPW * (NS + 1);
+  p = (char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
   V.cnt = (int*)p; p += sizeof(int) * EPW * (LMAX + 1);
   V.wcnt = (int*)p; p += sizeof(int) * LMAX * 4;
   V.lane = (int8_t*)p; p += EPW * NS;
   V.tgt = (int8_t*)p; p += EPW * NS;
   p = (char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
   V.bal = (unsigned long long*)p; p += 16 * sizeof(unsigned long long);
-  V.red = (T*)p;
+  V.red = (T*)p; p += 8 * sizeof(T);
+  p = (char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
+  V.pq = (PairRec<T>*)p; p += sizeof(PairRec<T>) * EPW * NS;
+  V.pq_n = (int*)p;
   return V;
 }
 
 size_t host_view_bytes(int dtype, int EPW, int NS, int n_lanes) {
   return dtype == TTRL_F64
-             ? view_bytes_t(8, sizeof(LaneT<double>), sizeof(LEnt<double>), EPW, NS, n_lanes)
-             : view_bytes_t(4, sizeof(LaneT<float>), sizeof(LEnt<float>), EPW, NS, n_lanes);
+             ? view_bytes_t(8, sizeof(LaneT<double>), EPW, NS, n_lanes)
+             : view_bytes_t(4, sizeof(LaneT<float>), EPW, NS, n_lanes);
 }
 
 template <typename T>
@@ -362,11 +388,12 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
       lane_local(L, x, y, s, r);
       const bool on = present && fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl;
       const unsigned long long m = (__ballot(on) >> sh) & seg;
+      const int pos = on ? __popcll(m & ((1ull << i) - 1)) : -1;
       if (on) {
-        LEnt<T> e{};
-        e.s = s; e.idx = i;
-        V.ent[((size_t)l * EPW + le) * NSP + __popcll(m & ((1ull << i) - 1))] = e;
+        V.key[((size_t)l * EPW + le) * NSP + pos] = s;
+        V.idx[((size_t)l * EPW + le) * NSP + pos] = (uint8_t)i;
       }
+      V.mypos[(size_t)l * EPW * NS + le * NS + i] = (short)pos;
       const int c = __popcll(m);
       mx = c > mx ? c : mx;
       if (i == 0) cnt[l] = c;
@@ -404,11 +431,12 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
         off += w < wave ? wc : 0;
         c += wc;
       }
+      const int pos = on ? off + __popcll(b & ((1ull << lane) - 1)) : -1;
       if (on) {
-        LEnt<T> e{};
-        e.s = s; e.idx = i;
-        V.ent[(size_t)l * NSP + off + __popcll(b & ((1ull << lane) - 1))] = e;
+        V.key[(size_t)l * NSP + pos] = s;
+        V.idx[(size_t)l * NSP + pos] = (uint8_t)i;
       }
+      V.mypos[(size_t)l * NS + i] = (short)pos;
       mx = c > mx ? c : mx;
       if (i == 0) cnt[l] = c;
       if (want_closest) {
@@ -472,32 +500,39 @@ __device__ __forceinline__ void scan_neighbours(const View<T>& V, int le, int se
   const int* cnt = V.cnt + le * (LMAX + 1);
   const int mx = cnt[LMAX];
   T sf[NQ], sr[NQ];
-  int n[NQ];
-  const LEnt<T>* row[NQ];
+  int n[NQ], me[NQ], fp[NQ], rp[NQ];
+  const T* row[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    sf[q] = K<T>::inf(); sr[q] = -K<T>::inf(); f[q] = -1; r[q] = -1;
+    sf[q] = K<T>::inf(); sr[q] = -K<T>::inf(); fp[q] = -1; rp[q] = -1;
     const int l = ql[q] < 0 ? 0 : ql[q];
-    row[q] = V.ent + ((size_t)l * EPW + le) * NSP;
+    row[q] = V.key + ((size_t)l * EPW + le) * NSP;
     n[q] = ql[q] < 0 ? 0 : cnt[l];
+    me[q] = V.mypos[(size_t)l * EPW * NS + le * NS + self];  // self is skipped by position
   }
-  constexpr int U = NQ == 1 ? 4 : 2;
+  constexpr int U = NQ == 1 ? 8 : 4;
   for (int k0 = 0; k0 < mx; k0 += U) {
-    LEnt<T> e[NQ][U];
+    T sv[NQ][U];
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
 #pragma unroll
-      for (int u = 0; u < U; ++u) e[q][u] = row[q][k0 + u];
+      for (int u = 0; u < U; ++u) sv[q][u] = row[q][k0 + u];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
-        const T sv = e[q][u].s;
-        const bool ok = k0 + u < n[q] && e[q][u].idx != self;
-        if (ok && s[q] <= sv && sv <= sf[q]) { sf[q] = sv; f[q] = e[q][u].idx; }
-        if (ok && sv < s[q] && sv > sr[q]) { sr[q] = sv; r[q] = e[q][u].idx; }
+        const int kk = k0 + u;
+        const bool ok = kk < n[q] && kk != me[q];
+        if (ok && s[q] <= sv[q][u] && sv[q][u] <= sf[q]) { sf[q] = sv[q][u]; fp[q] = kk; }
+        if (ok && sv[q][u] < s[q] && sv[q][u] > sr[q]) { sr[q] = sv[q][u]; rp[q] = kk; }
       }
     }
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const uint8_t* ix = V.idx + ((size_t)(ql[q] < 0 ? 0 : ql[q]) * EPW + le) * NSP;
+    f[q] = fp[q] >= 0 ? (int)ix[fp[q]] : -1;
+    r[q] = rp[q] >= 0 ? (int)ix[rp[q]] : -1;
   }
 }
 
@@ -513,7 +548,7 @@ enum { FL_CRASHED = 1, FL_IMPACT = 2, FL_LC = 4 };
 // and written once); each phase loads the few fields it needs into registers, so no state is
 // live across phases and the kernel runs at high occupancy without spilling.
 template <typename T, int NS, int EPW>
-__global__ void __launch_bounds__(NS* EPW, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES : 4)
+__global__ void __launch_bounds__(NS* EPW, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES : (sizeof(T) == 8 ? 2 : 4))
 simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int32_t* __restrict__ actions,
                 int frames, double dt_d, int mode, int ablate) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -760,21 +795,29 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       }
       const int cl = project_all<T, NS, EPW>(V, P, nl, tid, le, i, present, x, y, h, !(ablate & A_NO_LANE));
       if (present && !(ablate & A_NO_LANE)) V.lane[me] = (int8_t)cl;  // on_state_update kinematics.py:170-177
+      if (i == 0) V.pq_n[le] = 0;
       __syncthreads();
 
       // collisions for all pairs (road.py:474-476, objects.py:91-137), impact: last writer.
       // Pass 1 (pipelined LDS loads): 1-D prefilter |dx| <= R, with R >= every pair's
-      // threshold (diag + v*dt, v <= env max), so no pair the reference tests is dropped.
-      // Pass 2: the reference's exact norm test and SAT on the candidates, in index order.
+      // threshold (diag + v*dt, v <= env max), so no pair the reference tests is dropped;
+      // each lower-index vehicle then applies the reference's exact norm test to its pairs
+      // (its own speed is the asymmetric threshold's) and queues the survivors.
+      // Pass 2: the queued SATs run one pair per lane, each pair once.
+      // Pass 3: every vehicle folds its pairs' results with the last-writer rule
+      // (impact from the largest j > i that will intersect, else the largest i' < i).
+      // A queue overflow (> NS pairs in an env) falls back to the per-vehicle sweep.
       const T vmax = env_max<T, NS, EPW>(present ? fabs(V.v[me]) : T(0), V, tid);
-      if (present && !(ablate & A_NO_COLL)) {
-        const T thr0 = (T(P.diagonal) + T(P.diagonal)) / T(2);
-        const T Rw = thr0 + vmax * dt + T(1);
-        bool has_gt = false, has_lt = false, crash = false;
-        T gx = T(0), gy = T(0), lx = T(0), ly = T(0);
-        constexpr int CH = NS < 64 ? NS : 64;
+      const bool do_coll = !(ablate & A_NO_COLL);
+      const T thr0 = (T(P.diagonal) + T(P.diagonal)) / T(2);
+      const T Rw = thr0 + vmax * dt + T(1);
+      constexpr int CH = NS < 64 ? NS : 64;
+      if (present && do_coll) {
+        const T xi = V.x[me], yi = V.y[me], vi = V.v[me];
+        const T thr = thr0 + vi * dt;
 #pragma unroll
         for (int c0 = 0; c0 < NS; c0 += CH) {
+          if (c0 + CH <= i + 1) continue;  // only partners j > i
           unsigned long long m = 0;
 #pragma unroll
           for (int j1 = 0; j1 < CH; j1 += 8) {
@@ -783,36 +826,78 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             for (int u = 0; u < 8; ++u) xs[u] = V.x[eb + c0 + j1 + u];
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-              if (!(fabs(xs[u] - x) > Rw)) m |= 1ull << (j1 + u);
+              if (!(fabs(xs[u] - xi) > Rw)) m |= 1ull << (j1 + u);
           }
-          if (i >= c0 && i < c0 + CH) m &= ~(1ull << (i - c0));
+          if (i >= c0) m &= ~((2ull << (i - c0)) - 1);  // keep j > i
           while (m) {
             const int j = c0 + __ffsll((long long)m) - 1;
             m &= m - 1;
-            const T xi = V.x[me], yi = V.y[me], vi = V.v[me];
+            const T dx = V.x[eb + j] - xi, dy = V.y[eb + j] - yi;
+            const T d2 = dx * dx + dy * dy;
+            if (d2 > (thr + T(1)) * (thr + T(1))) continue;  // far: skip the exact test
+            if (sqrt(d2) > thr) continue;                     // objects.py:123-133 exact
+            const int q = atomicAdd(&V.pq_n[le], 1);
+            if (q < NS) { V.pq[le * NS + q].i = (short)i; V.pq[le * NS + q].j = (short)j; }
+          }
+        }
+      }
+      __syncthreads();
+      const int npairs = do_coll ? V.pq_n[le] : 0;
+      if (npairs <= NS) {
+        for (int q = i; q < npairs; q += NS) {
+          PairRec<T>& r = V.pq[le * NS + q];
+          const int a = eb + r.i, b = eb + r.j;
+          bool inter, will;
+          T tx, ty;
+          sat_pair(P, V.x[a], V.y[a], V.ch[a], V.sh[a], V.v[a], V.x[b], V.y[b], V.ch[b], V.sh[b], V.v[b], dt,
+                   inter, will, tx, ty);
+          r.tx = tx; r.ty = ty; r.res = (inter ? 1 : 0) | (will ? 2 : 0);
+        }
+      }
+      __syncthreads();
+      if (present && do_coll && npairs > 0) {
+        bool crash = false;
+        int best_gt = -1, best_lt = -1;
+        T gx = T(0), gy = T(0), lx = T(0), ly = T(0);
+        if (npairs <= NS) {
+          for (int q = 0; q < npairs; ++q) {
+            const PairRec<T> r = V.pq[le * NS + q];
+            if (r.i == i) {
+              if (r.res & 1) crash = true;
+              if ((r.res & 2) && r.j > best_gt) { best_gt = r.j; gx = r.tx / T(2); gy = r.ty / T(2); }
+            } else if (r.j == i) {
+              if (r.res & 1) crash = true;
+              if ((r.res & 2) && r.i > best_lt) { best_lt = r.i; lx = -r.tx / T(2); ly = -r.ty / T(2); }
+            }
+          }
+        } else {  // overflow: every vehicle sweeps all its partners in index order
+          const T xi = V.x[me], yi = V.y[me], vi = V.v[me];
+#pragma unroll 1
+          for (int j = 0; j < NS; ++j) {
+            if (j == i || fabs(V.x[eb + j] - xi) > Rw) continue;
             const T xj = V.x[eb + j], yj = V.y[eb + j], vj = V.v[eb + j];
             const bool lo = i < j;  // this vehicle is the reference's `self`
             const T dx = lo ? xj - xi : xi - xj, dy = lo ? yj - yi : yi - yj;
             const T thr = thr0 + (lo ? vi : vj) * dt;
             const T d2 = dx * dx + dy * dy;
-            if (d2 > (thr + T(1)) * (thr + T(1))) continue;  // far: skip the exact test
-            if (sqrt(d2) > thr) continue;                     // objects.py:123-133 exact
+            if (d2 > (thr + T(1)) * (thr + T(1))) continue;
+            if (sqrt(d2) > thr) continue;
             bool inter, will;
             T tx, ty;
             const T ci = V.ch[me], si = V.sh[me], cj = V.ch[eb + j], sj = V.sh[eb + j];
-            if (lo) sat_pair(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt, inter, will, tx, ty);
-            else sat_pair(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt, inter, will, tx, ty);
+            if (lo) sat_pair_ool(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt, inter, will, tx, ty);
+            else sat_pair_ool(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt, inter, will, tx, ty);
             if (will) {
-              if (lo) { has_gt = true; gx = tx / T(2); gy = ty / T(2); }
-              else { has_lt = true; lx = -tx / T(2); ly = -ty / T(2); }
+              if (lo) { best_gt = j; gx = tx / T(2); gy = ty / T(2); }
+              else { best_lt = j; lx = -tx / T(2); ly = -ty / T(2); }
             }
             if (inter) crash = true;
           }
         }
         int fl = V.flags[me];
         if (crash) fl |= FL_CRASHED;
-        if (has_gt) { fl |= FL_IMPACT; V.ix[me] = gx; V.iy[me] = gy; }
-        else if (has_lt) { fl |= FL_IMPACT; V.ix[me] = lx; V.iy[me] = ly; }
+        if (best_gt >= 0) { fl |= FL_IMPACT; V.ix[me] = gx; V.iy[me] = gy; }
+        else if (best_lt >= 0) { fl |= FL_IMPACT; V.ix[me] = lx; V.iy[me] = ly; }
         V.flags[me] = (uint8_t)fl;
       }
     }
