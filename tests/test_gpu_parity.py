@@ -204,3 +204,45 @@ def test_random_batch_rollout_vs_oracle(n, hip_device):
         o.simulate(h, acts, 15, 1 / 15)
         road.simulate(torch.from_numpy(acts), 15, 1 / 15)
         compare(dev, h, 1e-6)
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_close_pairs_collisions_vs_oracle(dtype, hip_device):
+    """Clusters of vehicles at random close poses (many pairs touching, near-touching or
+    sweeping into each other): Road.step's collision pass (crashed, impact) == the oracle's.
+    Exercises the SAT separation shortcut and the pair queue at its boundary cases."""
+    E, n = 2048, 6
+    rng = np.random.default_rng(7)
+    h = HostState(E, n)
+    spread = rng.uniform(4, 25, (E, 1))  # from pile-ups to near misses
+    h["x"][:] = 200 + spread * rng.uniform(-1, 1, (E, n))
+    h["y"][:] = rng.uniform(-2, 10, (E, n))
+    h["heading"][:] = rng.uniform(-0.7, 0.7, (E, n))
+    h["speed"][:] = rng.uniform(0, 35, (E, n))
+    h["target_speed"][:] = h["speed"]
+    h["steer"][:] = rng.uniform(-0.3, 0.3, (E, n))
+    h["acc"][:] = rng.uniform(-5, 5, (E, n))
+    h["lane"][:] = np.clip(np.round(h["y"] / 4), 0, 3).astype(np.int32)
+    h["target_lane"][:] = h["lane"]
+    h["kind"][:] = _abi.IDM
+    h["crashed"][:] = rng.random((E, n)) < 0.05
+    lanes = _abi.straight_lane_table(4)
+    o = Oracle(lanes, P)
+    dev = to_dev(h, hip_device, dtype)
+    road = BatchedRoad(RoadNetwork(lanes), dev, P)
+    for _ in range(3):
+        o.road_step(h, 1 / 15)
+        road.step(1 / 15)
+        torch.cuda.synchronize()
+        d = dev.to_numpy()
+        assert h["crashed"].sum() > E // 2  # the scene really is collision-heavy
+        bad = sum(int(np.sum(d[k] != h[k])) for k in ("crashed", "has_impact"))
+        if dtype == "f64":
+            assert bad == 0
+            imp = h["has_impact"].astype(bool)
+            for k in ("impact_x", "impact_y", "x", "y"):
+                sel = imp if k.startswith("impact") else slice(None)
+                assert np.max(np.abs(d[k][sel] - h[k][sel])) < 1e-9, k
+        else:
+            assert bad <= E * n * 2e-3, bad
+            dev.load_numpy(h.a)  # re-sync so fp32 drift does not compound

@@ -13,7 +13,7 @@ from topotrafficrl_amd.road import RoadNetwork  # noqa: E402
 from topotrafficrl_amd.state import BatchState  # noqa: E402
 
 VARIANTS = {"full": 0, "no_coll": 1, "no_mobil": 2, "no_abort": 4, "no_scan": 8, "no_steer": 16,
-            "no_kin": 32, "no_lane": 64, "no_idm": 128, "none": 255}
+            "no_kin": 32, "no_lane": 64, "no_idm": 128, "no_sat": 256, "no_pref": 512, "none": 255}
 
 
 def main(E=4096, N=64, rounds=5):

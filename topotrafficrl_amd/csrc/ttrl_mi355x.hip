@@ -29,12 +29,24 @@ __device__ __noinline__ double t_tan(double x) { return ::tan(x); }
 __device__ __noinline__ double t_atan(double x) { return ::atan(x); }
 __device__ __noinline__ double t_asin(double x) { return ::asin(x); }
 __device__ __noinline__ double t_pow(double x, double y) { return ::pow(x, y); }
+template <typename T> struct SinCos { T s, c; };
+// one shared argument reduction; ocml's sincos returns the same values as sin and cos
+__device__ __noinline__ SinCos<double> t_sincos(double x) {
+  SinCos<double> r;
+  ::sincos(x, &r.s, &r.c);
+  return r;
+}
 __device__ __forceinline__ float t_sin(float x) { return ::sinf(x); }
 __device__ __forceinline__ float t_cos(float x) { return ::cosf(x); }
 __device__ __forceinline__ float t_tan(float x) { return ::tanf(x); }
 __device__ __forceinline__ float t_atan(float x) { return ::atanf(x); }
 __device__ __forceinline__ float t_asin(float x) { return ::asinf(x); }
 __device__ __forceinline__ float t_pow(float x, float y) { return ::powf(x, y); }
+__device__ __forceinline__ SinCos<float> t_sincos(float x) {
+  SinCos<float> r;
+  ::sincosf(x, &r.s, &r.c);
+  return r;
+}
 
 constexpr int LMAX = TTRL_MAX_LANES;
 constexpr float FAR = 1e30f;  // x of absent slots in the LDS view: never within a collision window
@@ -190,6 +202,93 @@ __device__ TTRL_SAT_ATTR void sat_pair(const ttrl_params_t& P, T ax, T ay, T ac,
   ty = wi ? mind * axy : T(0);
 }
 
+// Conservative proof that sat_pair returns (false, false): some edge normal of either
+// rectangle separates a, swept by its relative displacement, from b by more than a margin
+// that dominates the rounding of the reference's corner/normal/projection arithmetic.
+// The 8 normals are +-u and +-w of each box (u = heading, w = its left normal); on axis n a
+// box projects to centre.n +- (hl |u.n| + hw |w.n|), and the sweep widens a's interval by
+// |D.n| at most.  Pairs it cannot separate go to the exact sat_pair.
+template <typename T> struct SepTol;
+template <> struct SepTol<double> { static constexpr double abs = 1e-6, rel = 1e-12, quad = 1e-14; };
+template <> struct SepTol<float> { static constexpr float abs = 1e-3f, rel = 1e-6f, quad = 1e-7f; };
+// The reference's projections run on corners and on normals rebuilt from corner differences:
+// near |x| their error grows like ulp(x) * |x| / edge, hence the quadratic term.
+template <typename T> __device__ __forceinline__ T sat_margin(T ax, T ay, T bx, T by) {
+  const T X = fmax(fmax(fabs(ax), fabs(ay)), fmax(fabs(bx), fabs(by)));
+  return T(SepTol<T>::abs) + T(SepTol<T>::rel) * X + T(SepTol<T>::quad) * X * X;
+}
+
+template <typename T>
+__device__ __forceinline__ bool sat_separated(const ttrl_params_t& P, T ax, T ay, T ac, T as, T av, T bx, T by, T bc,
+                                              T bs, T bv, T dt) {
+  const T hl = T(P.length) / T(2), hw = T(P.width) / T(2);
+  const T dx = bx - ax, dy = by - ay;
+  const T Dx = (av * ac - bv * bc) * dt, Dy = (av * as - bv * bs) * dt;
+  const T C = fabs(ac * bc + as * bs), S = fabs(as * bc - ac * bs);
+  const T ru = hl + hl * C + hw * S;  // both boxes' half extents along either box's u
+  const T rw = hw + hw * C + hl * S;  // ... along either box's w
+  const T m = sat_margin(ax, ay, bx, by);
+  const T g1 = fabs(dx * ac + dy * as) - fabs(Dx * ac + Dy * as) - ru;
+  const T g2 = fabs(dy * ac - dx * as) - fabs(Dy * ac - Dx * as) - rw;
+  const T g3 = fabs(dx * bc + dy * bs) - fabs(Dx * bc + Dy * bs) - ru;
+  const T g4 = fabs(dy * bc - dx * bs) - fabs(Dy * bc - Dx * bs) - rw;
+  return g1 > m || g2 > m || g3 > m || g4 > m;
+}
+
+// One edge normal of sat_pair, evaluated exactly as sat_pair's loop body does (same corners,
+// same normal normalisation, same projection, branch and sweep arithmetic): axis k < 4 is
+// edge k of a's polygon, k >= 4 edge k-4 of b's.  Returns the static and swept interval
+// distances and the normal oriented along the centre difference (the translation axis).
+template <typename T>
+__device__ __forceinline__ void sat_axis(const ttrl_params_t& P, int k, T ax, T ay, T ac, T as, T av, T bx, T by,
+                                         T bc, T bs, T bv, T dt, T& dd, T& dist, T& axx, T& axy) {
+  const T hl = T(P.length) / T(2), hw = T(P.width) / T(2);
+  const T lx[4] = {-hl, -hl, +hl, +hl}, ly[4] = {-hw, +hw, +hw, -hw};
+  T pa[4][2], pb[4][2];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    pa[c][0] = ac * lx[c] + (-as) * ly[c] + ax;
+    pa[c][1] = as * lx[c] + ac * ly[c] + ay;
+    pb[c][0] = bc * lx[c] + (-bs) * ly[c] + bx;
+    pb[c][1] = bs * lx[c] + bc * ly[c] + by;
+  }
+  const int e = k & 3, e1 = (e + 1) & 3;
+  const bool own_b = k >= 4;
+  // corners e and e+1 of the edge's polygon (selects, no dynamic register indexing)
+  T p1x = pa[0][0], p1y = pa[0][1], p2x = pa[1][0], p2y = pa[1][1];
+#pragma unroll
+  for (int c = 1; c < 4; ++c) {
+    if (e == c) { p1x = own_b ? pb[c][0] : pa[c][0]; p1y = own_b ? pb[c][1] : pa[c][1]; }
+    if (e1 == c) { p2x = own_b ? pb[c][0] : pa[c][0]; p2y = own_b ? pb[c][1] : pa[c][1]; }
+  }
+  if (e == 0) { p1x = own_b ? pb[0][0] : pa[0][0]; p1y = own_b ? pb[0][1] : pa[0][1]; }
+  if (e1 == 0) { p2x = own_b ? pb[0][0] : pa[0][0]; p2y = own_b ? pb[0][1] : pa[0][1]; }
+  T nx = -p2y + p1y, ny = p2x - p1x;
+  const T nn = sqrt(nx * nx + ny * ny);
+  nx /= nn; ny /= nn;
+  T mina = T(0), maxa = T(0), minb = T(0), maxb = T(0);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {  // the closing 5th point repeats corner 0: same min / max
+    const T p = pa[c][0] * nx + pa[c][1] * ny;
+    if (c == 0 || p < mina) mina = p;
+    if (c == 0 || p > maxa) maxa = p;
+    const T q = pb[c][0] * nx + pb[c][1] * ny;
+    if (c == 0 || q < minb) minb = q;
+    if (c == 0 || q > maxb) maxb = q;
+  }
+  dd = mina < minb ? minb - maxa : mina - maxb;
+  const T dax = av * ac * dt, day = av * as * dt, dbx = bv * bc * dt, dby = bv * bs * dt;
+  const T vp = nx * (dax - dbx) + ny * (day - dby);
+  if (vp < T(0)) mina += vp; else maxa += vp;
+  dist = mina < minb ? minb - maxa : mina - maxb;
+  const T cax = (((pa[0][0] + pa[1][0]) + pa[2][0]) + pa[3][0]) / T(4);
+  const T cay = (((pa[0][1] + pa[1][1]) + pa[2][1]) + pa[3][1]) / T(4);
+  const T cbx = (((pb[0][0] + pb[1][0]) + pb[2][0]) + pb[3][0]) / T(4);
+  const T cby = (((pb[0][1] + pb[1][1]) + pb[2][1]) + pb[3][1]) / T(4);
+  const T dx = cax - cbx, dy = cay - cby;
+  if (dx * nx + dy * ny > T(0)) { axx = nx; axy = ny; } else { axx = -nx; axy = -ny; }
+}
+
 // Out-of-line copy for the rare overflow sweep (keeps the hot path's register budget).
 template <typename T>
 __device__ __noinline__ void sat_pair_ool(const ttrl_params_t& P, T ax, T ay, T ac, T as, T av, T bx, T by, T bc,
@@ -213,6 +312,7 @@ template <typename T> struct PairRec {
 template <typename T> struct View {
   LaneT<T>* lanes;   // [LMAX]
   T *x, *y, *v, *ch, *sh, *ts;  // [EPW*NS] shared road view (read by other vehicles)
+  float* xf;                     // [EPW*NS] float copy of x for the collision window prefilter (== x for f32)
   T *h, *timer, *delta, *steer, *acc, *ix, *iy;  // [EPW*NS] per-vehicle state resident in LDS
   uint8_t *kind, *flags;         // [EPW*NS] flags: 1 crashed, 2 has_impact, 4 enable_lane_change
   int8_t* sidx;                  // [EPW*NS] MDPVehicle.speed_index
@@ -229,7 +329,7 @@ template <typename T> struct View {
 };
 
 inline __host__ __device__ size_t view_bytes_t(size_t t, size_t lane_sz, int EPW, int NS, int n_lanes) {
-  size_t b = lane_sz * n_lanes + t * (13 * EPW * NS) + 3 * EPW * NS;
+  size_t b = lane_sz * n_lanes + t * (13 * EPW * NS) + 3 * EPW * NS + (t == 8 ? 4 * EPW * NS : 0);
   b = (b + 15) & ~(size_t)15;
   b += (t + 1) * (size_t)n_lanes * EPW * (NS + 1) + 2 * (size_t)n_lanes * EPW * NS;
   b = (b + 15) & ~(size_t)15;
@@ -259,6 +359,8 @@ __device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lane
   V.acc = (T*)p; p += sizeof(T) * EPW * NS;
   V.ix = (T*)p; p += sizeof(T) * EPW * NS;
   V.iy = (T*)p; p += sizeof(T) * EPW * NS;
+  if constexpr (sizeof(T) == 8) { V.xf = (float*)p; p += sizeof(float) * EPW * NS; }
+  else V.xf = (float*)V.x;
   V.kind = (uint8_t*)p; p += EPW * NS;
   V.flags = (uint8_t*)p; p += EPW * NS;
   V.sidx = (int8_t*)p; p += EPW * NS;
@@ -539,7 +641,8 @@ __device__ __forceinline__ void scan_neighbours(const View<T>& V, int le, int se
 enum { MODE_META = 1, MODE_ACT = 2, MODE_STEP = 4 };
 // Diagnostic ablation bits (ttrl_diag_simulate only; results are then NOT the reference's).
 enum { A_NO_COLL = 1, A_NO_MOBIL = 2, A_NO_ABORT = 4, A_NO_SCAN = 8, A_NO_STEER = 16, A_NO_KIN = 32,
-       A_NO_LANE = 64, A_NO_IDM = 128 };
+       A_NO_LANE = 64, A_NO_IDM = 128, A_NO_SAT = 256, A_NO_PREF = 512,
+       A_SAT_SERIAL = 1024 /* one pair per lane (sat_pair) instead of one axis per lane; same results */ };
 
 enum { FL_CRASHED = 1, FL_IMPACT = 2, FL_LC = 4 };
 
@@ -572,8 +675,10 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
     if (slot) load_veh(a, st, k);
     else { a = Veh<T>{}; a.kind = TTRL_ABSENT; a.lane = -1; a.tgt = -1; }
     present = slot && a.kind != TTRL_ABSENT;
-    V.x[me] = present ? a.x : T(FAR); V.y[me] = a.y; V.v[me] = a.v; V.ts[me] = a.ts;
-    V.ch[me] = t_cos(a.h); V.sh[me] = t_sin(a.h);
+    V.x[me] = present ? a.x : T(FAR); V.y[me] = a.y;
+    if constexpr (sizeof(T) == 8) V.xf[me] = present ? (float)a.x : FAR; V.v[me] = a.v; V.ts[me] = a.ts;
+    const SinCos<T> sc = t_sincos(a.h);
+    V.ch[me] = sc.c; V.sh[me] = sc.s;
     V.h[me] = a.h; V.timer[me] = a.timer; V.delta[me] = a.delta; V.steer[me] = a.steer; V.acc[me] = a.acc;
     V.ix[me] = a.ix; V.iy[me] = a.iy;
     V.kind[me] = (uint8_t)(present ? a.kind : TTRL_ABSENT);
@@ -783,15 +888,18 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
           x += v * V.ch[me] * dt; y += v * V.sh[me] * dt; v += acc * dt;
         } else {
           const T beta = t_atan(T(1) / T(2) * t_tan(steer));
-          const T vx = v * t_cos(h + beta), vy = v * t_sin(h + beta);
+          const SinCos<T> hb = t_sincos(h + beta);
+          const T vx = v * hb.c, vy = v * hb.s;
           x += vx * dt; y += vy * dt;
           if (fl & FL_IMPACT) { x += V.ix[me]; y += V.iy[me]; fl = (fl | FL_CRASHED) & ~FL_IMPACT; }
           h += v * t_sin(beta) / (T(P.length) / T(2)) * dt;
           v += acc * dt;
-          V.ch[me] = t_cos(h); V.sh[me] = t_sin(h);
+          const SinCos<T> sc = t_sincos(h);
+          V.ch[me] = sc.c; V.sh[me] = sc.s;
         }
         V.flags[me] = (uint8_t)fl;
         V.x[me] = x; V.y[me] = y; V.h[me] = h; V.v[me] = v;
+        if constexpr (sizeof(T) == 8) V.xf[me] = (float)x;
       }
       const int cl = project_all<T, NS, EPW>(V, P, nl, tid, le, i, present, x, y, h, !(ablate & A_NO_LANE));
       if (present && !(ablate & A_NO_LANE)) V.lane[me] = (int8_t)cl;  // on_state_update kinematics.py:170-177
@@ -815,20 +923,24 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       if (present && do_coll) {
         const T xi = V.x[me], yi = V.y[me], vi = V.v[me];
         const T thr = thr0 + vi * dt;
+        // float window: |xf_j - xf_i| in float errs by < 1.2e-7 (|x_i| + |x_j|), far below the slack
+        const float xfi = V.xf[me];
+        const float Rwf = (float)Rw * 1.0001f + 1e-5f * fabsf(xfi) + 1e-3f;
 #pragma unroll
         for (int c0 = 0; c0 < NS; c0 += CH) {
           if (c0 + CH <= i + 1) continue;  // only partners j > i
           unsigned long long m = 0;
 #pragma unroll
           for (int j1 = 0; j1 < CH; j1 += 8) {
-            T xs[8];
+            float xs[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) xs[u] = V.x[eb + c0 + j1 + u];
+            for (int u = 0; u < 8; ++u) xs[u] = V.xf[eb + c0 + j1 + u];
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-              if (!(fabs(xs[u] - xi) > Rw)) m |= 1ull << (j1 + u);
+              if (!(fabsf(xs[u] - xfi) > Rwf)) m |= 1ull << (j1 + u);
           }
           if (i >= c0) m &= ~((2ull << (i - c0)) - 1);  // keep j > i
+          if (ablate & A_NO_PREF) m = 0;
           while (m) {
             const int j = c0 + __ffsll((long long)m) - 1;
             m &= m - 1;
@@ -836,6 +948,9 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             const T d2 = dx * dx + dy * dy;
             if (d2 > (thr + T(1)) * (thr + T(1))) continue;  // far: skip the exact test
             if (sqrt(d2) > thr) continue;                     // objects.py:123-133 exact
+            if (sat_separated(P, xi, yi, V.ch[me], V.sh[me], vi, V.x[eb + j], V.y[eb + j], V.ch[eb + j], V.sh[eb + j],
+                              V.v[eb + j], dt))
+              continue;  // provably (false, false): contributes nothing
             const int q = atomicAdd(&V.pq_n[le], 1);
             if (q < NS) { V.pq[le * NS + q].i = (short)i; V.pq[le * NS + q].j = (short)j; }
           }
@@ -843,7 +958,42 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       }
       __syncthreads();
       const int npairs = do_coll ? V.pq_n[le] : 0;
-      if (npairs <= NS) {
+      if (npairs <= NS && !(ablate & (A_NO_SAT | A_SAT_SERIAL))) {
+        // Pass 2: 8 lanes per queued pair, one of the reference's 8 edge normals each (sat_axis),
+        // combined in axis order: intersecting / will_intersect = no axis separates (ballot over
+        // the lane group); translation = the first strict minimum of |distance| (min over the
+        // group, ties to the lower axis), so the result equals sat_pair's.  Groups of 8 lanes
+        // never straddle a wave or an env, and are either fully active or fully idle.
+        for (int t0 = 0; t0 < npairs * 8; t0 += NS) {
+          const int t = t0 + i;
+          if (t < npairs * 8) {
+            const int q = t >> 3, kx = t & 7;
+            PairRec<T>& r = V.pq[le * NS + q];
+            const int a = eb + r.i, b = eb + r.j;
+            T dd, dist, axx, axy;
+            sat_axis(P, kx, V.x[a], V.y[a], V.ch[a], V.sh[a], V.v[a], V.x[b], V.y[b], V.ch[b], V.sh[b], V.v[b], dt,
+                     dd, dist, axx, axy);
+            const int g0 = (tid & 63) & ~7;
+            const bool inter = ((__ballot(dd > T(0)) >> g0) & 0xffull) == 0;
+            const bool will = ((__ballot(dist > T(0)) >> g0) & 0xffull) == 0;
+            T bm = fabs(dist);
+            if (bm != bm) bm = K<T>::inf();  // abs(nan) < min_distance is false: never chosen
+            int bk = kx;
+#pragma unroll
+            for (int off = 1; off < 8; off <<= 1) {
+              const T om = __shfl_xor(bm, off, 8);
+              const int ok = __shfl_xor(bk, off, 8);
+              const T ox = __shfl_xor(axx, off, 8), oy = __shfl_xor(axy, off, 8);
+              if (om < bm || (om == bm && ok < bk)) { bm = om; bk = ok; axx = ox; axy = oy; }
+            }
+            if (kx == 0) {
+              r.tx = will ? bm * axx : T(0);
+              r.ty = will ? bm * axy : T(0);
+              r.res = (inter ? 1 : 0) | (will ? 2 : 0);
+            }
+          }
+        }
+      } else if (npairs <= NS && !(ablate & A_NO_SAT)) {
         for (int q = i; q < npairs; q += NS) {
           PairRec<T>& r = V.pq[le * NS + q];
           const int a = eb + r.i, b = eb + r.j;
@@ -885,6 +1035,9 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             bool inter, will;
             T tx, ty;
             const T ci = V.ch[me], si = V.sh[me], cj = V.ch[eb + j], sj = V.sh[eb + j];
+            if (lo ? sat_separated(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt)
+                   : sat_separated(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt))
+              continue;
             if (lo) sat_pair_ool(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt, inter, will, tx, ty);
             else sat_pair_ool(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt, inter, will, tx, ty);
             if (will) {
