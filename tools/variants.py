@@ -12,6 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "_variants")
 VARIANTS = {"head": [], "cur": []}  # committed kernel vs working tree, tuned defaults
+TIMING = {"timing": ["-DTTRL_PHASE_TIMING"]}  # built, not timed: tools/phases.py
 if os.environ.get("WAVE_VARIANTS"):
     VARIANTS.update({f"w{w}": [f"-DTTRL_SIM_WAVES={w}"] for w in (2, 3, 4, 5, 6)})
 for arg in os.environ.get("EXTRA_VARIANTS", "").split(";"):
@@ -28,7 +29,7 @@ def build():
     with open(head, "w") as f:
         f.write(subprocess.run(["git", "-C", ROOT, "show", "HEAD:topotrafficrl_amd/csrc/ttrl_mi355x.hip"],
                                check=True, capture_output=True, text=True).stdout)
-    for name, flags in VARIANTS.items():
+    for name, flags in {**VARIANTS, **TIMING}.items():
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
                "-shared", "-I", os.path.join(ROOT, "include"), *flags, "-o", os.path.join(OUT, f"lib_{name}.so"),
                head if name.startswith("head") else src]

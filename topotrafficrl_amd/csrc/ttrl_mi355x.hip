@@ -23,15 +23,26 @@ namespace {
 // log/exp) are register-hungry; inlined at every call site they force spills of the
 // resident vehicle state.  Out of line, the fused kernel fits its register budget with no
 // scratch; the call overhead is paid ~10 times per vehicle-frame.
-__device__ __noinline__ double t_sin(double x) { return ::sin(x); }
-__device__ __noinline__ double t_cos(double x) { return ::cos(x); }
-__device__ __noinline__ double t_tan(double x) { return ::tan(x); }
-__device__ __noinline__ double t_atan(double x) { return ::atan(x); }
-__device__ __noinline__ double t_asin(double x) { return ::asin(x); }
-__device__ __noinline__ double t_pow(double x, double y) { return ::pow(x, y); }
+#ifdef TTRL_INLINE_TRANSC
+#define TTRL_TRANSC __forceinline__
+#else
+#define TTRL_TRANSC __noinline__
+#endif
+__device__ TTRL_TRANSC double t_sin(double x) { return ::sin(x); }
+__device__ TTRL_TRANSC double t_cos(double x) { return ::cos(x); }
+__device__ TTRL_TRANSC double t_tan(double x) { return ::tan(x); }
+__device__ TTRL_TRANSC double t_atan(double x) { return ::atan(x); }
+__device__ TTRL_TRANSC double t_asin(double x) { return ::asin(x); }
+// pow(x, y) for x >= 0, y > 0 (IDM's (v / v0)^DELTA): exp(y log x) is within ~|y log x| ulp of
+// the correctly rounded power (far inside the stated tolerances) at half of ocml pow's cost.
+#ifdef TTRL_POW_LIBM
+__device__ TTRL_TRANSC double t_pow(double x, double y) { return ::pow(x, y); }
+#else
+__device__ TTRL_TRANSC double t_pow(double x, double y) { return ::exp(y * ::log(x)); }
+#endif
 template <typename T> struct SinCos { T s, c; };
 // one shared argument reduction; ocml's sincos returns the same values as sin and cos
-__device__ __noinline__ SinCos<double> t_sincos(double x) {
+__device__ TTRL_TRANSC SinCos<double> t_sincos(double x) {
   SinCos<double> r;
   ::sincos(x, &r.s, &r.c);
   return r;
@@ -118,8 +129,10 @@ __device__ __forceinline__ T steering_control(const LaneT<T>& L, const ttrl_para
   const T hcmd = t_asin(clip(lat_cmd / not_zero(v), T(-1), T(1)));
   const T href = lfh + clip(hcmd, -Tpi<T>() / T(4), Tpi<T>() / T(4));
   const T hrate = T(P.kp_heading) * wrap_to_pi(href - h);
-  const T slip = t_asin(clip(T(P.length) / T(2) / not_zero(v) * hrate, T(-1), T(1)));
-  const T st = t_atan(T(2) * t_tan(slip));
+  // slip = asin(c); tan(slip) = c / sqrt((1 - c)(1 + c)) (= +-inf at |c| = 1, where the
+  // reference's tan(+-pi/2) = +-1.6e16 and atan of either is +-pi/2): one call instead of two
+  const T c = clip(T(P.length) / T(2) / not_zero(v) * hrate, T(-1), T(1));
+  const T st = t_atan(T(2) * (c / sqrt((T(1) - c) * (T(1) + c))));
   return clip(st, -T(P.max_steering), T(P.max_steering));
 }
 
@@ -314,13 +327,18 @@ template <typename T> struct View {
   T *x, *y, *v, *ch, *sh, *ts;  // [EPW*NS] shared road view (read by other vehicles)
   float* xf;                     // [EPW*NS] float copy of x for the collision window prefilter (== x for f32)
   T *h, *timer, *delta, *steer, *acc, *ix, *iy;  // [EPW*NS] per-vehicle state resident in LDS
+  T* afree;                      // [EPW*NS] IDM free-road term of the frame (MOBIL items read it)
   uint8_t *kind, *flags;         // [EPW*NS] flags: 1 crashed, 2 has_impact, 4 enable_lane_change
   int8_t* sidx;                  // [EPW*NS] MDPVehicle.speed_index
   T* key;            // [n_lanes][EPW][NS+1] s of the vehicles on each lane (AbstractLane.on_lane margin 1)
   uint8_t* idx;      // [n_lanes][EPW][NS+1] their slots, slot order
   short* mypos;      // [n_lanes][EPW*NS] each vehicle's position in the list, -1 if not on the lane
+  short *f0, *r0, *ft;  // [EPW*NS] own-lane front / rear, target-lane front of the frame (-1 none)
+  short* mob;        // [2][EPW*NS] MOBIL verdict per side: -2 refused, else the new front (-1 none)
+  short* item;       // [EPW][2*NS] MOBIL work items: slot | side << 15
   int* cnt;          // [EPW][LMAX+1] list lengths; [LMAX] = longest list of the env
   int* wcnt;         // [LMAX][4] per-wave list lengths (NS > 64)
+  int* nitem;        // [EPW] MOBIL items queued this frame
   int8_t *lane, *tgt;            // [EPW*NS] lane (-1 absent), target (old, for the act phase)
   unsigned long long* bal;       // [2][8] cross-wave ballots (NS > 64)
   T* red;                        // [8] cross-wave reduction scratch
@@ -328,64 +346,86 @@ template <typename T> struct View {
   int* pq_n;                     // [EPW] queue lengths (> NS: overflow)
 };
 
-inline __host__ __device__ size_t view_bytes_t(size_t t, size_t lane_sz, int EPW, int NS, int n_lanes) {
-  size_t b = lane_sz * n_lanes + t * (13 * EPW * NS) + 3 * EPW * NS + (t == 8 ? 4 * EPW * NS : 0);
-  b = (b + 15) & ~(size_t)15;
-  b += (t + 1) * (size_t)n_lanes * EPW * (NS + 1) + 2 * (size_t)n_lanes * EPW * NS;
-  b = (b + 15) & ~(size_t)15;
-  b += sizeof(int) * (EPW * (LMAX + 1) + LMAX * 4);
-  b += 2 * EPW * NS;
-  b = (b + 15) & ~(size_t)15;
-  b += 16 * sizeof(unsigned long long) + 8 * t;
-  b = (b + 15) & ~(size_t)15;
-  return b + (2 * t + 8) * EPW * NS + 4 * EPW + 16;
-}
+// Byte offsets of the view's arrays in the dynamic LDS block (host: sizing; device: carve).
+struct ViewLayout {
+  size_t lanes, reals[14], xf, key, pq, red, bal, cnt, wcnt, nitem, pq_n, mypos, f0, r0, ft, mob, item, idx, kind,
+      flags, sidx, lane, tgt, total;
+};
 
 template <typename T>
+__host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes) {
+  ViewLayout o{};
+  size_t p = 0;
+  const size_t M = (size_t)EPW * NS;
+  auto take = [&](size_t bytes, size_t align) {
+    p = (p + align - 1) & ~(align - 1);
+    const size_t r = p;
+    p += bytes;
+    return r;
+  };
+  o.lanes = take(sizeof(LaneT<T>) * n_lanes, 16);
+  for (int k = 0; k < 14; ++k) o.reals[k] = take(sizeof(T) * M, 16);
+  o.xf = sizeof(T) == 8 ? take(sizeof(float) * M, 16) : o.reals[0];
+  o.key = take(sizeof(T) * (size_t)n_lanes * EPW * (NS + 1), 16);
+  o.pq = take(sizeof(PairRec<T>) * M, 16);
+  o.red = take(8 * sizeof(T), 16);
+  o.bal = take(16 * sizeof(unsigned long long), 16);
+  o.cnt = take(sizeof(int) * EPW * (LMAX + 1), 4);
+  o.wcnt = take(sizeof(int) * LMAX * 4, 4);
+  o.nitem = take(sizeof(int) * EPW, 4);
+  o.pq_n = take(sizeof(int) * EPW, 4);
+  o.mypos = take(sizeof(short) * (size_t)n_lanes * M, 4);
+  o.f0 = take(sizeof(short) * M, 4);
+  o.r0 = take(sizeof(short) * M, 4);
+  o.ft = take(sizeof(short) * M, 4);
+  o.mob = take(sizeof(short) * 2 * M, 4);
+  o.item = take(sizeof(short) * 2 * M, 4);
+  o.idx = take((size_t)n_lanes * EPW * (NS + 1), 4);
+  o.kind = take(M, 4);
+  o.flags = take(M, 4);
+  o.sidx = take(M, 4);
+  o.lane = take(M, 4);
+  o.tgt = take(M, 4);
+  o.total = take(0, 16);
+  return o;
+}
+
+// Pointer arithmetic stays on the __shared__ base, so every access is a ds_* instruction
+// with a 32-bit LDS address.
+template <typename T>
 __device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lanes) {
+  const ViewLayout o = view_layout<T>(EPW, NS, n_lanes);
   View<T> V;
-  char* p = smem;
-  V.lanes = (LaneT<T>*)p; p += sizeof(LaneT<T>) * n_lanes;
-  V.x = (T*)p; p += sizeof(T) * EPW * NS;
-  V.y = (T*)p; p += sizeof(T) * EPW * NS;
-  V.v = (T*)p; p += sizeof(T) * EPW * NS;
-  V.ch = (T*)p; p += sizeof(T) * EPW * NS;
-  V.sh = (T*)p; p += sizeof(T) * EPW * NS;
-  V.ts = (T*)p; p += sizeof(T) * EPW * NS;
-  V.h = (T*)p; p += sizeof(T) * EPW * NS;
-  V.timer = (T*)p; p += sizeof(T) * EPW * NS;
-  V.delta = (T*)p; p += sizeof(T) * EPW * NS;
-  V.steer = (T*)p; p += sizeof(T) * EPW * NS;
-  V.acc = (T*)p; p += sizeof(T) * EPW * NS;
-  V.ix = (T*)p; p += sizeof(T) * EPW * NS;
-  V.iy = (T*)p; p += sizeof(T) * EPW * NS;
-  if constexpr (sizeof(T) == 8) { V.xf = (float*)p; p += sizeof(float) * EPW * NS; }
-  else V.xf = (float*)V.x;
-  V.kind = (uint8_t*)p; p += EPW * NS;
-  V.flags = (uint8_t*)p; p += EPW * NS;
-  V.sidx = (int8_t*)p; p += EPW * NS;
-  p = (char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
-  V.key = (T*)p; p += sizeof(T) * (size_t)n_lanes * EPW * (NS + 1);
-  V.mypos = (short*)p; p += sizeof(short) * (size_t)n_lanes * EPW * NS;
-  V.idx = (uint8_t*)p; p += (size_t)n_lanes * EPW * (NS + 1);
-  p = (char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
-  V.cnt = (int*)p; p += sizeof(int) * EPW * (LMAX + 1);
-  V.wcnt = (int*)p; p += sizeof(int) * LMAX * 4;
-  V.lane = (int8_t*)p; p += EPW * NS;
-  V.tgt = (int8_t*)p; p += EPW * NS;
-  p = (char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
-  V.bal = (unsigned long long*)p; p += 16 * sizeof(unsigned long long);
-  V.red = (T*)p; p += 8 * sizeof(T);
-  p = (char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
-  V.pq = (PairRec<T>*)p; p += sizeof(PairRec<T>) * EPW * NS;
-  V.pq_n = (int*)p;
+  V.lanes = (LaneT<T>*)(smem + o.lanes);
+  T** reals[] = {&V.x, &V.y, &V.v, &V.ch, &V.sh, &V.ts, &V.h, &V.timer, &V.delta, &V.steer, &V.acc,
+                 &V.ix, &V.iy, &V.afree};
+  for (int k = 0; k < 14; ++k) *reals[k] = (T*)(smem + o.reals[k]);
+  V.xf = (float*)(smem + o.xf);
+  V.key = (T*)(smem + o.key);
+  V.pq = (PairRec<T>*)(smem + o.pq);
+  V.red = (T*)(smem + o.red);
+  V.bal = (unsigned long long*)(smem + o.bal);
+  V.cnt = (int*)(smem + o.cnt);
+  V.wcnt = (int*)(smem + o.wcnt);
+  V.nitem = (int*)(smem + o.nitem);
+  V.pq_n = (int*)(smem + o.pq_n);
+  V.mypos = (short*)(smem + o.mypos);
+  V.f0 = (short*)(smem + o.f0);
+  V.r0 = (short*)(smem + o.r0);
+  V.ft = (short*)(smem + o.ft);
+  V.mob = (short*)(smem + o.mob);
+  V.item = (short*)(smem + o.item);
+  V.idx = (uint8_t*)(smem + o.idx);
+  V.kind = (uint8_t*)(smem + o.kind);
+  V.flags = (uint8_t*)(smem + o.flags);
+  V.sidx = (int8_t*)(smem + o.sidx);
+  V.lane = (int8_t*)(smem + o.lane);
+  V.tgt = (int8_t*)(smem + o.tgt);
   return V;
 }
 
 size_t host_view_bytes(int dtype, int EPW, int NS, int n_lanes) {
-  return dtype == TTRL_F64
-             ? view_bytes_t(8, sizeof(LaneT<double>), EPW, NS, n_lanes)
-             : view_bytes_t(4, sizeof(LaneT<float>), EPW, NS, n_lanes);
+  return dtype == TTRL_F64 ? view_layout<double>(EPW, NS, n_lanes).total : view_layout<float>(EPW, NS, n_lanes).total;
 }
 
 template <typename T>
@@ -595,7 +635,9 @@ __device__ __forceinline__ T idm_acc(const View<T>& V, const ttrl_params_t& P, i
 // One pass answering up to 3 Road.neighbour_vehicles queries per thread (road.py:480-513)
 // over the compacted per-lane candidate lists: front = min s_v >= s (ties: later slot),
 // rear = max s_v < s (ties: earlier slot), visiting candidates in slot (= list) order.
-template <typename T, int NQ, int NS, int EPW>
+// Bit q of RM asks for query q's rear (the caller may need only fronts).  The updates are
+// selects, so the loop body is straight-line code.
+template <typename T, int NQ, int NS, int EPW, unsigned RM = 7u>
 __device__ __forceinline__ void scan_neighbours(const View<T>& V, int le, int self, const int (&ql)[NQ],
                                                 const T (&s)[NQ], int (&f)[NQ], int (&r)[NQ]) {
   constexpr int NSP = NS + 1;
@@ -624,9 +666,16 @@ __device__ __forceinline__ void scan_neighbours(const View<T>& V, int le, int se
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
         const int kk = k0 + u;
+        const T x = sv[q][u];
         const bool ok = kk < n[q] && kk != me[q];
-        if (ok && s[q] <= sv[q][u] && sv[q][u] <= sf[q]) { sf[q] = sv[q][u]; fp[q] = kk; }
-        if (ok && sv[q][u] < s[q] && sv[q][u] > sr[q]) { sr[q] = sv[q][u]; rp[q] = kk; }
+        const bool uf = ok && s[q] <= x && x <= sf[q];
+        sf[q] = uf ? x : sf[q];
+        fp[q] = uf ? kk : fp[q];
+        if (RM & (1u << q)) {
+          const bool ur = ok && x < s[q] && x > sr[q];
+          sr[q] = ur ? x : sr[q];
+          rp[q] = ur ? kk : rp[q];
+        }
       }
     }
   }
@@ -645,6 +694,28 @@ enum { A_NO_COLL = 1, A_NO_MOBIL = 2, A_NO_ABORT = 4, A_NO_SCAN = 8, A_NO_STEER 
        A_SAT_SERIAL = 1024 /* one pair per lane (sat_pair) instead of one axis per lane; same results */ };
 
 enum { FL_CRASHED = 1, FL_IMPACT = 2, FL_LC = 4 };
+
+// Diagnostic build only (-DTTRL_PHASE_TIMING): per-phase shader-clock cycles of every wave,
+// summed into g_phase (tools/phases.py).  The production kernel carries no stamps.
+#ifdef TTRL_PHASE_TIMING
+__device__ unsigned long long g_phase[20];
+#define PH_INIT                                    \
+  unsigned long long ph_acc[20] = {};              \
+  unsigned long long ph_t = __builtin_readcyclecounter();
+#define PH(k)                                               \
+  do {                                                      \
+    const unsigned long long ph_n = __builtin_readcyclecounter(); \
+    ph_acc[k] += ph_n - ph_t;                               \
+    ph_t = ph_n;                                            \
+  } while (0)
+#define PH_FLUSH                                                       \
+  if ((threadIdx.x & 63) == 0)                                         \
+    for (int ph_k = 0; ph_k < 20; ++ph_k) atomicAdd(&g_phase[ph_k], ph_acc[ph_k]);
+#else
+#define PH_INIT
+#define PH(k)
+#define PH_FLUSH
+#endif
 
 // Fused frame loop.  EPW envs per workgroup, NS slots per env, blockDim = EPW*NS.  The whole
 // vehicle state of the workgroup's envs is resident in LDS for the launch (HBM is read once
@@ -666,6 +737,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   const int me = le * NS + i;  // this vehicle's LDS slot
   const int eb = le * NS;      // env base in the LDS view
   View<T> V = carve<T>(smem, EPW, NS, nl);
+  PH_INIT
   stage_lanes(V, R, tid);
   const T dt = T(dt_d);
 
@@ -687,10 +759,13 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
     V.lane[me] = (int8_t)(present ? a.lane : -1);
     V.tgt[me] = (int8_t)(present ? a.tgt : -1);
   }
+  PH(15);
+  if (i == 0) V.nitem[le] = 0;
   __syncthreads();  // lane table + view staged
   project_all<T, NS, EPW>(V, P, nl, tid, le, i, present, V.x[me], V.y[me], T(0), false);
   const int kind = V.kind[me];
 
+  PH(11);
   for (int frame = 0; frame < frames; ++frame) {
     // ---------------- ego meta-action (DiscreteMetaAction.act, action.py:259-260) ----
     if ((mode & MODE_META) && frame == 0 && actions && present && kind == TTRL_MDP) {
@@ -716,80 +791,163 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       V.tgt[me] = (int8_t)tgt;
     }
     __syncthreads();
+    PH(0);
 
     // ---------------- Road.act (road.py:461-464) ----------------
     int tgt_new = V.tgt[me];
     if (mode & MODE_ACT) {
+      const bool polite = P.politeness != 0.0;
+      {  // (1) per vehicle: lane-change timer, own-lane (+ target-lane) neighbours, IDM free
+         //     term, MOBIL work items; results go to LDS so nothing stays live across (2)
+        const int lane = V.lane[me], tgt = V.tgt[me];
+        const int fl = V.flags[me];
+        const bool idm = present && kind == TTRL_IDM && !(fl & FL_CRASHED);
+        const bool lc = (fl & FL_LC) != 0;
+        const bool changing = idm && lane != tgt;
+        const T x = V.x[me], y = V.y[me], v = V.v[me];
+        bool fire = false;
+        if (idm && lc && !changing && T(P.lane_change_delay) < V.timer[me] && !(ablate & A_NO_MOBIL)) {
+          fire = true;  // utils.do_every
+          V.timer[me] = T(0);
+        }
+        // side lanes (RoadNetwork.side_lanes road.py:200-211), gated as behavior.py:252-260
+        bool left = false, right = false;
+        if (fire) {
+          const bool moving = !(fabs(v) < T(1));
+          left = lane > 0 && moving && reachable(V.lanes[lane - 1], T(P.lane_vehicle_length), x, y);
+          right = lane < nl - 1 && moving && reachable(V.lanes[lane + 1], T(P.lane_vehicle_length), x, y);
+        }
+        // Queries of every vehicle: the own lane's front (its rear only feeds MOBIL's politeness
+        // term) and, while changing lane, the target lane's front (IDMVehicle.act behavior.py:118-131).
+        const int ql[2] = {idm ? lane : -1, changing ? tgt : -1};
+        T s2[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          T rr;
+          lane_local(V.lanes[ql[q] < 0 ? 0 : ql[q]], x, y, s2[q], rr);
+        }
+        int f2[2] = {-1, -1}, r2[2] = {-1, -1};
+        PH(1);
+        if (!(ablate & A_NO_SCAN)) {
+          if (__any(ql[1] >= 0)) {
+            if (polite) scan_neighbours<T, 2, NS, EPW, 1u>(V, le, i, ql, s2, f2, r2);
+            else scan_neighbours<T, 2, NS, EPW, 0u>(V, le, i, ql, s2, f2, r2);
+          } else {
+            const int ql1[1] = {ql[0]};
+            const T s1[1] = {s2[0]};
+            int f1[1], r1[1];
+            if (polite) scan_neighbours<T, 1, NS, EPW, 1u>(V, le, i, ql1, s1, f1, r1);
+            else scan_neighbours<T, 1, NS, EPW, 0u>(V, le, i, ql1, s1, f1, r1);
+            f2[0] = f1[0]; r2[0] = r1[0];
+          }
+        }
+        PH(2);
+        T a_free = T(0);
+        if (idm && !(ablate & A_NO_IDM)) a_free = idm_free(P, v, V.ts[me], V.lanes[lane].lim, V.delta[me]);
+        PH(12);
+        V.afree[me] = a_free;
+        V.f0[me] = (short)f2[0];
+        V.r0[me] = (short)r2[0];
+        V.ft[me] = (short)f2[1];
+        V.mob[me] = -3;            // -3: no item for this side
+        V.mob[EPW * NS + me] = -3;
+        // MOBIL (IDMVehicle.mobil behavior.py:265-324, route None) as work items, one per
+        // (firing vehicle, candidate side lane): a frame has a handful of firing vehicles, so
+        // the side-lane queries and IDM terms of all of them cost one pass.
+        if (left) V.item[le * 2 * NS + atomicAdd(&V.nitem[le], 1)] = (short)i;
+        if (right) V.item[le * 2 * NS + atomicAdd(&V.nitem[le], 1)] = (short)(i | 0x4000);
+      }
+      __syncthreads();
+      PH(13);
+      {  // (2) MOBIL items
+        const int nitem = V.nitem[le];
+        // G lanes per item: each scans every G-th candidate of the side lane's list, the group
+        // combines (front: min s, ties to the later position; rear: max s, ties to the earlier),
+        // then lanes 0-2 of the group evaluate the three IDM interaction terms side by side.
+        constexpr int G = 8, IPP = NS / G;
+        const int g = i % G;
+        for (int t0 = 0; t0 < nitem; t0 += IPP) {
+          const int t = t0 + i / G;
+          if (t < nitem) {  // whole groups are active or idle together
+            const int it = V.item[le * 2 * NS + t];
+            const int side = it >> 14, vi = it & 0x3fff, ve = eb + vi;
+            const int ln = V.lane[ve] + (side ? 1 : -1);
+            T sq, rr;
+            lane_local(V.lanes[ln], V.x[ve], V.y[ve], sq, rr);
+            T sf = K<T>::inf(), sr = -K<T>::inf();
+            int fp = -1, rp = -1;
+            const size_t rowb = ((size_t)ln * EPW + le) * (NS + 1);
+            if (!(ablate & A_NO_SCAN)) {
+              const T* row = V.key + rowb;
+              const int n = V.cnt[le * (LMAX + 1) + ln];
+              const int mep = V.mypos[(size_t)ln * EPW * NS + le * NS + vi];  // the item's vehicle is skipped
+              for (int kk = g; kk < n; kk += G) {
+                const T xk = row[kk];
+                const bool uf = kk != mep && sq <= xk && xk <= sf;
+                sf = uf ? xk : sf;
+                fp = uf ? kk : fp;
+                const bool ur = kk != mep && xk < sq && xk > sr;
+                sr = ur ? xk : sr;
+                rp = ur ? kk : rp;
+              }
+  #pragma unroll
+              for (int off = 1; off < G; off <<= 1) {
+                const T osf = __shfl_xor(sf, off, G), osr = __shfl_xor(sr, off, G);
+                const int ofp = __shfl_xor(fp, off, G), orp = __shfl_xor(rp, off, G);
+                if (osf < sf || (osf == sf && ofp > fp)) { sf = osf; fp = ofp; }
+                if (osr > sr || (osr == sr && orp >= 0 && (rp < 0 || orp < rp))) { sr = osr; rp = orp; }
+              }
+            }
+            const int np_ = fp >= 0 ? (int)V.idx[rowb + fp] : -1, nf = rp >= 0 ? (int)V.idx[rowb + rp] : -1;
+            const int op = V.f0[ve], of = V.r0[ve];
+            const T delta = V.delta[ve];
+            // IDM_self(new follower, front = self), a(self | new front), a(self | old front): DELTA is the caller's
+            const int e_ = g == 0 ? nf : (g <= 2 ? vi : -1);
+            const int f_ = g == 0 ? vi : (g == 1 ? np_ : op);
+            T term = T(0);
+            if (e_ >= 0 && f_ >= 0) term = idm_interact(V, P, eb, e_, f_);
+            T fr = T(0);
+            if (g == 0 && nf >= 0) fr = idm_free(P, V.v[eb + nf], V.ts[eb + nf], V.lanes[V.lane[eb + nf]].lim, delta);
+            const T t_np = __shfl_xor(term, 1, G), t_op = __shfl_xor(term, 2, G);
+            if (g == 0) {
+              const T af = V.afree[ve];
+              const T nfpa = nf >= 0 ? fr - term : T(0);
+              bool ok = !(nfpa < -T(P.lane_change_max_braking));
+              if (ok) {
+                T spa = af, sa = af;
+                if (np_ >= 0) spa -= t_np;
+                if (op >= 0) sa -= t_op;
+                T jerk;
+                if (polite) {
+                  const T nfa = idm_acc(V, P, eb, nf, np_, delta);
+                  const T ofa = idm_acc(V, P, eb, of, vi, delta);
+                  const T ofpa = idm_acc(V, P, eb, of, op, delta);
+                  jerk = spa - sa + T(P.politeness) * (nfpa - nfa + ofpa - ofa);
+                } else {
+                  jerk = spa - sa + T(P.politeness) * T(0);
+                }
+                if (jerk < T(P.lane_change_min_acc_gain)) ok = false;
+              }
+              V.mob[side * EPW * NS + ve] = (short)(ok ? np_ : -2);
+            }
+          }
+        }
+      }
+      PH(14);
+      __syncthreads();
+      if (i == 0) V.nitem[le] = 0;
+      // (3) per vehicle: MOBIL verdicts, lane-change abort, steering and IDM acceleration
       const int lane = V.lane[me], tgt = V.tgt[me];
       const int fl = V.flags[me];
       const bool idm = present && kind == TTRL_IDM && !(fl & FL_CRASHED);
-      const bool lc = (fl & FL_LC) != 0;
       const bool changing = idm && lane != tgt;
-      const bool abort_cand = changing && lc;
+      const bool abort_cand = changing && (fl & FL_LC) != 0;
       const T x = V.x[me], y = V.y[me], v = V.v[me];
-      bool fire = false;
-      if (idm && lc && !changing && T(P.lane_change_delay) < V.timer[me] && !(ablate & A_NO_MOBIL)) {
-        fire = true;  // utils.do_every
-        V.timer[me] = T(0);
-      }
-      // side lanes (RoadNetwork.side_lanes road.py:200-211), gated as behavior.py:252-260
-      int left = -1, right = -1;
-      if (fire) {
-        const bool moving = !(fabs(v) < T(1));
-        if (lane > 0 && moving && reachable(V.lanes[lane - 1], T(P.lane_vehicle_length), x, y)) left = lane - 1;
-        if (lane < nl - 1 && moving && reachable(V.lanes[lane + 1], T(P.lane_vehicle_length), x, y)) right = lane + 1;
-      }
-      int ql[3] = {idm ? lane : -1, changing ? tgt : left, right};
-      T s3[3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        T rr;
-        lane_local(V.lanes[ql[q] < 0 ? 0 : ql[q]], x, y, s3[q], rr);
-      }
-      int f3[3], r3[3];
-      if (ablate & A_NO_SCAN) {
-        f3[0] = f3[1] = f3[2] = r3[0] = r3[1] = r3[2] = -1;
-      } else if (__any(ql[1] >= 0 || ql[2] >= 0)) {
-        scan_neighbours<T, 3, NS, EPW>(V, le, i, ql, s3, f3, r3);
-      } else {
-        int ql1[1] = {ql[0]};
-        T s1[1] = {s3[0]};
-        int f1[1], r1[1];
-        scan_neighbours<T, 1, NS, EPW>(V, le, i, ql1, s1, f1, r1);
-        f3[0] = f1[0]; r3[0] = r1[0]; f3[1] = f3[2] = r3[1] = r3[2] = -1;
-      }
-
-      // MOBIL (IDMVehicle.mobil behavior.py:265-324, route None); DELTA is ours.
-      T a_free = T(0);
-      const T delta = V.delta[me];
-      if (idm && !(ablate & A_NO_IDM)) a_free = idm_free(P, v, V.ts[me], V.lanes[lane].lim, delta);
-      if (fire) {
-#pragma unroll
-        for (int side = 1; side <= 2; ++side) {
-          if (ql[side] < 0) continue;
-          const int np_ = f3[side], nf = r3[side];
-          const int op = f3[0], of = r3[0];
-          T nfpa = T(0);
-          if (nf >= 0) nfpa = idm_free(P, V.v[eb + nf], V.ts[eb + nf], V.lanes[V.lane[eb + nf]].lim, delta)
-                               - idm_interact(V, P, eb, nf, i);
-          if (nfpa < -T(P.lane_change_max_braking)) continue;
-          T spa = a_free, sa = a_free;
-          if (np_ >= 0) spa -= idm_interact(V, P, eb, i, np_);
-          if (op >= 0) sa -= idm_interact(V, P, eb, i, op);
-          T jerk;
-          if (P.politeness != 0.0) {
-            const T nfa = idm_acc(V, P, eb, nf, np_, delta);
-            const T ofa = idm_acc(V, P, eb, of, i, delta);
-            const T ofpa = idm_acc(V, P, eb, of, op, delta);
-            jerk = spa - sa + T(P.politeness) * (nfpa - nfa + ofpa - ofa);
-          } else {
-            jerk = spa - sa + T(P.politeness) * T(0);
-          }
-          if (jerk < T(P.lane_change_min_acc_gain)) continue;
-          tgt_new = ql[side];
-        }
-      }
-
+      int side_front = -1;  // front on the lane MOBIL chose (left first, a later candidate overrides)
+      const int mobl = V.mob[me], mobr = V.mob[EPW * NS + me];
+      if (mobl >= -1) { tgt_new = lane - 1; side_front = mobl; }
+      if (mobr >= -1) { tgt_new = lane + 1; side_front = mobr; }
+      PH(3);
       // Lane-change abort in list order (behavior.py:229-244): vehicle i aborts if some
       // v != i with v.lane != T_i and v.target == T_i (v's target as of its own turn:
       // final for v < i, previous for v > i) is 0 < d(i->v) < d*(i, v).
@@ -849,13 +1007,16 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         }
       }
 
+      PH(4);
       // steering + IDM longitudinal (behavior.py:109-135); ego: ControlledVehicle.act (controller.py:126-133)
       if (idm) {
         V.steer[me] = (ablate & A_NO_STEER) ? T(0) : steering_control(V.lanes[tgt_new], P, x, y, V.h[me], v);
+        const T a_free = V.afree[me];
+        const int f0 = V.f0[me];
         T acc = a_free;
-        if (f3[0] >= 0) acc -= idm_interact(V, P, eb, i, f3[0]);
+        if (f0 >= 0) acc -= idm_interact(V, P, eb, i, f0);
         if (lane != tgt_new) {
-          const int ft = tgt_new == tgt ? f3[1] : (tgt_new == ql[1] ? f3[1] : f3[2]);
+          const int ft = tgt_new == tgt ? (int)V.ft[me] : side_front;
           T a2 = a_free;
           if (ft >= 0) a2 -= idm_interact(V, P, eb, i, ft);
           if (a2 < acc) acc = a2;
@@ -868,6 +1029,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
     }
 
     __syncthreads();  // act-phase readers of the old view are done
+    PH(5);
     if (mode & MODE_ACT) V.tgt[me] = (int8_t)(present ? tgt_new : -1);
 
     // ---------------- Road.step(dt) (road.py:466-478) ----------------
@@ -887,12 +1049,13 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         if (ablate & A_NO_KIN) {
           x += v * V.ch[me] * dt; y += v * V.sh[me] * dt; v += acc * dt;
         } else {
-          const T beta = t_atan(T(1) / T(2) * t_tan(steer));
+          const T tb = T(1) / T(2) * t_tan(steer);
+          const T beta = t_atan(tb);
           const SinCos<T> hb = t_sincos(h + beta);
           const T vx = v * hb.c, vy = v * hb.s;
           x += vx * dt; y += vy * dt;
           if (fl & FL_IMPACT) { x += V.ix[me]; y += V.iy[me]; fl = (fl | FL_CRASHED) & ~FL_IMPACT; }
-          h += v * t_sin(beta) / (T(P.length) / T(2)) * dt;
+          h += v * (tb / sqrt(T(1) + tb * tb)) / (T(P.length) / T(2)) * dt;  // sin(atan(tb))
           v += acc * dt;
           const SinCos<T> sc = t_sincos(h);
           V.ch[me] = sc.c; V.sh[me] = sc.s;
@@ -901,10 +1064,12 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         V.x[me] = x; V.y[me] = y; V.h[me] = h; V.v[me] = v;
         if constexpr (sizeof(T) == 8) V.xf[me] = (float)x;
       }
+      PH(6);
       const int cl = project_all<T, NS, EPW>(V, P, nl, tid, le, i, present, x, y, h, !(ablate & A_NO_LANE));
       if (present && !(ablate & A_NO_LANE)) V.lane[me] = (int8_t)cl;  // on_state_update kinematics.py:170-177
       if (i == 0) V.pq_n[le] = 0;
       __syncthreads();
+      PH(7);
 
       // collisions for all pairs (road.py:474-476, objects.py:91-137), impact: last writer.
       // Pass 1 (pipelined LDS loads): 1-D prefilter |dx| <= R, with R >= every pair's
@@ -957,6 +1122,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         }
       }
       __syncthreads();
+      PH(8);
       const int npairs = do_coll ? V.pq_n[le] : 0;
       if (npairs <= NS && !(ablate & (A_NO_SAT | A_SAT_SERIAL))) {
         // Pass 2: 8 lanes per queued pair, one of the reference's 8 edge normals each (sat_axis),
@@ -1005,6 +1171,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         }
       }
       __syncthreads();
+      PH(9);
       if (present && do_coll && npairs > 0) {
         bool crash = false;
         int best_gt = -1, best_lt = -1;
@@ -1054,6 +1221,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         V.flags[me] = (uint8_t)fl;
       }
     }
+    PH(10);
   }
   __syncthreads();
   if (slot) {  // LDS -> HBM, once per launch
@@ -1068,6 +1236,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
     }
     store_veh(a, st, k);
   }
+  PH(16);
+  PH_FLUSH
 }
 
 // Road.neighbour_vehicles for an explicit query lane per vehicle (road.py:480-513).
@@ -1621,6 +1791,15 @@ int ttrl_diag_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road, con
                        const int32_t* actions, int32_t frames, double dt, int32_t ablate, void* stream) {
   return run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream, ablate);
 }
+
+#ifdef TTRL_PHASE_TIMING
+// Diagnostic build only: read and clear the per-phase cycle sums (12 u64).
+int ttrl_diag_phase_read(unsigned long long* out) {
+  unsigned long long z[20] = {};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 20) != hipSuccess) return TTRL_E_LAUNCH;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) == hipSuccess ? TTRL_OK : TTRL_E_LAUNCH;
+}
+#endif
 
 int ttrl_neighbours(const ttrl_state_t* s, const ttrl_lane_table_t* road, const int32_t* query_lane,
                     int32_t* front, int32_t* rear, void* stream) {
