@@ -341,14 +341,13 @@ template <typename T> struct View {
   int* nitem;        // [EPW] MOBIL items queued this frame
   int8_t *lane, *tgt;            // [EPW*NS] lane (-1 absent), target (old, for the act phase)
   unsigned long long* bal;       // [2][8] cross-wave ballots (NS > 64)
-  T* red;                        // [8] cross-wave reduction scratch
   PairRec<T>* pq;                // [EPW][NS] close vehicle pairs of the frame (collision queue)
   int* pq_n;                     // [EPW] queue lengths (> NS: overflow)
 };
 
 // Byte offsets of the view's arrays in the dynamic LDS block (host: sizing; device: carve).
 struct ViewLayout {
-  size_t lanes, reals[14], xf, key, pq, red, bal, cnt, wcnt, nitem, pq_n, mypos, f0, r0, ft, mob, item, idx, kind,
+  size_t lanes, reals[14], xf, key, pq, bal, cnt, wcnt, nitem, pq_n, mypos, f0, r0, ft, mob, item, idx, kind,
       flags, sidx, lane, tgt, total;
 };
 
@@ -368,7 +367,6 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes) 
   o.xf = sizeof(T) == 8 ? take(sizeof(float) * M, 16) : o.reals[0];
   o.key = take(sizeof(T) * (size_t)n_lanes * EPW * (NS + 1), 16);
   o.pq = take(sizeof(PairRec<T>) * M, 16);
-  o.red = take(8 * sizeof(T), 16);
   o.bal = take(16 * sizeof(unsigned long long), 16);
   o.cnt = take(sizeof(int) * EPW * (LMAX + 1), 4);
   o.wcnt = take(sizeof(int) * LMAX * 4, 4);
@@ -403,7 +401,6 @@ __device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lane
   V.xf = (float*)(smem + o.xf);
   V.key = (T*)(smem + o.key);
   V.pq = (PairRec<T>*)(smem + o.pq);
-  V.red = (T*)(smem + o.red);
   V.bal = (unsigned long long*)(smem + o.bal);
   V.cnt = (int*)(smem + o.cnt);
   V.wcnt = (int*)(smem + o.wcnt);
@@ -437,25 +434,6 @@ __device__ __forceinline__ void stage_lanes(View<T>& V, const ttrl_lane_table_t&
     L.forb = R.forbidden[tid]; L._pad = 0;
     V.lanes[tid] = L;
   }
-}
-
-// Max over the NS slots of an env (all threads of the workgroup must call it).
-template <typename T, int NS, int EPW>
-__device__ __forceinline__ T env_max(T v, const View<T>& V, int tid) {
-  constexpr int W = NS < 64 ? NS : 64;
-#pragma unroll
-  for (int off = 1; off < W; off <<= 1) {
-    const T o = __shfl_xor(v, off);
-    v = v > o ? v : o;
-  }
-  if constexpr (NS > 64) {
-    __syncthreads();
-    if ((tid & 63) == 0) V.red[tid >> 6] = v;
-    __syncthreads();
-#pragma unroll
-    for (int w = 0; w < NS / 64; ++w) v = v > V.red[w] ? v : V.red[w];
-  }
-  return v;
 }
 
 // Per-thread vehicle registers.
@@ -595,13 +573,18 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
   return best;
 }
 
-// IDM free-road term  COMFORT_ACC_MAX * (1 - (max(v,0)/|not_zero(v0)|)^DELTA)  (behavior.py:172-183)
+// IDM free-road term  COMFORT_ACC_MAX * (1 - (max(v,0)/|not_zero(v0)|)^DELTA)  (behavior.py:172-183),
+// v0 = clip(target_speed, 0, speed_limit); idm_ratio is the power's base.
 template <typename T>
-__device__ __forceinline__ T idm_free(const ttrl_params_t& P, T v, T ts, T lim, T delta) {
+__device__ __forceinline__ T idm_ratio(T v, T ts, T lim) {
   ts = clip(ts, T(0), lim);
   T vv = v;
-  if (!(vv > T(0))) vv = (T(0) > vv) ? T(0) : vv;
-  return T(P.comfort_acc_max) * (T(1) - t_pow(vv / fabs(not_zero(ts)), delta));
+  if (!(vv > T(0))) vv = (T(0) > vv) ? T(0) : vv;  // Python max(v, 0)
+  return vv / fabs(not_zero(ts));
+}
+template <typename T>
+__device__ __forceinline__ T idm_free(const ttrl_params_t& P, T v, T ts, T lim, T delta) {
+  return T(P.comfort_acc_max) * (T(1) - t_pow(idm_ratio(v, ts, lim), delta));
 }
 
 // IDM interaction term  COMFORT_ACC_MAX * (desired_gap(e, f) / not_zero(d))^2 (behavior.py:185-189,
@@ -1009,8 +992,12 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
 
       PH(4);
       // steering + IDM longitudinal (behavior.py:109-135); ego: ControlledVehicle.act (controller.py:126-133)
+      const bool mdp = present && kind == TTRL_MDP;
+      if (idm || mdp) {  // one steering pass for both kinds (the ego steers to its own target)
+        V.steer[me] = (idm && (ablate & A_NO_STEER)) ? T(0)
+                                                    : steering_control(V.lanes[idm ? tgt_new : tgt], P, x, y, V.h[me], v);
+      }
       if (idm) {
-        V.steer[me] = (ablate & A_NO_STEER) ? T(0) : steering_control(V.lanes[tgt_new], P, x, y, V.h[me], v);
         const T a_free = V.afree[me];
         const int f0 = V.f0[me];
         T acc = a_free;
@@ -1022,8 +1009,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
           if (a2 < acc) acc = a2;
         }
         V.acc[me] = clip(acc, -T(P.acc_max), T(P.acc_max));
-      } else if (present && kind == TTRL_MDP) {
-        V.steer[me] = steering_control(V.lanes[tgt], P, x, y, V.h[me], v);
+      } else if (mdp) {
         V.acc[me] = T(P.kp_a) * (V.ts[me] - v);
       }
     }
@@ -1049,13 +1035,17 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         if (ablate & A_NO_KIN) {
           x += v * V.ch[me] * dt; y += v * V.sh[me] * dt; v += acc * dt;
         } else {
+          // beta = atan(tan(steer) / 2) enters only through cos / sin of beta and of h + beta:
+          // cos(beta) = 1 / sqrt(1 + tb^2), sin(beta) = tb cos(beta), and h + beta by the
+          // angle sum on the resident cos / sin of h (a few ulp from the reference's direct
+          // cos(h + beta), far inside the stated tolerances)
           const T tb = T(1) / T(2) * t_tan(steer);
-          const T beta = t_atan(tb);
-          const SinCos<T> hb = t_sincos(h + beta);
-          const T vx = v * hb.c, vy = v * hb.s;
+          const T cb = T(1) / sqrt(T(1) + tb * tb), sb = tb * cb;
+          const T c0 = V.ch[me], s0 = V.sh[me];
+          const T vx = v * (c0 * cb - s0 * sb), vy = v * (s0 * cb + c0 * sb);
           x += vx * dt; y += vy * dt;
           if (fl & FL_IMPACT) { x += V.ix[me]; y += V.iy[me]; fl = (fl | FL_CRASHED) & ~FL_IMPACT; }
-          h += v * (tb / sqrt(T(1) + tb * tb)) / (T(P.length) / T(2)) * dt;  // sin(atan(tb))
+          h += v * sb / (T(P.length) / T(2)) * dt;
           v += acc * dt;
           const SinCos<T> sc = t_sincos(h);
           V.ch[me] = sc.c; V.sh[me] = sc.s;
@@ -1080,10 +1070,10 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       // Pass 3: every vehicle folds its pairs' results with the last-writer rule
       // (impact from the largest j > i that will intersect, else the largest i' < i).
       // A queue overflow (> NS pairs in an env) falls back to the per-vehicle sweep.
-      const T vmax = env_max<T, NS, EPW>(present ? fabs(V.v[me]) : T(0), V, tid);
       const bool do_coll = !(ablate & A_NO_COLL);
       const T thr0 = (T(P.diagonal) + T(P.diagonal)) / T(2);
-      const T Rw = thr0 + vmax * dt + T(1);
+      // the pair (i, j > i) is tested against thr0 + v_i dt: i's own speed bounds its window
+      const T Rw = thr0 + fabs(V.v[me]) * dt + T(1);
       constexpr int CH = NS < 64 ? NS : 64;
       if (present && do_coll) {
         const T xi = V.x[me], yi = V.y[me], vi = V.v[me];
@@ -1191,9 +1181,10 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
           const T xi = V.x[me], yi = V.y[me], vi = V.v[me];
 #pragma unroll 1
           for (int j = 0; j < NS; ++j) {
-            if (j == i || fabs(V.x[eb + j] - xi) > Rw) continue;
+            if (j == i) continue;
             const T xj = V.x[eb + j], yj = V.y[eb + j], vj = V.v[eb + j];
             const bool lo = i < j;  // this vehicle is the reference's `self`
+            if (fabs(xj - xi) > thr0 + fabs(lo ? vi : vj) * dt + T(1)) continue;
             const T dx = lo ? xj - xi : xi - xj, dy = lo ? yj - yi : yi - yj;
             const T thr = thr0 + (lo ? vi : vj) * dt;
             const T d2 = dx * dx + dy * dy;
