@@ -194,6 +194,17 @@ def main():
                      "alg_bytes_per_vehicle_step": (rd + wr) / 15.0},
         "env_steps_per_s": world * E * args.steps / elapsed,
     }
+    if pmc and pmc.get("valu_insts_per_wave") and pmc.get("sq_waves"):
+        # Secondary roofline: the path is VALU/LDS-latency bound.  VALU wave-
+        # instructions per launch (SQ_INSTS_VALU from the committed profile of this kernel) at the
+        # 2-cycle wave64 issue of a 32-lane SIMD, against every SIMD's issue cycles in the live
+        # kernel time (a lower bound on VALU busy time: f64 ops issue at half that rate).
+        insts = pmc["valu_insts_per_wave"] * pmc["sq_waves"]
+        clk = pmc.get("effective_clock_ghz") or 2.4
+        out["valu"] = {"insts_per_launch": insts, "issue_cycles_lower_bound": 2 * insts,
+                       "simd_cycles": 1024 * clk * 1e9 * kern_ms * 1e-3,
+                       "busy_frac_lower_bound": 2 * insts / (1024 * clk * 1e9 * kern_ms * 1e-3),
+                       "source": "profiles/pmc_traffic.json (SQ_INSTS_VALU, SQ_WAVES, GRBM clock)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(N, C["obs"] if C["obs"]["type"] == "Kinematics" else GRID7,
                                            args.cpu_seconds)
