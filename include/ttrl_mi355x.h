@@ -204,6 +204,17 @@ int ttrl_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* road,
 int ttrl_reset_highway(const ttrl_state_t* s, const ttrl_lane_table_t* road,
                        const ttrl_params_t* p, const ttrl_reset_cfg_t* cfg,
                        const uint64_t* pcg, void* stream);
+/* Scene init seeded on the device: env e draws from numpy's
+ * default_rng(SeedSequence(entropy[e*n_words .. e*n_words+n_words-1])) (each uint32 word one
+ * entropy int), replacing AbstractEnv.reset (abstract.py:188-214) for the envs with
+ * mask[e] != 0 (mask NULL: all envs).  No host round trip: the masked auto-reset path. */
+int ttrl_reset_highway_seeded(const ttrl_state_t* s, const ttrl_lane_table_t* road,
+                              const ttrl_params_t* p, const ttrl_reset_cfg_t* cfg,
+                              const uint32_t* entropy, int32_t n_words, const uint8_t* mask,
+                              void* stream);
+/* Host helper: the initial PCG64 state {state_hi, state_lo, inc_hi, inc_lo} of
+ * np.random.PCG64(SeedSequence(entropy words)) (numpy bit_generator.pyx / pcg64.h). */
+int ttrl_seed_pcg64(const uint32_t* entropy, int32_t n_words, uint64_t* state4);
 /* Per-env reward [E] float32, terminated/truncated [E] uint8, given time [E] float64. */
 int ttrl_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* road,
                  const ttrl_reward_cfg_t* cfg, const double* time, float* reward,

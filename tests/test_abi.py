@@ -85,3 +85,19 @@ def test_product_refuses_cpu_tensors():
         road.act()
     with pytest.raises(RuntimeError):
         road.simulate(torch.zeros(2, dtype=torch.int32))
+
+
+def test_device_seeding_matches_numpy_seedsequence():
+    """ttrl_seed_pcg64 (the SeedSequence -> PCG64 seeding the reset kernel runs on the device)
+    equals numpy's np.random.PCG64(SeedSequence(entropy)) state for single and multi-word entropy."""
+    import numpy as np
+    lib = _lib.load()
+    rng = np.random.default_rng(0)
+    cases = [[0], [1], [12345], [2 ** 32 - 1], [5, 0, 1], [7, 3, 2], list(rng.integers(0, 2 ** 32, 6))]
+    cases += [list(rng.integers(0, 2 ** 32, k)) for k in (1, 2, 3, 4, 5, 9)]
+    for ent in cases:
+        w = np.asarray(ent, dtype=np.uint32)
+        out = np.zeros(4, dtype=np.uint64)
+        assert lib.ttrl_seed_pcg64(w.ctypes.data, len(w), out.ctypes.data) == 0
+        assert np.array_equal(out, _abi.pcg64_states([[int(v) for v in ent]])[0]), ent
+    assert lib.ttrl_seed_pcg64(None, 1, None) == -1

@@ -97,3 +97,82 @@ def test_occupancy_grid_env(dtype, hip_device):
     assert obs.shape == (8, 7, 32, 32)
     obs, *_ = env.step(torch.ones(8, dtype=torch.int64))
     assert float(obs[:, 0].sum()) >= 8  # the ego occupies the centre cell of every env
+
+
+def test_masked_auto_reset_replays_numpy_seed(hip_device):
+    """Device-side auto-reset: env e reset with seed s restarts its k-th new episode as
+    np.random.default_rng([s & 0xffffffff, s >> 32, k]) would, only where the mask is set."""
+    E, N, s = 8, 24, 5
+    env = make(E, N)
+    env.reset(seed=s)
+    for _ in range(2):
+        env.step(torch.ones(E, dtype=torch.int64))
+    before = env.state.to_numpy()
+    mask = torch.tensor([1, 0, 1, 0, 0, 1, 0, 1], dtype=torch.bool, device=hip_device)
+    env.time.fill_(2.0)
+    env._auto_reset(mask)
+    after = env.state.to_numpy()
+    o = Oracle(env.network.table, env.params)
+    ref = HostState(E, N)
+    o.reset_highway(ref, env.reset_cfg, [[s + e, 0, 1] for e in range(E)])
+    m = mask.cpu().numpy()
+    for k in ("x", "y", "heading", "speed", "target_speed", "timer", "delta", "lane", "kind", "crashed"):
+        assert np.array_equal(after[k][m], ref[k][m].astype(after[k].dtype)), k
+        assert np.array_equal(after[k][~m], before[k][~m]), k
+    assert torch.equal(env.time.cpu(), torch.where(mask.cpu(), 0.0, 2.0).double())
+    env._auto_reset(mask)  # the second new episode of the same envs: k = 2
+    o.reset_highway(ref, env.reset_cfg, [[s + e, 0, 2] for e in range(E)])
+    assert np.array_equal(env.state.to_numpy()["x"][m], ref["x"][m])
+
+
+def test_reset_with_seeds_beyond_32_bits(hip_device):
+    """Seeds >= 2^32 (multi-word SeedSequence entropy) take the host-seeded path: same scenes."""
+    E, N = 4, 16
+    env = make(E, N)
+    base = 2 ** 33 + 7
+    env.reset(seed=base)
+    o = Oracle(env.network.table, env.params)
+    ref = HostState(E, N)
+    o.reset_highway(ref, env.reset_cfg, [base + e for e in range(E)])
+    got = env.state.to_numpy()
+    for k in ("x", "y", "speed", "delta", "lane"):
+        assert np.array_equal(got[k], ref[k]), k
+
+
+def test_auto_reset_in_step_returns_new_first_observation(hip_device):
+    env = make(8, 20, duration=2, auto_reset=True)
+    env.reset(seed=3)
+    env.step(torch.ones(8, dtype=torch.int64))
+    obs, rew, term, trunc, info = env.step(torch.ones(8, dtype=torch.int64))
+    assert bool(trunc.all())
+    assert "final_observation" in info and not torch.equal(info["final_observation"], obs)
+    fresh = make(8, 20)
+    fresh.reset(seed=3)
+    fresh._entropy.copy_(env._entropy)
+    fresh._entropy[:, 2] -= 1  # _auto_reset advances the episode counter itself
+    fresh._auto_reset(torch.ones(8, dtype=torch.bool, device=hip_device))
+    assert torch.equal(obs, fresh.observation_type.observe())
+
+
+def test_returned_observations_are_not_overwritten(hip_device):
+    """Like the reference's df.values.copy(), an obs kept by the caller survives later steps
+    (a trainer records (s, a, r, s') pairs across steps)."""
+    env = make(4, 20)
+    o0, _ = env.reset(seed=4)
+    keep = o0.clone()
+    o1, *_ = env.step(torch.ones(4, dtype=torch.int64))
+    assert torch.equal(o0, keep) and not torch.equal(o0, o1)
+
+
+def test_dqn_training_in_the_loop(hip_device):
+    """Trainer hooks + batched DQN learning on the device: replay memory fills from the env,
+    the double-DQN residual is minimised, the target net syncs, finished envs auto-reset."""
+    env = make(64, 32, duration=12, auto_reset=True)
+    agent = BatchedDQNAgent(hip_device, config={"batch_size": 64, "memory_capacity": 2048, "target_update": 4})
+    ev = BatchedEvaluation(env, agent, num_episodes=1, sim_seed=0, max_steps=10)
+    params0 = [p.detach().clone() for p in agent.policy.value_net.parameters()]
+    ev.run_episodes()
+    L = agent.learner
+    assert len(L.memory) == 640 and L.steps == 10 and torch.isfinite(L.last_loss)
+    assert any(not torch.equal(a, b) for a, b in zip(params0, agent.policy.value_net.parameters()))
+    assert float(env.time.max()) == 10.0

@@ -258,8 +258,9 @@ def pcg64_states(seeds) -> np.ndarray:
     np.random.default_rng(seed) == Generator(PCG64(SeedSequence(seed)))."""
     out = np.zeros((len(seeds), 4), dtype=np.uint64)
     m = (1 << 64) - 1
-    for i, s in enumerate(seeds):
-        st = np.random.PCG64(int(s)).state["state"]
+    for i, s in enumerate(seeds):  # an int seed or a list of entropy ints (SeedSequence semantics)
+        st = np.random.PCG64(np.random.SeedSequence([int(v) for v in s] if isinstance(s, (list, tuple, np.ndarray))
+                                                    else int(s))).state["state"]
         out[i] = [(st["state"] >> 64) & m, st["state"] & m, (st["inc"] >> 64) & m, st["inc"] & m]
     return out
 

@@ -25,6 +25,8 @@ _SIGS = {
     "ttrl_observe_kinematics": ([_P, _P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_observe_grid": ([_P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_reset_highway": ([_P, _P, _P, _P, _P, _P], C.c_int),
+    "ttrl_reset_highway_seeded": ([_P, _P, _P, _P, _P, C.c_int32, _P, _P], C.c_int),
+    "ttrl_seed_pcg64": ([_P, C.c_int32, _P], C.c_int),
     "ttrl_rewards": ([_P, _P, _P, _P, _P, _P, _P, _P], C.c_int),
 }
 EXPORTS = [k for k in _SIGS]
@@ -46,7 +48,11 @@ def load(path: str | None = None) -> C.CDLL:
         raise ImportError(f"HIP library not built: {p} (run __graft_entry__.build())")
     lib = C.CDLL(p)
     for name, (args, res) in _SIGS.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if path is None:
+                raise ImportError(f"{p} lacks {name}: rebuild it")
+            continue  # an older build loaded for comparison (tools/variants.py)
         fn.argtypes = args
         fn.restype = res
     if lib.ttrl_abi_version() != 1:

@@ -1563,21 +1563,96 @@ __device__ __forceinline__ unsigned pcg_bounded(Pcg& g, unsigned n) {  // Genera
   return (unsigned)(m >> 32);
 }
 
+// numpy's SeedSequence(entropy words) -> generate_state(4, uint64) -> PCG64 seeding
+// (numpy/random/bit_generator.pyx SeedSequence.mix_entropy / generate_state with pool_size 4,
+// _pcg64.pyx + pcg64.h pcg64_set_seed: state = 0, inc = 2 * initseq + 1, step, state += seed,
+// step).  Host and device, so np.random.default_rng([w0, w1, ...]) scenes can be generated on
+// the GPU without a host round trip (device-side auto-reset) and the seeding tested on the CPU.
+struct SeedSeq {
+  static constexpr unsigned INIT_A = 0x43b0d7e5u, MULT_A = 0x931e8875u, INIT_B = 0x8b51f9ddu, MULT_B = 0x58f38dedu;
+  static constexpr unsigned MIX_L = 0xca01f9ddu, MIX_R = 0x4973f715u;
+  __host__ __device__ static unsigned hashmix(unsigned v, unsigned& h) {
+    v ^= h;
+    h *= MULT_A;
+    v *= h;
+    v ^= v >> 16;
+    return v;
+  }
+  __host__ __device__ static unsigned mix(unsigned x, unsigned y) {
+    unsigned r = MIX_L * x - MIX_R * y;
+    r ^= r >> 16;
+    return r;
+  }
+  // words: the entropy as uint32 words (numpy coerces each Python int < 2^32 to one word)
+  __host__ __device__ static void pcg64_seed(const unsigned* words, int n, unsigned long long out[4]) {
+    unsigned pool[4];
+    unsigned h = INIT_A;
+    for (int i = 0; i < 4; ++i) pool[i] = hashmix(i < n ? words[i] : 0u, h);
+    for (int s = 0; s < 4; ++s)
+      for (int d = 0; d < 4; ++d)
+        if (s != d) pool[d] = mix(pool[d], hashmix(pool[s], h));
+    for (int s = 4; s < n; ++s)
+      for (int d = 0; d < 4; ++d) pool[d] = mix(pool[d], hashmix(words[s], h));
+    unsigned st[8];
+    unsigned hb = INIT_B;
+    for (int i = 0; i < 8; ++i) {
+      unsigned v = pool[i & 3];
+      v ^= hb;
+      hb *= MULT_B;
+      v *= hb;
+      v ^= v >> 16;
+      st[i] = v;
+    }
+    unsigned long long w[4];
+    for (int i = 0; i < 4; ++i) w[i] = (unsigned long long)st[2 * i] | ((unsigned long long)st[2 * i + 1] << 32);
+    // pcg64_set_seed(seed = w[0] << 64 | w[1], inc = w[2] << 64 | w[3]), srandom_r
+    const unsigned long long Mh = 0x2360ED051FC65DA4ull, Ml = 0x4385DF649FCCF645ull;
+    unsigned long long inc_h = (w[2] << 1) | (w[3] >> 63), inc_l = (w[3] << 1) | 1ull;
+    auto step = [&](unsigned long long& sh, unsigned long long& sl) {
+      const unsigned long long lo = sl * Ml;
+#ifdef __HIP_DEVICE_COMPILE__
+      const unsigned long long hi = __umul64hi(sl, Ml) + sh * Ml + sl * Mh;
+#else
+      const unsigned long long hi = (unsigned long long)(((unsigned __int128)sl * Ml) >> 64) + sh * Ml + sl * Mh;
+#endif
+      sl = lo + inc_l;
+      sh = hi + inc_h + (sl < lo ? 1ull : 0ull);
+    };
+    unsigned long long sh = 0, sl = 0;
+    step(sh, sl);
+    const unsigned long long ol = sl;
+    sl += w[1];
+    sh += w[0] + (sl < ol ? 1ull : 0ull);
+    step(sh, sl);
+    out[0] = sh; out[1] = sl; out[2] = inc_h; out[3] = inc_l;
+  }
+};
+
 // Scene generation: ego MDPVehicle, then n-1 x IDMVehicle.create_random
 // (kinematics.py:50-104) + randomize_behavior (behavior.py:66-69), the numpy RNG stream
 // reproduced bit for bit.  One thread per env (the spawn order is sequential by nature).
+// Either `pcg` holds each env's initial PCG64 state ({state_hi, state_lo, inc_hi, inc_lo}) or
+// `words` holds each env's SeedSequence entropy ([E][n_words] uint32); `mask` (optional)
+// restricts the reset to the envs with mask[e] != 0, leaving the others untouched.
 template <typename T>
 __global__ void reset_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_reset_cfg_t cfg,
-                             const unsigned long long* __restrict__ pcg) {
+                             const unsigned long long* __restrict__ pcg, const unsigned* __restrict__ words,
+                             int n_words, const uint8_t* __restrict__ mask) {
   const int env = blockIdx.x * blockDim.x + threadIdx.x;
-  if (env >= st.n_envs) return;
+  if (env >= st.n_envs || (mask && !mask[env])) return;
   const int N = st.n_veh, nl = R.n_lanes;
   const size_t b = (size_t)env * N;
   T* X = (T*)st.x; T* Y = (T*)st.y; T* Hh = (T*)st.heading; T* Vv = (T*)st.speed; T* TS = (T*)st.target_speed;
   T* TM = (T*)st.timer; T* DL = (T*)st.delta;
   Pcg g;
-  g.st = U128{pcg[4 * env], pcg[4 * env + 1]};
-  g.inc = U128{pcg[4 * env + 2], pcg[4 * env + 3]};
+  unsigned long long s4[4];
+  if (pcg) {
+    for (int k = 0; k < 4; ++k) s4[k] = pcg[4 * env + k];
+  } else {
+    SeedSeq::pcg64_seed(words + (size_t)env * n_words, n_words, s4);
+  }
+  g.st = U128{s4[0], s4[1]};
+  g.inc = U128{s4[2], s4[3]};
   g.has32 = false; g.u32 = 0;
   double smax[LMAX];
   auto closest = [&](double x, double y, double h) {
@@ -1850,11 +1925,39 @@ int ttrl_reset_highway(const ttrl_state_t* s, const ttrl_lane_table_t* road, con
   const int blocks = (s->n_envs + 63) / 64;
   if (s->dtype == TTRL_F64)
     hipLaunchKernelGGL(reset_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg,
-                       (const unsigned long long*)pcg);
+                       (const unsigned long long*)pcg, (const unsigned*)nullptr, 0, (const uint8_t*)nullptr);
   else
     hipLaunchKernelGGL(reset_kernel<float>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg,
-                       (const unsigned long long*)pcg);
+                       (const unsigned long long*)pcg, (const unsigned*)nullptr, 0, (const uint8_t*)nullptr);
   return launch_status();
+}
+
+int ttrl_reset_highway_seeded(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                              const ttrl_reset_cfg_t* cfg, const uint32_t* entropy, int32_t n_words,
+                              const uint8_t* mask, void* stream) {
+  int rc = check_state(s, road);
+  if (rc) return rc;
+  if (!p || !cfg || !entropy || n_words < 1 || n_words > 64 || cfg->n_vehicles < 1 || cfg->n_vehicles > s->n_veh ||
+      cfg->ego_lane < 0 || cfg->ego_lane >= road->n_lanes || p->n_target_speeds < 1 || p->n_target_speeds > 8)
+    return TTRL_E_ARG;
+  if (s->n_envs == 0) return TTRL_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int blocks = (s->n_envs + 63) / 64;
+  if (s->dtype == TTRL_F64)
+    hipLaunchKernelGGL(reset_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg,
+                       (const unsigned long long*)nullptr, (const unsigned*)entropy, (int)n_words, mask);
+  else
+    hipLaunchKernelGGL(reset_kernel<float>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg,
+                       (const unsigned long long*)nullptr, (const unsigned*)entropy, (int)n_words, mask);
+  return launch_status();
+}
+
+int ttrl_seed_pcg64(const uint32_t* entropy, int32_t n_words, uint64_t* state4) {
+  if (!entropy || !state4 || n_words < 1 || n_words > 64) return TTRL_E_ARG;
+  unsigned long long o[4];
+  SeedSeq::pcg64_seed((const unsigned*)entropy, n_words, o);
+  for (int k = 0; k < 4; ++k) state4[k] = o[k];
+  return TTRL_OK;
 }
 
 int ttrl_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_reward_cfg_t* cfg,

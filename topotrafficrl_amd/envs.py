@@ -25,11 +25,31 @@ from .state import BatchState
 
 def reset_highway(state: BatchState, network: RoadNetwork, params: _abi.Params, cfg: _abi.ResetCfg, seeds) -> None:
     """Scene generation on the device, bit-exact with ``np.random.default_rng(seed)`` per env."""
-    pcg = torch.from_numpy(_abi.pcg64_states([int(s) for s in seeds]).view(np.int64)).to(state.device)
-    if pcg.shape[0] != state.n_envs:
+    seeds = [int(s) for s in seeds]
+    if len(seeds) != state.n_envs:
         raise ValueError("one seed per env required")
+    if all(0 <= s < 2 ** 32 for s in seeds):  # SeedSequence(seed) is the single entropy word: seeded on the device
+        words = torch.tensor(np.asarray(seeds, dtype=np.uint32).view(np.int32), device=state.device).view(-1, 1)
+        reset_highway_seeded(state, network, params, cfg, words)
+        return
+    pcg = torch.from_numpy(_abi.pcg64_states(seeds).view(np.int64)).to(state.device)
     _lib.call("ttrl_reset_highway", C.byref(state.struct()), C.byref(network.table), C.byref(params),
               C.byref(cfg), pcg.data_ptr(), torch.cuda.current_stream(state.device).cuda_stream)
+
+
+def reset_highway_seeded(state: BatchState, network: RoadNetwork, params: _abi.Params, cfg: _abi.ResetCfg,
+                         entropy: torch.Tensor, mask: torch.Tensor | None = None) -> None:
+    """Device-seeded scene init: env e replays ``np.random.default_rng(list(entropy[e]))`` (uint32
+    words, stored as int32), only where ``mask[e]`` (uint8/bool [E]) is set; no host round trip."""
+    if entropy.dim() != 2 or entropy.shape[0] != state.n_envs or entropy.dtype != torch.int32:
+        raise ValueError("entropy must be an int32 [n_envs, n_words] tensor of uint32 words")
+    if entropy.device != state.device or (mask is not None and mask.device != state.device):
+        raise ValueError("entropy / mask must live on the state's device")
+    entropy = entropy.contiguous()
+    m = None if mask is None else mask.to(torch.uint8).contiguous()
+    _lib.call("ttrl_reset_highway_seeded", C.byref(state.struct()), C.byref(network.table), C.byref(params),
+              C.byref(cfg), entropy.data_ptr(), int(entropy.shape[1]), None if m is None else m.data_ptr(),
+              torch.cuda.current_stream(state.device).cuda_stream)
 
 
 class VecHighwayEnv:
@@ -120,6 +140,9 @@ class VecHighwayEnv:
         self._reward = torch.zeros(self.num_envs, dtype=torch.float32, device=self.device)
         self._term = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
         self._trunc = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
+        # auto-reset entropy per env: [seed lo word, seed hi word, episode]; episode k >= 1 of an env
+        # reset with seed s replays np.random.default_rng([s & 0xffffffff, s >> 32, k])
+        self._entropy = torch.zeros(self.num_envs, 3, dtype=torch.int32, device=self.device)
         self.define_spaces()
 
     @property
@@ -157,6 +180,10 @@ class VecHighwayEnv:
         self.steps = 0
         self.done = False
         reset_highway(self.state, self.network, self.params, self.reset_cfg, seeds)
+        ent = np.zeros((self.num_envs, 3), dtype=np.uint32)
+        ent[:, 0] = [s & 0xFFFFFFFF for s in seeds]
+        ent[:, 1] = [(s >> 32) & 0xFFFFFFFF for s in seeds]
+        self._entropy.copy_(torch.from_numpy(ent.view(np.int32)))
         obs = self.observation_type.observe()
         return obs, self._info(obs, None)
 
@@ -170,7 +197,12 @@ class VecHighwayEnv:
         reward, terminated, truncated = self._rewards_and_dones()
         info = self._info(obs, action)
         if self.config["auto_reset"]:
-            self._auto_reset(terminated | truncated)
+            # finished envs restart on the device; obs is the new episode's first observation and
+            # info["final_observation"] the finished episode's last (no host round trip)
+            done = terminated | truncated
+            info["final_observation"], info["final_mask"] = obs, done
+            self._auto_reset(done)
+            obs = self.observation_type.observe()
         return obs, reward, terminated, truncated, info
 
     def _simulate(self, action=None) -> None:
@@ -194,16 +226,10 @@ class VecHighwayEnv:
                 "action": action}
 
     def _auto_reset(self, done: torch.Tensor) -> None:
-        """Opt-in auto-reset of finished envs."""
-        if not bool(done.any()):
-            return
-        fresh = BatchState(self.num_envs, self.state.n_veh, device=self.device, dtype=self.state.dtype)
-        self.shuffle_seed += 1
-        seeds = [s + 7919 * (self.steps + 1) for s in self._seeds(self.shuffle_seed)]
-        reset_highway(fresh, self.network, self.params, self.reset_cfg, seeds)
-        m = done.view(-1, 1)
-        for k, v in self.state.t.items():
-            v.copy_(torch.where(m, fresh.t[k], v))
+        """Masked auto-reset of finished envs on the device."""
+        d = done.to(torch.int32)
+        self._entropy[:, 2] += d
+        reset_highway_seeded(self.state, self.network, self.params, self.reset_cfg, self._entropy, d)
         self.time.masked_fill_(done, 0.0)
 
     def get_available_actions(self):

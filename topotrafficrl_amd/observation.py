@@ -83,7 +83,9 @@ class BatchedKinematicObservation(BatchedObservationType):
             self.cfg.shuffle_seed = int(self.env.shuffle_seed)
             self.cfg.shuffle_offset = self._calls
         self._calls += 1
-        self._out, self._ids = kinematics(road.state, road.network, road.params, self.cfg, self._out, self._ids)
+        # a fresh output per call (the caching allocator makes it free): like the reference's
+        # df.values.copy(), a returned observation is never overwritten by a later step
+        self._out, self._ids = kinematics(road.state, road.network, road.params, self.cfg)
         return self._out
 
     @property
@@ -111,7 +113,7 @@ class BatchedOccupancyGridObservation(BatchedObservationType):
 
     def observe(self) -> torch.Tensor:
         road = self.env.road
-        self._out = occupancy_grid(road.state, road.network, road.params, self.cfg, self._out)
+        self._out = occupancy_grid(road.state, road.network, road.params, self.cfg)  # fresh per call
         return self._out
 
 

@@ -20,16 +20,21 @@ import numpy as np
 import torch
 
 from .agent import EgoAttentionPolicy
+from .dqn import DEFAULT_CONFIG, DQNLearner
 
 logger = logging.getLogger(__name__)
 
 
 class BatchedDQNAgent:
-    """Acting side of DQNAgent (deep_q_network/pytorch.py, abstract.py) for batched observations."""
+    """DQNAgent (deep_q_network/pytorch.py, abstract.py) for batched observations: acting with
+    the EgoAttention-2h value net and epsilon-greedy exploration, learning with the batched
+    replay memory / double-DQN residual / Adam / target sync of ``dqn.DQNLearner``."""
 
     def __init__(self, device, n_actions: int = 5, seed: int = 0, config: dict | None = None):
         self.policy = EgoAttentionPolicy(device, n_actions=n_actions, seed=seed)
-        self.config = {"gamma": 0.95, **(config or {})}  # baseline.json:7
+        self.config = {**DEFAULT_CONFIG, **(config or {})}
+        self.seed_value = seed
+        self.learner = None  # built on the first record (the observation shape is known then)
         self.training = True
         self.writer = None
 
@@ -41,8 +46,21 @@ class BatchedDQNAgent:
         return self.policy.act(observation)
 
     def record(self, state, action, reward, next_state, done, info):
-        """Replay/training updates are SURVEY.md §8(f) 'next' (DQN training)."""
-        raise NotImplementedError()
+        """AbstractDQNAgent.record (abstract.py:37-63) for a batch of transitions.  With an
+        auto-resetting env the finished envs' ``next_state`` is the episode's last observation
+        (info["final_observation"]), not the next episode's first."""
+        if not self.training:
+            return None
+        if info and "final_observation" in info and "final_mask" in info:
+            m = info["final_mask"].view(-1, *[1] * (next_state.dim() - 1))
+            next_state = torch.where(m, info["final_observation"], next_state)
+        if self.learner is None:
+            self.learner = DQNLearner(self.policy.value_net, tuple(state.shape[1:]), self.policy.device, self.config,
+                                      seed=self.seed_value + 7)
+        loss = self.learner.record(state, action, reward, next_state, done)
+        if loss is not None and self.writer is not None:
+            self.writer.add_scalar("agent/loss", float(loss), self.learner.steps)
+        return loss
 
     def seed(self, seed=None):
         if seed is not None:
@@ -62,13 +80,18 @@ class BatchedDQNAgent:
     def save(self, filename):
         """DQNAgent.save (pytorch.py:82-86): {'state_dict', 'optimizer'}."""
         Path(filename).parent.mkdir(parents=True, exist_ok=True)
-        torch.save({"state_dict": self.policy.value_net.state_dict(), "optimizer": None}, filename)
+        opt = self.learner.optimizer.state_dict() if self.learner is not None else None
+        torch.save({"state_dict": self.policy.value_net.state_dict(), "optimizer": opt}, filename)
         return filename
 
     def load(self, filename):
-        """DQNAgent.load (pytorch.py:88-93), weights only."""
+        """DQNAgent.load (pytorch.py:88-93), weights_only."""
         ckpt = torch.load(filename, map_location=self.policy.device, weights_only=True)
         self.policy.value_net.load_state_dict(ckpt["state_dict"])
+        if self.learner is not None:
+            self.learner.target_net.load_state_dict(ckpt["state_dict"])
+            if ckpt.get("optimizer"):
+                self.learner.optimizer.load_state_dict(ckpt["optimizer"])
         return filename
 
 
