@@ -61,11 +61,13 @@ class EgoAttention(nn.Module):
         k = self.key_all(x).view(b, n, self.h, self.dph).permute(0, 2, 1, 3)
         v = self.value_all(x).view(b, n, self.h, self.dph).permute(0, 2, 1, 3)
         q = self.query_ego(ego).view(b, 1, self.h, self.dph).permute(0, 2, 1, 3)
-        scores = torch.matmul(q, k.transpose(-2, -1)) / math.sqrt(self.dph)
+        # one query per env: the [1 x d] @ [d x n] products as broadcast multiply + reduce
+        # (a batched GEMM of 16k 1x32x15 problems is ~20x slower on hipBLASLt)
+        scores = (q * k).sum(-1, keepdim=True).transpose(-2, -1) / math.sqrt(self.dph)
         if mask is not None:
             scores = scores.masked_fill(mask.view(b, 1, 1, n).repeat(1, self.h, 1, 1), -1e9)
         p = F.softmax(scores, dim=-1)
-        out = torch.matmul(p, v)
+        out = (p.transpose(-2, -1) * v).sum(-2, keepdim=True)
         return (self.attention_combine(out.reshape(b, self.f)) + ego.squeeze(1)) / 2, p
 
 
@@ -92,7 +94,8 @@ class EgoAttentionNetwork(nn.Module):
         return self
 
     def forward(self, x):
-        ego, others = x[:, 0:1, :], x[:, 1:, :]
+        # contiguous copies: hipBLASLt takes a 6x slower path on the strided [:, 1:, :] view
+        ego, others = x[:, 0:1, :].contiguous(), x[:, 1:, :].contiguous()
         mask = x[:, :, self.presence_idx:self.presence_idx + 1] < 0.5
         att, _ = self.attention_layer(self.ego_embedding(ego), self.others_embedding(others), mask)
         return self.output_layer(att)
@@ -122,12 +125,16 @@ class EgoAttentionPolicy:
         return self.value_net(obs)
 
     @torch.no_grad()
-    def act(self, obs: torch.Tensor, t: int | None = None) -> torch.Tensor:
-        t = self.time if t is None else t
-        self.time = t + 1
+    def act(self, obs: torch.Tensor, t: int | None = None, epsilon: torch.Tensor | None = None) -> torch.Tensor:
+        """Greedy on Q with probability 1 - epsilon(t), uniform otherwise.  ``epsilon`` (a device
+        scalar) overrides the schedule: a captured graph refreshes it before every replay."""
+        if epsilon is None:
+            t = self.time if t is None else t
+            self.time = t + 1
+            epsilon = self.epsilon(t)
         q = self.value_net(obs)
         greedy = q.argmax(dim=1)
         e = obs.shape[0]
         u = torch.rand(e, device=self.device, generator=self.gen)
         rnd = torch.randint(0, self.n_actions, (e,), device=self.device, generator=self.gen)
-        return torch.where(u < self.epsilon(t), rnd, greedy)
+        return torch.where(u < epsilon, rnd, greedy)
