@@ -150,6 +150,21 @@ typedef struct ttrl_grid_cfg {
   double lane_perception_distance;/* 100 (fill_road_layer_by_lanes)             */
 } ttrl_grid_cfg_t;
 
+/* TimeToCollisionObservation config (observation.py:114-151, finite_mdp.py:104-167). */
+typedef struct ttrl_ttc_cfg {
+  int32_t horizon_bins;           /* int(horizon * policy_frequency) (10)       */
+  int32_t obs_lanes, obs_speeds;  /* 3, 3 (observation.py:139, :146)           */
+  int32_t _pad;
+  double time_quantization;       /* 1 / policy_frequency                       */
+} ttrl_ttc_cfg_t;
+
+/* LidarObservation config (observation.py:677-768). */
+typedef struct ttrl_lidar_cfg {
+  int32_t cells;                  /* 16 (<= 64)                                 */
+  int32_t normalize;              /* divide by maximum_range                    */
+  double maximum_range;           /* 60                                         */
+} ttrl_lidar_cfg_t;
+
 /* Highway scene generator config. */
 typedef struct ttrl_reset_cfg {
   int32_t n_vehicles;             /* vehicles actually spawned per env (<= n_veh) */
@@ -198,6 +213,15 @@ int ttrl_observe_kinematics(const ttrl_state_t* s, const ttrl_lane_table_t* road
 int ttrl_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* road,
                       const ttrl_params_t* p, const ttrl_grid_cfg_t* cfg,
                       float* out, void* stream);
+/* Time-to-collision grid of the ego (compute_ttc_grid finite_mdp.py:104-167 + the lane / speed
+ * windows of TimeToCollisionObservation.observe observation.py:126-151):
+ * out [E][obs_speeds][obs_lanes][horizon_bins] float32. */
+int ttrl_observe_ttc(const ttrl_state_t* s, const ttrl_lane_table_t* road,
+                     const ttrl_params_t* p, const ttrl_ttc_cfg_t* cfg, float* out, void* stream);
+/* Lidar of the ego (LidarObservation.trace observation.py:704-752): out [E][cells][2] float32
+ * {distance, relative speed along the ray}, divided by maximum_range if normalize. */
+int ttrl_observe_lidar(const ttrl_state_t* s, const ttrl_lane_table_t* road,
+                       const ttrl_params_t* p, const ttrl_lidar_cfg_t* cfg, float* out, void* stream);
 /* Scene generation, bit-exact with numpy.random.Generator(PCG64) draws:
  * pcg [E][4] uint64 = {state_hi, state_lo, inc_hi, inc_lo} per env (from
  * SeedSequence on the host); writes all state rows (slots >= n_vehicles absent). */

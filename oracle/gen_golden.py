@@ -42,9 +42,14 @@ def _import_reference():
     from ttrl_env.vehicle.behavior import IDMVehicle
     from ttrl_env.vehicle.controller import MDPVehicle
     from ttrl_env.vehicle.kinematics import Vehicle
+    for sub in ("envs", "envs.common"):  # skip the package __init__s (they import gymnasium), as above
+        m = types.ModuleType("ttrl_env." + sub)
+        m.__path__ = [os.path.join(REF, "ttrl_env", *sub.split("."))]
+        sys.modules["ttrl_env." + sub] = m
+    from ttrl_env.envs.common import finite_mdp  # the module itself imports only utils and Vehicle
     return types.SimpleNamespace(utils=utils, StraightLane=StraightLane, Road=Road,
                                  RoadNetwork=RoadNetwork, IDMVehicle=IDMVehicle,
-                                 MDPVehicle=MDPVehicle, Vehicle=Vehicle)
+                                 MDPVehicle=MDPVehicle, Vehicle=Vehicle, finite_mdp=finite_mdp)
 
 
 R = _import_reference()
@@ -240,6 +245,81 @@ def grid_obs(road, cfg):
     return np.nan_to_num(grid).astype(np.float32)
 
 
+def ttc_obs(road, horizon=10, policy_frequency=1):
+    """TimeToCollisionObservation.observe (observation.py:126-151) around the reference's own
+    compute_ttc_grid (finite_mdp.py:104-167)."""
+    ego = road.vehicles[0]
+    env = types.SimpleNamespace(vehicle=ego, road=road, config={"policy_frequency": policy_frequency})
+    grid = R.finite_mdp.compute_ttc_grid(env, vehicle=ego, time_quantization=1 / policy_frequency,
+                                         horizon=horizon)
+    padding = np.ones(np.shape(grid))
+    padded_grid = np.concatenate([padding, grid, padding], axis=1)
+    obs_lanes = 3
+    l0 = grid.shape[1] + ego.lane_index[2] - obs_lanes // 2
+    lf = grid.shape[1] + ego.lane_index[2] + obs_lanes // 2
+    clamped_grid = padded_grid[:, l0: lf + 1, :]
+    repeats = np.ones(clamped_grid.shape[0])
+    repeats[np.array([0, -1])] += clamped_grid.shape[0]
+    padded_grid = np.repeat(clamped_grid, repeats.astype(int), axis=0)
+    obs_speeds = 3
+    v0 = grid.shape[0] + ego.speed_index - obs_speeds // 2
+    vf = grid.shape[0] + ego.speed_index + obs_speeds // 2
+    clamped_grid = padded_grid[v0: vf + 1, :, :]
+    return clamped_grid.astype(np.float32)
+
+
+def lidar_obs(road, cells=16, maximum_range=60.0, normalize=True):
+    """LidarObservation.observe / trace (observation.py:694-768) with the reference's
+    utils.rect_corners and utils.distance_to_rect."""
+    ego = road.vehicles[0]
+    angle = 2 * np.pi / cells
+    origin, origin_velocity = ego.position.copy(), ego.velocity
+    grid = np.ones((cells, 2)) * maximum_range
+
+    def position_to_angle(position):
+        return np.arctan2(position[1] - origin[1], position[0] - origin[0]) + angle / 2
+
+    def angle_to_index(a):
+        return int(np.floor(a / angle)) % cells
+
+    def index_to_direction(index):
+        return np.array([np.cos(index * angle), np.sin(index * angle)])
+
+    for obstacle in road.vehicles + road.objects:
+        if obstacle is ego or not obstacle.solid:
+            continue
+        center_distance = np.linalg.norm(obstacle.position - origin)
+        if center_distance > maximum_range:
+            continue
+        center_index = angle_to_index(position_to_angle(obstacle.position))
+        distance = center_distance - obstacle.WIDTH / 2
+        if distance <= grid[center_index, 0]:
+            direction = index_to_direction(center_index)
+            velocity = (obstacle.velocity - origin_velocity).dot(direction)
+            grid[center_index, :] = [distance, velocity]
+        corners = R.utils.rect_corners(obstacle.position, obstacle.LENGTH, obstacle.WIDTH, obstacle.heading)
+        angles = [position_to_angle(corner) for corner in corners]
+        min_angle, max_angle = min(angles), max(angles)
+        if min_angle < -np.pi / 2 < np.pi / 2 < max_angle:
+            min_angle, max_angle = max_angle, min_angle + 2 * np.pi
+        start, end = angle_to_index(min_angle), angle_to_index(max_angle)
+        if start < end:
+            indexes = np.arange(start, end + 1)
+        else:
+            indexes = np.hstack([np.arange(start, cells), np.arange(0, end + 1)])
+        for index in indexes:
+            direction = index_to_direction(index)
+            ray = [origin, origin + maximum_range * direction]
+            distance = R.utils.distance_to_rect(ray, corners)
+            if distance <= grid[index, 0]:
+                velocity = (obstacle.velocity - origin_velocity).dot(direction)
+                grid[index, :] = [distance, velocity]
+    obs = grid.copy()
+    if normalize:
+        obs /= maximum_range
+    return obs
+
+
 # ---------------------------------------------------------------- rollout
 def rollout(road, policy_steps: int, seed: int, frames_per_step: int = 15, obs=True):
     """AbstractEnv._simulate (abstract.py:252-282): frame 0 of each policy step applies the
@@ -249,13 +329,15 @@ def rollout(road, policy_steps: int, seed: int, frames_per_step: int = 15, obs=T
     actions = rng.integers(0, 5, size=policy_steps).astype(np.int32)
     states = [snapshot(road)]
     acts, nbrs = [], []
-    kin5, kin15, kid5, kid15, grid, grid2 = [], [], [], [], [], []
+    kin5, kin15, kid5, kid15, grid, grid2, ttc, lidar = [], [], [], [], [], [], [], []
 
     def observe():
         o, i = kinematics_obs(road, KIN_DEFAULT); kin5.append(o); kid5.append(i)
         o, i = kinematics_obs(road, KIN_ENVJSON); kin15.append(o); kid15.append(i)
         grid.append(grid_obs(road, GRID_DENSE))
         grid2.append(grid_obs(road, GRID_ONROAD))
+        ttc.append(ttc_obs(road))
+        lidar.append(lidar_obs(road))
 
     if obs:
         observe()
@@ -280,6 +362,7 @@ def rollout(road, policy_steps: int, seed: int, frames_per_step: int = 15, obs=T
         out["kin5"] = np.stack(kin5); out["kin5_ids"] = np.stack(kid5)
         out["kin15"] = np.stack(kin15); out["kin15_ids"] = np.stack(kid15)
         out["grid7"] = np.stack(grid); out["grid_onroad"] = np.stack(grid2)
+        out["ttc"] = np.stack(ttc); out["lidar"] = np.stack(lidar)
     return out
 
 

@@ -83,6 +83,8 @@ _SIGS = {
     "oracle_observe_grid": [C.c_void_p] * 5,
     "oracle_reset_highway": [C.c_void_p] * 5,
     "oracle_rewards": [C.c_void_p] * 7,
+    "oracle_observe_ttc": [C.c_void_p] * 5,
+    "oracle_observe_lidar": [C.c_void_p] * 5,
 }
 
 
@@ -138,6 +140,20 @@ class Oracle:
         self._ok(self.lib.oracle_observe_kinematics(C.byref(s), C.byref(self.lanes), C.byref(self.params),
                                                     C.byref(cfg), out.ctypes.data, ids.ctypes.data))
         return out, ids
+
+    def observe_ttc(self, h: HostState, cfg: _abi.TtcCfg):
+        s = h.struct()
+        out = np.zeros((h.E, cfg.obs_speeds, cfg.obs_lanes, cfg.horizon_bins), dtype=np.float32)
+        self._ok(self.lib.oracle_observe_ttc(C.byref(s), C.byref(self.lanes), C.byref(self.params), C.byref(cfg),
+                                             out.ctypes.data))
+        return out
+
+    def observe_lidar(self, h: HostState, cfg: _abi.LidarCfg):
+        s = h.struct()
+        out = np.zeros((h.E, cfg.cells, 2), dtype=np.float32)
+        self._ok(self.lib.oracle_observe_lidar(C.byref(s), C.byref(self.lanes), C.byref(self.params), C.byref(cfg),
+                                               out.ctypes.data))
+        return out
 
     def observe_grid(self, h: HostState, cfg: _abi.GridCfg):
         s = h.struct()

@@ -667,3 +667,156 @@ int oracle_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl
   }
   return 0;
 }
+
+/* ---------------------------------------------------------------------------------------
+ * TimeToCollisionObservation (observation.py:114-151) over compute_ttc_grid
+ * (finite_mdp.py:104-167), on the single straight road: every vehicle is on the ego's road
+ * with the same lane count, so `lane = [other.lane_index[2]]` (finite_mdp.py:142-149).
+ */
+int oracle_observe_ttc(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                       const ttrl_ttc_cfg_t* cfg, float* out) {
+  if (check(s) || !cfg || !out) return TTRL_E_ARG;
+  S o = view(s);
+  const int NS = P->n_target_speeds, NL = R->n_lanes, T = cfg->horizon_bins;
+  const int OL = cfg->obs_lanes, OS = cfg->obs_speeds;
+#pragma omp parallel
+  {
+  double* grid = (double*)malloc(sizeof(double) * NS * NL * T);
+#pragma omp for schedule(static)
+  for (int e = 0; e < o.E; ++e) {
+    const int base = e * o.N, ego = base;
+    for (int k = 0; k < NS * NL * T; ++k) grid[k] = 0;
+    const double ec = cos(o.h[ego]), es = sin(o.h[ego]);
+    for (int si = 0; si < NS; ++si) {
+      const double ego_speed = P->target_speeds[si];             /* index_to_speed controller.py:317-324 */
+      for (int j = 0; j < o.N; ++j) {                             /* env.road.vehicles, list order */
+        const int k = base + j;
+        if (j == 0 || o.kind[k] == TTRL_ABSENT || ego_speed == o.v[k]) continue;
+        const double margin = P->length / 2 + P->length / 2;
+        const double pts[3][2] = {{0, 1}, {-margin, 0.5}, {margin, 0.5}};
+        for (int c = 0; c < 3; ++c) {
+          const double distance = lane_distance(&o, R, base, 0, j) + pts[c][0];
+          const double proj = o.v[k] * (cos(o.h[k]) * ec + sin(o.h[k]) * es);
+          const double ttc = distance / not_zero(ego_speed - proj);
+          if (ttc < 0) continue;
+          const int l = o.lane[k];
+          const double q = ttc / cfg->time_quantization;
+          const double times[2] = {q, ceil(q)};                   /* int() of a non-negative value */
+          for (int u = 0; u < 2; ++u) {
+            if (!(times[u] < (double)T)) continue;
+            const int t = (int)times[u];
+            double* g = &grid[(si * NL + l) * T + t];
+            if (pts[c][1] > *g) *g = pts[c][1];                    /* np.maximum */
+          }
+        }
+      }
+    }
+    /* observation.py:136-151: pad lanes with ones, window of obs_lanes around the ego's
+     * lane; repeat the first / last speed rows (1 + NS) times, window of obs_speeds */
+    const int lane = o.lane[ego], sidx = o.sidx[ego];
+    float* ob = out + (size_t)e * OS * OL * T;
+    for (int a = 0; a < OS; ++a) {
+      const int row = NS + sidx - OS / 2 + a;                      /* row of the repeated array */
+      int sp = row < 1 + NS ? 0 : (row >= 2 * NS ? NS - 1 : row - NS);
+      for (int b = 0; b < OL; ++b) {
+        const int l = lane - OL / 2 + b;
+        for (int t = 0; t < T; ++t)
+          ob[(a * OL + b) * T + t] = (l < 0 || l >= NL) ? 1.0f : (float)grid[(sp * NL + l) * T + t];
+      }
+    }
+  }
+  free(grid);
+  }
+  return TTRL_OK;
+}
+
+/* utils.distance_to_rect utils.py:386-413 for the ray [r, q] and rectangle corners a, b, c, d */
+static double distance_to_rect(const double r[2], const double q[2], double c[4][2]) {
+  double ux = c[1][0] - c[0][0], uy = c[1][1] - c[0][1], vx = c[3][0] - c[0][0], vy = c[3][1] - c[0][1];
+  const double nu = sqrt(ux * ux + uy * uy), nv = sqrt(vx * vx + vy * vy);
+  ux /= nu; uy /= nu; vx /= nv; vy /= nv;
+  const double qrx = q[0] - r[0], qry = q[1] - r[1];
+  const double rqu = qrx * ux + qry * uy, rqv = qrx * vx + qry * vy;
+  double i1[2] = {((c[0][0] - r[0]) * ux + (c[0][1] - r[1]) * uy) / rqu,
+                  ((c[1][0] - r[0]) * ux + (c[1][1] - r[1]) * uy) / rqu};
+  double i2[2] = {((c[0][0] - r[0]) * vx + (c[0][1] - r[1]) * vy) / rqv,
+                  ((c[3][0] - r[0]) * vx + (c[3][1] - r[1]) * vy) / rqv};
+  if (!(rqu >= 0)) { const double t = i1[0]; i1[0] = i1[1]; i1[1] = t; }
+  if (!(rqv >= 0)) { const double t = i2[0]; i2[0] = i2[1]; i2[1] = t; }
+  if (interval_distance(i1[0], i1[1], i2[0], i2[1]) <= 0 && interval_distance(0, 1, i1[0], i1[1]) <= 0 &&
+      interval_distance(0, 1, i2[0], i2[1]) <= 0)
+    return (i1[0] > i2[0] ? i1[0] : i2[0]) * sqrt(qrx * qrx + qry * qry);
+  return INFINITY;
+}
+
+static int angle_to_index(double angle, double step, int cells) {  /* observation.py:761-762 */
+  long k = (long)floor(angle / step) % cells;
+  return (int)(k < 0 ? k + cells : k);
+}
+
+/* LidarObservation.trace observation.py:704-752 (obstacles: the other vehicles, list order) */
+int oracle_observe_lidar(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                         const ttrl_lidar_cfg_t* cfg, float* out) {
+  (void)R;
+  if (check(s) || !cfg || !out || cfg->cells < 1 || cfg->cells > 64) return TTRL_E_ARG;
+  S o = view(s);
+  const int C = cfg->cells;
+  const double range = cfg->maximum_range, step = 2 * PI / C;
+#pragma omp parallel for schedule(static)
+  for (int e = 0; e < o.E; ++e) {
+    const int base = e * o.N, ego = base;
+    double grid[64][2];
+    for (int c = 0; c < C; ++c) grid[c][0] = grid[c][1] = range;
+    const double ox = o.x[ego], oy = o.y[ego];
+    const double ovx = o.v[ego] * cos(o.h[ego]), ovy = o.v[ego] * sin(o.h[ego]);
+    for (int j = 1; j < o.N; ++j) {
+      const int k = base + j;
+      if (o.kind[k] == TTRL_ABSENT) continue;
+      const double dx = o.x[k] - ox, dy = o.y[k] - oy;
+      const double center_distance = sqrt(dx * dx + dy * dy);
+      if (center_distance > range) continue;
+      const double vx = o.v[k] * cos(o.h[k]) - ovx, vy = o.v[k] * sin(o.h[k]) - ovy;
+      const int ci = angle_to_index(atan2(dy, dx) + step / 2, step, C);
+      const double distance = center_distance - P->width / 2;
+      if (distance <= grid[ci][0]) {
+        grid[ci][0] = distance;
+        grid[ci][1] = vx * cos(ci * step) + vy * sin(ci * step);
+      }
+      /* utils.rect_corners utils.py:126-155: rotation @ corners + center */
+      const double hl = P->length / 2, hw = P->width / 2, c = cos(o.h[k]), sn = sin(o.h[k]);
+      const double lc[4][2] = {{-hl, -hw}, {-hl, hw}, {hl, hw}, {hl, -hw}};
+      double corners[4][2];
+      double amin = 0, amax = 0;
+      for (int q = 0; q < 4; ++q) {
+        corners[q][0] = c * lc[q][0] + (-sn) * lc[q][1] + o.x[k];
+        corners[q][1] = sn * lc[q][0] + c * lc[q][1] + o.y[k];
+        const double a = atan2(corners[q][1] - oy, corners[q][0] - ox) + step / 2;
+        if (q == 0 || a < amin) amin = a;
+        if (q == 0 || a > amax) amax = a;
+      }
+      if (amin < -PI / 2 && -PI / 2 < PI / 2 && PI / 2 < amax) {  /* corners wrap around +pi */
+        const double t = amin;
+        amin = amax;
+        amax = t + 2 * PI;
+      }
+      const int start = angle_to_index(amin, step, C), end = angle_to_index(amax, step, C);
+      const int n = start < end ? end - start + 1 : (C - start) + end + 1;
+      for (int u = 0; u < n; ++u) {
+        const int idx = start < end ? start + u : (u < C - start ? start + u : u - (C - start));
+        const double dirx = cos(idx * step), diry = sin(idx * step);
+        const double r[2] = {ox, oy}, qq[2] = {ox + range * dirx, oy + range * diry};
+        const double d = distance_to_rect(r, qq, corners);
+        if (d <= grid[idx][0]) {
+          grid[idx][0] = d;
+          grid[idx][1] = vx * dirx + vy * diry;
+        }
+      }
+    }
+    float* ob = out + (size_t)e * C * 2;
+    for (int c = 0; c < C; ++c) {
+      ob[2 * c] = (float)(cfg->normalize ? grid[c][0] / range : grid[c][0]);
+      ob[2 * c + 1] = (float)(cfg->normalize ? grid[c][1] / range : grid[c][1]);
+    }
+  }
+  return TTRL_OK;
+}

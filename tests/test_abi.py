@@ -35,7 +35,7 @@ def test_library_loads_and_exports_every_declared_symbol():
 def test_ctypes_mirror_matches_c_layout(tmp_path):
     structs = {"ttrl_lane_table_t": _abi.LaneTable, "ttrl_params_t": _abi.Params, "ttrl_state_t": _abi.State,
                "ttrl_kin_cfg_t": _abi.KinCfg, "ttrl_grid_cfg_t": _abi.GridCfg, "ttrl_reset_cfg_t": _abi.ResetCfg,
-               "ttrl_reward_cfg_t": _abi.RewardCfg}
+               "ttrl_reward_cfg_t": _abi.RewardCfg, "ttrl_ttc_cfg_t": _abi.TtcCfg, "ttrl_lidar_cfg_t": _abi.LidarCfg}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "ttrl_mi355x.h"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')

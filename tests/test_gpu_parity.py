@@ -246,3 +246,42 @@ def test_close_pairs_collisions_vs_oracle(dtype, hip_device):
         else:
             assert bad <= E * n * 2e-3, bad
             dev.load_numpy(h.a)  # re-sync so fp32 drift does not compound
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+@pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.split("/")[-1][:-4])
+def test_ttc_and_lidar_vs_golden(path, dtype, hip_device):
+    """TimeToCollision (reference compute_ttc_grid) and Lidar observations on the GPU."""
+    from topotrafficrl_amd.observation import lidar, time_to_collision
+    d = load_golden(path)
+    lanes = _abi.lane_table_from_arrays(d["lane_table"])
+    net = RoadNetwork(lanes)
+    for p in range(int(d["meta"][2]) + 1):
+        dev = to_dev(HostState.from_golden(d, 15 * p), hip_device, dtype)
+        ttc = time_to_collision(dev, net, P, _abi.ttc_cfg()).cpu().numpy()[0]
+        lid = lidar(dev, net, P, _abi.lidar_cfg()).cpu().numpy()[0]
+        if dtype == "f64":
+            assert np.array_equal(ttc, d["ttc"][p])
+            assert np.max(np.abs(lid - d["lidar"][p])) <= 1e-6
+        else:  # fp32: a cell whose time or ray boundary falls within fp32 rounding may move
+            assert np.mean(ttc != d["ttc"][p]) <= 0.02
+            assert np.mean(np.abs(lid - d["lidar"][p]) > 1e-3) <= 0.05
+
+
+def test_ttc_and_lidar_random_batch_vs_oracle(hip_device):
+    """Many envs, padded slots, crashes: GPU == oracle (f64)."""
+    E, n = 64, 48
+    lanes = _abi.straight_lane_table(4)
+    o = Oracle(lanes, P)
+    h = HostState(E, n)
+    o.reset_highway(h, _abi.reset_cfg(40, lanes), list(range(E)))
+    o.simulate(h, np.random.default_rng(0).integers(0, 5, E).astype(np.int32), 15, 1 / 15)
+    dev = to_dev(h, hip_device)
+    net = RoadNetwork(lanes)
+    from topotrafficrl_amd.observation import lidar, time_to_collision
+    for cells, rng_ in ((16, 60.0), (64, 35.0), (7, 100.0)):
+        lc = _abi.lidar_cfg(cells, rng_)
+        assert np.max(np.abs(lidar(dev, net, P, lc).cpu().numpy() - o.observe_lidar(h, lc))) <= 1e-6
+    for hz, pf in ((10, 1), (5, 2)):
+        tc = _abi.ttc_cfg(hz, pf)
+        assert np.array_equal(time_to_collision(dev, net, P, tc).cpu().numpy(), o.observe_ttc(h, tc))

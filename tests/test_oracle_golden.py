@@ -4,7 +4,8 @@ unmodified reference (oracle/gen_golden.py).  CPU only.
 Pinned here: Road.act/Road.step per frame (positions/speeds/headings to 1e-12, every
 discrete field exact), the fused 15-frame policy step, Road.neighbour_vehicles,
 Kinematics (5x5 default, 15x7 env.json) and OccupancyGrid (7x32x32 dense, 4x11x11 on_road)
-observations bit-identical, and the numpy-PCG64 scene generator bit-identical.
+observations bit-identical, TimeToCollision exact and Lidar to float32 rounding, and the
+numpy-PCG64 scene generator bit-identical.
 """
 import numpy as np
 import pytest
@@ -90,6 +91,19 @@ def test_observations(name, cases):
         assert np.array_equal(obs[0], d["kin15"][p]) and np.array_equal(ids[0], d["kin15_ids"][p])
         assert np.array_equal(o.observe_grid(h, G7)[0], d["grid7"][p])
         assert np.array_equal(o.observe_grid(h, GR)[0], d["grid_onroad"][p])
+
+
+@pytest.mark.parametrize("name", [IDS(p) for p in golden_files()])
+def test_ttc_and_lidar_observations(name, cases):
+    """TimeToCollision (the reference's own compute_ttc_grid, finite_mdp.py:104-167) exact;
+    Lidar (LidarObservation.trace over utils.rect_corners / distance_to_rect) to float32."""
+    d = cases[name]
+    o = Oracle(_abi.lane_table_from_arrays(d["lane_table"]), P)
+    for p in range(int(d["meta"][2]) + 1):
+        h = HostState.from_golden(d, 15 * p)
+        assert np.array_equal(o.observe_ttc(h, _abi.ttc_cfg())[0], d["ttc"][p])
+        lid = o.observe_lidar(h, _abi.lidar_cfg())[0]
+        assert np.max(np.abs(lid - d["lidar"][p])) <= 1e-6 * (1 + np.max(np.abs(d["lidar"][p])))
 
 
 @pytest.mark.parametrize("name", [IDS(p) for p in golden_files("highway_*")])

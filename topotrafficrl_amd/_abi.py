@@ -88,6 +88,15 @@ class RewardCfg(C.Structure):
                 ("duration", C.c_double)]
 
 
+class TtcCfg(C.Structure):
+    _fields_ = [("horizon_bins", C.c_int32), ("obs_lanes", C.c_int32), ("obs_speeds", C.c_int32),
+                ("_pad", C.c_int32), ("time_quantization", C.c_double)]
+
+
+class LidarCfg(C.Structure):
+    _fields_ = [("cells", C.c_int32), ("normalize", C.c_int32), ("maximum_range", C.c_double)]
+
+
 # ----------------------------------------------------------------------------- builders
 def straight_lane_table(lanes: int = 4, start: float = 0.0, length: float = 10000.0, angle: float = 0.0,
                         speed_limit: float = 30.0, width: float = 4.0, forbidden=None) -> LaneTable:
@@ -250,6 +259,26 @@ def reward_cfg(collision_reward=-1.0, high_speed_reward=0.4, reward_speed_range=
     c.speed_lo, c.speed_hi = float(reward_speed_range[0]), float(reward_speed_range[1])
     c.normalize_reward, c.offroad_terminal = int(normalize_reward), int(offroad_terminal)
     c.duration = float(duration)
+    return c
+
+
+def ttc_cfg(horizon: float = 10, policy_frequency: float = 1, **_ignored) -> TtcCfg:
+    """TimeToCollisionObservation(horizon) (observation.py:114-151) at the env's policy frequency."""
+    c = TtcCfg()
+    c.horizon_bins = int(horizon * policy_frequency)
+    c.obs_lanes, c.obs_speeds = 3, 3
+    c.time_quantization = 1.0 / float(policy_frequency)
+    if not 1 <= c.horizon_bins <= 64:
+        raise ValueError("TTC horizon * policy_frequency must be in [1, 64]")
+    return c
+
+
+def lidar_cfg(cells: int = 16, maximum_range: float = 60.0, normalize: bool = True, **_ignored) -> LidarCfg:
+    """LidarObservation(cells, maximum_range, normalize) (observation.py:681-698)."""
+    c = LidarCfg()
+    c.cells, c.maximum_range, c.normalize = int(cells), float(maximum_range), int(bool(normalize))
+    if not 1 <= c.cells <= 64:
+        raise ValueError("Lidar cells must be in [1, 64]")
     return c
 
 

@@ -24,6 +24,8 @@ _SIGS = {
     "ttrl_neighbours": ([_P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_observe_kinematics": ([_P, _P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_observe_grid": ([_P, _P, _P, _P, _P, _P], C.c_int),
+    "ttrl_observe_ttc": ([_P, _P, _P, _P, _P, _P], C.c_int),
+    "ttrl_observe_lidar": ([_P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_reset_highway": ([_P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_reset_highway_seeded": ([_P, _P, _P, _P, _P, C.c_int32, _P, _P], C.c_int),
     "ttrl_seed_pcg64": ([_P, C.c_int32, _P], C.c_int),

@@ -1563,6 +1563,175 @@ __device__ __forceinline__ unsigned pcg_bounded(Pcg& g, unsigned n) {  // Genera
   return (unsigned)(m >> 32);
 }
 
+// ---------------------------------------------------------------------------------------
+// TimeToCollisionObservation (observation.py:114-151) over compute_ttc_grid
+// (finite_mdp.py:104-167).  One 64-thread workgroup per env, one lane per other vehicle;
+// grid cells are `np.maximum` of costs {0.5, 1}, kept as OR-ed bits in LDS (bit0: 0.5 seen,
+// bit1: 1 seen), so the list order of the reference's loop does not matter.
+template <typename T>
+__global__ void __launch_bounds__(64) ttc_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P,
+                                                     ttrl_ttc_cfg_t cfg, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* grid = (int*)smem;
+  const int env = blockIdx.x, tid = threadIdx.x;
+  const int N = st.n_veh, NS = P.n_target_speeds, NL = R.n_lanes, TB = cfg.horizon_bins;
+  const size_t base = (size_t)env * N;
+  for (int c = tid; c < NS * NL * TB; c += 64) grid[c] = 0;
+  __syncthreads();
+  const T* X = (const T*)st.x; const T* Y = (const T*)st.y; const T* H = (const T*)st.heading;
+  const T* Vv = (const T*)st.speed;
+  const int el = st.lane[base];
+  const T ex = X[base], ey = Y[base];
+  const T ec = t_cos(H[base]), es = t_sin(H[base]);
+  const T sdx = T(R.dir_x[el]), sdy = T(R.dir_y[el]), sx0 = T(R.start_x[el]), sy0 = T(R.start_y[el]);
+  const T s_ego = (ex - sx0) * sdx + (ey - sy0) * sdy;
+  for (int j = 1 + tid; j < N; j += 64) {
+    if (st.kind[base + j] == TTRL_ABSENT) continue;
+    const T vo = Vv[base + j];
+    const T ld = (X[base + j] - sx0) * sdx + (Y[base + j] - sy0) * sdy - s_ego;  // lane_distance_to
+    const T proj = vo * (t_cos(H[base + j]) * ec + t_sin(H[base + j]) * es);
+    const int lo = st.lane[base + j];
+    const T margin = T(P.length) / T(2) + T(P.length) / T(2);
+    for (int si = 0; si < NS; ++si) {
+      const T ego_speed = T(P.target_speeds[si]);
+      if (ego_speed == vo) continue;
+      const T den = not_zero(ego_speed - proj);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const T m = c == 0 ? T(0) : (c == 1 ? -margin : margin);
+        const T ttc = (ld + m) / den;
+        if (ttc < T(0)) continue;
+        const T q = ttc / T(cfg.time_quantization);
+        const T tq[2] = {q, ceil(q)};
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          if (tq[u] < T(TB)) atomicOr(&grid[(si * NL + lo) * TB + (int)tq[u]], c == 0 ? 2 : 1);
+      }
+    }
+  }
+  __syncthreads();
+  // observation.py:136-151: lane window padded with ones, speed rows repeated at the ends
+  const int OS = cfg.obs_speeds, OL = cfg.obs_lanes, sidx = st.speed_index[base];
+  float* ob = out + (size_t)env * OS * OL * TB;
+  for (int k = tid; k < OS * OL * TB; k += 64) {
+    const int a = k / (OL * TB), b = (k / TB) % OL, t = k % TB;
+    const int row = NS + sidx - OS / 2 + a;
+    const int sp = row < 1 + NS ? 0 : (row >= 2 * NS ? NS - 1 : row - NS);
+    const int l = el - OL / 2 + b;
+    float v = 1.0f;
+    if (l >= 0 && l < NL) {
+      const int g = grid[(sp * NL + l) * TB + t];
+      v = (g & 2) ? 1.0f : ((g & 1) ? 0.5f : 0.0f);
+    }
+    ob[k] = v;
+  }
+}
+
+// utils.distance_to_rect utils.py:386-413 (ray [r, q], rectangle corners c[0..3])
+template <typename T>
+__device__ __forceinline__ T ray_rect(T rx, T ry, T qx, T qy, const T (&c)[4][2]) {
+  T ux = c[1][0] - c[0][0], uy = c[1][1] - c[0][1], vx = c[3][0] - c[0][0], vy = c[3][1] - c[0][1];
+  const T nu = sqrt(ux * ux + uy * uy), nv = sqrt(vx * vx + vy * vy);
+  ux /= nu; uy /= nu; vx /= nv; vy /= nv;
+  const T qrx = qx - rx, qry = qy - ry;
+  const T rqu = qrx * ux + qry * uy, rqv = qrx * vx + qry * vy;
+  T a0 = ((c[0][0] - rx) * ux + (c[0][1] - ry) * uy) / rqu, a1 = ((c[1][0] - rx) * ux + (c[1][1] - ry) * uy) / rqu;
+  T b0 = ((c[0][0] - rx) * vx + (c[0][1] - ry) * vy) / rqv, b1 = ((c[3][0] - rx) * vx + (c[3][1] - ry) * vy) / rqv;
+  if (!(rqu >= T(0))) { const T t = a0; a0 = a1; a1 = t; }
+  if (!(rqv >= T(0))) { const T t = b0; b0 = b1; b1 = t; }
+  auto idist = [](T mina, T maxa, T minb, T maxb) { return mina < minb ? minb - maxa : mina - maxb; };
+  if (idist(a0, a1, b0, b1) <= T(0) && idist(T(0), T(1), a0, a1) <= T(0) && idist(T(0), T(1), b0, b1) <= T(0))
+    return (a0 > b0 ? a0 : b0) * sqrt(qrx * qrx + qry * qry);
+  return K<T>::inf();
+}
+
+__device__ __forceinline__ unsigned long long ordered_bits(double d) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(d);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+// LidarObservation.trace (observation.py:704-752).  The reference updates a cell whenever a
+// candidate's distance is <= the cell's current one, obstacle by obstacle in list order (its
+// centre cell, then the cells its corners span): the final cell is the minimum distance, and
+// among equal distances the last candidate in that order.  One workgroup per env, one lane per
+// obstacle: pass 1 takes the LDS min of the ordered distance bits, pass 2 the max order among
+// the candidates at that minimum, pass 3 lets that candidate write its relative speed.
+template <typename T>
+__global__ void __launch_bounds__(64) lidar_obs_kernel(ttrl_state_t st, ttrl_params_t P, ttrl_lidar_cfg_t cfg,
+                                                       float* __restrict__ out) {
+  __shared__ unsigned long long key[64];
+  __shared__ int ord[64];
+  __shared__ double dist[64], vel[64];
+  const int env = blockIdx.x, tid = threadIdx.x;
+  const int N = st.n_veh, C = cfg.cells;
+  const size_t base = (size_t)env * N;
+  const double range = cfg.maximum_range;
+  const T step = T(2) * Tpi<T>() / T(C);
+  if (tid < C) { key[tid] = ordered_bits(range); ord[tid] = -1; dist[tid] = range; vel[tid] = range; }
+  __syncthreads();
+  const T* X = (const T*)st.x; const T* Y = (const T*)st.y; const T* H = (const T*)st.heading;
+  const T* Vv = (const T*)st.speed;
+  const T ox = X[base], oy = Y[base];
+  const T ovx = Vv[base] * t_cos(H[base]), ovy = Vv[base] * t_sin(H[base]);
+  auto to_index = [&](T a) {  // int(floor(a / step)) % cells, Python modulo
+    long k = (long)floor(a / step) % C;
+    return (int)(k < 0 ? k + C : k);
+  };
+  for (int pass = 0; pass < 3; ++pass) {
+    for (int j = 1 + tid; j < N; j += 64) {
+      if (st.kind[base + j] == TTRL_ABSENT) continue;
+      const T dx = X[base + j] - ox, dy = Y[base + j] - oy;
+      const T center_distance = sqrt(dx * dx + dy * dy);
+      if (center_distance > T(range)) continue;
+      const T c = t_cos(H[base + j]), sn = t_sin(H[base + j]);
+      const T vx = Vv[base + j] * c - ovx, vy = Vv[base + j] * sn - ovy;
+      auto offer = [&](int cell, T d, int order) {
+        if (d != d) return;  // NaN never satisfies distance <= grid
+        const unsigned long long kb = ordered_bits((double)d);
+        if (pass == 0) atomicMin(&key[cell], kb);
+        else if (kb == key[cell]) {
+          if (pass == 1) atomicMax(&ord[cell], order);
+          else if (ord[cell] == order) {
+            dist[cell] = (double)d;
+            vel[cell] = (double)(vx * t_cos(T(cell) * step) + vy * t_sin(T(cell) * step));
+          }
+        }
+      };
+      offer(to_index(atan2(dy, dx) + step / T(2)), center_distance - T(P.width) / T(2), 2 * j);
+      const T hl = T(P.length) / T(2), hw = T(P.width) / T(2);
+      const T lc[4][2] = {{-hl, -hw}, {-hl, hw}, {hl, hw}, {hl, -hw}};
+      T cr[4][2];
+      T amin = T(0), amax = T(0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // utils.rect_corners utils.py:126-155
+        cr[q][0] = c * lc[q][0] + (-sn) * lc[q][1] + X[base + j];
+        cr[q][1] = sn * lc[q][0] + c * lc[q][1] + Y[base + j];
+        const T a = atan2(cr[q][1] - oy, cr[q][0] - ox) + step / T(2);
+        if (q == 0 || a < amin) amin = a;
+        if (q == 0 || a > amax) amax = a;
+      }
+      if (amin < -Tpi<T>() / T(2) && Tpi<T>() / T(2) < amax) {  // corners wrap around +pi
+        const T t = amin;
+        amin = amax;
+        amax = t + T(2) * Tpi<T>();
+      }
+      const int start = to_index(amin), end = to_index(amax);
+      const int n = start < end ? end - start + 1 : (C - start) + end + 1;
+      for (int u = 0; u < n; ++u) {
+        const int idx = start < end ? start + u : (u < C - start ? start + u : u - (C - start));
+        const T dirx = t_cos(T(idx) * step), diry = t_sin(T(idx) * step);
+        offer(idx, ray_rect(ox, oy, ox + T(range) * dirx, oy + T(range) * diry, cr), 2 * j + 1);
+      }
+    }
+    __syncthreads();
+  }
+  if (tid < C) {  // observe(): obs /= maximum_range when normalize
+    const double div = cfg.normalize ? range : 1.0;
+    out[((size_t)env * C + tid) * 2] = (float)(dist[tid] / div);
+    out[((size_t)env * C + tid) * 2 + 1] = (float)(vel[tid] / div);
+  }
+}
+
 // numpy's SeedSequence(entropy words) -> generate_state(4, uint64) -> PCG64 seeding
 // (numpy/random/bit_generator.pyx SeedSequence.mix_entropy / generate_state with pool_size 4,
 // _pcg64.pyx + pcg64.h pcg64_set_seed: state = 0, inc = 2 * initseq + 1, step, state += seed,
@@ -1910,6 +2079,37 @@ int ttrl_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
     hipLaunchKernelGGL(grid_obs_kernel<double>, dim3(s->n_envs), dim3(256), lds, st, *s, *road, *p, *cfg, out);
   else
     hipLaunchKernelGGL(grid_obs_kernel<float>, dim3(s->n_envs), dim3(256), lds, st, *s, *road, *p, *cfg, out);
+  return launch_status();
+}
+
+int ttrl_observe_ttc(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                     const ttrl_ttc_cfg_t* cfg, float* out, void* stream) {
+  int rc = check_state(s, road);
+  if (rc) return rc;
+  if (!p || !cfg || !out || cfg->horizon_bins < 1 || cfg->horizon_bins > 64 || cfg->obs_lanes < 1 ||
+      cfg->obs_speeds < 1 || !(cfg->time_quantization > 0) || p->n_target_speeds < 1 || p->n_target_speeds > 8)
+    return TTRL_E_ARG;
+  if (s->n_envs == 0) return TTRL_OK;
+  const size_t lds = sizeof(int) * p->n_target_speeds * road->n_lanes * cfg->horizon_bins;
+  hipStream_t st = (hipStream_t)stream;
+  if (s->dtype == TTRL_F64)
+    hipLaunchKernelGGL(ttc_obs_kernel<double>, dim3(s->n_envs), dim3(64), lds, st, *s, *road, *p, *cfg, out);
+  else
+    hipLaunchKernelGGL(ttc_obs_kernel<float>, dim3(s->n_envs), dim3(64), lds, st, *s, *road, *p, *cfg, out);
+  return launch_status();
+}
+
+int ttrl_observe_lidar(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                       const ttrl_lidar_cfg_t* cfg, float* out, void* stream) {
+  int rc = check_state(s, road);
+  if (rc) return rc;
+  if (!p || !cfg || !out || cfg->cells < 1 || cfg->cells > 64 || !(cfg->maximum_range > 0)) return TTRL_E_ARG;
+  if (s->n_envs == 0) return TTRL_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (s->dtype == TTRL_F64)
+    hipLaunchKernelGGL(lidar_obs_kernel<double>, dim3(s->n_envs), dim3(64), 0, st, *s, *p, *cfg, out);
+  else
+    hipLaunchKernelGGL(lidar_obs_kernel<float>, dim3(s->n_envs), dim3(64), 0, st, *s, *p, *cfg, out);
   return launch_status();
 }
 

@@ -2,9 +2,11 @@
 
 ``BatchedKinematicObservation``     <- KinematicObservation      observation.py:154-275
 ``BatchedOccupancyGridObservation`` <- OccupancyGridObservation  observation.py:278-498
+``BatchedTimeToCollisionObservation`` <- TimeToCollisionObservation observation.py:114-151
+``BatchedLidarObservation``         <- LidarObservation          observation.py:677-768
 ``observation_factory``             <- observation_factory       observation.py:771-793
 
-Both accept the reference's config dict keys; ``observe()`` returns a float32 device
+All accept the reference's config dict keys; ``observe()`` returns a float32 device
 tensor [n_envs, ...] computed by the HIP kernels for every env's ego.
 """
 from __future__ import annotations
@@ -41,6 +43,25 @@ def occupancy_grid(state, network, params, cfg: _abi.GridCfg, out=None):
     if out is None:
         out = torch.empty(shape, dtype=torch.float32, device=state.device)
     _lib.call("ttrl_observe_grid", C.byref(state.struct()), C.byref(network.table), C.byref(params),
+              C.byref(cfg), out.data_ptr(), _stream(state.device))
+    return out
+
+
+def time_to_collision(state, network, params, cfg: _abi.TtcCfg, out=None):
+    """TimeToCollisionObservation.observe for every env: [E, 3 speeds, 3 lanes, T] float32."""
+    shape = (state.n_envs, cfg.obs_speeds, cfg.obs_lanes, cfg.horizon_bins)
+    if out is None:
+        out = torch.empty(shape, dtype=torch.float32, device=state.device)
+    _lib.call("ttrl_observe_ttc", C.byref(state.struct()), C.byref(network.table), C.byref(params),
+              C.byref(cfg), out.data_ptr(), _stream(state.device))
+    return out
+
+
+def lidar(state, network, params, cfg: _abi.LidarCfg, out=None):
+    """LidarObservation.observe for every env: [E, cells, 2] float32 (distance, relative speed)."""
+    if out is None:
+        out = torch.empty((state.n_envs, cfg.cells, 2), dtype=torch.float32, device=state.device)
+    _lib.call("ttrl_observe_lidar", C.byref(state.struct()), C.byref(network.table), C.byref(params),
               C.byref(cfg), out.data_ptr(), _stream(state.device))
     return out
 
@@ -117,6 +138,36 @@ class BatchedOccupancyGridObservation(BatchedObservationType):
         return self._out
 
 
+class BatchedTimeToCollisionObservation(BatchedObservationType):
+    def __init__(self, env, horizon: int = 10, **kwargs):
+        super().__init__(env)
+        self.horizon = horizon
+        self.cfg = _abi.ttc_cfg(horizon, env.config["policy_frequency"])
+
+    def space(self):
+        return Box(low=0, high=1, shape=(self.cfg.obs_speeds, self.cfg.obs_lanes, self.cfg.horizon_bins),
+                   dtype="float32")
+
+    def observe(self) -> torch.Tensor:
+        road = self.env.road
+        return time_to_collision(road.state, road.network, road.params, self.cfg)
+
+
+class BatchedLidarObservation(BatchedObservationType):
+    def __init__(self, env, cells: int = 16, maximum_range: float = 60, normalize: bool = True, **kwargs):
+        super().__init__(env)
+        self.cells, self.maximum_range, self.normalize = cells, maximum_range, normalize
+        self.cfg = _abi.lidar_cfg(cells, maximum_range, normalize)
+
+    def space(self):
+        high = 1 if self.normalize else self.maximum_range
+        return Box(low=-high, high=high, shape=(self.cells, 2), dtype="float32")
+
+    def observe(self) -> torch.Tensor:
+        road = self.env.road
+        return lidar(road.state, road.network, road.params, self.cfg)
+
+
 def observation_factory(env, config: dict) -> BatchedObservationType:
     """observation.py:771-793 for the hot-path types."""
     t = config["type"]
@@ -124,7 +175,11 @@ def observation_factory(env, config: dict) -> BatchedObservationType:
         return BatchedKinematicObservation(env, **config)
     if t == "OccupancyGrid":
         return BatchedOccupancyGridObservation(env, **config)
-    if t in ("TimeToCollision", "KinematicsGoal", "GrayscaleObservation", "AttributesObservation",
-             "MultiAgentObservation", "TupleObservation", "LidarObservation", "ExitObservation"):
+    if t == "TimeToCollision":
+        return BatchedTimeToCollisionObservation(env, **config)
+    if t == "LidarObservation":
+        return BatchedLidarObservation(env, **config)
+    if t in ("KinematicsGoal", "GrayscaleObservation", "AttributesObservation", "MultiAgentObservation",
+             "TupleObservation", "ExitObservation"):
         raise NotImplementedError(f"observation type {t!r} is SURVEY.md §8(f) 'next' / out of scope")
     raise ValueError("Unknown observation type")
