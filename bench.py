@@ -110,10 +110,18 @@ def main():
 
     from topotrafficrl_amd import sharding
     rank, local, world = sharding.world()
+    # TTRL_BENCH_SHARED_GPU=1 (rehearsal on a one-GPU box): every rank on cuda:0, gloo for the
+    # barrier and the max-over-ranks reduction; the real multi-GPU run uses one GPU per rank + RCCL
+    shared = os.environ.get("TTRL_BENCH_SHARED_GPU") == "1"
+    if shared:
+        local = 0
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -187,7 +195,7 @@ def main():
     elapsed = time.perf_counter() - t0
     road.simulate = orig_sim
     kern_ms = float(np.mean(kern_warm)) if sg is not None else float(np.mean([s.elapsed_time(e) for s, e in ev]))
-    elapsed = sharding.max_over_ranks(elapsed, device=dev)
+    elapsed = sharding.max_over_ranks(elapsed, device=None if shared else dev)
 
     veh_steps = world * E * N * 15 * args.steps
     value = veh_steps / elapsed
