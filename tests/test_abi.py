@@ -16,7 +16,7 @@ HEADER = os.path.join(ROOT, "include", "ttrl_mi355x.h")
 
 def declared():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^int (ttrl_\w+)\(", txt, re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t) (ttrl_\w+)\(", txt, re.M)))
 
 
 def test_library_loads_and_exports_every_declared_symbol():

@@ -198,3 +198,23 @@ def test_step_graph_replays_the_same_rollout(hip_device):
         o2, r2, te2, tr2 = sg.replay()
         assert torch.equal(o1, o2) and torch.equal(r1, r2) and torch.equal(te1, te2)
     assert torch.equal(eager.state["x"], graphed.state["x"])
+
+
+@pytest.mark.parametrize("B", [1, 5, 64, 1000])
+def test_fused_ego_attention_matches_torch_forward(B, hip_device):
+    """ttrl_ego_attention_q (fused HIP forward) == the torch EgoAttentionNetwork in float32."""
+    from topotrafficrl_amd.agent import EgoAttentionNetwork
+    net = EgoAttentionNetwork(5).reset(torch.Generator().manual_seed(B)).to(hip_device)
+    g = torch.Generator(device=hip_device).manual_seed(B)
+    x = torch.rand(B, 15, 7, device=hip_device, generator=g) * 2 - 1
+    x[:, :, 0] = (torch.rand(B, 15, device=hip_device, generator=g) < 0.7).float()
+    x[:, 0, 0] = 1.0
+    if B >= 5:
+        x[3, :, 0] = 0.0  # every entity masked: uniform softmax
+    ref = net(x)
+    got = net.fused_q(x)
+    assert torch.allclose(got, ref, rtol=1e-4, atol=1e-5), float((got - ref).abs().max())
+    # packed weights follow parameter updates
+    with torch.no_grad():
+        net.output_layer.predict.bias.add_(1.0)
+    assert torch.allclose(net.fused_q(x), net(x), rtol=1e-4, atol=1e-5)

@@ -30,6 +30,8 @@ _SIGS = {
     "ttrl_reset_highway_seeded": ([_P, _P, _P, _P, _P, C.c_int32, _P, _P], C.c_int),
     "ttrl_seed_pcg64": ([_P, C.c_int32, _P], C.c_int),
     "ttrl_rewards": ([_P, _P, _P, _P, _P, _P, _P, _P], C.c_int),
+    "ttrl_ego_attention_sizes": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P], C.c_int64),
+    "ttrl_ego_attention_q": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, C.c_int32, _P, _P, _P], C.c_int),
 }
 EXPORTS = [k for k in _SIGS]
 

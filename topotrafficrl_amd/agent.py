@@ -12,6 +12,7 @@ no host round trip between env.step and the next action.
 """
 from __future__ import annotations
 
+import ctypes as C
 import math
 
 import torch
@@ -93,6 +94,52 @@ class EgoAttentionNetwork(nn.Module):
                         m.bias.zero_()
         return self
 
+    def packed_weights(self) -> torch.Tensor:
+        """The weights in the ttrl_ego_attention_q packed layout (include/ttrl_mi355x.h), cached
+        until a parameter changes (optimizer steps bump the tensors' versions)."""
+        ps = [self.ego_embedding.layers[0], self.ego_embedding.layers[1], self.others_embedding.layers[0],
+              self.others_embedding.layers[1]]
+        a = self.attention_layer
+        h = self.output_layer
+        tensors = []
+        for lin in ps[:2]:
+            tensors += [lin.weight, lin.bias]
+        for lin in ps[2:]:
+            tensors += [lin.weight, lin.bias]
+        tensors += [a.value_all.weight, a.key_all.weight, a.query_ego.weight, a.attention_combine.weight]
+        tensors += [h.layers[0].weight, h.layers[0].bias, h.layers[1].weight, h.layers[1].bias,
+                    h.predict.weight, h.predict.bias]
+        key = tuple((t.data_ptr(), t._version) for t in tensors)
+        if getattr(self, "_packed_key", None) != key:
+            self._packed = torch.cat([t.detach().reshape(-1).float() for t in tensors]).contiguous()
+            self._packed_key = key
+        return self._packed
+
+    def fused_supported(self) -> bool:
+        e = self.ego_embedding
+        return (len(e.layers) == 2 and e.layers[0].out_features == 64 and e.layers[1].out_features == 64
+                and len(self.others_embedding.layers) == 2 and self.attention_layer.f == 64
+                and len(self.output_layer.layers) == 2 and self.output_layer.layers[0].out_features == 64
+                and self.output_layer.layers[1].out_features == 64 and self.output_layer.predict is not None
+                and self.presence_idx == 0 and e.layers[0].in_features in (5, 7, 8))
+
+    @torch.no_grad()
+    def fused_q(self, x: torch.Tensor) -> torch.Tensor:
+        """Q-values through the fused HIP forward (ttrl_ego_attention_q): inference only."""
+        from . import _lib
+        x = x.contiguous().float()
+        B, NE, F_ = x.shape
+        A = self.output_layer.predict.out_features
+        w = self.packed_weights()
+        lib = _lib.load()
+        n_scratch = C.c_int64()
+        lib.ttrl_ego_attention_sizes(F_, A, B, NE, C.byref(n_scratch))
+        scratch = torch.empty(int(n_scratch.value), dtype=torch.float32, device=x.device)
+        q = torch.empty((B, A), dtype=torch.float32, device=x.device)
+        _lib.call("ttrl_ego_attention_q", x.data_ptr(), B, NE, F_, self.attention_layer.h, w.data_ptr(), A,
+                  scratch.data_ptr(), q.data_ptr(), torch.cuda.current_stream(x.device).cuda_stream)
+        return q
+
     def forward(self, x):
         # contiguous copies: hipBLASLt takes a 6x slower path on the strided [:, 1:, :] view
         ego, others = x[:, 0:1, :].contiguous(), x[:, 1:, :].contiguous()
@@ -105,8 +152,9 @@ class EgoAttentionPolicy:
     """Batched DQN acting: Q = value_net(obs[E, V, F]); epsilon-greedy on the device."""
 
     def __init__(self, device, n_actions: int = 5, seed: int = 0, tau: float = 15000.0, temperature: float = 1.0,
-                 final_temperature: float = 0.05):
+                 final_temperature: float = 0.05, fused: bool = True):
         self.device = torch.device(device)
+        self.fused = fused  # acting through the fused HIP forward on a GPU (training uses the torch graph)
         g = torch.Generator(device="cpu")
         g.manual_seed(seed)
         self.value_net = EgoAttentionNetwork(n_actions).reset(g).to(self.device).eval()
@@ -122,6 +170,8 @@ class EgoAttentionPolicy:
 
     @torch.no_grad()
     def q_values(self, obs: torch.Tensor) -> torch.Tensor:
+        if self.fused and obs.device.type == "cuda" and self.value_net.fused_supported():
+            return self.value_net.fused_q(obs)
         return self.value_net(obs)
 
     @torch.no_grad()
@@ -132,7 +182,7 @@ class EgoAttentionPolicy:
             t = self.time if t is None else t
             self.time = t + 1
             epsilon = self.epsilon(t)
-        q = self.value_net(obs)
+        q = self.q_values(obs)
         greedy = q.argmax(dim=1)
         e = obs.shape[0]
         u = torch.rand(e, device=self.device, generator=self.gen)
