@@ -241,11 +241,12 @@ int ttrl_reset_highway_seeded(const ttrl_state_t* s, const ttrl_lane_table_t* ro
 int ttrl_seed_pcg64(const uint32_t* entropy, int32_t n_words, uint64_t* state4);
 /* EgoAttention Q-values for config 5 (ttrl_agent models.py:157-312, ego_attention_2h.json), float32:
  * obs [batch][n_entities][n_features] (feature 0 = presence), q [batch][n_actions].
- * weights: one packed buffer, torch Linear layouts ([out][in] row-major) in this order:
- *   ego_embedding  W1 [64][F], b1 [64], W2 [64][64], b2 [64]
- *   others_embedding W1 [64][F], b1 [64], W2 [64][64], b2 [64]
+ * weights: one packed buffer, every matrix transposed from torch's Linear.weight to [in][out]
+ * (row-major), in this order:
+ *   ego_embedding  W1 [F][64], b1 [64], W2 [64][64], b2 [64]
+ *   others_embedding W1 [F][64], b1 [64], W2 [64][64], b2 [64]
  *   attention value_all [64][64], key_all [64][64], query_ego [64][64], attention_combine [64][64]
- *   output_layer   W1 [64][64], b1 [64], W2 [64][64], b2 [64], predict W [A][64], b [A]
+ *   output_layer   W1 [64][64], b1 [64], W2 [64][64], b2 [64], predict W [64][A], b [A]
  * ttrl_ego_attention_sizes returns the packed length (floats) and sets *scratch_floats to the
  * scratch the forward needs (caller-allocated device memory). */
 int64_t ttrl_ego_attention_sizes(int32_t n_features, int32_t n_actions, int32_t batch, int32_t n_entities,

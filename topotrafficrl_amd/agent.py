@@ -111,7 +111,9 @@ class EgoAttentionNetwork(nn.Module):
                     h.predict.weight, h.predict.bias]
         key = tuple((t.data_ptr(), t._version) for t in tensors)
         if getattr(self, "_packed_key", None) != key:
-            self._packed = torch.cat([t.detach().reshape(-1).float() for t in tensors]).contiguous()
+            # matrices as [in][out] (Linear.weight transposed): coalesced reads in the kernels
+            self._packed = torch.cat([(t.detach().t() if t.dim() == 2 else t.detach()).reshape(-1).float()
+                                      for t in tensors]).contiguous()
             self._packed_key = key
         return self._packed
 

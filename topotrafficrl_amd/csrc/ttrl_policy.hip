@@ -40,60 +40,88 @@ __host__ __device__ inline PolicyLayout policy_layout(int F, int A) {
   return L;
 }
 
+constexpr int RB = 256;  // rows (lanes) per rows_kernel block
+
+// acc[o] += sum_k Wt[k][o] * in[k] in outer-product order: each k step is 64 independent FMAs
+// (no serial accumulation chain) fed by broadcast float4 reads of the [in][out] weights.
+__device__ __forceinline__ void dense64(const float4* __restrict__ wt, const float (&in)[HD], float (&acc)[HD]) {
+#pragma unroll
+  for (int k = 0; k < HD; ++k) {
+#pragma unroll
+    for (int o = 0; o < HD; o += 4) {
+      const float4 w = wt[(k * HD + o) / 4];
+      acc[o] = fmaf(w.x, in[k], acc[o]);
+      acc[o + 1] = fmaf(w.y, in[k], acc[o + 1]);
+      acc[o + 2] = fmaf(w.z, in[k], acc[o + 2]);
+      acc[o + 3] = fmaf(w.w, in[k], acc[o + 3]);
+    }
+  }
+}
+
 template <int F>
-__global__ void __launch_bounds__(64) rows_kernel(const float* __restrict__ obs, int B, int NE,
+__global__ void __launch_bounds__(RB) rows_kernel(const float* __restrict__ obs, int B, int NE,
                                                   const float* __restrict__ W, int A, float* __restrict__ KT,
                                                   float* __restrict__ VT, float* __restrict__ ET) {
+  // the block's weights (embedding W1, b1, W2, b2, then key / value), transposed to [in][out]
+  // in LDS once; every lane of the block multiplies by the same weights (broadcast reads)
+  __shared__ float4 w2t[HD * HD / 4], wkt[HD * HD / 4], wvt[HD * HD / 4];
+  __shared__ float w1t[F * HD], b1s[HD], b2s[HD];
   const PolicyLayout L = policy_layout(F, A);
-  const int ego_blocks = (B + 63) / 64;
+  const int ego_blocks = (B + RB - 1) / RB;
   const bool ego = (int)blockIdx.x < ego_blocks;
-  const long t = ego ? (long)blockIdx.x * 64 + threadIdx.x : (long)(blockIdx.x - ego_blocks) * 64 + threadIdx.x;
+  const float* w1 = W + (ego ? L.e1w : L.o1w);
+  const float* b1 = W + (ego ? L.e1b : L.o1b);
+  const float* w2 = W + (ego ? L.e2w : L.o2w);
+  const float* b2 = W + (ego ? L.e2b : L.o2b);
+  const int tid = threadIdx.x;
+  float* w2f = reinterpret_cast<float*>(w2t);
+  float* wkf = reinterpret_cast<float*>(wkt);
+  float* wvf = reinterpret_cast<float*>(wvt);
+  for (int i = tid; i < HD * HD; i += RB) {  // packed matrices are [in][out] already
+    w2f[i] = w2[i];
+    wkf[i] = W[L.wk + i];
+    wvf[i] = W[L.wv + i];
+  }
+  for (int i = tid; i < HD * F; i += RB) w1t[i] = w1[i];
+  if (tid < HD) { b1s[tid] = b1[tid]; b2s[tid] = b2[tid]; }
+  __syncthreads();
+  const long t = ego ? (long)blockIdx.x * RB + tid : (long)(blockIdx.x - ego_blocks) * RB + tid;
   const long n_rows = ego ? B : (long)B * (NE - 1);
-  const bool live = t < n_rows;
+  if (t >= n_rows) return;
   const long env = ego ? t : t / (NE - 1);
   const int j = ego ? 0 : 1 + (int)(t % (NE - 1));
   const long row = env * NE + j;
   const long R = (long)B * NE;
   float x[F];
 #pragma unroll
-  for (int k = 0; k < F; ++k) x[k] = live ? obs[row * F + k] : 0.0f;
-  const float* w1 = W + (ego ? L.e1w : L.o1w);
-  const float* b1 = W + (ego ? L.e1b : L.o1b);
-  const float* w2 = W + (ego ? L.e2w : L.o2w);
-  const float* b2 = W + (ego ? L.e2b : L.o2b);
-  float h1[HD], h2[HD];
+  for (int k = 0; k < F; ++k) x[k] = obs[row * F + k];
+  float h1[HD], acc[HD];
 #pragma unroll
-  for (int o = 0; o < HD; ++o) {
-    float a = b1[o];
+  for (int o = 0; o < HD; ++o) h1[o] = b1s[o];
 #pragma unroll
-    for (int k = 0; k < F; ++k) a = fmaf(w1[o * F + k], x[k], a);
-    h1[o] = a > 0.0f ? a : 0.0f;
-  }
+  for (int k = 0; k < F; ++k)
 #pragma unroll
-  for (int o = 0; o < HD; ++o) {
-    float a = b2[o];
+    for (int o = 0; o < HD; ++o) h1[o] = fmaf(w1t[k * HD + o], x[k], h1[o]);
 #pragma unroll
-    for (int k = 0; k < HD; ++k) a = fmaf(w2[o * HD + k], h1[k], a);
-    h2[o] = a > 0.0f ? a : 0.0f;
-  }
-  if (!live) return;
+  for (int o = 0; o < HD; ++o) { h1[o] = h1[o] > 0.0f ? h1[o] : 0.0f; acc[o] = b2s[o]; }
+  dense64(w2t, h1, acc);
+  float h2[HD];
+#pragma unroll
+  for (int o = 0; o < HD; ++o) h2[o] = acc[o] > 0.0f ? acc[o] : 0.0f;
   if (ego)
 #pragma unroll
     for (int o = 0; o < HD; ++o) ET[(long)o * B + env] = h2[o];
-#pragma unroll 4
-  for (int o = 0; o < HD; ++o) {
-    float k_ = 0.0f, v_ = 0.0f;
 #pragma unroll
-    for (int k = 0; k < HD; ++k) {
-      k_ = fmaf(W[L.wk + o * HD + k], h2[k], k_);
-      v_ = fmaf(W[L.wv + o * HD + k], h2[k], v_);
-    }
-    KT[(long)o * R + row] = k_;
-    VT[(long)o * R + row] = v_;
-  }
+  for (int o = 0; o < HD; ++o) acc[o] = 0.0f;
+  dense64(wkt, h2, acc);
+#pragma unroll
+  for (int o = 0; o < HD; ++o) { KT[(long)o * R + row] = acc[o]; acc[o] = 0.0f; }
+  dense64(wvt, h2, acc);
+#pragma unroll
+  for (int o = 0; o < HD; ++o) VT[(long)o * R + row] = acc[o];
 }
 
-constexpr int EPB = 4;  // envs per wave in env_kernel
+constexpr int EPB = 8;  // envs per wave in env_kernel
 
 template <int F>
 __global__ void __launch_bounds__(64) env_kernel(const float* __restrict__ obs, int B, int NE, int heads,
@@ -102,7 +130,7 @@ __global__ void __launch_bounds__(64) env_kernel(const float* __restrict__ obs, 
                                                  float* __restrict__ Q) {
   const PolicyLayout L = policy_layout(F, A);
   __shared__ float vec[EPB][HD];       // the vector being multiplied (q input, value mix, ...)
-  __shared__ float prob[EPB][8][32];   // softmax weights [head][entity]
+  __shared__ float prob[EPB][8][32];   // softmax weights [head][entity] (heads * NE <= 64)
   const int o = threadIdx.x;
   const int dph = HD / heads;
   const long R = (long)B * NE;
@@ -120,7 +148,7 @@ __global__ void __launch_bounds__(64) env_kernel(const float* __restrict__ obs, 
 #pragma unroll
   for (int u = 0; u < EPB; ++u) q[u] = 0.0f;
   for (int k = 0; k < HD; ++k) {
-    const float w = W[L.wq + o * HD + k];
+    const float w = W[L.wq + k * HD + o];  // [in][out]: coalesced across lanes
 #pragma unroll
     for (int u = 0; u < EPB; ++u) q[u] = fmaf(w, vec[u][k], q[u]);
   }
@@ -175,7 +203,7 @@ __global__ void __launch_bounds__(64) env_kernel(const float* __restrict__ obs, 
 #pragma unroll
   for (int u = 0; u < EPB; ++u) att[u] = 0.0f;
   for (int k = 0; k < HD; ++k) {
-    const float w = W[L.wc + o * HD + k];
+    const float w = W[L.wc + k * HD + o];
 #pragma unroll
     for (int u = 0; u < EPB; ++u) att[u] = fmaf(w, vec[u][k], att[u]);
   }
@@ -190,7 +218,7 @@ __global__ void __launch_bounds__(64) env_kernel(const float* __restrict__ obs, 
 #pragma unroll
     for (int u = 0; u < EPB; ++u) a[u] = W[offs_b[layer] + o];
     for (int k = 0; k < HD; ++k) {
-      const float w = W[offs_w[layer] + o * HD + k];
+      const float w = W[offs_w[layer] + k * HD + o];
 #pragma unroll
       for (int u = 0; u < EPB; ++u) a[u] = fmaf(w, vec[u][k], a[u]);
     }
@@ -204,7 +232,7 @@ __global__ void __launch_bounds__(64) env_kernel(const float* __restrict__ obs, 
     const long b = (long)blockIdx.x * EPB + u;
     if (b < B) {
       float a = W[L.pb + act];
-      for (int k = 0; k < HD; ++k) a = fmaf(W[L.pw + act * HD + k], vec[u][k], a);
+      for (int k = 0; k < HD; ++k) a = fmaf(W[L.pw + k * A + act], vec[u][k], a);
       Q[b * A + act] = a;
     }
   }
@@ -217,8 +245,8 @@ int launch(const float* obs, int B, int NE, int heads, const float* W, int A, fl
   float* KT = scratch;
   float* VT = KT + HD * R;
   float* ET = VT + HD * R;
-  const int blocks1 = (B + 63) / 64 + (int)((B * (long)(NE - 1) + 63) / 64);
-  hipLaunchKernelGGL(rows_kernel<F>, dim3(blocks1), dim3(64), 0, st, obs, B, NE, W, A, KT, VT, ET);
+  const int blocks1 = (B + RB - 1) / RB + (int)((B * (long)(NE - 1) + RB - 1) / RB);
+  hipLaunchKernelGGL(rows_kernel<F>, dim3(blocks1), dim3(RB), 0, st, obs, B, NE, W, A, KT, VT, ET);
   hipLaunchKernelGGL(env_kernel<F>, dim3((B + EPB - 1) / EPB), dim3(64), 0, st, obs, B, NE, heads, W, A, KT, VT,
                      ET, Q);
   return hipGetLastError() == hipSuccess ? TTRL_OK : TTRL_E_LAUNCH;
