@@ -285,3 +285,33 @@ def test_ttc_and_lidar_random_batch_vs_oracle(hip_device):
     for hz, pf in ((10, 1), (5, 2)):
         tc = _abi.ttc_cfg(hz, pf)
         assert np.array_equal(time_to_collision(dev, net, P, tc).cpu().numpy(), o.observe_ttc(h, tc))
+
+
+def test_collision_pair_queue_overflow_vs_oracle(hip_device):
+    """Pile-ups with more close pairs than slots (> NS queued pairs in an env) take the
+    per-vehicle sweep fallback; results must still equal the oracle."""
+    E, n = 64, 60
+    rng = np.random.default_rng(11)
+    h = HostState(E, n)
+    h["x"][:] = 500 + rng.uniform(-12, 12, (E, n))
+    h["y"][:] = rng.uniform(-2, 14, (E, n))
+    h["heading"][:] = rng.uniform(-0.4, 0.4, (E, n))
+    h["speed"][:] = rng.uniform(0, 30, (E, n))
+    h["target_speed"][:] = h["speed"]
+    h["lane"][:] = np.clip(np.round(h["y"] / 4), 0, 3).astype(np.int32)
+    h["target_lane"][:] = h["lane"]
+    h["kind"][:] = _abi.IDM
+    lanes = _abi.straight_lane_table(4)
+    o = Oracle(lanes, P)
+    dev = to_dev(h, hip_device)
+    road = BatchedRoad(RoadNetwork(lanes), dev, P)
+    for _ in range(2):
+        o.road_step(h, 1 / 15)
+        road.step(1 / 15)
+        torch.cuda.synchronize()
+        d = dev.to_numpy()
+        for k in ("crashed", "has_impact"):
+            assert np.array_equal(d[k], h[k]), k
+        imp = h["has_impact"].astype(bool)
+        for k in ("impact_x", "impact_y"):
+            assert np.max(np.abs(d[k][imp] - h[k][imp])) < 1e-9, k
