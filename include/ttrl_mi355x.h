@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define TTRL_ABI_VERSION 1
+#define TTRL_ABI_VERSION 2
 #define TTRL_MAX_LANES 16
 
 enum { TTRL_F32 = 0, TTRL_F64 = 1 };
@@ -51,12 +51,14 @@ enum { TTRL_ABSENT = 0, TTRL_MDP = 1, TTRL_IDM = 2 };
 /* DiscreteMetaAction.ACTIONS_ALL (action.py:204). */
 enum { TTRL_LANE_LEFT = 0, TTRL_IDLE = 1, TTRL_LANE_RIGHT = 2, TTRL_FASTER = 3, TTRL_SLOWER = 4 };
 
+/* Lane geometry classes (lane.py): StraightLane :159-213, SineLane :235-290, CircularLane :293-350. */
+enum { TTRL_LANE_STRAIGHT = 0, TTRL_LANE_SINE = 1, TTRL_LANE_CIRCULAR = 2 };
+
 /*
- * One straight road "0"->"1" with n_lanes parallel StraightLanes in graph order
- * (RoadNetwork.straight_road_network, road.py:291-321; StraightLane lane.py:159-213).
- * Derived geometry (direction, length, heading) is computed on the host with
- * the same float64 formulas as StraightLane.__init__ and passed in.
- * Shared by every env of a batch.
+ * One road "0"->"1" with n_lanes lanes in graph order (RoadNetwork.straight_road_network,
+ * road.py:291-321, or any single-edge network of Straight / Sine / Circular lanes).
+ * Derived geometry (direction, length, heading) is computed on the host with the same
+ * float64 formulas as the lane constructors and passed in.  Shared by every env of a batch.
  */
 typedef struct ttrl_lane_table {
   int32_t n_lanes;
@@ -66,6 +68,10 @@ typedef struct ttrl_lane_table {
   double length[TTRL_MAX_LANES], width[TTRL_MAX_LANES];
   double heading[TTRL_MAX_LANES], speed_limit[TTRL_MAX_LANES];
   int32_t forbidden[TTRL_MAX_LANES];
+  int32_t type[TTRL_MAX_LANES];                            /* TTRL_LANE_*                      */
+  double amplitude[TTRL_MAX_LANES], pulsation[TTRL_MAX_LANES], phase[TTRL_MAX_LANES];  /* SineLane */
+  double center_x[TTRL_MAX_LANES], center_y[TTRL_MAX_LANES], radius[TTRL_MAX_LANES];   /* Circular */
+  double start_phase[TTRL_MAX_LANES], direction[TTRL_MAX_LANES];  /* direction: +1 clockwise, -1 */
 } ttrl_lane_table_t;
 
 /*

@@ -37,7 +37,7 @@ def _import_reference():
     pkg.__path__ = [os.path.join(REF, "ttrl_env")]
     sys.modules["ttrl_env"] = pkg
     from ttrl_env import utils
-    from ttrl_env.road.lane import StraightLane
+    from ttrl_env.road.lane import CircularLane, SineLane, StraightLane
     from ttrl_env.road.road import Road, RoadNetwork
     from ttrl_env.vehicle.behavior import IDMVehicle
     from ttrl_env.vehicle.controller import MDPVehicle
@@ -47,7 +47,8 @@ def _import_reference():
         m.__path__ = [os.path.join(REF, "ttrl_env", *sub.split("."))]
         sys.modules["ttrl_env." + sub] = m
     from ttrl_env.envs.common import finite_mdp  # the module itself imports only utils and Vehicle
-    return types.SimpleNamespace(utils=utils, StraightLane=StraightLane, Road=Road,
+    return types.SimpleNamespace(utils=utils, StraightLane=StraightLane, SineLane=SineLane,
+                                 CircularLane=CircularLane, Road=Road,
                                  RoadNetwork=RoadNetwork, IDMVehicle=IDMVehicle,
                                  MDPVehicle=MDPVehicle, Vehicle=Vehicle, finite_mdp=finite_mdp)
 
@@ -80,6 +81,47 @@ def make_highway(n: int, seed: int, lanes: int = 4):
         v.randomize_behavior()
         road.vehicles.append(v)
     return road
+
+
+def make_curved(kind: str, n: int, seed: int, lanes: int = 3):
+    """The highway scene of make_highway on a single-edge road of curved lanes: parallel
+    SineLanes (amplitude 5 m, wavelength 200 m) or concentric CircularLanes (radius 200 + 4 i m,
+    a clockwise half circle) -- lane.py:235-350, built with the reference constructors."""
+    reset_idm_constants()
+    net = R.RoadNetwork()
+    for i in range(lanes):
+        if kind == "sine":
+            lane = R.SineLane([0.0, 4.0 * i], [10000.0, 4.0 * i], amplitude=5.0, pulsation=2 * np.pi / 200,
+                              phase=0.0, speed_limit=30)
+        else:
+            lane = R.CircularLane([0.0, 0.0], 200.0 + 4.0 * i, -np.pi / 2, np.pi / 2, clockwise=True, speed_limit=30)
+        net.add_lane("0", "1", lane)
+    road = R.Road(network=net, np_random=np.random.default_rng(seed))
+    lane = net.get_lane(("0", "1", 1))
+    ego = R.MDPVehicle(road, lane.position(50.0, 0.0), lane.heading_at(50.0), 25.0)
+    road.vehicles.append(ego)
+    for _ in range(n - 1):
+        v = R.IDMVehicle.create_random(road, spacing=1)
+        v.randomize_behavior()
+        road.vehicles.append(v)
+    return road
+
+
+def lane_geometry(road):
+    """[L, 16] rows: type, start_x, start_y, end_x, end_y, width, speed_limit, amplitude, pulsation,
+    phase, center_x, center_y, radius, start_phase, end_phase, clockwise (_abi.lane_table_from_arrays)."""
+    rows = []
+    for ln in road.network.lanes_list():
+        if isinstance(ln, R.CircularLane):
+            rows.append([2, 0, 0, 0, 0, ln.width, ln.speed_limit, 0, 0, 0, ln.center[0], ln.center[1], ln.radius,
+                         ln.start_phase, ln.end_phase, 1.0 if ln.clockwise else 0.0])
+        elif isinstance(ln, R.SineLane):
+            rows.append([1, ln.start[0], ln.start[1], ln.end[0], ln.end[1], ln.width, ln.speed_limit, ln.amplitude,
+                         ln.pulsation, ln.phase, 0, 0, 0, 0, 0, 0])
+        else:
+            rows.append([0, ln.start[0], ln.start[1], ln.end[0], ln.end[1], ln.width, ln.speed_limit,
+                         0, 0, 0, 0, 0, 0, 0, 0, 0])
+    return np.array(rows, dtype=np.float64)
 
 
 def make_dense(n: int, seed: int, lanes: int = 4):
@@ -384,12 +426,23 @@ def main():
     for n in (16, 64):
         for seed in (0, 1):
             cases.append(("dense", n, seed, 2))
+    for kind in ("sine", "arc"):
+        for seed in (0, 1):
+            cases.append((kind, 32, seed, 4))
     for kind, n, seed, steps in cases:
-        road = make_highway(n, seed) if kind == "highway" else make_dense(n, seed)
+        if kind == "highway":
+            road = make_highway(n, seed)
+        elif kind == "dense":
+            road = make_dense(n, seed)
+        else:
+            road = make_curved(kind, n, seed)
         d = rollout(road, steps, seed)
-        d["meta"] = np.array([n, seed, steps, 15, 4], dtype=np.int64)
-        d["lane_table"] = np.array([[l.start[0], l.start[1], l.end[0], l.end[1], l.width, l.speed_limit]
-                                    for l in road.network.lanes_list()])
+        d["meta"] = np.array([n, seed, steps, 15, len(road.network.lanes_list())], dtype=np.int64)
+        if kind in ("highway", "dense"):
+            d["lane_table"] = np.array([[l.start[0], l.start[1], l.end[0], l.end[1], l.width, l.speed_limit]
+                                        for l in road.network.lanes_list()])
+        else:
+            d["lane_table"] = lane_geometry(road)
         name = f"{kind}_n{n}_s{seed}"
         stats(name, d)
         np.savez_compressed(os.path.join(OUT, name + ".npz"), **d)

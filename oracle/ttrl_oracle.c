@@ -62,11 +62,45 @@ static double lmap(double v, double x0, double x1, double y0, double y1) {
   return y0 + (v - x0) * (y1 - y0) / (x1 - x0);
 }
 
-/* StraightLane.local_coordinates lane.py:209-213 (np.dot of 2-vectors) */
+/* local_coordinates: StraightLane lane.py:209-213 (np.dot of 2-vectors), SineLane :275-279,
+ * CircularLane :327-334 */
 static void local(const ttrl_lane_table_t* R, int l, double px, double py, double* s, double* r) {
+  if (R->type[l] == TTRL_LANE_CIRCULAR) {
+    double dx = px - R->center_x[l], dy = py - R->center_y[l];
+    double phi = atan2(dy, dx);
+    phi = R->start_phase[l] + wrap_to_pi(phi - R->start_phase[l]);
+    double rr = sqrt(dx * dx + dy * dy);
+    *s = R->direction[l] * (phi - R->start_phase[l]) * R->radius[l];
+    *r = R->direction[l] * (R->radius[l] - rr);
+    return;
+  }
   double dx = px - R->start_x[l], dy = py - R->start_y[l];
   *s = dx * R->dir_x[l] + dy * R->dir_y[l];
   *r = dx * (-R->dir_y[l]) + dy * R->dir_x[l];
+  if (R->type[l] == TTRL_LANE_SINE) *r = *r - R->amplitude[l] * sin(R->pulsation[l] * *s + R->phase[l]);
+}
+/* heading_at: StraightLane :197-198, SineLane :269-273, CircularLane :318-321 */
+static double heading_at(const ttrl_lane_table_t* R, int l, double s) {
+  if (R->type[l] == TTRL_LANE_SINE)
+    return R->heading[l] + atan(R->amplitude[l] * R->pulsation[l] * cos(R->pulsation[l] * s + R->phase[l]));
+  if (R->type[l] == TTRL_LANE_CIRCULAR) {
+    double phi = R->direction[l] * s / R->radius[l] + R->start_phase[l];
+    return phi + PI / 2 * R->direction[l];
+  }
+  return R->heading[l];
+}
+/* position: StraightLane :199-204, SineLane :263-267, CircularLane :313-316 */
+static void position(const ttrl_lane_table_t* R, int l, double s, double r, double* x, double* y) {
+  if (R->type[l] == TTRL_LANE_CIRCULAR) {
+    double phi = R->direction[l] * s / R->radius[l] + R->start_phase[l];
+    double k = R->radius[l] - r * R->direction[l];
+    *x = R->center_x[l] + k * cos(phi);
+    *y = R->center_y[l] + k * sin(phi);
+    return;
+  }
+  if (R->type[l] == TTRL_LANE_SINE) r = r + R->amplitude[l] * sin(R->pulsation[l] * s + R->phase[l]);
+  *x = R->start_x[l] + s * R->dir_x[l] + r * (-R->dir_y[l]);
+  *y = R->start_y[l] + s * R->dir_y[l] + r * R->dir_x[l];
 }
 /* AbstractLane.on_lane lane.py:80-102 */
 static int on_lane(const ttrl_lane_table_t* R, const ttrl_params_t* P, int l, double s, double r, double margin) {
@@ -83,7 +117,7 @@ static int closest_lane(const ttrl_lane_table_t* R, double px, double py, double
   int best = 0; double bd = 0;
   for (int l = 0; l < R->n_lanes; ++l) {
     double s, r; local(R, l, px, py, &s, &r);
-    double ang = fabs(wrap_to_pi(heading - R->heading[l]));
+    double ang = fabs(wrap_to_pi(heading - heading_at(R, l, s)));
     double a = s - R->length[l]; if (!(a > 0)) a = 0;   /* Python max(s - len, 0) */
     double b = 0 - s; if (!(b > 0)) b = 0;
     double d = fabs(r) + a + b + 1.0 * ang;
@@ -187,7 +221,7 @@ static void change_lane_policy(S* o, const ttrl_lane_table_t* R, const ttrl_para
 static double steering_control(const S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base, int i, int l) {
   double s, r; local(R, l, o->x[base + i], o->y[base + i], &s, &r);
   double v = o->v[base + i];
-  double lane_future_heading = R->heading[l];                 /* heading_at(s + v*TAU_PURSUIT) */
+  double lane_future_heading = heading_at(R, l, s + v * P->tau_pursuit);
   double lat_cmd = -P->kp_lateral * r;
   double hcmd = asin(clipd(lat_cmd / not_zero(v), -1, 1));
   double href = lane_future_heading + clipd(hcmd, -PI / 4, PI / 4);
@@ -439,7 +473,7 @@ static double feature(const S* o, const ttrl_lane_table_t* R, int k, int f) {
       double s, r; local(R, o->lane[k], o->x[k], o->y[k], &s, &r);
       if (f == TTRL_F_LONG_OFF) return s;
       if (f == TTRL_F_LAT_OFF) return r;
-      return wrap_to_pi(o->h[k] - R->heading[o->lane[k]]);
+      return wrap_to_pi(o->h[k] - heading_at(R, o->lane[k], s));  /* local_angle lane.py:145-147 */
     }
   }
   return 0;
@@ -526,8 +560,8 @@ int oracle_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* R, const
           for (long i = 0; i < n; ++i) {
             double wp = i == 0 ? start : (i == 1 ? start + spacing : start + i * d1);
             wp = clipd(wp, 0, R->length[l]);
-            double px = R->start_x[l] + wp * R->dir_x[l] + 0 * (-R->dir_y[l]);
-            double py = R->start_y[l] + wp * R->dir_y[l] + 0 * R->dir_x[l];
+            double px, py;
+            position(R, l, wp, 0, &px, &py);
             px -= o.x[ego]; py -= o.y[ego];
             long cx = (long)floor((px - cfg->grid_min_x) / cfg->step_x);
             long cy = (long)floor((py - cfg->grid_min_y) / cfg->step_y);
@@ -618,10 +652,11 @@ int oracle_reset_highway(const ttrl_state_t* s, const ttrl_lane_table_t* R, cons
     }
     /* ego: MDPVehicle(road, lane.position(x, 0), lane.heading_at(x), speed) */
     int l = cfg->ego_lane;
-    double ex = R->start_x[l] + cfg->ego_x * R->dir_x[l] + 0.0 * (-R->dir_y[l]);
-    double ey = R->start_y[l] + cfg->ego_x * R->dir_y[l] + 0.0 * R->dir_x[l];
-    o.kind[base] = TTRL_MDP; o.x[base] = ex; o.y[base] = ey; o.h[base] = R->heading[l]; o.v[base] = cfg->ego_speed;
-    o.lane[base] = o.tgt[base] = closest_lane(R, ex, ey, R->heading[l]);
+    double ex, ey;
+    position(R, l, cfg->ego_x, 0.0, &ex, &ey);
+    const double eh = heading_at(R, l, cfg->ego_x);
+    o.kind[base] = TTRL_MDP; o.x[base] = ex; o.y[base] = ey; o.h[base] = eh; o.v[base] = cfg->ego_speed;
+    o.lane[base] = o.tgt[base] = closest_lane(R, ex, ey, eh);
     o.sidx[base] = speed_to_index(P, cfg->ego_speed);
     o.ts[base] = P->target_speeds[o.sidx[base]];
     for (int i = 1; i < cfg->n_vehicles; ++i) {
@@ -636,9 +671,8 @@ int oracle_reset_highway(const ttrl_state_t* s, const ttrl_lane_table_t* R, cons
       }
       x0 += offset * pcg_uniform(&g, 0.9, 1.1);
       o.kind[k] = TTRL_IDM; o.lc[k] = (uint8_t)cfg->lane_change;
-      o.x[k] = R->start_x[lid] + x0 * R->dir_x[lid] + 0.0 * (-R->dir_y[lid]);
-      o.y[k] = R->start_y[lid] + x0 * R->dir_y[lid] + 0.0 * R->dir_x[lid];
-      o.h[k] = R->heading[lid]; o.v[k] = sp; o.ts[k] = sp;
+      position(R, lid, x0, 0.0, &o.x[k], &o.y[k]);
+      o.h[k] = heading_at(R, lid, x0); o.v[k] = sp; o.ts[k] = sp;
       o.lane[k] = o.tgt[k] = closest_lane(R, o.x[k], o.y[k], o.h[k]);
       o.timer[k] = pymod((o.x[k] + o.y[k]) * PI, P->lane_change_delay);
       o.delta[k] = pcg_uniform(&g, cfg->delta_lo, cfg->delta_hi);

@@ -20,6 +20,12 @@ def golden_files(pattern="*.npz"):
     return sorted(glob.glob(os.path.join(GOLDEN, pattern)))
 
 
+def scene_files():
+    """Scenes built by the highway scene generator (create_random): the straight highways and
+    the curved-lane roads (SineLane, CircularLane); the dense scenes are hand-placed."""
+    return sorted(golden_files("highway_*") + golden_files("sine_*") + golden_files("arc_*"))
+
+
 def load_golden(path):
     with np.load(path) as d:
         return {k: d[k] for k in d.files}

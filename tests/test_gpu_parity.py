@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden_files, load_golden
+from conftest import golden_files, load_golden, scene_files
 from oracle.oracle import HostState, Oracle
 from topotrafficrl_amd import _abi
 from topotrafficrl_amd.observation import kinematics, occupancy_grid
@@ -154,7 +154,7 @@ def test_observations_vs_golden(path, dtype, hip_device):
     tol = 0.0 if dtype == "f64" else 2e-4
     for p in range(int(d["meta"][2]) + 1):
         dev = to_dev(HostState.from_golden(d, 15 * p), hip_device, dtype)
-        for cfg, key in ((KD, "kin5"), (K15, "kin15")):
+        for cfg, key in ((_abi.kin_cfg(lanes_on_road=int(d["meta"][4])), "kin5"), (K15, "kin15")):
             obs, ids = kinematics(dev, net, P, cfg)
             assert np.max(np.abs(obs.cpu().numpy()[0] - d[key][p])) <= tol
             if dtype == "f64":
@@ -169,20 +169,29 @@ def test_observations_vs_golden(path, dtype, hip_device):
 
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
-@pytest.mark.parametrize("path", golden_files("highway_*"), ids=lambda p: p.split("/")[-1][:-4])
+@pytest.mark.parametrize("path", scene_files(), ids=lambda p: p.split("/")[-1][:-4])
 def test_reset_matches_reference_scene(path, dtype, hip_device):
-    """GPU scene generation reproduces numpy default_rng(seed) draws of create_random."""
+    """GPU scene generation reproduces numpy default_rng(seed) draws of create_random.
+    Straight lanes: bit-exact.  Curved lanes place vehicles through sin/cos/atan2, which the
+    device math library rounds within 1 ulp rather than correctly: continuous fields there are
+    held to 1e-11 relative (f64; the lane-change timer is (x + y) * pi mod 1, which scales a
+    position's rounding by ~600 on a 200 m arc) and every discrete field stays exact."""
     from topotrafficrl_amd.envs import reset_highway
     d = load_golden(path)
     n, seed = int(d["meta"][0]), int(d["meta"][1])
     lanes = _abi.lane_table_from_arrays(d["lane_table"])
+    curved = any(lanes.type[i] != _abi.LANE_STRAIGHT for i in range(lanes.n_lanes))
     dev = BatchState(1, n, device=hip_device, dtype=dtype)
     reset_highway(dev, RoadNetwork(lanes), P, _abi.reset_cfg(n, lanes), [seed])
     g = HostState.from_golden(d, 0)
     got = dev.to_numpy()
     for k in ["x", "y", "heading", "speed", "target_speed", "timer", "delta"]:
         ref = g[k].astype(np.float32) if dtype == "f32" else g[k]
-        assert np.array_equal(got[k], ref), k
+        if curved:
+            tol = 1e-11 if dtype == "f64" else 1e-5
+            assert np.max(np.abs(got[k] - ref) / (1 + np.abs(ref))) <= tol, k
+        else:
+            assert np.array_equal(got[k], ref), k
     for k in ["lane", "target_lane", "kind", "speed_index", "lane_change"]:
         assert np.array_equal(got[k], g[k]), k
 

@@ -10,7 +10,7 @@ numpy-PCG64 scene generator bit-identical.
 import numpy as np
 import pytest
 
-from conftest import golden_files, load_golden
+from conftest import golden_files, load_golden, scene_files
 from oracle.oracle import HostState, Oracle
 from topotrafficrl_amd import _abi
 
@@ -85,7 +85,7 @@ def test_observations(name, cases):
     o = Oracle(_abi.lane_table_from_arrays(d["lane_table"]), P)
     for p in range(int(d["meta"][2]) + 1):
         h = HostState.from_golden(d, 15 * p)
-        obs, ids = o.observe_kinematics(h, KD)
+        obs, ids = o.observe_kinematics(h, _abi.kin_cfg(lanes_on_road=int(d["meta"][4])))
         assert np.array_equal(obs[0], d["kin5"][p]) and np.array_equal(ids[0], d["kin5_ids"][p])
         obs, ids = o.observe_kinematics(h, K15)
         assert np.array_equal(obs[0], d["kin15"][p]) and np.array_equal(ids[0], d["kin15_ids"][p])
@@ -106,7 +106,7 @@ def test_ttc_and_lidar_observations(name, cases):
         assert np.max(np.abs(lid - d["lidar"][p])) <= 1e-6 * (1 + np.max(np.abs(d["lidar"][p])))
 
 
-@pytest.mark.parametrize("name", [IDS(p) for p in golden_files("highway_*")])
+@pytest.mark.parametrize("name", [IDS(p) for p in scene_files()])
 def test_scene_generation_matches_reference_rng(name, cases):
     d = cases[name]
     n, seed = int(d["meta"][0]), int(d["meta"][1])

@@ -37,7 +37,14 @@ class LaneTable(C.Structure):
                 ("dir_x", C.c_double * MAX_LANES), ("dir_y", C.c_double * MAX_LANES),
                 ("length", C.c_double * MAX_LANES), ("width", C.c_double * MAX_LANES),
                 ("heading", C.c_double * MAX_LANES), ("speed_limit", C.c_double * MAX_LANES),
-                ("forbidden", C.c_int32 * MAX_LANES)]
+                ("forbidden", C.c_int32 * MAX_LANES), ("type", C.c_int32 * MAX_LANES),
+                ("amplitude", C.c_double * MAX_LANES), ("pulsation", C.c_double * MAX_LANES),
+                ("phase", C.c_double * MAX_LANES), ("center_x", C.c_double * MAX_LANES),
+                ("center_y", C.c_double * MAX_LANES), ("radius", C.c_double * MAX_LANES),
+                ("start_phase", C.c_double * MAX_LANES), ("direction", C.c_double * MAX_LANES)]
+
+
+LANE_STRAIGHT, LANE_SINE, LANE_CIRCULAR = 0, 1, 2
 
 
 class Params(C.Structure):
@@ -121,18 +128,55 @@ def straight_lane_table(lanes: int = 4, start: float = 0.0, length: float = 1000
     return t
 
 
+def _set_straight(t: LaneTable, i: int, start, end, width, speed_limit):
+    """StraightLane.__init__ lane.py:162-194 (float64, the reference's own expressions)."""
+    s, e = np.asarray(start, dtype=np.float64), np.asarray(end, dtype=np.float64)
+    ln = np.linalg.norm(e - s)
+    d = (e - s) / ln
+    t.start_x[i], t.start_y[i], t.dir_x[i], t.dir_y[i] = s[0], s[1], d[0], d[1]
+    t.length[i], t.width[i], t.speed_limit[i] = ln, width, speed_limit
+    t.heading[i] = np.arctan2(e[1] - s[1], e[0] - s[0])
+
+
 def lane_table_from_arrays(table: np.ndarray) -> LaneTable:
-    """[L, 6] rows (start_x, start_y, end_x, end_y, width, speed_limit), as dumped by gen_golden."""
+    """[L, 6] straight rows (start_x, start_y, end_x, end_y, width, speed_limit), or [L, 16]
+    geometry rows (type, those 6, amplitude, pulsation, phase, center_x, center_y, radius,
+    start_phase, end_phase, clockwise), as dumped by gen_golden."""
+    table = np.asarray(table, dtype=np.float64)
     t = LaneTable()
     t.n_lanes = len(table)
-    for i, (sx, sy, ex, ey, w, lim) in enumerate(np.asarray(table, dtype=np.float64)):
-        s, e = np.array([sx, sy]), np.array([ex, ey])
-        ln = np.linalg.norm(e - s)
-        d = (e - s) / ln
-        t.start_x[i], t.start_y[i], t.dir_x[i], t.dir_y[i] = sx, sy, d[0], d[1]
-        t.length[i], t.width[i], t.speed_limit[i] = ln, w, lim
-        t.heading[i] = np.arctan2(e[1] - s[1], e[0] - s[0])
+    for i, row in enumerate(table):
+        if len(row) == 6:
+            row = np.concatenate([[LANE_STRAIGHT], row, np.zeros(9)])
+        typ, sx, sy, ex, ey, w, lim, amp, puls, ph, cx, cy, rad, sph, eph, cw = row
+        t.type[i] = int(typ)
+        if int(typ) == LANE_CIRCULAR:  # CircularLane.__init__ lane.py:296-315
+            d = 1.0 if cw else -1.0
+            t.center_x[i], t.center_y[i], t.radius[i], t.start_phase[i], t.direction[i] = cx, cy, rad, sph, d
+            t.length[i] = rad * (eph - sph) * d
+            t.width[i], t.speed_limit[i] = w, lim
+        else:
+            _set_straight(t, i, (sx, sy), (ex, ey), w, lim)
+            t.amplitude[i], t.pulsation[i], t.phase[i] = amp, puls, ph
     return t
+
+
+def sine_lane_table(lanes: int = 4, length: float = 10000.0, amplitude: float = 5.0,
+                    pulsation: float = 2 * np.pi / 200, phase: float = 0.0, speed_limit: float = 30.0,
+                    width: float = 4.0) -> LaneTable:
+    """``lanes`` parallel SineLanes (lane.py:235-290) from (0, 4i) to (length, 4i)."""
+    rows = [[LANE_SINE, 0.0, 4.0 * i, length, 4.0 * i, width, speed_limit, amplitude, pulsation, phase,
+             0, 0, 0, 0, 0, 0] for i in range(lanes)]
+    return lane_table_from_arrays(np.array(rows))
+
+
+def circular_lane_table(lanes: int = 3, center=(0.0, 0.0), radius: float = 200.0, start_phase: float = -np.pi / 2,
+                        end_phase: float = np.pi / 2, clockwise: bool = True, speed_limit: float = 30.0,
+                        width: float = 4.0) -> LaneTable:
+    """``lanes`` concentric CircularLanes (lane.py:293-350), radius + 4 i."""
+    rows = [[LANE_CIRCULAR, 0, 0, 0, 0, width, speed_limit, 0, 0, 0, center[0], center[1], radius + 4.0 * i,
+             start_phase, end_phase, 1.0 if clockwise else 0.0] for i in range(lanes)]
+    return lane_table_from_arrays(np.array(rows))
 
 
 def default_params(target_speeds=None, **overrides) -> Params:

@@ -97,34 +97,108 @@ template <typename T> __device__ __forceinline__ T lmap(T v, T x0, T x1, T y0, T
   return y0 + (v - x0) * (y1 - y0) / (x1 - x0);  // utils.py:29-31
 }
 
-// Lane table staged in LDS as T (StraightLane lane.py:159-213).
+// Lane table staged in LDS as T: StraightLane lane.py:159-213, SineLane :235-290,
+// CircularLane :293-350 (type: TTRL_LANE_*; a uniform branch on a straight-only road).
 template <typename T> struct LaneT {
   T sx, sy, dx, dy, len, w, hd, lim;
-  int forb, _pad;
+  T amp, puls, ph;                  // SineLane
+  T cx, cy, rad, sph, dirn;         // CircularLane
+  int forb, type;
 };
 
+// Out of line, with scalar arguments (a struct argument would be materialised in scratch):
+// the curved lanes' trigonometry stays off the straight-road register budget.
+template <typename T> struct Pair { T a, b; };
 template <typename T>
+__device__ __noinline__ Pair<T> curved_local(int type, T px, T py, T sx, T sy, T ux, T uy, T amp, T puls, T ph,
+                                             T cx, T cy, T rad, T sph, T dirn) {
+  Pair<T> o;
+  if (type == TTRL_LANE_SINE) {  // SineLane.local_coordinates lane.py:275-279
+    const T dx = px - sx, dy = py - sy;
+    o.a = dx * ux + dy * uy;
+    o.b = dx * (-uy) + dy * ux - amp * t_sin(puls * o.a + ph);
+  } else {  // CircularLane.local_coordinates lane.py:327-334
+    const T dx = px - cx, dy = py - cy;
+    T phi = atan2(dy, dx);
+    phi = sph + wrap_to_pi(phi - sph);
+    const T rr = sqrt(dx * dx + dy * dy);
+    o.a = dirn * (phi - sph) * rad;
+    o.b = dirn * (rad - rr);
+  }
+  return o;
+}
+
+// CV = false: the caller's road is straight-only (the hot simulate kernel is instantiated
+// both ways), so the curved call sites -- and the registers they pin -- are compiled out.
+template <bool CV = true, typename T>
 __device__ __forceinline__ void lane_local(const LaneT<T>& L, T px, T py, T& s, T& r) {
-  T dx = px - L.sx, dy = py - L.sy;
-  s = dx * L.dx + dy * L.dy;
-  r = dx * (-L.dy) + dy * L.dx;
+  if (!CV || L.type == TTRL_LANE_STRAIGHT) {  // StraightLane.local_coordinates lane.py:209-213
+    T dx = px - L.sx, dy = py - L.sy;
+    s = dx * L.dx + dy * L.dy;
+    r = dx * (-L.dy) + dy * L.dx;
+  } else {
+    const Pair<T> o = curved_local(L.type, px, py, L.sx, L.sy, L.dx, L.dy, L.amp, L.puls, L.ph, L.cx, L.cy, L.rad,
+                                   L.sph, L.dirn);
+    s = o.a;
+    r = o.b;
+  }
+}
+
+template <typename T>
+__device__ __noinline__ T curved_heading(int type, T s, T hd, T amp, T puls, T ph, T rad, T sph, T dirn) {
+  if (type == TTRL_LANE_SINE)  // SineLane.heading_at lane.py:269-273
+    return hd + t_atan(amp * puls * t_cos(puls * s + ph));
+  const T phi = dirn * s / rad + sph;  // CircularLane.heading_at lane.py:318-321
+  return phi + Tpi<T>() / T(2) * dirn;
+}
+
+template <bool CV = true, typename T>
+__device__ __forceinline__ T heading_at(const LaneT<T>& L, T s) {
+  return !CV || L.type == TTRL_LANE_STRAIGHT ? L.hd : curved_heading(L.type, s, L.hd, L.amp, L.puls, L.ph, L.rad, L.sph, L.dirn);
+}
+
+// AbstractLane.position for every lane class (lane.py:199-204, :263-267, :313-316)
+template <typename T>
+__device__ __forceinline__ void lane_position(const LaneT<T>& L, T s, T r, T& x, T& y) {
+  if (L.type == TTRL_LANE_CIRCULAR) {
+    const T phi = L.dirn * s / L.rad + L.sph;
+    const T k = L.rad - r * L.dirn;
+    x = L.cx + k * t_cos(phi);
+    y = L.cy + k * t_sin(phi);
+    return;
+  }
+  if (L.type == TTRL_LANE_SINE) r = r + L.amp * t_sin(L.puls * s + L.ph);
+  x = L.sx + s * L.dx + r * (-L.dy);
+  y = L.sy + s * L.dy + r * L.dx;
+}
+
+template <typename T>
+__host__ __device__ inline LaneT<T> make_lane(const ttrl_lane_table_t& R, int l) {
+  LaneT<T> L;
+  L.sx = T(R.start_x[l]); L.sy = T(R.start_y[l]); L.dx = T(R.dir_x[l]); L.dy = T(R.dir_y[l]);
+  L.len = T(R.length[l]); L.w = T(R.width[l]); L.hd = T(R.heading[l]); L.lim = T(R.speed_limit[l]);
+  L.amp = T(R.amplitude[l]); L.puls = T(R.pulsation[l]); L.ph = T(R.phase[l]);
+  L.cx = T(R.center_x[l]); L.cy = T(R.center_y[l]); L.rad = T(R.radius[l]); L.sph = T(R.start_phase[l]);
+  L.dirn = T(R.direction[l]);
+  L.forb = R.forbidden[l]; L.type = R.type[l];
+  return L;
 }
 
 // AbstractLane.is_reachable_from lane.py:104-118
-template <typename T>
+template <bool CV = true, typename T>
 __device__ __forceinline__ bool reachable(const LaneT<T>& L, T vl, T px, T py) {
   if (L.forb) return false;
   T s, r;
-  lane_local(L, px, py, s, r);
+  lane_local<CV>(L, px, py, s, r);
   return fabs(r) <= T(2) * L.w && T(0) <= s && s < L.len + vl;
 }
 
 // ControlledVehicle.steering_control controller.py:145-187
-template <typename T>
+template <bool CV = true, typename T>
 __device__ __forceinline__ T steering_control(const LaneT<T>& L, const ttrl_params_t& P, T x, T y, T h, T v) {
   T s, r;
-  lane_local(L, x, y, s, r);
-  const T lfh = L.hd;  // heading_at(s + v * TAU_PURSUIT) of a straight lane
+  lane_local<CV>(L, x, y, s, r);
+  const T lfh = heading_at<CV>(L, s + v * T(P.tau_pursuit));  // lane_future_heading
   const T lat_cmd = -T(P.kp_lateral) * r;
   const T hcmd = t_asin(clip(lat_cmd / not_zero(v), T(-1), T(1)));
   const T href = lfh + clip(hcmd, -Tpi<T>() / T(4), Tpi<T>() / T(4));
@@ -427,13 +501,7 @@ size_t host_view_bytes(int dtype, int EPW, int NS, int n_lanes) {
 
 template <typename T>
 __device__ __forceinline__ void stage_lanes(View<T>& V, const ttrl_lane_table_t& R, int tid) {
-  if (tid < R.n_lanes) {
-    LaneT<T> L;
-    L.sx = T(R.start_x[tid]); L.sy = T(R.start_y[tid]); L.dx = T(R.dir_x[tid]); L.dy = T(R.dir_y[tid]);
-    L.len = T(R.length[tid]); L.w = T(R.width[tid]); L.hd = T(R.heading[tid]); L.lim = T(R.speed_limit[tid]);
-    L.forb = R.forbidden[tid]; L._pad = 0;
-    V.lanes[tid] = L;
-  }
+  if (tid < R.n_lanes) V.lanes[tid] = make_lane<T>(R, tid);
 }
 
 // Per-thread vehicle registers.
@@ -491,7 +559,7 @@ __device__ __forceinline__ void store_veh(const Veh<T>& a, const ttrl_state_t& s
 // slot order (ballot + popcount prefix), so neighbour scans visit only real candidates in
 // the reference's list order; returns the closest lane (RoadNetwork.get_closest_lane_index
 // road.py:55-71, distance_with_heading lane.py:132-147).  All threads must call it.
-template <typename T, int NS, int EPW>
+template <typename T, int NS, int EPW, bool CV = true>
 __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t& P, int nl, int tid, int le, int i,
                                            bool present, T x, T y, T h, bool want_closest) {
   constexpr int NSP = NS + 1;
@@ -505,7 +573,7 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
     for (int l = 0; l < nl; ++l) {
       const LaneT<T> L = V.lanes[l];
       T s, r;
-      lane_local(L, x, y, s, r);
+      lane_local<CV>(L, x, y, s, r);
       const bool on = present && fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl;
       const unsigned long long m = (__ballot(on) >> sh) & seg;
       const int pos = on ? __popcll(m & ((1ull << i) - 1)) : -1;
@@ -518,8 +586,9 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
       mx = c > mx ? c : mx;
       if (i == 0) cnt[l] = c;
       if (want_closest) {
-        if (l == 0 || L.hd != prev_hd) ang = fabs(wrap_to_pi(h - L.hd));
-        prev_hd = L.hd;
+        const T hdl = heading_at<CV>(L, s);  // distance_with_heading lane.py:132-147
+        if (l == 0 || hdl != prev_hd) ang = fabs(wrap_to_pi(h - hdl));
+        prev_hd = hdl;
         T a = s - L.len; if (!(a > T(0))) a = T(0);
         T b = T(0) - s; if (!(b > T(0))) b = T(0);
         const T d = fabs(r) + a + b + T(1) * ang;
@@ -532,7 +601,7 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
     for (int l = 0; l < nl; ++l) {
       const LaneT<T> L = V.lanes[l];
       T s, r;
-      lane_local(L, x, y, s, r);
+      lane_local<CV>(L, x, y, s, r);
       const bool on = present && fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl;
       const unsigned long long b = __ballot(on);
       if (lane == 0) V.wcnt[l * 4 + wave] = __popcll(b);
@@ -541,7 +610,7 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
     for (int l = 0; l < nl; ++l) {
       const LaneT<T> L = V.lanes[l];
       T s, r;
-      lane_local(L, x, y, s, r);
+      lane_local<CV>(L, x, y, s, r);
       const bool on = present && fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl;
       const unsigned long long b = __ballot(on);
       int off = 0, c = 0;
@@ -560,8 +629,9 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
       mx = c > mx ? c : mx;
       if (i == 0) cnt[l] = c;
       if (want_closest) {
-        if (l == 0 || L.hd != prev_hd) ang = fabs(wrap_to_pi(h - L.hd));
-        prev_hd = L.hd;
+        const T hdl = heading_at<CV>(L, s);  // distance_with_heading lane.py:132-147
+        if (l == 0 || hdl != prev_hd) ang = fabs(wrap_to_pi(h - hdl));
+        prev_hd = hdl;
         T a = s - L.len; if (!(a > T(0))) a = T(0);
         T bb = T(0) - s; if (!(bb > T(0))) bb = T(0);
         const T d = fabs(r) + a + bb + T(1) * ang;
@@ -589,12 +659,12 @@ __device__ __forceinline__ T idm_free(const ttrl_params_t& P, T v, T ts, T lim, 
 
 // IDM interaction term  COMFORT_ACC_MAX * (desired_gap(e, f) / not_zero(d))^2 (behavior.py:185-189,
 // desired_gap :192-217, lane_distance_to objects.py:182-197 along e's current lane).
-template <typename T>
+template <bool CV = true, typename T>
 __device__ __forceinline__ T idm_interact(const View<T>& V, const ttrl_params_t& P, int eb, int e, int f) {
   const LaneT<T> L = V.lanes[V.lane[eb + e]];
   T s1, r1, s0, r0;
-  lane_local(L, V.x[eb + f], V.y[eb + f], s1, r1);
-  lane_local(L, V.x[eb + e], V.y[eb + e], s0, r0);
+  lane_local<CV>(L, V.x[eb + f], V.y[eb + f], s1, r1);
+  lane_local<CV>(L, V.x[eb + e], V.y[eb + e], s0, r0);
   const T d = s1 - s0;
   const T ev = V.v[eb + e], ec = V.ch[eb + e], es = V.sh[eb + e];
   const T fv = V.v[eb + f], fc = V.ch[eb + f], fs = V.sh[eb + f];
@@ -606,12 +676,12 @@ __device__ __forceinline__ T idm_interact(const View<T>& V, const ttrl_params_t&
 }
 
 // Full IDMVehicle.acceleration(ego=e, front=f) with the caller's DELTA (behavior.py:150-190).
-template <typename T>
+template <bool CV = true, typename T>
 __device__ __forceinline__ T idm_acc(const View<T>& V, const ttrl_params_t& P, int eb, int e, int f, T delta) {
   if (e < 0) return T(0);
   const LaneT<T> L = V.lanes[V.lane[eb + e]];
   T a = idm_free(P, V.v[eb + e], V.ts[eb + e], L.lim, delta);
-  if (f >= 0) a -= idm_interact(V, P, eb, e, f);
+  if (f >= 0) a -= idm_interact<CV>(V, P, eb, e, f);
   return a;
 }
 
@@ -704,7 +774,7 @@ __device__ unsigned long long g_phase[20];
 // vehicle state of the workgroup's envs is resident in LDS for the launch (HBM is read once
 // and written once); each phase loads the few fields it needs into registers, so no state is
 // live across phases and the kernel runs at high occupancy without spilling.
-template <typename T, int NS, int EPW>
+template <typename T, int NS, int EPW, bool CV>
 __global__ void __launch_bounds__(NS* EPW, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES : (sizeof(T) == 8 ? 2 : 4))
 simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int32_t* __restrict__ actions,
                 int frames, double dt_d, int mode, int ablate) {
@@ -745,7 +815,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   PH(15);
   if (i == 0) V.nitem[le] = 0;
   __syncthreads();  // lane table + view staged
-  project_all<T, NS, EPW>(V, P, nl, tid, le, i, present, V.x[me], V.y[me], T(0), false);
+  project_all<T, NS, EPW, CV>(V, P, nl, tid, le, i, present, V.x[me], V.y[me], T(0), false);
   const int kind = V.kind[me];
 
   PH(11);
@@ -764,11 +834,11 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       } else if (act == TTRL_LANE_LEFT || act == TTRL_LANE_RIGHT) {  // controller.py:103-124
         int id = tgt + (act == TTRL_LANE_RIGHT ? 1 : -1);
         id = id < 0 ? 0 : (id > nl - 1 ? nl - 1 : id);
-        if (reachable(V.lanes[id], T(P.lane_vehicle_length), x, y)) tgt = id;
+        if (reachable<CV>(V.lanes[id], T(P.lane_vehicle_length), x, y)) tgt = id;
       }
       // ControlledVehicle.act low-level control (controller.py:126-133); Road.act recomputes
       // the same values this frame, the standalone ttrl_meta_action returns them.
-      V.steer[me] = steering_control(V.lanes[tgt], P, x, y, h, v);
+      V.steer[me] = steering_control<CV>(V.lanes[tgt], P, x, y, h, v);
       V.acc[me] = T(P.kp_a) * (ts - v);
       V.ts[me] = ts;
       V.tgt[me] = (int8_t)tgt;
@@ -797,8 +867,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         bool left = false, right = false;
         if (fire) {
           const bool moving = !(fabs(v) < T(1));
-          left = lane > 0 && moving && reachable(V.lanes[lane - 1], T(P.lane_vehicle_length), x, y);
-          right = lane < nl - 1 && moving && reachable(V.lanes[lane + 1], T(P.lane_vehicle_length), x, y);
+          left = lane > 0 && moving && reachable<CV>(V.lanes[lane - 1], T(P.lane_vehicle_length), x, y);
+          right = lane < nl - 1 && moving && reachable<CV>(V.lanes[lane + 1], T(P.lane_vehicle_length), x, y);
         }
         // Queries of every vehicle: the own lane's front (its rear only feeds MOBIL's politeness
         // term) and, while changing lane, the target lane's front (IDMVehicle.act behavior.py:118-131).
@@ -807,7 +877,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           T rr;
-          lane_local(V.lanes[ql[q] < 0 ? 0 : ql[q]], x, y, s2[q], rr);
+          lane_local<CV>(V.lanes[ql[q] < 0 ? 0 : ql[q]], x, y, s2[q], rr);
         }
         int f2[2] = {-1, -1}, r2[2] = {-1, -1};
         PH(1);
@@ -856,7 +926,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             const int side = it >> 14, vi = it & 0x3fff, ve = eb + vi;
             const int ln = V.lane[ve] + (side ? 1 : -1);
             T sq, rr;
-            lane_local(V.lanes[ln], V.x[ve], V.y[ve], sq, rr);
+            lane_local<CV>(V.lanes[ln], V.x[ve], V.y[ve], sq, rr);
             T sf = K<T>::inf(), sr = -K<T>::inf();
             int fp = -1, rp = -1;
             const size_t rowb = ((size_t)ln * EPW + le) * (NS + 1);
@@ -888,7 +958,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             const int e_ = g == 0 ? nf : (g <= 2 ? vi : -1);
             const int f_ = g == 0 ? vi : (g == 1 ? np_ : op);
             T term = T(0);
-            if (e_ >= 0 && f_ >= 0) term = idm_interact(V, P, eb, e_, f_);
+            if (e_ >= 0 && f_ >= 0) term = idm_interact<CV>(V, P, eb, e_, f_);
             T fr = T(0);
             if (g == 0 && nf >= 0) fr = idm_free(P, V.v[eb + nf], V.ts[eb + nf], V.lanes[V.lane[eb + nf]].lim, delta);
             const T t_np = __shfl_xor(term, 1, G), t_op = __shfl_xor(term, 2, G);
@@ -902,9 +972,9 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
                 if (op >= 0) sa -= t_op;
                 T jerk;
                 if (polite) {
-                  const T nfa = idm_acc(V, P, eb, nf, np_, delta);
-                  const T ofa = idm_acc(V, P, eb, of, vi, delta);
-                  const T ofpa = idm_acc(V, P, eb, of, op, delta);
+                  const T nfa = idm_acc<CV>(V, P, eb, nf, np_, delta);
+                  const T ofa = idm_acc<CV>(V, P, eb, of, vi, delta);
+                  const T ofpa = idm_acc<CV>(V, P, eb, of, op, delta);
                   jerk = spa - sa + T(P.politeness) * (nfpa - nfa + ofpa - ofa);
                 } else {
                   jerk = spa - sa + T(P.politeness) * T(0);
@@ -942,8 +1012,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
           if (!(lane != Ti && tv == Ti)) return false;
           const LaneT<T> L = V.lanes[V.lane[eb + ii]];
           T s1, r1, s0, r0;
-          lane_local(L, x, y, s1, r1);
-          lane_local(L, V.x[eb + ii], V.y[eb + ii], s0, r0);
+          lane_local<CV>(L, x, y, s1, r1);
+          lane_local<CV>(L, V.x[eb + ii], V.y[eb + ii], s0, r0);
           const T d = s1 - s0;
           const T ev = V.v[eb + ii], ec = V.ch[eb + ii], es = V.sh[eb + ii];
           const T dvx = ev * ec - v * V.ch[me], dvy = ev * es - v * V.sh[me];
@@ -995,17 +1065,17 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       const bool mdp = present && kind == TTRL_MDP;
       if (idm || mdp) {  // one steering pass for both kinds (the ego steers to its own target)
         V.steer[me] = (idm && (ablate & A_NO_STEER)) ? T(0)
-                                                    : steering_control(V.lanes[idm ? tgt_new : tgt], P, x, y, V.h[me], v);
+                                                    : steering_control<CV>(V.lanes[idm ? tgt_new : tgt], P, x, y, V.h[me], v);
       }
       if (idm) {
         const T a_free = V.afree[me];
         const int f0 = V.f0[me];
         T acc = a_free;
-        if (f0 >= 0) acc -= idm_interact(V, P, eb, i, f0);
+        if (f0 >= 0) acc -= idm_interact<CV>(V, P, eb, i, f0);
         if (lane != tgt_new) {
           const int ft = tgt_new == tgt ? (int)V.ft[me] : side_front;
           T a2 = a_free;
-          if (ft >= 0) a2 -= idm_interact(V, P, eb, i, ft);
+          if (ft >= 0) a2 -= idm_interact<CV>(V, P, eb, i, ft);
           if (a2 < acc) acc = a2;
         }
         V.acc[me] = clip(acc, -T(P.acc_max), T(P.acc_max));
@@ -1055,7 +1125,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         if constexpr (sizeof(T) == 8) V.xf[me] = (float)x;
       }
       PH(6);
-      const int cl = project_all<T, NS, EPW>(V, P, nl, tid, le, i, present, x, y, h, !(ablate & A_NO_LANE));
+      const int cl = project_all<T, NS, EPW, CV>(V, P, nl, tid, le, i, present, x, y, h, !(ablate & A_NO_LANE));
       if (present && !(ablate & A_NO_LANE)) V.lane[me] = (int8_t)cl;  // on_state_update kinematics.py:170-177
       if (i == 0) V.pq_n[le] = 0;
       __syncthreads();
@@ -1283,7 +1353,7 @@ __device__ __forceinline__ T feature(const LaneT<T>& L, int f, T x, T y, T h, T 
       lane_local(L, x, y, ls, lr);
       if (f == TTRL_F_LONG_OFF) return ls;
       if (f == TTRL_F_LAT_OFF) return lr;
-      return wrap_to_pi(h - L.hd);
+      return wrap_to_pi(h - heading_at(L, ls));  // AbstractLane.local_angle lane.py:127-130
     }
     default: return T(0);
   }
@@ -1318,13 +1388,7 @@ kinematics_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttr
   const bool slot = env_ok && i < N;
   const size_t k = (size_t)env * N + i, k0 = (size_t)env * N;
   {
-    if (tid < R.n_lanes) {
-      LaneT<T> L;
-      L.sx = T(R.start_x[tid]); L.sy = T(R.start_y[tid]); L.dx = T(R.dir_x[tid]); L.dy = T(R.dir_y[tid]);
-      L.len = T(R.length[tid]); L.w = T(R.width[tid]); L.hd = T(R.heading[tid]); L.lim = T(R.speed_limit[tid]);
-      L.forb = R.forbidden[tid]; L._pad = 0;
-      s_lanes[tid] = L;
-    }
+    if (tid < R.n_lanes) s_lanes[tid] = make_lane<T>(R, tid);
     if (i == 0) s_cnt[le] = 0;
   }
   const int V = cfg.vehicles_count, F = cfg.n_features;
@@ -1447,11 +1511,7 @@ grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid
     const T x = ((const T*)st.x)[k], y = ((const T*)st.y)[k], h = ((const T*)st.heading)[k];
     const T v = ((const T*)st.speed)[k];
     const int ln = st.lane[k];
-    LaneT<T> L, EL;
-    L.sx = T(R.start_x[ln]); L.sy = T(R.start_y[ln]); L.dx = T(R.dir_x[ln]); L.dy = T(R.dir_y[ln]);
-    L.len = T(R.length[ln]); L.w = T(R.width[ln]); L.hd = T(R.heading[ln]); L.lim = T(R.speed_limit[ln]); L.forb = 0;
-    EL.sx = T(R.start_x[elane]); EL.sy = T(R.start_y[elane]); EL.dx = T(R.dir_x[elane]); EL.dy = T(R.dir_y[elane]);
-    EL.len = T(R.length[elane]); EL.w = T(R.width[elane]); EL.hd = T(R.heading[elane]); EL.lim = T(0); EL.forb = 0;
+    const LaneT<T> L = make_lane<T>(R, ln), EL = make_lane<T>(R, elane);
     const T c = t_cos(h), s = t_sin(h), ec = t_cos(eh), es = t_sin(eh);
     T rx = x - ex, ry = y - ey;
     for (int ci = 0; ci < F; ++ci) {
@@ -1473,15 +1533,17 @@ grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid
     const T spacing = T(cfg.step_x) < T(cfg.step_y) ? T(cfg.step_x) : T(cfg.step_y);
     const T lpd = T(cfg.lane_perception_distance);
     for (int l = 0; l < R.n_lanes; ++l) {
-      const T sx = T(R.start_x[l]), sy = T(R.start_y[l]), dx = T(R.dir_x[l]), dy = T(R.dir_y[l]);
-      const T origin = (ex - sx) * dx + (ey - sy) * dy;
+      const LaneT<T> L = make_lane<T>(R, l);
+      T origin, olat;
+      lane_local(L, ex, ey, origin, olat);
       const T start = origin - lpd, stop = origin + lpd;
       const long n = (long)ceil((stop - start) / spacing);
       const T d1 = (start + spacing) - start;
       for (long q = tid; q < n; q += blockDim.x) {
         T wp = q == 0 ? start : (q == 1 ? start + spacing : start + T(q) * d1);
         wp = clip(wp, T(0), T(R.length[l]));
-        T px = sx + wp * dx + T(0) * (-dy), py = sy + wp * dy + T(0) * dx;
+        T px, py;
+        lane_position(L, wp, T(0), px, py);
         px -= ex; py -= ey;
         const T fx = floor((px - T(cfg.grid_min_x)) / T(cfg.step_x));
         const T fy = floor((py - T(cfg.grid_min_y)) / T(cfg.step_y));
@@ -1583,12 +1645,15 @@ __global__ void __launch_bounds__(64) ttc_obs_kernel(ttrl_state_t st, ttrl_lane_
   const int el = st.lane[base];
   const T ex = X[base], ey = Y[base];
   const T ec = t_cos(H[base]), es = t_sin(H[base]);
-  const T sdx = T(R.dir_x[el]), sdy = T(R.dir_y[el]), sx0 = T(R.start_x[el]), sy0 = T(R.start_y[el]);
-  const T s_ego = (ex - sx0) * sdx + (ey - sy0) * sdy;
+  const LaneT<T> EL = make_lane<T>(R, el);
+  T s_ego, r_ego;
+  lane_local(EL, ex, ey, s_ego, r_ego);
   for (int j = 1 + tid; j < N; j += 64) {
     if (st.kind[base + j] == TTRL_ABSENT) continue;
     const T vo = Vv[base + j];
-    const T ld = (X[base + j] - sx0) * sdx + (Y[base + j] - sy0) * sdy - s_ego;  // lane_distance_to
+    T s_o, r_o;
+    lane_local(EL, X[base + j], Y[base + j], s_o, r_o);
+    const T ld = s_o - s_ego;  // lane_distance_to objects.py:182-197
     const T proj = vo * (t_cos(H[base + j]) * ec + t_sin(H[base + j]) * es);
     const int lo = st.lane[base + j];
     const T margin = T(P.length) / T(2) + T(P.length) / T(2);
@@ -1827,9 +1892,10 @@ __global__ void reset_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t
   auto closest = [&](double x, double y, double h) {
     int best = 0; double bd = 0;
     for (int l = 0; l < nl; ++l) {
-      const double dx = x - R.start_x[l], dy = y - R.start_y[l];
-      const double s = dx * R.dir_x[l] + dy * R.dir_y[l], r = dx * (-R.dir_y[l]) + dy * R.dir_x[l];
-      const double ang = fabs(wrap_to_pi(h - R.heading[l]));
+      const LaneT<double> L = make_lane<double>(R, l);
+      double s, r;
+      lane_local(L, x, y, s, r);
+      const double ang = fabs(wrap_to_pi(h - heading_at(L, s)));
       double a = s - R.length[l]; if (!(a > 0)) a = 0;
       double c = 0 - s; if (!(c > 0)) c = 0;
       const double d = fabs(r) + a + c + 1.0 * ang;
@@ -1839,7 +1905,8 @@ __global__ void reset_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t
   };
   auto track = [&](double x, double y, bool first) {
     for (int l = 0; l < nl; ++l) {
-      const double s = (x - R.start_x[l]) * R.dir_x[l] + (y - R.start_y[l]) * R.dir_y[l];
+      double s, r;
+      lane_local(make_lane<double>(R, l), x, y, s, r);
       if (first || s > smax[l]) smax[l] = s;
     }
   };
@@ -1852,10 +1919,12 @@ __global__ void reset_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t
   }
   {
     const int l = cfg.ego_lane;
-    const double ex = R.start_x[l] + cfg.ego_x * R.dir_x[l] + 0.0 * (-R.dir_y[l]);
-    const double ey = R.start_y[l] + cfg.ego_x * R.dir_y[l] + 0.0 * R.dir_x[l];
-    st.kind[b] = TTRL_MDP; X[b] = T(ex); Y[b] = T(ey); Hh[b] = T(R.heading[l]); Vv[b] = T(cfg.ego_speed);
-    const int ln = closest(ex, ey, R.heading[l]);
+    const LaneT<double> L = make_lane<double>(R, l);
+    double ex, ey;
+    lane_position(L, cfg.ego_x, 0.0, ex, ey);
+    const double eh = heading_at(L, cfg.ego_x);
+    st.kind[b] = TTRL_MDP; X[b] = T(ex); Y[b] = T(ey); Hh[b] = T(eh); Vv[b] = T(cfg.ego_speed);
+    const int ln = closest(ex, ey, eh);
     st.lane[b] = st.target_lane[b] = ln;
     const int si = speed_to_index(P, cfg.ego_speed);
     st.speed_index[b] = si;
@@ -1869,11 +1938,13 @@ __global__ void reset_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t
     const double offset = cfg.spacing * (12 + 1.0 * sp) * cfg.density_factor;
     double x0 = smax[lid];
     x0 += offset * (0.9 + (1.1 - 0.9) * pcg_double(g));
-    const double px = R.start_x[lid] + x0 * R.dir_x[lid] + 0.0 * (-R.dir_y[lid]);
-    const double py = R.start_y[lid] + x0 * R.dir_y[lid] + 0.0 * R.dir_x[lid];
+    const LaneT<double> L = make_lane<double>(R, lid);
+    double px, py;
+    lane_position(L, x0, 0.0, px, py);
+    const double ph = heading_at(L, x0);
     st.kind[k] = TTRL_IDM; st.lane_change[k] = (uint8_t)cfg.lane_change;
-    X[k] = T(px); Y[k] = T(py); Hh[k] = T(R.heading[lid]); Vv[k] = T(sp); TS[k] = T(sp);
-    const int ln = closest(px, py, R.heading[lid]);
+    X[k] = T(px); Y[k] = T(py); Hh[k] = T(ph); Vv[k] = T(sp); TS[k] = T(sp);
+    const int ln = closest(px, py, ph);
     st.lane[k] = st.target_lane[k] = ln;
     TM[k] = T(pymod((px + py) * 3.141592653589793, P.lane_change_delay));
     DL[k] = T(cfg.delta_lo + (cfg.delta_hi - cfg.delta_lo) * pcg_double(g));
@@ -1891,8 +1962,8 @@ __global__ void rewards_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_reward
   const T v = ((const T*)st.speed)[k], x = ((const T*)st.x)[k], y = ((const T*)st.y)[k];
   const int l = st.lane[k];
   const T hs = clip(lmap(v, T(cfg.speed_lo), T(cfg.speed_hi), T(0), T(1)), T(0), T(1));
-  const T dx = x - T(R.start_x[l]), dy = y - T(R.start_y[l]);
-  const T s = dx * T(R.dir_x[l]) + dy * T(R.dir_y[l]), r = dx * (-T(R.dir_y[l])) + dy * T(R.dir_x[l]);
+  T s, r;
+  lane_local(make_lane<T>(R, l), x, y, s, r);
   const bool onroad = fabs(r) <= T(R.width[l]) / T(2) + T(0) && -T(5) <= s && s < T(R.length[l]) + T(5);
   const bool crashed = st.crashed[k] != 0;
   T rw = T(cfg.collision_reward) * T(crashed ? 1 : 0) + T(cfg.high_speed_reward) * hs;
@@ -1927,8 +1998,14 @@ int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_par
   const int blocks = (s.n_envs + EPW - 1) / EPW;
   if (blocks == 0) return TTRL_OK;
   const size_t lds = host_view_bytes(sizeof(T) == 8 ? TTRL_F64 : TTRL_F32, EPW, NS, R.n_lanes);
-  hipLaunchKernelGGL((simulate_kernel<T, NS, EPW>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, P, actions,
-                     frames, dt, mode, ablate);
+  bool curved = false;
+  for (int l = 0; l < R.n_lanes; ++l) curved |= R.type[l] != TTRL_LANE_STRAIGHT;
+  if (curved)
+    hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, true>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, P,
+                       actions, frames, dt, mode, ablate);
+  else
+    hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, false>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, P,
+                       actions, frames, dt, mode, ablate);
   return launch_status();
 }
 

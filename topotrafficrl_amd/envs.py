@@ -84,6 +84,9 @@ class VecHighwayEnv:
             "other_vehicles_type": "ttrl_env.vehicle.behavior.IDMVehicle",
             "manual_control": False,
             # scene
+            "road": "straight",            # lane geometry: "straight" | "sine" | "circular" (lane.py:235-350)
+            "road_params": {},             # sine: amplitude, pulsation, phase; circular: center, radius,
+                                           # start_phase, end_phase, clockwise
             "lanes_count": 4,
             "road_length": 10000.0,
             "speed_limit": 30.0,
@@ -125,8 +128,16 @@ class VecHighwayEnv:
         if slots < n:
             raise ValueError("vehicle_slots < vehicles_count")
         self.device = torch.device(c["device"])
-        self.network = RoadNetwork.straight_road_network(int(c["lanes_count"]), length=float(c["road_length"]),
-                                                         speed_limit=float(c["speed_limit"]))
+        lanes, rp, lim = int(c["lanes_count"]), dict(c["road_params"]), float(c["speed_limit"])
+        if c["road"] == "straight":
+            self.network = RoadNetwork.straight_road_network(lanes, length=float(c["road_length"]), speed_limit=lim,
+                                                             **rp)
+        elif c["road"] == "sine":
+            self.network = RoadNetwork.sine_road_network(lanes, length=float(c["road_length"]), speed_limit=lim, **rp)
+        elif c["road"] == "circular":
+            self.network = RoadNetwork.circular_road_network(lanes, speed_limit=lim, **rp)
+        else:
+            raise ValueError(f"unknown road geometry {c['road']!r}")
         act_cfg = dict(c["action"])
         self.params = _abi.default_params(target_speeds=act_cfg.get("target_speeds"), **dict(c["idm"]))
         self.state = BatchState(self.num_envs, slots, device=self.device, dtype=c["dtype"])

@@ -17,10 +17,23 @@ from .state import BatchState
 
 
 class RoadNetwork:
-    """A single straight road "0" -> "1" with parallel StraightLanes (road.py:291-321)."""
+    """A single road "0" -> "1" with parallel lanes: StraightLanes (road.py:291-321) or the
+    curved SineLane / CircularLane classes (lane.py:235-350)."""
 
     def __init__(self, table: _abi.LaneTable):
         self.table = table
+
+    @classmethod
+    def sine_road_network(cls, lanes: int = 4, length: float = 10000, amplitude: float = 5.0,
+                          pulsation: float = 2 * 3.141592653589793 / 200, phase: float = 0.0,
+                          speed_limit: float = 30) -> "RoadNetwork":
+        return cls(_abi.sine_lane_table(lanes, length, amplitude, pulsation, phase, speed_limit))
+
+    @classmethod
+    def circular_road_network(cls, lanes: int = 3, center=(0.0, 0.0), radius: float = 200.0,
+                              start_phase: float = -3.141592653589793 / 2, end_phase: float = 3.141592653589793 / 2,
+                              clockwise: bool = True, speed_limit: float = 30) -> "RoadNetwork":
+        return cls(_abi.circular_lane_table(lanes, center, radius, start_phase, end_phase, clockwise, speed_limit))
 
     @classmethod
     def straight_road_network(cls, lanes: int = 4, start: float = 0, length: float = 10000, angle: float = 0,
