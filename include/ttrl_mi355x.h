@@ -33,8 +33,10 @@
 extern "C" {
 #endif
 
-#define TTRL_ABI_VERSION 2
-#define TTRL_MAX_LANES 16
+#define TTRL_ABI_VERSION 3
+#define TTRL_MAX_LANES 32
+#define TTRL_MAX_ROADS 32
+#define TTRL_ROUTE_MAX 4
 
 enum { TTRL_F32 = 0, TTRL_F64 = 1 };
 
@@ -55,14 +57,17 @@ enum { TTRL_LANE_LEFT = 0, TTRL_IDLE = 1, TTRL_LANE_RIGHT = 2, TTRL_FASTER = 3, 
 enum { TTRL_LANE_STRAIGHT = 0, TTRL_LANE_SINE = 1, TTRL_LANE_CIRCULAR = 2 };
 
 /*
- * One road "0"->"1" with n_lanes lanes in graph order (RoadNetwork.straight_road_network,
- * road.py:291-321, or any single-edge network of Straight / Sine / Circular lanes).
- * Derived geometry (direction, length, heading) is computed on the host with the same
- * float64 formulas as the lane constructors and passed in.  Shared by every env of a batch.
+ * A RoadNetwork (road.py:21-389) flattened in lanes_list() order: lane l belongs to road
+ * road[l] = the (from, to) node pair, roads numbered in graph order, and is lane lane_id[l]
+ * of that road.  A single road "0"->"1" (RoadNetwork.straight_road_network road.py:291-321,
+ * or parallel Sine / Circular lanes) is n_roads = 1; the intersection of IntersectionEnv
+ * (intersection_env.py:141-249) is 20 lanes on 20 roads.  Derived geometry (direction,
+ * length, heading) is computed on the host with the float64 formulas of the lane
+ * constructors.  Shared by every env of a batch.
  */
 typedef struct ttrl_lane_table {
   int32_t n_lanes;
-  int32_t _pad;
+  int32_t n_roads;
   double start_x[TTRL_MAX_LANES], start_y[TTRL_MAX_LANES];
   double dir_x[TTRL_MAX_LANES], dir_y[TTRL_MAX_LANES];   /* direction; lateral = (-dir_y, dir_x) */
   double length[TTRL_MAX_LANES], width[TTRL_MAX_LANES];
@@ -72,6 +77,15 @@ typedef struct ttrl_lane_table {
   double amplitude[TTRL_MAX_LANES], pulsation[TTRL_MAX_LANES], phase[TTRL_MAX_LANES];  /* SineLane */
   double center_x[TTRL_MAX_LANES], center_y[TTRL_MAX_LANES], radius[TTRL_MAX_LANES];   /* Circular */
   double start_phase[TTRL_MAX_LANES], direction[TTRL_MAX_LANES];  /* direction: +1 clockwise, -1 */
+  /* network topology (all zero for a single road: road 0, lane_id = l) */
+  int32_t road[TTRL_MAX_LANES];      /* road of each lane                                   */
+  int32_t lane_id[TTRL_MAX_LANES];   /* index of the lane within its road                   */
+  int32_t priority[TTRL_MAX_LANES];  /* AbstractLane.priority (RegulatedRoad)               */
+  int32_t exit_lane[TTRL_MAX_LANES]; /* 1: an "il*" -> "o*" lane (has_arrived, _clear_vehicles) */
+  int32_t road_from[TTRL_MAX_ROADS], road_to[TTRL_MAX_ROADS];    /* node ids                */
+  int32_t road_first[TTRL_MAX_ROADS], road_n[TTRL_MAX_ROADS];    /* first lane, lane count  */
+  int32_t regulation_frequency;      /* RegulatedRoad.REGULATION_FREQUENCY (2); 0 = Road    */
+  int32_t _pad2;
 } ttrl_lane_table_t;
 
 /*
@@ -107,8 +121,11 @@ typedef struct ttrl_params {
 } ttrl_params_t;
 
 /*
- * Batched vehicle state, struct-of-arrays, row-major [n_envs][n_veh].
- * Real fields have dtype `dtype` (float or double); vehicle 0 of an env is the ego.
+ * Batched vehicle state, struct-of-arrays, row-major [n_envs][n_veh], slots in the order of
+ * the reference's road.vehicles list.  Real fields have dtype `dtype` (float or double).
+ * The ego (env.vehicle) is the env's first TTRL_MDP slot: slot 0 on the highway, after the
+ * initial traffic in the intersection.
+ * The route / regulation fields may be NULL for a single-road network without regulation.
  */
 typedef struct ttrl_state {
   int32_t n_envs;
@@ -122,6 +139,11 @@ typedef struct ttrl_state {
   int32_t *speed_index;           /* MDPVehicle.speed_index (ego rows)         */
   uint8_t *kind;                  /* TTRL_ABSENT / TTRL_MDP / TTRL_IDM         */
   uint8_t *crashed, *has_impact, *lane_change; /* crashed, impact!=None, enable_lane_change */
+  int8_t *route_road, *route_lane; /* [E][N][TTRL_ROUTE_MAX] ControlledVehicle.route entries:
+                                      road id, lane id within the road (-1 = None)           */
+  int8_t *route_n;                /* route length, -1 = route None                          */
+  uint8_t *yielding;              /* RegulatedRoad: is_yielding                             */
+  int32_t *reg_steps;             /* [E] RegulatedRoad.steps (frames since the road was made) */
 } ttrl_state_t;
 
 /* KinematicObservation config (observation.py:159-196).  Feature codes below. */

@@ -38,6 +38,11 @@ class HostState:
             self.a[f] = np.zeros((n_envs, n_veh), dtype=np.uint8)
         self.a["speed_index"][:] = -1
         self.a["delta"][:] = 4.0
+        for f in _abi.ROUTE_FIELDS:
+            self.a[f] = np.full((n_envs, n_veh, _abi.ROUTE_MAX), -1, dtype=np.int8)
+        self.a["route_n"] = np.full((n_envs, n_veh), -1, dtype=np.int8)
+        self.a["yielding"] = np.zeros((n_envs, n_veh), dtype=np.uint8)
+        self.a["reg_steps"] = np.zeros(n_envs, dtype=np.int32)
 
     def __getitem__(self, k):
         return self.a[k]
@@ -70,6 +75,32 @@ class HostState:
         h.a["kind"][:, :n] = _abi.IDM
         h.a["kind"][:, 0] = _abi.MDP
         h.a["lane_change"][:, 1:n] = 1  # IDMVehicle.enable_lane_change; the MDP ego has none
+        return h
+
+    @classmethod
+    def from_ix(cls, d, key: str, index, envs: int = 1, pad_to: int | None = None) -> "HostState":
+        """Rows of a gen_golden_ix.py npz: ``d[f"{key}_{field}"][index]`` (key "pre", "post",
+        "frame", "act"; index an int or a tuple (step, frame)); vehicles in list order, absent
+        slots (kind 0) where the list is shorter."""
+        get = lambda f: np.asarray(d[f"{key}_{f}"][index])  # noqa: E731
+        n = get("x").shape[0]
+        N = pad_to or n
+        h = cls(envs, N)
+        for f in _abi.REAL_FIELDS:
+            v = get(f).astype(np.float64)
+            if f.startswith("impact"):
+                v = np.nan_to_num(v, nan=0.0)
+            h.a[f][:, :n] = v
+        for f in ("lane", "target_lane", "speed_index"):
+            h.a[f][:, :n] = get(f)
+        for f in ("crashed", "kind", "yielding"):
+            h.a[f][:, :n] = get(f)
+        h.a["has_impact"][:, :n] = np.isfinite(get("impact_x")).astype(np.uint8)
+        h.a["lane_change"][:, :n] = (get("kind") == _abi.IDM).astype(np.uint8)
+        h.a["route_n"][:, :n] = get("route_n")
+        for f in _abi.ROUTE_FIELDS:
+            h.a[f][:, :n] = get(f)
+        h.a["reg_steps"][:] = get("reg_steps")
         return h
 
 

@@ -26,6 +26,9 @@ typedef struct {
   double *x, *y, *h, *v, *ts, *timer, *delta, *steer, *acc, *ix, *iy;
   int32_t *lane, *tgt, *sidx;
   uint8_t *kind, *crashed, *hasimp, *lc;
+  int8_t *rroad, *rlane, *rn;   /* route entries [E*N][TTRL_ROUTE_MAX], length (-1 = None) */
+  uint8_t* yield;
+  int32_t* reg;
 } S;
 
 static S view(const ttrl_state_t* s) {
@@ -36,6 +39,7 @@ static S view(const ttrl_state_t* s) {
   o.steer = (double*)s->steer; o.acc = (double*)s->acc; o.ix = (double*)s->impact_x; o.iy = (double*)s->impact_y;
   o.lane = s->lane; o.tgt = s->target_lane; o.sidx = s->speed_index;
   o.kind = s->kind; o.crashed = s->crashed; o.hasimp = s->has_impact; o.lc = s->lane_change;
+  o.rroad = s->route_road; o.rlane = s->route_lane; o.rn = s->route_n; o.yield = s->yielding; o.reg = s->reg_steps;
   return o;
 }
 
@@ -126,6 +130,70 @@ static int closest_lane(const ttrl_lane_table_t* R, double px, double py, double
   return best;
 }
 
+/* AbstractLane.distance lane.py:127-130 */
+static double lane_dist(const ttrl_lane_table_t* R, int l, double px, double py) {
+  double s, r; local(R, l, px, py, &s, &r);
+  double a = s - R->length[l]; if (0 > a) a = 0;
+  double b = 0 - s; if (0 > b) b = 0;
+  return fabs(r) + a + b;
+}
+/* AbstractLane.after_end lane.py:120-125 */
+static int after_end(const ttrl_lane_table_t* R, const ttrl_params_t* P, int l, double px, double py) {
+  double s, r; local(R, l, px, py, &s, &r);
+  return s > R->length[l] - P->lane_vehicle_length / 2;
+}
+/* RoadNetwork.next_lane_given_next_road road.py:136-154 */
+static int next_given(const ttrl_lane_table_t* R, int cur_road, int id, int nroad, int nid, double px, double py,
+                      double* dist) {
+  if (R->road_n[cur_road] == R->road_n[nroad]) {
+    if (nid < 0) nid = id;
+  } else {
+    double bd = 0;
+    for (int l = 0; l < R->road_n[nroad]; ++l) {
+      double d = lane_dist(R, R->road_first[nroad] + l, px, py);
+      if (l == 0 || d < bd) { bd = d; nid = l; }             /* min(): first minimum */
+    }
+  }
+  *dist = lane_dist(R, R->road_first[nroad] + nid, px, py);
+  return nid;
+}
+/* RoadNetwork.next_lane road.py:73-134, with the route popped in place as in Python */
+static int next_lane(S* o, const ttrl_lane_table_t* R, int k, int cur, double x, double y) {
+  const int rd = R->road[cur], id = R->lane_id[cur], to = R->road_to[rd];
+  int nroad = -1, nid = -1;
+  if (o->rn && o->rn[k] > 0) {
+    int8_t* rr = o->rroad + (size_t)k * TTRL_ROUTE_MAX;
+    int8_t* rl = o->rlane + (size_t)k * TTRL_ROUTE_MAX;
+    if (rr[0] == rd) {                                        /* route.pop(0) */
+      for (int q = 0; q + 1 < TTRL_ROUTE_MAX; ++q) { rr[q] = rr[q + 1]; rl[q] = rl[q + 1]; }
+      rr[TTRL_ROUTE_MAX - 1] = rl[TTRL_ROUTE_MAX - 1] = -1;
+      o->rn[k] -= 1;
+    }
+    if (o->rn[k] > 0 && R->road_from[rr[0]] == to) { nroad = rr[0]; nid = rl[0]; }
+  }
+  double s, r, px, py;
+  local(R, cur, x, y, &s, &r);
+  position(R, cur, s, 0, &px, &py);                           /* projected position */
+  double d;
+  if (nroad < 0) {
+    int found = 0; double bd = 0;
+    for (int q = 0; q < R->n_roads; ++q) {
+      if (R->road_from[q] != to) continue;
+      int cand = next_given(R, rd, id, q, -1, px, py, &d);
+      if (!found || d < bd) { bd = d; nroad = q; nid = cand; found = 1; }
+    }
+    if (!found) return cur;                                   /* KeyError: no road leaves `to` */
+  } else {
+    nid = next_given(R, rd, id, nroad, nid, px, py, &d);
+  }
+  return R->road_first[nroad] + nid;
+}
+/* ControlledVehicle.follow_road controller.py:135-143 */
+static void follow_road(S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base, int i) {
+  const int k = base + i;
+  if (after_end(R, P, o->tgt[k], o->x[k], o->y[k])) o->tgt[k] = next_lane(o, R, k, o->tgt[k], o->x[k], o->y[k]);
+}
+
 /* RoadObject.lane_distance_to objects.py:182-197 (along `self`'s current lane) */
 static double lane_distance(const S* o, const ttrl_lane_table_t* R, int base, int self, int other) {
   int l = o->lane[base + self];
@@ -174,7 +242,8 @@ static double idm_acc(const S* o, const ttrl_lane_table_t* R, const ttrl_params_
   return a;
 }
 
-/* IDMVehicle.mobil behavior.py:265-324 (route None) */
+static int sgn(int x) { return (x > 0) - (x < 0); }
+/* IDMVehicle.mobil behavior.py:265-324 */
 static int mobil(const S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base, int self, int l) {
   double d = o->delta[base + self];
   int np_, nf; neighbour(o, R, P, base, self, l, &np_, &nf);
@@ -183,6 +252,13 @@ static int mobil(const S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P,
   if (nfpa < -P->lane_change_max_braking) return 0;
   int op, of; neighbour(o, R, P, base, self, o->lane[base + self], &op, &of);
   double spa = idm_acc(o, R, P, base, d, self, np_);
+  const int k = base + self;
+  if (o->rn && o->rn[k] > 0 && o->rlane[(size_t)k * TTRL_ROUTE_MAX] >= 0) {  /* planned lane (:296-304) */
+    const int tid = R->lane_id[o->tgt[k]];
+    if (sgn(R->lane_id[l] - tid) != sgn(o->rlane[(size_t)k * TTRL_ROUTE_MAX] - tid)) return 0;
+    if (spa < -P->lane_change_max_braking) return 0;
+    return 1;
+  }
   double sa = idm_acc(o, R, P, base, d, self, op);
   double ofa = idm_acc(o, R, P, base, d, of, self);
   double ofpa = idm_acc(o, R, P, base, d, of, op);
@@ -195,6 +271,7 @@ static int mobil(const S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P,
 static void change_lane_policy(S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base, int self) {
   int lane = o->lane[base + self], tgt = o->tgt[base + self];
   if (lane != tgt) {
+    if (R->road[lane] != R->road[tgt]) return;                 /* not the same road: no abort (:231) */
     for (int j = 0; j < o->N; ++j) {
       if (j == self || o->kind[base + j] == TTRL_ABSENT) continue;
       if (o->lane[base + j] != tgt && o->tgt[base + j] == tgt) {
@@ -208,8 +285,8 @@ static void change_lane_policy(S* o, const ttrl_lane_table_t* R, const ttrl_para
   if (!(P->lane_change_delay < o->timer[base + self])) return;   /* utils.do_every */
   o->timer[base + self] = 0;
   int cand[2], nc = 0;                                             /* RoadNetwork.side_lanes road.py:200-211 */
-  if (lane > 0) cand[nc++] = lane - 1;
-  if (lane < R->n_lanes - 1) cand[nc++] = lane + 1;
+  if (R->lane_id[lane] > 0) cand[nc++] = lane - 1;
+  if (R->lane_id[lane] < R->road_n[R->road[lane]] - 1) cand[nc++] = lane + 1;
   for (int k = 0; k < nc; ++k) {
     if (!reachable(R, P, cand[k], o->x[base + self], o->y[base + self])) continue;
     if (fabs(o->v[base + self]) < 1) continue;
@@ -234,7 +311,7 @@ static double steering_control(const S* o, const ttrl_lane_table_t* R, const ttr
 /* IDMVehicle.act behavior.py:93-137 */
 static void idm_act(S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base, int i) {
   if (o->crashed[base + i]) return;
-  /* follow_road (controller.py:135-143): single-segment road, next_lane is a no-op (road.py:129-130) */
+  follow_road(o, R, P, base, i);
   if (o->lc[base + i]) change_lane_policy(o, R, P, base, i);
   double st = steering_control(o, R, P, base, i, o->tgt[base + i]);
   st = clipd(st, -P->max_steering, P->max_steering);
@@ -252,10 +329,13 @@ static void idm_act(S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, in
 
 /* ControlledVehicle.act controller.py:89-133 with action in {None, LANE_LEFT, LANE_RIGHT, IDLE} */
 static void controlled_act(S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base, int i, int action) {
+  follow_road(o, R, P, base, i);
   if (action == TTRL_LANE_RIGHT || action == TTRL_LANE_LEFT) {
-    int id = o->tgt[base + i] + (action == TTRL_LANE_RIGHT ? 1 : -1);
+    const int t = o->tgt[base + i], rd = R->road[t];
+    int id = R->lane_id[t] + (action == TTRL_LANE_RIGHT ? 1 : -1);
     if (id < 0) id = 0;
-    if (id > R->n_lanes - 1) id = R->n_lanes - 1;
+    if (id > R->road_n[rd] - 1) id = R->road_n[rd] - 1;
+    id += R->road_first[rd];
     if (reachable(R, P, id, o->x[base + i], o->y[base + i])) o->tgt[base + i] = id;
   }
   double st = steering_control(o, R, P, base, i, o->tgt[base + i]);
@@ -374,6 +454,99 @@ static void handle_collisions(S* o, const ttrl_params_t* P, int base, int i, int
   if (inter) { o->crashed[a] = 1; o->crashed[b] = 1; }
 }
 
+/* ---------------------------------------------------------------- RegulatedRoad (regulation.py) */
+/* RoadNetwork.position_heading_along_route road.py:352-389 for ControlledVehicle.
+ * predict_trajectory_constant_speed controller.py:228-247 at times 0.25 .. 2.75 (np.arange(0.25, 3, 0.25)) */
+enum { PRED_T = 11 };
+static void predict(const S* o, const ttrl_lane_table_t* R, int k, double px[PRED_T], double py[PRED_T],
+                    double ph[PRED_T]) {
+  const int cur = o->lane[k];
+  double s0, r0; local(R, cur, o->x[k], o->y[k], &s0, &r0);
+  const int n = (o->rn && o->rn[k] > 0) ? o->rn[k] : 1;     /* route or [lane_index] */
+  const int8_t* rr = o->rn ? o->rroad + (size_t)k * TTRL_ROUTE_MAX : 0;
+  const int8_t* rl = o->rn ? o->rlane + (size_t)k * TTRL_ROUTE_MAX : 0;
+  const int use_route = o->rn && o->rn[k] > 0;
+  for (int t = 0; t < PRED_T; ++t) {
+    const double tt = 0.25 + t * 0.25;
+    double L = s0 + o->v[k] * tt;
+    int idx = 0, lane;
+#define RESOLVE(q) (use_route ? R->road_first[rr[q]] + (rl[q] >= 0 ? rl[q] \
+                      : (R->lane_id[cur] < R->road_n[R->road[cur]] ? R->lane_id[cur] : 0)) : cur)
+    lane = RESOLVE(0);
+    while (n - idx > 1 && L > R->length[lane]) { L -= R->length[lane]; ++idx; lane = RESOLVE(idx); }
+#undef RESOLVE
+    position(R, lane, L, 0, &px[t], &py[t]);
+    ph[t] = heading_at(R, lane, L);
+  }
+}
+/* utils.point_in_rotated_rectangle utils.py:75-91 (rotation by +angle, as written) */
+static int point_in_rect(double x, double y, double cx, double cy, double l, double w, double a) {
+  double c = cos(a), s = sin(a);
+  double dx = x - cx, dy = y - cy;
+  double u = c * dx + (-s) * dy, v = s * dx + c * dy;
+  return -l / 2 <= u && u <= l / 2 && -w / 2 <= v && v <= w / 2;
+}
+/* utils.has_corner_inside utils.py:158-172 over rect_corners(include_midpoints, include_center) :126-155 */
+static int corner_inside(double c1x, double c1y, double l1, double w1, double a1, double c2x, double c2y, double l2,
+                         double w2, double a2) {
+  const double hl = l1 / 2, hw = w1 / 2;
+  const double px[9] = {-hl, -hl, hl, hl, 0, -hl, hl, 0, 0};
+  const double py[9] = {-hw, hw, hw, -hw, 0, 0, 0, -hw, hw};
+  double c = cos(a1), s = sin(a1);
+  for (int q = 0; q < 9; ++q) {
+    double x = c * px[q] + (-s) * py[q] + c1x, y = s * px[q] + c * py[q] + c1y;
+    if (point_in_rect(x, y, c2x, c2y, l2, w2, a2)) return 1;
+  }
+  return 0;
+}
+/* RegulatedRoad.is_conflict_possible regulation.py:80-103 */
+static int conflict(const ttrl_params_t* P, const double* ax, const double* ay, const double* ah, const double* bx,
+                    const double* by, const double* bh) {
+  const double l = 1.5 * P->length, w = 0.9 * P->width;
+  for (int t = 0; t < PRED_T; ++t) {
+    double dx = bx[t] - ax[t], dy = by[t] - ay[t];
+    if (sqrt(dx * dx + dy * dy) > P->length) continue;
+    if (corner_inside(ax[t], ay[t], l, w, ah[t], bx[t], by[t], l, w, bh[t]) ||
+        corner_inside(bx[t], by[t], l, w, bh[t], ax[t], ay[t], l, w, ah[t]))
+      return 1;
+  }
+  return 0;
+}
+/* RegulatedRoad.respect_priorities regulation.py:62-77 (front_distance_to objects.py:204-205) */
+static int respect(const S* o, const ttrl_lane_table_t* R, int a, int b) {
+  const int pa = R->priority[o->lane[a]], pb = R->priority[o->lane[b]];
+  if (pa > pb) return b;
+  if (pa < pb) return a;
+  double fab = cos(o->h[a]) * (o->x[b] - o->x[a]) + sin(o->h[a]) * (o->y[b] - o->y[a]);
+  double fba = cos(o->h[b]) * (o->x[a] - o->x[b]) + sin(o->h[b]) * (o->y[a] - o->y[b]);
+  return fab > fba ? a : b;
+}
+/* RegulatedRoad.enforce_road_rules regulation.py:34-60 (YIELD_DURATION = 0: a yield lasts until
+ * the next enforcement) */
+static void enforce_road_rules(S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base) {
+  const int N = o->N;
+  for (int i = 0; i < N; ++i) {
+    const int k = base + i;
+    if (o->kind[k] != TTRL_ABSENT && o->yield[k]) { o->ts[k] = R->speed_limit[o->lane[k]]; o->yield[k] = 0; }
+  }
+  double* px = malloc(sizeof(double) * 3 * PRED_T * N);
+  double *py = px + PRED_T * N, *ph = py + PRED_T * N;
+  for (int i = 0; i < N; ++i)
+    if (o->kind[base + i] != TTRL_ABSENT) predict(o, R, base + i, px + PRED_T * i, py + PRED_T * i, ph + PRED_T * i);
+  for (int i = 0; i < N; ++i) {
+    if (o->kind[base + i] == TTRL_ABSENT) continue;
+    for (int j = i + 1; j < N; ++j) {
+      if (o->kind[base + j] == TTRL_ABSENT) continue;
+      if (!conflict(P, px + PRED_T * i, py + PRED_T * i, ph + PRED_T * i, px + PRED_T * j, py + PRED_T * j,
+                    ph + PRED_T * j))
+        continue;
+      const int y = respect(o, R, base + i, base + j);
+      if (o->kind[y] == TTRL_IDM) { o->ts[y] = 0; o->yield[y] = 1; }
+    }
+  }
+  free(px);
+}
+
 static int check(const ttrl_state_t* s) {
   if (!s || s->dtype != TTRL_F64 || s->n_envs < 0 || s->n_veh <= 0) return TTRL_E_ARG;
   return 0;
@@ -387,8 +560,8 @@ int oracle_meta_action(const ttrl_state_t* s, const ttrl_lane_table_t* R, const 
     if (actions[e] < 0 || actions[e] > 4) return TTRL_E_ARG;
   for (int e = 0; e < o.E; ++e) {
     int base = e * o.N;
-    if (o.kind[base] != TTRL_MDP) continue;
-    mdp_act(&o, R, P, base, 0, actions[e]);
+    for (int i = 0; i < o.N; ++i)             /* the env's controlled vehicle: its first MDPVehicle */
+      if (o.kind[base + i] == TTRL_MDP) { mdp_act(&o, R, P, base, i, actions[e]); break; }
   }
   return 0;
 }
@@ -415,6 +588,11 @@ int oracle_road_step(const ttrl_state_t* s, const ttrl_lane_table_t* R, const tt
 #pragma omp parallel for schedule(static)
   for (int e = 0; e < o.E; ++e) {
     int base = e * o.N;
+    if (R->regulation_frequency > 0 && o.reg) {               /* RegulatedRoad.step regulation.py:28-32 */
+      o.reg[e] += 1;
+      const int period = (int)(1.0 / dt / R->regulation_frequency);
+      if (period > 0 && o.reg[e] % period == 0) enforce_road_rules(&o, R, P, base);
+    }
     for (int i = 0; i < o.N; ++i)
       if (o.kind[base + i] != TTRL_ABSENT) vehicle_step(&o, R, P, base, i, dt);
     for (int i = 0; i < o.N; ++i) {

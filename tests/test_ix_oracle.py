@@ -1,0 +1,84 @@
+"""The intersection scenario (intersection-v0, the reference's training scenario) on the float64
+oracle against golden episodes captured from the reference's RoadNetwork / RegulatedRoad /
+IDMVehicle / MDPVehicle (oracle/gen_golden_ix.py).  CPU only.
+
+Pinned here per frame: route following (ControlledVehicle.follow_road, RoadNetwork.next_lane
+with the route popped in place), RegulatedRoad.enforce_road_rules every 7th frame (trajectory
+prediction along the route, rotated-rectangle conflicts, priorities), CircularLane turns, and
+the usual IDM / steering / kinematics / collisions, over a 20-lane, 20-road network."""
+import numpy as np
+import pytest
+
+from conftest import golden_files, load_golden
+from oracle.oracle import HostState, Oracle
+from topotrafficrl_amd import _abi
+
+LONGI = {0: _abi.SLOWER, 1: _abi.IDLE, 2: _abi.FASTER}  # DiscreteMetaAction.ACTIONS_LONGI action.py:207
+P_IX = _abi.default_params(target_speeds=[0, 4.5, 9], distance_wanted=7.0, comfort_acc_max=6.0,
+                           comfort_acc_min=-3.0)  # intersection_env.py:258-261
+CONT = ["x", "y", "heading", "speed", "target_speed", "timer", "steer", "acc"]
+DISC = ["lane", "target_lane", "crashed", "has_impact", "speed_index", "kind", "yielding", "route_n",
+        "route_road", "route_lane"]
+IDS = lambda p: p.split("/")[-1][:-4]  # noqa: E731
+
+
+def ix_lanes(d):
+    t = _abi.lane_table_from_arrays(d["lane_table"])
+    return _abi.set_network(t, d["lane_net"], regulation_frequency=2)
+
+
+def check(h: HostState, g: HostState, tol: float, n: int):
+    for k in CONT:
+        err = np.max(np.abs(h[k][:, :n] - g[k][:, :n]) / (1 + np.abs(g[k][:, :n])))
+        assert err <= tol, (k, err)
+    imp = g["has_impact"][:, :n].astype(bool)
+    for k in ("impact_x", "impact_y"):
+        assert np.max(np.abs(h[k][:, :n][imp] - g[k][:, :n][imp]), initial=0.0) <= tol, k
+    for k in DISC:
+        assert np.array_equal(h[k][:, :n], g[k][:, :n]), k
+    assert np.array_equal(h["reg_steps"], g["reg_steps"])
+
+
+@pytest.mark.parametrize("path", golden_files("ix_*"), ids=IDS)
+def test_ix_every_frame(path):
+    d = load_golden(path)
+    o = Oracle(ix_lanes(d), P_IX)
+    steps = int(d["meta"][1])
+    for p in range(steps):
+        n = int((d["pre_kind"][p] > 0).sum())
+        h = HostState.from_ix(d, "pre", p)
+        o.meta_action(h, [LONGI[int(d["actions"][p])]])
+        for f in range(15):
+            if f > 0:
+                h = HostState.from_ix(d, "frame", (p, f - 1))
+            o.road_act(h)
+            check(h, HostState.from_ix(d, "act", (p, f)), 1e-12, n)
+            o.road_step(h)
+            check(h, HostState.from_ix(d, "frame", (p, f)), 1e-12, n)
+
+
+@pytest.mark.parametrize("path", golden_files("ix_*"), ids=IDS)
+def test_ix_policy_steps(path):
+    """The fused 15-frame step from each pre-step state."""
+    d = load_golden(path)
+    o = Oracle(ix_lanes(d), P_IX)
+    for p in range(int(d["meta"][1])):
+        n = int((d["pre_kind"][p] > 0).sum())
+        h = HostState.from_ix(d, "pre", p)
+        o.simulate(h, [LONGI[int(d["actions"][p])]], 15, 1 / 15)
+        check(h, HostState.from_ix(d, "frame", (p, 14)), 1e-7, n)
+
+
+def test_ix_fixtures_exercise_the_scenario():
+    """Route pops, turns onto CircularLanes, yields and crashes all occur in the fixtures."""
+    pops = yields = turns = crashes = 0
+    for path in golden_files("ix_*"):
+        d = load_golden(path)
+        rn = d["frame_route_n"]
+        pops += int(((rn[:, 1:] < rn[:, :-1]) & (rn[:, 1:] >= 0)).sum())
+        yields += int(d["frame_yielding"].sum())
+        circ = np.asarray(d["lane_table"])[:, 0] == _abi.LANE_CIRCULAR
+        lanes = d["frame_lane"][d["frame_kind"] > 0]
+        turns += int(circ[lanes].sum())
+        crashes += int(d["post_crashed"][-1].sum())
+    assert pops > 10 and yields > 10 and turns > 100 and crashes > 0, (pops, yields, turns, crashes)

@@ -11,7 +11,9 @@ import ctypes as C
 
 import numpy as np
 
-MAX_LANES = 16
+MAX_LANES = 32
+MAX_ROADS = 32
+ROUTE_MAX = 4
 N_FEATURES = 14
 F32, F64 = 0, 1
 ABSENT, MDP, IDM = 0, 1, 2
@@ -26,13 +28,16 @@ REAL_FIELDS = ["x", "y", "heading", "speed", "target_speed", "timer", "delta",
                "steer", "acc", "impact_x", "impact_y"]
 I32_FIELDS = ["lane", "target_lane", "speed_index"]
 U8_FIELDS = ["kind", "crashed", "has_impact", "lane_change"]
-ALL_FIELDS = REAL_FIELDS + I32_FIELDS + U8_FIELDS
+# network / regulation fields: shapes [E, N, ROUTE_MAX], [E, N], [E]
+ROUTE_FIELDS = ["route_road", "route_lane"]
+NET_FIELDS = ROUTE_FIELDS + ["route_n", "yielding", "reg_steps"]
+ALL_FIELDS = REAL_FIELDS + I32_FIELDS + U8_FIELDS + NET_FIELDS
 
 ERRORS = {-1: "TTRL_E_ARG (bad argument)", -2: "TTRL_E_LAUNCH (HIP error)", -3: "TTRL_E_UNSUPPORTED"}
 
 
 class LaneTable(C.Structure):
-    _fields_ = [("n_lanes", C.c_int32), ("_pad", C.c_int32),
+    _fields_ = [("n_lanes", C.c_int32), ("n_roads", C.c_int32),
                 ("start_x", C.c_double * MAX_LANES), ("start_y", C.c_double * MAX_LANES),
                 ("dir_x", C.c_double * MAX_LANES), ("dir_y", C.c_double * MAX_LANES),
                 ("length", C.c_double * MAX_LANES), ("width", C.c_double * MAX_LANES),
@@ -41,7 +46,12 @@ class LaneTable(C.Structure):
                 ("amplitude", C.c_double * MAX_LANES), ("pulsation", C.c_double * MAX_LANES),
                 ("phase", C.c_double * MAX_LANES), ("center_x", C.c_double * MAX_LANES),
                 ("center_y", C.c_double * MAX_LANES), ("radius", C.c_double * MAX_LANES),
-                ("start_phase", C.c_double * MAX_LANES), ("direction", C.c_double * MAX_LANES)]
+                ("start_phase", C.c_double * MAX_LANES), ("direction", C.c_double * MAX_LANES),
+                ("road", C.c_int32 * MAX_LANES), ("lane_id", C.c_int32 * MAX_LANES),
+                ("priority", C.c_int32 * MAX_LANES), ("exit_lane", C.c_int32 * MAX_LANES),
+                ("road_from", C.c_int32 * MAX_ROADS), ("road_to", C.c_int32 * MAX_ROADS),
+                ("road_first", C.c_int32 * MAX_ROADS), ("road_n", C.c_int32 * MAX_ROADS),
+                ("regulation_frequency", C.c_int32), ("_pad2", C.c_int32)]
 
 
 LANE_STRAIGHT, LANE_SINE, LANE_CIRCULAR = 0, 1, 2
@@ -105,6 +115,36 @@ class LidarCfg(C.Structure):
 
 
 # ----------------------------------------------------------------------------- builders
+def _single_road(t: "LaneTable") -> "LaneTable":
+    """Topology of one road "0" -> "1" holding every lane (road 0, lane_id = l)."""
+    t.n_roads = 1
+    for i in range(t.n_lanes):
+        t.road[i], t.lane_id[i] = 0, i
+    t.road_from[0], t.road_to[0], t.road_first[0], t.road_n[0] = 0, 1, 0, t.n_lanes
+    return t
+
+
+def set_network(t: "LaneTable", net: np.ndarray, regulation_frequency: int = 0) -> "LaneTable":
+    """Topology rows [L, 6] (road, from node, to node, priority, exit flag, lane id) in
+    lanes_list order, as dumped by oracle/gen_golden_ix.network_tables."""
+    net = np.asarray(net, dtype=np.int64)
+    if len(net) != t.n_lanes:
+        raise ValueError("one topology row per lane")
+    n_roads = int(net[:, 0].max()) + 1
+    if n_roads > MAX_ROADS:
+        raise ValueError(f"at most {MAX_ROADS} roads")
+    t.n_roads = n_roads
+    for i, (rd, fr, to, prio, ex, lid) in enumerate(net):
+        t.road[i], t.lane_id[i], t.priority[i], t.exit_lane[i] = int(rd), int(lid), int(prio), int(ex)
+        if lid == 0:
+            t.road_from[rd], t.road_to[rd], t.road_first[rd] = int(fr), int(to), i
+        t.road_n[rd] += 1
+    for i in range(t.n_lanes):  # lanes of a road are contiguous, in id order (lanes_list order)
+        if t.road_first[t.road[i]] + t.lane_id[i] != i:
+            raise ValueError("the lanes of a road must be contiguous and in id order")
+    t.regulation_frequency = int(regulation_frequency)
+    return t
+
 def straight_lane_table(lanes: int = 4, start: float = 0.0, length: float = 10000.0, angle: float = 0.0,
                         speed_limit: float = 30.0, width: float = 4.0, forbidden=None) -> LaneTable:
     """RoadNetwork.straight_road_network (road.py:291-321) + StraightLane.__init__ (lane.py:162-194)."""
@@ -125,7 +165,7 @@ def straight_lane_table(lanes: int = 4, start: float = 0.0, length: float = 1000
         t.heading[i] = float(np.arctan2(e[1] - o[1], e[0] - o[0]))
         t.speed_limit[i] = float(speed_limit)
         t.forbidden[i] = int(bool(forbidden[i])) if forbidden is not None else 0
-    return t
+    return _single_road(t)
 
 
 def _set_straight(t: LaneTable, i: int, start, end, width, speed_limit):
@@ -158,7 +198,7 @@ def lane_table_from_arrays(table: np.ndarray) -> LaneTable:
         else:
             _set_straight(t, i, (sx, sy), (ex, ey), w, lim)
             t.amplitude[i], t.pulsation[i], t.phase[i] = amp, puls, ph
-    return t
+    return _single_road(t)
 
 
 def sine_lane_table(lanes: int = 4, length: float = 10000.0, amplitude: float = 5.0,

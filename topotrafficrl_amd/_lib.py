@@ -59,7 +59,7 @@ def load(path: str | None = None) -> C.CDLL:
             continue  # an older build loaded for comparison (tools/variants.py)
         fn.argtypes = args
         fn.restype = res
-    if lib.ttrl_abi_version() != 2:
+    if lib.ttrl_abi_version() != 3:
         raise ImportError("ABI version mismatch with include/ttrl_mi355x.h")
     if path is None:
         _lib = lib

@@ -1,8 +1,8 @@
 """Batched vehicle state: struct-of-arrays device tensors laid out [n_envs, n_veh].
 
 One row per env, one column per slot of the reference's ``road.vehicles`` list
-(slot 0 = the ego / ``env.vehicle``).  The per-vehicle attributes of the
-reference objects map to fields as follows:
+(the ego / ``env.vehicle`` is the env's first MDP slot: slot 0 on the highway).
+The per-vehicle attributes of the reference objects map to fields as follows:
 
     position -> x, y            heading -> heading          speed -> speed
     target_speed, timer, DELTA -> target_speed, timer, delta
@@ -12,6 +12,8 @@ reference objects map to fields as follows:
     MDPVehicle.speed_index      -> speed_index
     class                       -> kind (ABSENT / MDP / IDM)
     crashed, enable_lane_change -> crashed, lane_change
+    route (list of lane indexes | None) -> route_road, route_lane [.., ROUTE_MAX], route_n
+    RegulatedRoad is_yielding / steps   -> yielding, reg_steps [n_envs]
 """
 from __future__ import annotations
 
@@ -41,6 +43,11 @@ class BatchState:
             self.t[f] = torch.zeros(shape, dtype=torch.uint8, device=self.device)
         self.t["speed_index"].fill_(-1)
         self.t["delta"].fill_(4.0)
+        for f in _abi.ROUTE_FIELDS:  # ControlledVehicle.route, RegulatedRoad state
+            self.t[f] = torch.full(shape + (_abi.ROUTE_MAX,), -1, dtype=torch.int8, device=self.device)
+        self.t["route_n"] = torch.full(shape, -1, dtype=torch.int8, device=self.device)
+        self.t["yielding"] = torch.zeros(shape, dtype=torch.uint8, device=self.device)
+        self.t["reg_steps"] = torch.zeros(self.n_envs, dtype=torch.int32, device=self.device)
         self._struct = None
 
     def __getitem__(self, k: str) -> torch.Tensor:
