@@ -38,8 +38,11 @@ def to_dev(h: HostState, device, dtype="f64", pad_to=None):
     b = BatchState(h.E, N, device=device, dtype=dtype)
     arr = {}
     for k, v in h.a.items():
-        full = np.zeros((h.E, N), dtype=v.dtype)
-        if k == "speed_index":
+        if v.ndim == 1:  # per-env fields
+            arr[k] = v
+            continue
+        full = np.zeros((h.E, N) + v.shape[2:], dtype=v.dtype)
+        if k in ("speed_index", "route_n") or k in _abi.ROUTE_FIELDS:
             full[:] = -1
         full[:, :h.N] = v
         arr[k] = full

@@ -5,7 +5,13 @@ IDMVehicle / MDPVehicle (oracle/gen_golden_ix.py).  CPU only.
 Pinned here per frame: route following (ControlledVehicle.follow_road, RoadNetwork.next_lane
 with the route popped in place), RegulatedRoad.enforce_road_rules every 7th frame (trajectory
 prediction along the route, rotated-rectangle conflicts, priorities), CircularLane turns, and
-the usual IDM / steering / kinematics / collisions, over a 20-lane, 20-road network."""
+the usual IDM / steering / kinematics / collisions, over a 20-lane, 20-road network.
+
+Tolerance: one frame 1e-9 relative (the highway holds 1e-12).  A vehicle braked to a stop
+(target speed 0 while yielding) on a CircularLane steers through asin(2.5 / not_zero(v) *
+heading_rate) with not_zero(v) = 0.01: the 1-ulp differences between libm's and numpy's atan2
+reach the steering angle multiplied by ~1e3 (seen: 4.5e-10 on ix_s3, v = 6e-6 m/s).  Every
+discrete field stays exact."""
 import numpy as np
 import pytest
 
@@ -52,9 +58,9 @@ def test_ix_every_frame(path):
             if f > 0:
                 h = HostState.from_ix(d, "frame", (p, f - 1))
             o.road_act(h)
-            check(h, HostState.from_ix(d, "act", (p, f)), 1e-12, n)
+            check(h, HostState.from_ix(d, "act", (p, f)), 1e-9, n)
             o.road_step(h)
-            check(h, HostState.from_ix(d, "frame", (p, f)), 1e-12, n)
+            check(h, HostState.from_ix(d, "frame", (p, f)), 1e-9, n)
 
 
 @pytest.mark.parametrize("path", golden_files("ix_*"), ids=IDS)

@@ -104,6 +104,7 @@ template <typename T> struct LaneT {
   T amp, puls, ph;                  // SineLane
   T cx, cy, rad, sph, dirn;         // CircularLane
   int forb, type;
+  int road, lid, rfirst, rn, prio;  // network: road, id within it, the road's first lane and lane count
 };
 
 // Out of line, with scalar arguments (a struct argument would be materialised in scratch):
@@ -181,6 +182,8 @@ __host__ __device__ inline LaneT<T> make_lane(const ttrl_lane_table_t& R, int l)
   L.cx = T(R.center_x[l]); L.cy = T(R.center_y[l]); L.rad = T(R.radius[l]); L.sph = T(R.start_phase[l]);
   L.dirn = T(R.direction[l]);
   L.forb = R.forbidden[l]; L.type = R.type[l];
+  L.road = R.road[l]; L.lid = R.lane_id[l]; L.rfirst = R.road_first[R.road[l]]; L.rn = R.road_n[R.road[l]];
+  L.prio = R.priority[l];
   return L;
 }
 
@@ -388,6 +391,12 @@ __device__ __noinline__ void sat_pair_ool(const ttrl_params_t& P, T ax, T ay, T 
 // vehicles that are on it (keys) and their slots (idx), in slot order; each vehicle also
 // records its own position in the lists it belongs to (mypos, -1 if not on the lane).
 
+// Road topology of the network (ttrl_lane_table_t road_*), staged in LDS for the route helpers.
+struct RoadTab {
+  int from[TTRL_MAX_ROADS], to[TTRL_MAX_ROADS], first[TTRL_MAX_ROADS], n[TTRL_MAX_ROADS];
+  int n_roads;
+};
+
 // A close pair (i < j) queued for the SAT test, and its result.
 template <typename T> struct PairRec {
   T tx, ty;
@@ -417,16 +426,23 @@ template <typename T> struct View {
   unsigned long long* bal;       // [2][8] cross-wave ballots (NS > 64)
   PairRec<T>* pq;                // [EPW][NS] close vehicle pairs of the frame (collision queue)
   int* pq_n;                     // [EPW] queue lengths (> NS: overflow)
+  // NET_GRAPH only (null otherwise)
+  int8_t *rroad, *rlane;         // [EPW*NS][TTRL_ROUTE_MAX] routes
+  int8_t* rn;                    // [EPW*NS] route lengths (-1 None)
+  uint8_t* ynew;                 // [EPW*NS] RegulatedRoad: yields decided this enforcement
+  RoadTab* rt;                   // road topology
+  T *px, *py, *ph;               // [EPW*NS][PRED_T] predicted poses (is_conflict_possible)
 };
+constexpr int PRED_T = 11;       // np.arange(0.25, 3, 0.25) (regulation.py:86)
 
 // Byte offsets of the view's arrays in the dynamic LDS block (host: sizing; device: carve).
 struct ViewLayout {
   size_t lanes, reals[14], xf, key, pq, bal, cnt, wcnt, nitem, pq_n, mypos, f0, r0, ft, mob, item, idx, kind,
-      flags, sidx, lane, tgt, total;
+      flags, sidx, lane, tgt, pred, rroad, rlane, rn, ynew, rt, total;
 };
 
 template <typename T>
-__host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes) {
+__host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, bool graph = false) {
   ViewLayout o{};
   size_t p = 0;
   const size_t M = (size_t)EPW * NS;
@@ -458,6 +474,14 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes) 
   o.sidx = take(M, 4);
   o.lane = take(M, 4);
   o.tgt = take(M, 4);
+  if (graph) {
+    o.pred = take(sizeof(T) * 3 * PRED_T * M, 16);
+    o.rroad = take(TTRL_ROUTE_MAX * M, 4);
+    o.rlane = take(TTRL_ROUTE_MAX * M, 4);
+    o.rn = take(M, 4);
+    o.ynew = take(M, 4);
+    o.rt = take(sizeof(RoadTab), 4);
+  }
   o.total = take(0, 16);
   return o;
 }
@@ -465,8 +489,8 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes) 
 // Pointer arithmetic stays on the __shared__ base, so every access is a ds_* instruction
 // with a 32-bit LDS address.
 template <typename T>
-__device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lanes) {
-  const ViewLayout o = view_layout<T>(EPW, NS, n_lanes);
+__device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lanes, bool graph = false) {
+  const ViewLayout o = view_layout<T>(EPW, NS, n_lanes, graph);
   View<T> V;
   V.lanes = (LaneT<T>*)(smem + o.lanes);
   T** reals[] = {&V.x, &V.y, &V.v, &V.ch, &V.sh, &V.ts, &V.h, &V.timer, &V.delta, &V.steer, &V.acc,
@@ -492,11 +516,23 @@ __device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lane
   V.sidx = (int8_t*)(smem + o.sidx);
   V.lane = (int8_t*)(smem + o.lane);
   V.tgt = (int8_t*)(smem + o.tgt);
+  if (graph) {
+    const size_t M = (size_t)EPW * NS;
+    V.px = (T*)(smem + o.pred);
+    V.py = V.px + PRED_T * M;
+    V.ph = V.py + PRED_T * M;
+    V.rroad = (int8_t*)(smem + o.rroad);
+    V.rlane = (int8_t*)(smem + o.rlane);
+    V.rn = (int8_t*)(smem + o.rn);
+    V.ynew = (uint8_t*)(smem + o.ynew);
+    V.rt = (RoadTab*)(smem + o.rt);
+  }
   return V;
 }
 
-size_t host_view_bytes(int dtype, int EPW, int NS, int n_lanes) {
-  return dtype == TTRL_F64 ? view_layout<double>(EPW, NS, n_lanes).total : view_layout<float>(EPW, NS, n_lanes).total;
+size_t host_view_bytes(int dtype, int EPW, int NS, int n_lanes, bool graph = false) {
+  return dtype == TTRL_F64 ? view_layout<double>(EPW, NS, n_lanes, graph).total
+                           : view_layout<float>(EPW, NS, n_lanes, graph).total;
 }
 
 template <typename T>
@@ -643,6 +679,127 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
   return best;
 }
 
+// ------------------------------------------------------------------ road network / routes
+// Network mode of the simulate kernel: one straight road (the highway), one road of curved
+// lanes, or a graph of roads with routes and RegulatedRoad priorities (the intersection).
+enum { NET_STRAIGHT = 0, NET_CURVED = 1, NET_GRAPH = 2 };
+
+// AbstractLane.distance lane.py:127-130
+template <typename T>
+__device__ T lane_dist(const LaneT<T>& L, T px, T py) {
+  T s, r;
+  lane_local(L, px, py, s, r);
+  T a = s - L.len; if (T(0) > a) a = T(0);
+  T b = T(0) - s; if (T(0) > b) b = T(0);
+  return fabs(r) + a + b;
+}
+
+// RoadNetwork.next_lane_given_next_road road.py:136-154
+template <typename T>
+__device__ int next_given(const LaneT<T>* lanes, const RoadTab& R, int cur_road, int id, int nroad, int nid, T px,
+                          T py, T& dist) {
+  if (R.n[cur_road] == R.n[nroad]) {
+    if (nid < 0) nid = id;
+  } else {
+    T bd = T(0);
+    for (int l = 0; l < R.n[nroad]; ++l) {
+      const T d = lane_dist(lanes[R.first[nroad] + l], px, py);
+      if (l == 0 || d < bd) { bd = d; nid = l; }
+    }
+  }
+  dist = lane_dist(lanes[R.first[nroad] + nid], px, py);
+  return nid;
+}
+
+// ControlledVehicle.follow_road controller.py:135-143 + RoadNetwork.next_lane road.py:73-134:
+// at the end of the target lane, continue on the route (popping its head in place) or on the
+// leaving road whose lane is closest to the projected position.  Out of line: it runs a few
+// times per vehicle and route.  `rr`/`rl`/`rn`: the vehicle's route in LDS.
+template <typename T>
+__device__ __noinline__ int follow_road(const LaneT<T>* lanes, const RoadTab& R, T vl, int tgt, T x, T y, int8_t* rr,
+                                        int8_t* rl, int8_t* rn) {
+  const LaneT<T>& L = lanes[tgt];
+  T s, r;
+  lane_local(L, x, y, s, r);
+  if (!(s > L.len - vl / T(2))) return tgt;  // AbstractLane.after_end lane.py:120-125
+  const int rd = L.road, id = L.lid, to = R.to[rd];
+  int nroad = -1, nid = -1;
+  int n = *rn;
+  if (n > 0) {
+    if (rr[0] == rd) {  // route.pop(0)
+      for (int q = 0; q + 1 < TTRL_ROUTE_MAX; ++q) { rr[q] = rr[q + 1]; rl[q] = rl[q + 1]; }
+      rr[TTRL_ROUTE_MAX - 1] = rl[TTRL_ROUTE_MAX - 1] = -1;
+      *rn = (int8_t)(--n);
+    }
+    if (n > 0 && R.from[rr[0]] == to) { nroad = rr[0]; nid = rl[0]; }
+  }
+  T px, py;
+  lane_position(L, s, T(0), px, py);  // projected position
+  T d;
+  if (nroad < 0) {
+    bool found = false;
+    T bd = T(0);
+    for (int q = 0; q < R.n_roads; ++q) {
+      if (R.from[q] != to) continue;
+      const int cand = next_given(lanes, R, rd, id, q, -1, px, py, d);
+      if (!found || d < bd) { bd = d; nroad = q; nid = cand; found = true; }
+    }
+    if (!found) return tgt;  // KeyError: no road leaves `to`
+  } else {
+    nid = next_given(lanes, R, rd, id, nroad, nid, px, py, d);
+  }
+  return R.first[nroad] + nid;
+}
+
+// ControlledVehicle.predict_trajectory_constant_speed controller.py:228-247 through
+// RoadNetwork.position_heading_along_route road.py:352-389: the poses at t = 0.25 .. 2.75 s
+// along the route (route None or empty: the current lane), written to p*[0 .. PRED_T).
+template <typename T>
+__device__ __noinline__ void predict_poses(const LaneT<T>* lanes, const RoadTab& R, int cur, T x, T y, T v,
+                                           const int8_t* rr, const int8_t* rl, int rn, T* px, T* py, T* ph) {
+  T s0, r0;
+  lane_local(lanes[cur], x, y, s0, r0);
+  const bool route = rn > 0;
+  const int n = route ? rn : 1;
+  const int cid = lanes[cur].lid < lanes[cur].rn ? lanes[cur].lid : 0;  // None -> the current lane id
+  for (int t = 0; t < PRED_T; ++t) {
+    T L = s0 + v * (T(0.25) + T(t) * T(0.25));
+    int idx = 0;
+    int lane = route ? R.first[rr[0]] + (rl[0] >= 0 ? rl[0] : cid) : cur;
+    while (n - idx > 1 && L > lanes[lane].len) {
+      L -= lanes[lane].len;
+      ++idx;
+      lane = R.first[rr[idx]] + (rl[idx] >= 0 ? rl[idx] : cid);
+    }
+    T ex, ey;
+    lane_position(lanes[lane], L, T(0), ex, ey);
+    px[t] = ex; py[t] = ey;
+    ph[t] = heading_at(lanes[lane], L);
+  }
+}
+
+// utils.rotated_rectangles_intersect utils.py:113-123: has_corner_inside both ways over the 9
+// rect_corners points (corners, centre, edge midpoints, :126-155), each tested with
+// point_in_rotated_rectangle :75-91 (which rotates by +angle, as written).
+template <typename T>
+__device__ __noinline__ bool rects_intersect(T ax, T ay, T ah, T bx, T by, T bh, T l, T w) {
+  const SinCos<T> ca = t_sincos(ah), cb = t_sincos(bh);
+  const T hl = l / T(2), hw = w / T(2);
+  const T qx[9] = {-hl, -hl, hl, hl, T(0), -hl, hl, T(0), T(0)};
+  const T qy[9] = {-hw, hw, hw, -hw, T(0), T(0), T(0), -hw, hw};
+  for (int side = 0; side < 2; ++side) {
+    const T c1 = side ? cb.c : ca.c, s1 = side ? cb.s : ca.s, x1 = side ? bx : ax, y1 = side ? by : ay;
+    const T c2 = side ? ca.c : cb.c, s2 = side ? ca.s : cb.s, x2 = side ? ax : bx, y2 = side ? ay : by;
+    for (int q = 0; q < 9; ++q) {
+      const T px = c1 * qx[q] + (-s1) * qy[q] + x1, py = s1 * qx[q] + c1 * qy[q] + y1;
+      const T dx = px - x2, dy = py - y2;
+      const T u = c2 * dx + (-s2) * dy, v = s2 * dx + c2 * dy;
+      if (-l / T(2) <= u && u <= l / T(2) && -w / T(2) <= v && v <= w / T(2)) return true;
+    }
+  }
+  return false;
+}
+
 // IDM free-road term  COMFORT_ACC_MAX * (1 - (max(v,0)/|not_zero(v0)|)^DELTA)  (behavior.py:172-183),
 // v0 = clip(target_speed, 0, speed_limit); idm_ratio is the power's base.
 template <typename T>
@@ -746,7 +903,7 @@ enum { A_NO_COLL = 1, A_NO_MOBIL = 2, A_NO_ABORT = 4, A_NO_SCAN = 8, A_NO_STEER 
        A_NO_LANE = 64, A_NO_IDM = 128, A_NO_SAT = 256, A_NO_PREF = 512,
        A_SAT_SERIAL = 1024 /* one pair per lane (sat_pair) instead of one axis per lane; same results */ };
 
-enum { FL_CRASHED = 1, FL_IMPACT = 2, FL_LC = 4 };
+enum { FL_CRASHED = 1, FL_IMPACT = 2, FL_LC = 4, FL_YIELD = 8 };
 
 // Diagnostic build only (-DTTRL_PHASE_TIMING): per-phase shader-clock cycles of every wave,
 // summed into g_phase (tools/phases.py).  The production kernel carries no stamps.
@@ -774,10 +931,12 @@ __device__ unsigned long long g_phase[20];
 // vehicle state of the workgroup's envs is resident in LDS for the launch (HBM is read once
 // and written once); each phase loads the few fields it needs into registers, so no state is
 // live across phases and the kernel runs at high occupancy without spilling.
-template <typename T, int NS, int EPW, bool CV>
+template <typename T, int NS, int EPW, int NET>
 __global__ void __launch_bounds__(NS* EPW, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES : (sizeof(T) == 8 ? 2 : 4))
 simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int32_t* __restrict__ actions,
                 int frames, double dt_d, int mode, int ablate) {
+  constexpr bool CV = NET != NET_STRAIGHT;  // curved lane classes possible
+  constexpr bool GR = NET == NET_GRAPH;     // roads, routes, RegulatedRoad
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = NS * EPW;
   constexpr int WAVES = NT / 64 > 0 ? NT / 64 : 1;
@@ -789,9 +948,16 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   const size_t k = (size_t)env * N + i;
   const int me = le * NS + i;  // this vehicle's LDS slot
   const int eb = le * NS;      // env base in the LDS view
-  View<T> V = carve<T>(smem, EPW, NS, nl);
+  View<T> V = carve<T>(smem, EPW, NS, nl, GR);
   PH_INIT
   stage_lanes(V, R, tid);
+  if constexpr (GR) {
+    if (tid < TTRL_MAX_ROADS) {
+      V.rt->from[tid] = R.road_from[tid]; V.rt->to[tid] = R.road_to[tid];
+      V.rt->first[tid] = R.road_first[tid]; V.rt->n[tid] = R.road_n[tid];
+    }
+    if (tid == 0) V.rt->n_roads = R.n_roads;
+  }
   const T dt = T(dt_d);
 
   bool present;
@@ -811,7 +977,18 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
     V.sidx[me] = (int8_t)a.sidx;
     V.lane[me] = (int8_t)(present ? a.lane : -1);
     V.tgt[me] = (int8_t)(present ? a.tgt : -1);
+    if constexpr (GR) {
+      for (int q = 0; q < TTRL_ROUTE_MAX; ++q) {
+        V.rroad[me * TTRL_ROUTE_MAX + q] = slot ? st.route_road[k * TTRL_ROUTE_MAX + q] : (int8_t)-1;
+        V.rlane[me * TTRL_ROUTE_MAX + q] = slot ? st.route_lane[k * TTRL_ROUTE_MAX + q] : (int8_t)-1;
+      }
+      V.rn[me] = slot ? st.route_n[k] : (int8_t)-1;
+      if (slot && st.yielding[k]) V.flags[me] |= FL_YIELD;
+    }
   }
+  int reg = 0;  // RegulatedRoad.steps of this thread's env
+  if constexpr (GR) reg = env < st.n_envs ? st.reg_steps[env] : 0;
+  const int reg_period = GR && R.regulation_frequency > 0 ? (int)(1.0 / dt_d / R.regulation_frequency) : 0;
   PH(15);
   if (i == 0) V.nitem[le] = 0;
   __syncthreads();  // lane table + view staged
@@ -826,14 +1003,22 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       const T x = V.x[me], y = V.y[me], h = V.h[me], v = V.v[me];
       T ts = V.ts[me];
       int tgt = V.tgt[me];
+      if constexpr (GR)  // ControlledVehicle.act starts with follow_road (controller.py:98)
+        tgt = follow_road(V.lanes, *V.rt, T(P.lane_vehicle_length), tgt, x, y, V.rroad + me * TTRL_ROUTE_MAX,
+                          V.rlane + me * TTRL_ROUTE_MAX, V.rn + me);
       if (act == TTRL_FASTER || act == TTRL_SLOWER) {  // MDPVehicle.act controller.py:304-315
         int si = speed_to_index(P, v) + (act == TTRL_FASTER ? 1 : -1);
         si = si < 0 ? 0 : (si > P.n_target_speeds - 1 ? P.n_target_speeds - 1 : si);
         V.sidx[me] = (int8_t)si;
         ts = T(P.target_speeds[si]);
       } else if (act == TTRL_LANE_LEFT || act == TTRL_LANE_RIGHT) {  // controller.py:103-124
-        int id = tgt + (act == TTRL_LANE_RIGHT ? 1 : -1);
-        id = id < 0 ? 0 : (id > nl - 1 ? nl - 1 : id);
+        int id, lo = 0, hi = nl - 1;
+        if constexpr (GR) {  // clip within the target's road
+          const LaneT<T>& TL = V.lanes[tgt];
+          lo = TL.rfirst; hi = TL.rfirst + TL.rn - 1;
+        }
+        id = tgt + (act == TTRL_LANE_RIGHT ? 1 : -1);
+        id = id < lo ? lo : (id > hi ? hi : id);
         if (reachable<CV>(V.lanes[id], T(P.lane_vehicle_length), x, y)) tgt = id;
       }
       // ControlledVehicle.act low-level control (controller.py:126-133); Road.act recomputes
@@ -848,10 +1033,18 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
 
     // ---------------- Road.act (road.py:461-464) ----------------
     int tgt_new = V.tgt[me];
+    const int tgt0 = tgt_new;  // the target before this vehicle's act (what earlier vehicles saw)
     if (mode & MODE_ACT) {
       const bool polite = P.politeness != 0.0;
       {  // (1) per vehicle: lane-change timer, own-lane (+ target-lane) neighbours, IDM free
          //     term, MOBIL work items; results go to LDS so nothing stays live across (2)
+        if constexpr (GR) {  // follow_road opens IDMVehicle.act (not crashed) and ControlledVehicle.act
+          if (present && (kind == TTRL_MDP || !(V.flags[me] & FL_CRASHED))) {
+            tgt_new = follow_road(V.lanes, *V.rt, T(P.lane_vehicle_length), tgt_new, V.x[me], V.y[me],
+                                  V.rroad + me * TTRL_ROUTE_MAX, V.rlane + me * TTRL_ROUTE_MAX, V.rn + me);
+            V.tgt[me] = (int8_t)tgt_new;
+          }
+        }
         const int lane = V.lane[me], tgt = V.tgt[me];
         const int fl = V.flags[me];
         const bool idm = present && kind == TTRL_IDM && !(fl & FL_CRASHED);
@@ -867,8 +1060,14 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         bool left = false, right = false;
         if (fire) {
           const bool moving = !(fabs(v) < T(1));
-          left = lane > 0 && moving && reachable<CV>(V.lanes[lane - 1], T(P.lane_vehicle_length), x, y);
-          right = lane < nl - 1 && moving && reachable<CV>(V.lanes[lane + 1], T(P.lane_vehicle_length), x, y);
+          bool has_l = lane > 0, has_r = lane < nl - 1;
+          if constexpr (GR) {
+            const LaneT<T>& OL = V.lanes[lane];
+            has_l = OL.lid > 0;
+            has_r = OL.lid < OL.rn - 1;
+          }
+          left = has_l && moving && reachable<CV>(V.lanes[lane - 1], T(P.lane_vehicle_length), x, y);
+          right = has_r && moving && reachable<CV>(V.lanes[lane + 1], T(P.lane_vehicle_length), x, y);
         }
         // Queries of every vehicle: the own lane's front (its rear only feeds MOBIL's politeness
         // term) and, while changing lane, the target lane's front (IDMVehicle.act behavior.py:118-131).
@@ -966,7 +1165,15 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
               const T af = V.afree[ve];
               const T nfpa = nf >= 0 ? fr - term : T(0);
               bool ok = !(nfpa < -T(P.lane_change_max_braking));
-              if (ok) {
+              bool planned = false;  // a route with a planned lane (behavior.py:296-304)
+              if constexpr (GR) planned = V.rn[ve] > 0 && V.rlane[ve * TTRL_ROUTE_MAX] >= 0;
+              if (ok && planned) {
+                T spa = af;
+                if (np_ >= 0) spa -= t_np;
+                const int tid_ = V.lanes[V.tgt[ve]].lid, cid = V.lanes[ln].lid, rid = V.rlane[ve * TTRL_ROUTE_MAX];
+                const int s1 = (cid > tid_) - (cid < tid_), s2 = (rid > tid_) - (rid < tid_);
+                if (s1 != s2 || spa < -T(P.lane_change_max_braking)) ok = false;
+              } else if (ok) {
                 T spa = af, sa = af;
                 if (np_ >= 0) spa -= t_np;
                 if (op >= 0) sa -= t_op;
@@ -994,7 +1201,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       const int fl = V.flags[me];
       const bool idm = present && kind == TTRL_IDM && !(fl & FL_CRASHED);
       const bool changing = idm && lane != tgt;
-      const bool abort_cand = changing && (fl & FL_LC) != 0;
+      bool abort_cand = changing && (fl & FL_LC) != 0;
+      if constexpr (GR) abort_cand = abort_cand && V.lanes[lane].road == V.lanes[tgt].road;  // behavior.py:231
       const T x = V.x[me], y = V.y[me], v = V.v[me];
       int side_front = -1;  // front on the lane MOBIL chose (left first, a later candidate overrides)
       const int mobl = V.mob[me], mobr = V.mob[EPW * NS + me];
@@ -1008,7 +1216,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         auto contributes = [&](int ii) -> bool {
           if (!present || ii == i) return false;
           const int Ti = V.tgt[eb + ii];
-          const int tv = i < ii ? tgt_new : tgt;
+          const int tv = i < ii ? tgt_new : tgt0;
           if (!(lane != Ti && tv == Ti)) return false;
           const LaneT<T> L = V.lanes[V.lane[eb + ii]];
           T s1, r1, s0, r0;
@@ -1090,6 +1298,60 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
 
     // ---------------- Road.step(dt) (road.py:466-478) ----------------
     if (mode & MODE_STEP) {
+      if constexpr (GR) {
+        if (reg_period > 0) {  // RegulatedRoad.step regulation.py:28-32
+          ++reg;
+          const bool doreg = env < st.n_envs && reg % reg_period == 0;
+          if (__syncthreads_or(doreg)) {  // enforce_road_rules regulation.py:34-60, every env of the block in step
+            if (doreg && present) {
+              const int fl = V.flags[me];
+              if (fl & FL_YIELD) {  // YIELD_DURATION = 0: last enforcement's yields end now
+                V.ts[me] = V.lanes[V.lane[me]].lim;
+                V.flags[me] = (uint8_t)(fl & ~FL_YIELD);
+              }
+              predict_poses(V.lanes, *V.rt, (int)V.lane[me], V.x[me], V.y[me], V.v[me], V.rroad + me * TTRL_ROUTE_MAX,
+                            V.rlane + me * TTRL_ROUTE_MAX, (int)V.rn[me], V.px + me * PRED_T, V.py + me * PRED_T,
+                            V.ph + me * PRED_T);
+            }
+            V.ynew[me] = 0;
+            __syncthreads();
+            if (doreg) {  // every pair (a < b) once: thread i takes (i, i + d mod NS), d = 1 .. NS/2
+              for (int d = 1; d <= NS / 2; ++d) {
+                if (d == NS / 2 && i >= NS / 2) break;
+                const int j = (i + d) & (NS - 1);
+                const int a = i < j ? i : j, b = i < j ? j : i;
+                if (V.kind[eb + a] == TTRL_ABSENT || V.kind[eb + b] == TTRL_ABSENT) continue;
+                bool conflict = false;  // is_conflict_possible regulation.py:80-103
+                for (int t = 0; t < PRED_T && !conflict; ++t) {
+                  const int pa = (eb + a) * PRED_T + t, pb = (eb + b) * PRED_T + t;
+                  const T dx = V.px[pb] - V.px[pa], dy = V.py[pb] - V.py[pa];
+                  if (sqrt(dx * dx + dy * dy) > T(P.length)) continue;
+                  conflict = rects_intersect(V.px[pa], V.py[pa], V.ph[pa], V.px[pb], V.py[pb], V.ph[pb],
+                                             T(1.5) * T(P.length), T(0.9) * T(P.width));
+                }
+                if (!conflict) continue;
+                // respect_priorities regulation.py:62-77
+                const int qa = V.lanes[V.lane[eb + a]].prio, qb = V.lanes[V.lane[eb + b]].prio;
+                int yv;
+                if (qa > qb) yv = b;
+                else if (qa < qb) yv = a;
+                else {
+                  const int ka = eb + a, kb = eb + b;
+                  const T fab = V.ch[ka] * (V.x[kb] - V.x[ka]) + V.sh[ka] * (V.y[kb] - V.y[ka]);
+                  const T fba = V.ch[kb] * (V.x[ka] - V.x[kb]) + V.sh[kb] * (V.y[ka] - V.y[kb]);
+                  yv = fab > fba ? a : b;
+                }
+                if (V.kind[eb + yv] == TTRL_IDM) V.ynew[eb + yv] = 1;  // ControlledVehicle, not MDPVehicle
+              }
+            }
+            __syncthreads();
+            if (doreg && present && V.ynew[me]) {
+              V.ts[me] = T(0);
+              V.flags[me] |= FL_YIELD;
+            }
+          }
+        }
+      }
       T x = V.x[me], y = V.y[me], h = V.h[me];
       if (present) {
         T v = V.v[me], steer = V.steer[me], acc = V.acc[me];
@@ -1296,6 +1558,17 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       a.x = ((const T*)st.x)[k]; a.lane = st.lane[k]; a.tgt = st.target_lane[k];
     }
     store_veh(a, st, k);
+    if constexpr (GR) {
+      for (int q = 0; q < TTRL_ROUTE_MAX; ++q) {
+        st.route_road[k * TTRL_ROUTE_MAX + q] = V.rroad[me * TTRL_ROUTE_MAX + q];
+        st.route_lane[k * TTRL_ROUTE_MAX + q] = V.rlane[me * TTRL_ROUTE_MAX + q];
+      }
+      st.route_n[k] = V.rn[me];
+      st.yielding[k] = (fl & FL_YIELD) ? 1 : 0;
+    }
+  }
+  if constexpr (GR) {
+    if (i == 0 && env < st.n_envs) st.reg_steps[env] = reg;
   }
   PH(16);
   PH_FLUSH
@@ -1975,11 +2248,21 @@ __global__ void rewards_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_reward
 }
 
 // ------------------------------------------------------------------- launch helpers
+// A network beyond one road, or a RegulatedRoad: the simulate kernel's NET_GRAPH instance.
+bool is_graph(const ttrl_lane_table_t& R) { return R.n_roads > 1 || R.regulation_frequency > 0; }
+
 int check_state(const ttrl_state_t* s, const ttrl_lane_table_t* R) {
   if (!s || !R) return TTRL_E_ARG;
   if (s->dtype != TTRL_F32 && s->dtype != TTRL_F64) return TTRL_E_ARG;
   if (s->n_envs < 0 || s->n_veh < 1 || s->n_veh > 256) return TTRL_E_ARG;
   if (R->n_lanes < 1 || R->n_lanes > LMAX) return TTRL_E_ARG;
+  if (R->n_roads < 1 || R->n_roads > TTRL_MAX_ROADS || R->regulation_frequency < 0) return TTRL_E_ARG;
+  for (int l = 0; l < R->n_lanes; ++l)  // topology consistent (lanes of a road contiguous, in id order)
+    if (R->road[l] < 0 || R->road[l] >= R->n_roads || R->road_first[R->road[l]] + R->lane_id[l] != l ||
+        R->lane_id[l] >= R->road_n[R->road[l]])
+      return TTRL_E_ARG;
+  if (is_graph(*R) && (!s->route_road || !s->route_lane || !s->route_n || !s->yielding || !s->reg_steps))
+    return TTRL_E_ARG;
   const void* ptrs[] = {s->x, s->y, s->heading, s->speed, s->target_speed, s->timer, s->delta, s->steer, s->acc,
                         s->impact_x, s->impact_y, s->lane, s->target_lane, s->speed_index, s->kind, s->crashed,
                         s->has_impact, s->lane_change};
@@ -1997,15 +2280,19 @@ int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_par
                int frames, double dt, int mode, int ablate, hipStream_t stream) {
   const int blocks = (s.n_envs + EPW - 1) / EPW;
   if (blocks == 0) return TTRL_OK;
-  const size_t lds = host_view_bytes(sizeof(T) == 8 ? TTRL_F64 : TTRL_F32, EPW, NS, R.n_lanes);
+  const bool graph = is_graph(R);
+  const size_t lds = host_view_bytes(sizeof(T) == 8 ? TTRL_F64 : TTRL_F32, EPW, NS, R.n_lanes, graph);
   bool curved = false;
   for (int l = 0; l < R.n_lanes; ++l) curved |= R.type[l] != TTRL_LANE_STRAIGHT;
-  if (curved)
-    hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, true>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, P,
+  if (graph)
+    hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_GRAPH>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, P,
                        actions, frames, dt, mode, ablate);
+  else if (curved)
+    hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_CURVED>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R,
+                       P, actions, frames, dt, mode, ablate);
   else
-    hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, false>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, P,
-                       actions, frames, dt, mode, ablate);
+    hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_STRAIGHT>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R,
+                       P, actions, frames, dt, mode, ablate);
   return launch_status();
 }
 
