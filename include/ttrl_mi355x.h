@@ -23,6 +23,10 @@
  *   ttrl_reset_highway       scene init: Vehicle.create_random kinematics.py:50-104,
  *                            IDMVehicle.__init__/randomize_behavior behavior.py:48-69
  *   ttrl_rewards             reward/termination template  ttrl_env/envs/intersection_env.py:78-119
+ *   ttrl_ix_reset            IntersectionEnv._reset        ttrl_env/envs/intersection_env.py:135-318
+ *                            (_make_vehicles :251-318, _spawn_vehicle :320-348, AbstractEnv.reset abstract.py:188-214)
+ *   ttrl_ix_clear_spawn      IntersectionEnv.step tail     ttrl_env/envs/intersection_env.py:135-139
+ *                            (_clear_vehicles :350-362, _spawn_vehicle :320-348)
  */
 #ifndef TTRL_MI355X_H
 #define TTRL_MI355X_H
@@ -33,10 +37,13 @@
 extern "C" {
 #endif
 
-#define TTRL_ABI_VERSION 3
+#define TTRL_ABI_VERSION 4
 #define TTRL_MAX_LANES 32
 #define TTRL_MAX_ROADS 32
+#define TTRL_MAX_NODES 32
 #define TTRL_ROUTE_MAX 4
+#define TTRL_RNG_WORDS 5
+#define TTRL_IX_MAX_INIT 16
 
 enum { TTRL_F32 = 0, TTRL_F64 = 1 };
 
@@ -144,6 +151,10 @@ typedef struct ttrl_state {
   int8_t *route_n;                /* route length, -1 = route None                          */
   uint8_t *yielding;              /* RegulatedRoad: is_yielding                             */
   int32_t *reg_steps;             /* [E] RegulatedRoad.steps (frames since the road was made) */
+  uint64_t *rng;                  /* [E][TTRL_RNG_WORDS] AbstractEnv.np_random, numpy Generator(PCG64):
+                                     {state_hi, state_lo, inc_hi, inc_lo, has_uint32 << 32 | uinteger};
+                                     may be NULL unless a kernel draws from it (intersection
+                                     spawns, numpy-order shuffled observation)                  */
 } ttrl_state_t;
 
 /* KinematicObservation config (observation.py:159-196).  Feature codes below. */
@@ -158,7 +169,8 @@ typedef struct ttrl_kin_cfg {
   int32_t n_features;             /* F columns                                  */
   int32_t features[TTRL_N_FEATURES];
   int32_t absolute, normalize, clip, see_behind;
-  int32_t order_shuffled;         /* 0 sorted, 1 shuffled (Philox, seed+offset) */
+  int32_t order_shuffled;         /* 0 sorted, 1 shuffled (Philox, seed+offset),
+                                     2 shuffled with the env's np_random (state.rng), as the reference */
   int32_t _pad;
   double range_lo[TTRL_N_FEATURES], range_hi[TTRL_N_FEATURES];
   int32_t has_range[TTRL_N_FEATURES];
@@ -211,7 +223,41 @@ typedef struct ttrl_reward_cfg {
   double collision_reward, high_speed_reward, speed_lo, speed_hi;
   int32_t normalize_reward, offroad_terminal;
   double duration;                /* truncation time [s]                        */
+  double arrived_reward;          /* reward once has_arrived (intersection_env.py:85) */
+  double exit_distance;           /* has_arrived exit_distance (25, :364-369)   */
 } ttrl_reward_cfg_t;
+
+/*
+ * IntersectionEnv scene (intersection_env.py:17-55 default_config, :251-362).  Corners c = 0..3
+ * name the nodes "o"c / "ir"c / "il"c of _make_road; node ids are those of the lane table.
+ */
+typedef struct ttrl_ix_cfg {
+  int32_t initial_vehicle_count;  /* 10                                          */
+  int32_t warmup_frames;          /* simulation_steps (3) * simulation_frequency  */
+  double warmup_dt;               /* 1 / simulation_frequency                    */
+  double init_longitudinal[TTRL_IX_MAX_INIT]; /* np.linspace(0, 80, n)[t]        */
+  double spawn_probability;       /* 0.6                                         */
+  double spawn_offset;            /* 5: longitudinal + 5 + normal() * deviation  */
+  double spawn_speed;             /* 8: 8 + normal() * deviation                 */
+  double spawn_clear_distance;    /* 15                                          */
+  double challenger_longitudinal; /* 60                                          */
+  double challenger_position_deviation, challenger_speed_deviation;  /* 0.1, 0   */
+  double delta_lo, delta_hi;      /* IDMVehicle.DELTA_RANGE (randomize_behavior) */
+  int32_t n_corners;              /* 4                                           */
+  int32_t entry_lane[4];          /* lane ("o"c, "ir"c, 0)                       */
+  int32_t exit_node[4];           /* node "o"c                                   */
+  int32_t ego_lane;               /* ("o0", "ir0", 0)                            */
+  int32_t ego_destination;        /* corner of config["destination"]; -1: integers(1, 4) */
+  double ego_longitudinal, ego_deviation;  /* lane.position(60 + 5 * normal(1), 0) */
+  double ego_heading_s;           /* heading_at(60)                              */
+  double ego_speed;               /* ego lane speed limit                        */
+  double ego_clear_distance;      /* 20 ("prevent early collisions")            */
+  double leave_margin;            /* 4 * Vehicle.LENGTH (_clear_vehicles)        */
+  /* RoadNetwork.shortest_path(node, exit_node[c]) (road.py:159-188) as road ids, -1 padded;
+   * path_len 0 = no path (plan_route_to then keeps route = [lane_index]). */
+  int8_t path_road[TTRL_MAX_NODES][4][TTRL_ROUTE_MAX - 1];
+  int8_t path_len[TTRL_MAX_NODES][4];
+} ttrl_ix_cfg_t;
 
 int ttrl_abi_version(void);
 
@@ -237,6 +283,11 @@ int ttrl_neighbours(const ttrl_state_t* s, const ttrl_lane_table_t* road,
 int ttrl_observe_kinematics(const ttrl_state_t* s, const ttrl_lane_table_t* road,
                             const ttrl_params_t* p, const ttrl_kin_cfg_t* cfg,
                             float* out, int32_t* ids, void* stream);
+/* As ttrl_observe_kinematics, for the envs with mask[e] != 0 only (mask NULL: all); the other
+ * envs' rows and np_random are left untouched (masked auto-reset re-observation). */
+int ttrl_observe_kinematics_masked(const ttrl_state_t* s, const ttrl_lane_table_t* road,
+                                   const ttrl_params_t* p, const ttrl_kin_cfg_t* cfg, const uint8_t* mask,
+                                   float* out, int32_t* ids, void* stream);
 /* Occupancy grid of the ego: out [E][F][shape_x][shape_y] float32. */
 int ttrl_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* road,
                       const ttrl_params_t* p, const ttrl_grid_cfg_t* cfg,
@@ -282,7 +333,20 @@ int64_t ttrl_ego_attention_sizes(int32_t n_features, int32_t n_actions, int32_t 
 int ttrl_ego_attention_q(const float* obs, int32_t batch, int32_t n_entities, int32_t n_features,
                          int32_t heads, const float* weights, int32_t n_actions, float* scratch, float* q,
                          void* stream);
-/* Per-env reward [E] float32, terminated/truncated [E] uint8, given time [E] float64. */
+/* IntersectionEnv._reset for the envs with mask[e] != 0 (mask NULL: all): np_random =
+ * default_rng(SeedSequence(entropy[e][0..n_words-1])) into state.rng, then _make_vehicles:
+ * initial spawns, warmup_frames of Road.act/step (RegulatedRoad), the challenger, the ego
+ * MDPVehicle (appended after the traffic) and the removal of vehicles near it.  Requires the
+ * network fields and state.rng.  Vehicles beyond n_veh slots are dropped (draws still made). */
+int ttrl_ix_reset(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                  const ttrl_ix_cfg_t* cfg, const uint32_t* entropy, int32_t n_words, const uint8_t* mask,
+                  void* stream);
+/* IntersectionEnv.step tail after the observation and reward: _clear_vehicles (list order kept),
+ * then _spawn_vehicle(spawn_probability) drawing from state.rng; envs with mask[e] != 0. */
+int ttrl_ix_clear_spawn(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                        const ttrl_ix_cfg_t* cfg, const uint8_t* mask, void* stream);
+/* Per-env reward [E] float32, terminated/truncated [E] uint8, given time [E] float64, for the
+ * env's controlled vehicle (its first TTRL_MDP slot). */
 int ttrl_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* road,
                  const ttrl_reward_cfg_t* cfg, const double* time, float* reward,
                  uint8_t* terminated, uint8_t* truncated, void* stream);

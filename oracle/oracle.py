@@ -43,6 +43,7 @@ class HostState:
         self.a["route_n"] = np.full((n_envs, n_veh), -1, dtype=np.int8)
         self.a["yielding"] = np.zeros((n_envs, n_veh), dtype=np.uint8)
         self.a["reg_steps"] = np.zeros(n_envs, dtype=np.int32)
+        self.a["rng"] = np.zeros((n_envs, _abi.RNG_WORDS), dtype=np.uint64)
 
     def __getitem__(self, k):
         return self.a[k]
@@ -110,12 +111,15 @@ _SIGS = {
     "oracle_road_step": [C.c_void_p] * 3 + [C.c_double, C.c_void_p],
     "oracle_simulate": [C.c_void_p] * 4 + [C.c_int32, C.c_double, C.c_void_p],
     "oracle_neighbours": [C.c_void_p] * 6,
-    "oracle_observe_kinematics": [C.c_void_p] * 6,
+    "oracle_observe_kinematics": [C.c_void_p] * 7,
     "oracle_observe_grid": [C.c_void_p] * 5,
     "oracle_reset_highway": [C.c_void_p] * 5,
     "oracle_rewards": [C.c_void_p] * 7,
     "oracle_observe_ttc": [C.c_void_p] * 5,
     "oracle_observe_lidar": [C.c_void_p] * 5,
+    "oracle_ix_reset": [C.c_void_p] * 5,
+    "oracle_ix_clear_spawn": [C.c_void_p] * 5,
+    "oracle_rng_ops": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p],
 }
 
 
@@ -164,13 +168,43 @@ class Oracle:
                                             None if q is None else q.ctypes.data, f.ctypes.data, r.ctypes.data))
         return f, r
 
-    def observe_kinematics(self, h: HostState, cfg: _abi.KinCfg):
+    def observe_kinematics(self, h: HostState, cfg: _abi.KinCfg, mask=None, out=None):
         s = h.struct()
-        out = np.zeros((h.E, cfg.vehicles_count, cfg.n_features), dtype=np.float32)
+        if out is None:
+            out = np.zeros((h.E, cfg.vehicles_count, cfg.n_features), dtype=np.float32)
         ids = np.zeros((h.E, max(cfg.vehicles_count - 1, 0)), dtype=np.int32)
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
         self._ok(self.lib.oracle_observe_kinematics(C.byref(s), C.byref(self.lanes), C.byref(self.params),
-                                                    C.byref(cfg), out.ctypes.data, ids.ctypes.data))
+                                                    C.byref(cfg), None if m is None else m.ctypes.data,
+                                                    out.ctypes.data, ids.ctypes.data))
         return out, ids
+
+    def ix_reset(self, h: HostState, cfg: _abi.IxCfg, seeds, mask=None):
+        """IntersectionEnv.reset(seed) per env: np_random = default_rng(seed), then _reset."""
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        st = _abi.rng_states(seeds)
+        for e in range(h.E):
+            if m is None or m[e]:
+                h.a["rng"][e] = st[e]
+        s = h.struct()
+        self._ok(self.lib.oracle_ix_reset(C.byref(s), C.byref(self.lanes), C.byref(self.params), C.byref(cfg),
+                                          None if m is None else m.ctypes.data))
+
+    def ix_clear_spawn(self, h: HostState, cfg: _abi.IxCfg, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        s = h.struct()
+        self._ok(self.lib.oracle_ix_clear_spawn(C.byref(s), C.byref(self.lanes), C.byref(self.params),
+                                                C.byref(cfg), None if m is None else m.ctypes.data))
+
+    def rng_ops(self, state5: np.ndarray, ops, args) -> np.ndarray:
+        """numpy Generator draws restated in C (see oracle_rng_ops); state5 advanced in place."""
+        ops = np.ascontiguousarray(ops, dtype=np.int32)
+        args = np.ascontiguousarray(args, dtype=np.int32)
+        out = np.zeros(int(sum(2 if o == 3 else (a if o == 4 else 1) for o, a in zip(ops, args))), dtype=np.float64)
+        n = self.lib.oracle_rng_ops(state5.ctypes.data, ops.ctypes.data, args.ctypes.data, len(ops), out.ctypes.data)
+        if n < 0:
+            raise RuntimeError("oracle_rng_ops: bad op")
+        return out[:n]
 
     def observe_ttc(self, h: HostState, cfg: _abi.TtcCfg):
         s = h.struct()

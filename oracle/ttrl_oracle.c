@@ -29,6 +29,7 @@ typedef struct {
   int8_t *rroad, *rlane, *rn;   /* route entries [E*N][TTRL_ROUTE_MAX], length (-1 = None) */
   uint8_t* yield;
   int32_t* reg;
+  uint64_t* rng;                /* [E][TTRL_RNG_WORDS] np_random */
 } S;
 
 static S view(const ttrl_state_t* s) {
@@ -40,6 +41,7 @@ static S view(const ttrl_state_t* s) {
   o.lane = s->lane; o.tgt = s->target_lane; o.sidx = s->speed_index;
   o.kind = s->kind; o.crashed = s->crashed; o.hasimp = s->has_impact; o.lc = s->lane_change;
   o.rroad = s->route_road; o.rlane = s->route_lane; o.rn = s->route_n; o.yield = s->yielding; o.reg = s->reg_steps;
+  o.rng = s->rng;
   return o;
 }
 
@@ -68,6 +70,98 @@ static double lmap(double v, double x0, double x1, double y0, double y1) {
 
 /* local_coordinates: StraightLane lane.py:209-213 (np.dot of 2-vectors), SineLane :275-279,
  * CircularLane :327-334 */
+/* numpy PCG64 (pcg_setseq_128_xsl_rr_64): step, then output of the new state. */
+typedef struct { unsigned __int128 st, inc; int has32; uint32_t u32; } pcg_t;
+static const unsigned __int128 PCG_MULT =
+    ((unsigned __int128)0x2360ED051FC65DA4ULL << 64) | 0x4385DF649FCCF645ULL;
+static uint64_t pcg_next64(pcg_t* g) {
+  g->st = g->st * PCG_MULT + g->inc;
+  uint64_t hi = (uint64_t)(g->st >> 64), lo = (uint64_t)g->st;
+  uint64_t x = hi ^ lo; unsigned rot = (unsigned)(hi >> 58);
+  return (x >> rot) | (x << ((64 - rot) & 63));
+}
+static uint32_t pcg_next32(pcg_t* g) {
+  if (g->has32) { g->has32 = 0; return g->u32; }
+  uint64_t n = pcg_next64(g); g->has32 = 1; g->u32 = (uint32_t)(n >> 32); return (uint32_t)n;
+}
+static double pcg_double(pcg_t* g) { return (double)(pcg_next64(g) >> 11) * (1.0 / 9007199254740992.0); }
+/* Generator.integers(0, n) for 1 < n <= 2^32 (buffered Lemire, numpy distributions.c) */
+static uint32_t pcg_bounded(pcg_t* g, uint32_t n) {
+  if (n <= 1) return 0;
+  uint32_t rng = n - 1; uint64_t rexcl = (uint64_t)rng + 1;
+  uint64_t m = (uint64_t)pcg_next32(g) * rexcl;
+  uint32_t left = (uint32_t)m;
+  if (left < rexcl) {
+    uint32_t thr = (uint32_t)((0xFFFFFFFFULL - rng) % rexcl);
+    while (left < thr) { m = (uint64_t)pcg_next32(g) * rexcl; left = (uint32_t)m; }
+  }
+  return (uint32_t)(m >> 32);
+}
+static double pcg_uniform(pcg_t* g, double lo, double hi) { return lo + (hi - lo) * pcg_double(g); }
+
+
+/* ---- numpy.random.Generator over PCG64, restated (numpy 1.26 / 2.2 random/src/distributions/
+ * distributions.c and _generator.pyx; the reference draws through gymnasium's np_random,
+ * seeding.np_random = Generator(PCG64(SeedSequence(seed)))).  Pinned against numpy itself by
+ * tests/test_ix_rng.py. */
+static void rng_load(pcg_t* g, const uint64_t* w) {
+  g->st = ((unsigned __int128)w[0] << 64) | w[1];
+  g->inc = ((unsigned __int128)w[2] << 64) | w[3];
+  g->has32 = (int)(w[4] >> 32); g->u32 = (uint32_t)w[4];
+}
+static void rng_store(const pcg_t* g, uint64_t* w) {
+  w[0] = (uint64_t)(g->st >> 64); w[1] = (uint64_t)g->st;
+  w[2] = (uint64_t)(g->inc >> 64); w[3] = (uint64_t)g->inc;
+  w[4] = ((uint64_t)(g->has32 ? 1 : 0) << 32) | g->u32;
+}
+/* random_interval: uniform on [0, max] by masked rejection (Generator.shuffle) */
+static uint64_t pcg_interval(pcg_t* g, uint64_t max) {
+  if (max == 0) return 0;
+  uint64_t mask = max, v;
+  mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16; mask |= mask >> 32;
+  if (max <= 0xffffffffULL) { while ((v = (pcg_next32(g) & mask)) > max) {} }
+  else { while ((v = (pcg_next64(g) & mask)) > max) {} }
+  return v;
+}
+#include "../topotrafficrl_amd/csrc/ttrl_ziggurat.h"
+/* random_standard_normal: 256-entry ziggurat (ziggurat_constants.h) */
+static double pcg_normal(pcg_t* g) {
+  for (;;) {
+    uint64_t r = pcg_next64(g);
+    const int idx = (int)(r & 0xff);
+    r >>= 8;
+    const int sign = (int)(r & 0x1);
+    const uint64_t rabs = (r >> 1) & 0x000fffffffffffffULL;
+    double x = (double)rabs * ttrl_zig_wi[idx];
+    if (sign & 0x1) x = -x;
+    if (rabs < ttrl_zig_ki[idx]) return x;
+    if (idx == 0) {
+      for (;;) {
+        const double xx = -TTRL_ZIG_NOR_INV_R * log1p(-pcg_double(g));
+        const double yy = -log1p(-pcg_double(g));
+        if (yy + yy > xx * xx) return ((rabs >> 8) & 0x1) ? -(TTRL_ZIG_NOR_R + xx) : TTRL_ZIG_NOR_R + xx;
+      }
+    } else {
+      if (((ttrl_zig_fi[idx - 1] - ttrl_zig_fi[idx]) * pcg_double(g) + ttrl_zig_fi[idx]) < exp(-0.5 * x * x))
+        return x;
+    }
+  }
+}
+/* Generator.choice(pop, size, replace=False) for a small population: Floyd's algorithm, then
+ * _shuffle_int (random_bounded_uint64 draws) */
+static void pcg_choice_noreplace(pcg_t* g, int pop, int size, int* out) {
+  for (int j = pop - size; j < pop; ++j) {
+    const int val = (int)pcg_bounded(g, (uint32_t)j + 1);
+    int seen = 0;
+    for (int q = 0; q < j - (pop - size); ++q) seen |= out[q] == val;
+    out[j - (pop - size)] = seen ? j : val;
+  }
+  for (int i = size - 1; i >= 1; --i) {
+    const int j = (int)pcg_bounded(g, (uint32_t)i + 1);
+    const int t = out[i]; out[i] = out[j]; out[j] = t;
+  }
+}
+
 static void local(const ttrl_lane_table_t* R, int l, double px, double py, double* s, double* r) {
   if (R->type[l] == TTRL_LANE_CIRCULAR) {
     double dx = px - R->center_x[l], dy = py - R->center_y[l];
@@ -566,41 +660,45 @@ int oracle_meta_action(const ttrl_state_t* s, const ttrl_lane_table_t* R, const 
   return 0;
 }
 
-/* Road.act road.py:461-464 */
+/* Road.act road.py:461-464, one env */
+static void act_env(S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int e) {
+  int base = e * o->N;
+  for (int i = 0; i < o->N; ++i) {
+    if (o->kind[base + i] == TTRL_MDP) controlled_act(o, R, P, base, i, -1);
+    else if (o->kind[base + i] == TTRL_IDM) idm_act(o, R, P, base, i);
+  }
+}
+
+/* Road.step road.py:466-478, one env */
+static void step_env(S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int e, double dt) {
+  int base = e * o->N;
+  if (R->regulation_frequency > 0 && o->reg) {               /* RegulatedRoad.step regulation.py:28-32 */
+    o->reg[e] += 1;
+    const int period = (int)(1.0 / dt / R->regulation_frequency);
+    if (period > 0 && o->reg[e] % period == 0) enforce_road_rules(o, R, P, base);
+  }
+  for (int i = 0; i < o->N; ++i)
+    if (o->kind[base + i] != TTRL_ABSENT) vehicle_step(o, R, P, base, i, dt);
+  for (int i = 0; i < o->N; ++i) {
+    if (o->kind[base + i] == TTRL_ABSENT) continue;
+    for (int j = i + 1; j < o->N; ++j)
+      if (o->kind[base + j] != TTRL_ABSENT) handle_collisions(o, P, base, i, j, dt);
+  }
+}
+
 int oracle_road_act(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P, void* stream) {
   (void)stream; if (check(s)) return TTRL_E_ARG;
   S o = view(s);
 #pragma omp parallel for schedule(static)
-  for (int e = 0; e < o.E; ++e) {
-    int base = e * o.N;
-    for (int i = 0; i < o.N; ++i) {
-      if (o.kind[base + i] == TTRL_MDP) controlled_act(&o, R, P, base, i, -1);
-      else if (o.kind[base + i] == TTRL_IDM) idm_act(&o, R, P, base, i);
-    }
-  }
+  for (int e = 0; e < o.E; ++e) act_env(&o, R, P, e);
   return 0;
 }
 
-/* Road.step road.py:466-478 */
 int oracle_road_step(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P, double dt, void* stream) {
   (void)stream; if (check(s)) return TTRL_E_ARG;
   S o = view(s);
 #pragma omp parallel for schedule(static)
-  for (int e = 0; e < o.E; ++e) {
-    int base = e * o.N;
-    if (R->regulation_frequency > 0 && o.reg) {               /* RegulatedRoad.step regulation.py:28-32 */
-      o.reg[e] += 1;
-      const int period = (int)(1.0 / dt / R->regulation_frequency);
-      if (period > 0 && o.reg[e] % period == 0) enforce_road_rules(&o, R, P, base);
-    }
-    for (int i = 0; i < o.N; ++i)
-      if (o.kind[base + i] != TTRL_ABSENT) vehicle_step(&o, R, P, base, i, dt);
-    for (int i = 0; i < o.N; ++i) {
-      if (o.kind[base + i] == TTRL_ABSENT) continue;
-      for (int j = i + 1; j < o.N; ++j)
-        if (o.kind[base + j] != TTRL_ABSENT) handle_collisions(&o, P, base, i, j, dt);
-    }
-  }
+  for (int e = 0; e < o.E; ++e) step_env(&o, R, P, e, dt);
   return 0;
 }
 
@@ -633,6 +731,14 @@ int oracle_neighbours(const ttrl_state_t* s, const ttrl_lane_table_t* R, const t
   return 0;
 }
 
+/* AbstractEnv.vehicle: the env's controlled vehicle, its first MDPVehicle in list order
+ * (slot 0 on the highway; appended after the traffic in IntersectionEnv._make_vehicles). */
+static int ego_of(const S* o, int base) {
+  for (int i = 0; i < o->N; ++i)
+    if (o->kind[base + i] == TTRL_MDP) return i;
+  return -1;
+}
+
 /* ---------------------------------------------------------------- observations */
 /* Vehicle.to_dict kinematics.py:237-261 (route None => cos_d = sin_d = 0) */
 static double feature(const S* o, const ttrl_lane_table_t* R, int k, int f) {
@@ -657,10 +763,12 @@ static double feature(const S* o, const ttrl_lane_table_t* R, int k, int f) {
   return 0;
 }
 
-/* KinematicObservation.observe observation.py:233-275, order sorted/shuffled(ids only) */
+/* KinematicObservation.observe observation.py:233-275: order sorted, shuffled with the env's
+ * np_random (order_shuffled 2: np_random.shuffle(obs[1:]), :272-273), or ids only (1). */
 int oracle_observe_kinematics(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
-                              const ttrl_kin_cfg_t* cfg, float* out, int32_t* ids) {
-  (void)P; if (check(s)) return TTRL_E_ARG;
+                              const ttrl_kin_cfg_t* cfg, const uint8_t* mask, float* out, int32_t* ids) {
+  if (check(s)) return TTRL_E_ARG;
+  if (cfg->order_shuffled == 2 && (!s->rng || cfg->vehicles_count - 1 > 64)) return TTRL_E_ARG;
   S o = view(s);
   const int V = cfg->vehicles_count, F = cfg->n_features;
 #pragma omp parallel
@@ -669,15 +777,16 @@ int oracle_observe_kinematics(const ttrl_state_t* s, const ttrl_lane_table_t* R,
   double* key = (double*)malloc(sizeof(double) * o.N);
 #pragma omp for schedule(static)
   for (int e = 0; e < o.E; ++e) {
-    int base = e * o.N, ego = base;
+    if (mask && !mask[e]) continue;
+    int base = e * o.N, ei = ego_of(&o, base), ego = base + (ei < 0 ? 0 : ei);
     float* ob = out + (size_t)e * V * F;
     int nc = 0;
-    for (int j = 0; j < o.N; ++j) {              /* Road.close_objects_to road.py:427-433 */
+    for (int j = 0; j < o.N && ei >= 0; ++j) {   /* Road.close_objects_to road.py:427-433 */
       int k = base + j;
-      if (j == 0 || o.kind[k] == TTRL_ABSENT) continue;
+      if (j == ei || o.kind[k] == TTRL_ABSENT) continue;
       double dx = o.x[k] - o.x[ego], dy = o.y[k] - o.y[ego];
       if (!(sqrt(dx * dx + dy * dy) < cfg->perception_distance)) continue;
-      double ld = lane_distance(&o, R, base, 0, j);
+      double ld = lane_distance(&o, R, base, ei, j);
       if (!cfg->see_behind && !(-2 * P->length < ld)) continue;
       cand[nc] = j; key[nc] = fabs(ld); nc++;
     }
@@ -689,11 +798,22 @@ int oracle_observe_kinematics(const ttrl_state_t* s, const ttrl_lane_table_t* R,
         cand[b + 1] = cj; key[b + 1] = ck;
       }
     if (nc > V - 1) nc = V - 1;
-    for (int r = 0; r < V; ++r)
+    int perm[64];                                 /* output row 1 + t holds candidate row perm[t] */
+    for (int t = 0; t < V - 1 && t < 64; ++t) perm[t] = t;
+    if (cfg->order_shuffled == 2 && V - 1 > 1) {  /* Generator.shuffle: random_interval swaps */
+      pcg_t g; rng_load(&g, o.rng + (size_t)e * TTRL_RNG_WORDS);
+      for (int i = V - 2; i >= 1; --i) {
+        const int j = (int)pcg_interval(&g, (uint64_t)i);
+        const int t = perm[i]; perm[i] = perm[j]; perm[j] = t;
+      }
+      rng_store(&g, o.rng + (size_t)e * TTRL_RNG_WORDS);
+    }
+    for (int r = 0; r < V; ++r) {
+      const int q = r == 0 ? -1 : (cfg->order_shuffled == 2 ? perm[r - 1] : r - 1);
       for (int c = 0; c < F; ++c) {
         double val = 0;
-        if (r == 0 || r <= nc) {
-          int k = r == 0 ? ego : base + cand[r - 1];
+        if (ei >= 0 && (r == 0 || q < nc)) {
+          int k = r == 0 ? ego : base + cand[q];
           int f = cfg->features[c];
           val = feature(&o, R, k, f);
           if (r > 0 && !cfg->absolute && (f == TTRL_F_X || f == TTRL_F_Y || f == TTRL_F_VX || f == TTRL_F_VY))
@@ -705,6 +825,7 @@ int oracle_observe_kinematics(const ttrl_state_t* s, const ttrl_lane_table_t* R,
         }
         ob[r * F + c] = (float)val;
       }
+    }
     if (ids)
       for (int r = 0; r < V - 1; ++r) ids[e * (V - 1) + r] = r < nc ? cand[r] : -1;
   }
@@ -781,35 +902,6 @@ int oracle_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* R, const
 }
 
 /* ---------------------------------------------------------------- scene generation */
-/* numpy PCG64 (pcg_setseq_128_xsl_rr_64): step, then output of the new state. */
-typedef struct { unsigned __int128 st, inc; int has32; uint32_t u32; } pcg_t;
-static const unsigned __int128 PCG_MULT =
-    ((unsigned __int128)0x2360ED051FC65DA4ULL << 64) | 0x4385DF649FCCF645ULL;
-static uint64_t pcg_next64(pcg_t* g) {
-  g->st = g->st * PCG_MULT + g->inc;
-  uint64_t hi = (uint64_t)(g->st >> 64), lo = (uint64_t)g->st;
-  uint64_t x = hi ^ lo; unsigned rot = (unsigned)(hi >> 58);
-  return (x >> rot) | (x << ((64 - rot) & 63));
-}
-static uint32_t pcg_next32(pcg_t* g) {
-  if (g->has32) { g->has32 = 0; return g->u32; }
-  uint64_t n = pcg_next64(g); g->has32 = 1; g->u32 = (uint32_t)(n >> 32); return (uint32_t)n;
-}
-static double pcg_double(pcg_t* g) { return (double)(pcg_next64(g) >> 11) * (1.0 / 9007199254740992.0); }
-/* Generator.integers(0, n) for 1 < n <= 2^32 (buffered Lemire, numpy distributions.c) */
-static uint32_t pcg_bounded(pcg_t* g, uint32_t n) {
-  if (n <= 1) return 0;
-  uint32_t rng = n - 1; uint64_t rexcl = (uint64_t)rng + 1;
-  uint64_t m = (uint64_t)pcg_next32(g) * rexcl;
-  uint32_t left = (uint32_t)m;
-  if (left < rexcl) {
-    uint32_t thr = (uint32_t)((0xFFFFFFFFULL - rng) % rexcl);
-    while (left < thr) { m = (uint64_t)pcg_next32(g) * rexcl; left = (uint32_t)m; }
-  }
-  return (uint32_t)(m >> 32);
-}
-static double pcg_uniform(pcg_t* g, double lo, double hi) { return lo + (hi - lo) * pcg_double(g); }
-
 /* highway scene, SURVEY.md §3.C: ego MDPVehicle then create_random + randomize_behavior */
 int oracle_reset_highway(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
                          const ttrl_reset_cfg_t* cfg, const uint64_t* pcg) {
@@ -859,25 +951,219 @@ int oracle_reset_highway(const ttrl_state_t* s, const ttrl_lane_table_t* R, cons
   return 0;
 }
 
-/* IntersectionEnv._agent_reward / _is_terminated / _is_truncated template (intersection_env.py:78-119) */
+/* IntersectionEnv._agent_reward / _is_terminated / _is_truncated (intersection_env.py:78-119),
+ * has_arrived (:364-369), for the env's controlled vehicle */
 int oracle_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_reward_cfg_t* cfg,
                    const double* time, float* reward, uint8_t* terminated, uint8_t* truncated) {
   if (check(s)) return TTRL_E_ARG;
   S o = view(s);
   ttrl_params_t dummy; memset(&dummy, 0, sizeof dummy); dummy.lane_vehicle_length = 5.0;
   for (int e = 0; e < o.E; ++e) {
-    int k = e * o.N;
+    const int ei = ego_of(&o, e * o.N);
+    if (ei < 0) { reward[e] = 0; terminated[e] = 0; truncated[e] = (uint8_t)(time[e] >= cfg->duration); continue; }
+    int k = e * o.N + ei;
     double hs = clipd(lmap(o.v[k], cfg->speed_lo, cfg->speed_hi, 0, 1), 0, 1);
     double sr, rr; local(R, o.lane[k], o.x[k], o.y[k], &sr, &rr);
     int onroad = on_lane(R, &dummy, o.lane[k], sr, rr, 0.0);
-    double r = cfg->collision_reward * (double)o.crashed[k] + cfg->high_speed_reward * hs;
+    int arrived = R->exit_lane[o.lane[k]] && sr >= cfg->exit_distance;
+    double r = cfg->collision_reward * (double)o.crashed[k] + cfg->high_speed_reward * hs +
+               cfg->arrived_reward * (double)arrived;
+    if (arrived) r = cfg->arrived_reward;
     r *= (double)onroad;
-    if (cfg->normalize_reward) r = lmap(r, cfg->collision_reward, cfg->high_speed_reward, 0, 1);
+    if (cfg->normalize_reward) r = lmap(r, cfg->collision_reward, cfg->arrived_reward, 0, 1);
     reward[e] = (float)r;
-    terminated[e] = (uint8_t)(o.crashed[k] || (cfg->offroad_terminal && !onroad));
+    terminated[e] = (uint8_t)(o.crashed[k] || arrived || (cfg->offroad_terminal && !onroad));
     truncated[e] = (uint8_t)(time[e] >= cfg->duration);
   }
   return 0;
+}
+
+/* ---------------------------------------------------------------- intersection scenario */
+static void clear_slot(S* o, int k) {
+  o->kind[k] = TTRL_ABSENT; o->crashed[k] = 0; o->hasimp[k] = 0; o->lc[k] = 0;
+  o->x[k] = o->y[k] = o->h[k] = o->v[k] = o->ts[k] = o->timer[k] = o->steer[k] = o->acc[k] = 0;
+  o->ix[k] = o->iy[k] = 0; o->delta[k] = 4.0; o->lane[k] = o->tgt[k] = 0; o->sidx[k] = -1;
+  for (int q = 0; q < TTRL_ROUTE_MAX; ++q) o->rroad[k * TTRL_ROUTE_MAX + q] = o->rlane[k * TTRL_ROUTE_MAX + q] = -1;
+  o->rn[k] = -1; o->yield[k] = 0;
+}
+static void move_slot(S* o, int d, int k) {
+  o->kind[d] = o->kind[k]; o->crashed[d] = o->crashed[k]; o->hasimp[d] = o->hasimp[k]; o->lc[d] = o->lc[k];
+  o->x[d] = o->x[k]; o->y[d] = o->y[k]; o->h[d] = o->h[k]; o->v[d] = o->v[k]; o->ts[d] = o->ts[k];
+  o->timer[d] = o->timer[k]; o->delta[d] = o->delta[k]; o->steer[d] = o->steer[k]; o->acc[d] = o->acc[k];
+  o->ix[d] = o->ix[k]; o->iy[d] = o->iy[k]; o->lane[d] = o->lane[k]; o->tgt[d] = o->tgt[k]; o->sidx[d] = o->sidx[k];
+  for (int q = 0; q < TTRL_ROUTE_MAX; ++q) {
+    o->rroad[d * TTRL_ROUTE_MAX + q] = o->rroad[k * TTRL_ROUTE_MAX + q];
+    o->rlane[d * TTRL_ROUTE_MAX + q] = o->rlane[k * TTRL_ROUTE_MAX + q];
+  }
+  o->rn[d] = o->rn[k]; o->yield[d] = o->yield[k];
+}
+/* keep[j] for the present slots; survivors move down in list order, the tail is cleared */
+static void compact(S* o, int base, const int* keep) {
+  int w = 0;
+  for (int j = 0; j < o->N; ++j) {
+    if (o->kind[base + j] == TTRL_ABSENT || !keep[j]) continue;
+    if (w != j) move_slot(o, base + w, base + j);
+    w++;
+  }
+  for (int j = w; j < o->N; ++j) clear_slot(o, base + j);
+}
+static int count_of(const S* o, int base) {
+  int n = 0;
+  while (n < o->N && o->kind[base + n] != TTRL_ABSENT) n++;
+  return n;
+}
+/* ControlledVehicle.plan_route_to controller.py:71-87 over RoadNetwork.shortest_path road.py:159-188 */
+static void plan_route(S* o, const ttrl_lane_table_t* R, const ttrl_ix_cfg_t* C, int k, int corner) {
+  const int l = o->lane[k], road = R->road[l], node = R->road_to[road];
+  const int n = C->path_len[node][corner] > 0 ? C->path_len[node][corner] : 0;
+  for (int q = 0; q < TTRL_ROUTE_MAX; ++q) o->rroad[k * TTRL_ROUTE_MAX + q] = o->rlane[k * TTRL_ROUTE_MAX + q] = -1;
+  o->rroad[k * TTRL_ROUTE_MAX] = (int8_t)road; o->rlane[k * TTRL_ROUTE_MAX] = (int8_t)R->lane_id[l];
+  for (int q = 0; q < n; ++q) o->rroad[k * TTRL_ROUTE_MAX + 1 + q] = C->path_road[node][corner][q];
+  o->rn[k] = (int8_t)(1 + n);
+}
+/* IntersectionEnv._spawn_vehicle intersection_env.py:320-348 (IDMVehicle.make_on_lane objects.py:68-89,
+ * IDMVehicle.__init__ behavior.py:48-64, randomize_behavior :66-69) */
+static void ix_spawn(S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, const ttrl_ix_cfg_t* C, pcg_t* g,
+                     int base, double longitudinal, double pos_dev, double speed_dev, double prob, int go_straight) {
+  if (pcg_double(g) > prob) return;
+  int route[2];
+  pcg_choice_noreplace(g, 4, 2, route);
+  if (go_straight) route[1] = (route[0] + 2) % 4;
+  const int l = C->entry_lane[route[0]];
+  const double lon = longitudinal + C->spawn_offset + pcg_normal(g) * pos_dev;
+  const double sp = C->spawn_speed + pcg_normal(g) * speed_dev;
+  double px, py;
+  position(R, l, lon, 0.0, &px, &py);
+  const double ph = heading_at(R, l, lon);
+  for (int j = 0; j < o->N; ++j) {
+    const int k = base + j;
+    if (o->kind[k] == TTRL_ABSENT) continue;
+    const double dx = o->x[k] - px, dy = o->y[k] - py;
+    if (sqrt(dx * dx + dy * dy) < C->spawn_clear_distance) return;
+  }
+  const int n = count_of(o, base);
+  const double delta = pcg_uniform(g, C->delta_lo, C->delta_hi);  /* drawn even when no slot is left */
+  if (n >= o->N) return;
+  const int k = base + n;
+  clear_slot(o, k);
+  o->kind[k] = TTRL_IDM; o->lc[k] = 1;
+  o->x[k] = px; o->y[k] = py; o->h[k] = ph; o->v[k] = sp; o->ts[k] = sp;
+  o->lane[k] = o->tgt[k] = closest_lane(R, px, py, ph);
+  o->timer[k] = pymod((px + py) * PI, P->lane_change_delay);
+  plan_route(o, R, C, k, route[1]);
+  o->delta[k] = delta;
+}
+/* IntersectionEnv._clear_vehicles intersection_env.py:350-362 */
+static void ix_clear(S* o, const ttrl_lane_table_t* R, const ttrl_ix_cfg_t* C, int base) {
+  int keep[256];
+  for (int j = 0; j < o->N; ++j) {
+    const int k = base + j;
+    keep[j] = 1;
+    if (o->kind[k] != TTRL_IDM) continue;      /* controlled vehicles stay */
+    const int l = o->lane[k];
+    double s, r; local(R, l, o->x[k], o->y[k], &s, &r);
+    const int leaving = R->exit_lane[l] && s >= R->length[l] - C->leave_margin;
+    keep[j] = !(leaving || o->rn[k] < 0);
+  }
+  compact(o, base, keep);
+}
+
+/* IntersectionEnv._reset (intersection_env.py:135-137, _make_vehicles :251-318) from the
+ * np_random already seeded in state.rng */
+int oracle_ix_reset(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                    const ttrl_ix_cfg_t* C, const uint8_t* mask) {
+  if (check(s) || !s->rng || !s->route_n || s->n_veh > 256 || C->initial_vehicle_count > TTRL_IX_MAX_INIT)
+    return TTRL_E_ARG;
+  S o = view(s);
+#pragma omp parallel for schedule(static)
+  for (int e = 0; e < o.E; ++e) {
+    if (mask && !mask[e]) continue;
+    const int base = e * o.N;
+    pcg_t g; rng_load(&g, o.rng + (size_t)e * TTRL_RNG_WORDS);
+    for (int j = 0; j < o.N; ++j) clear_slot(&o, base + j);
+    o.reg[e] = 0;
+    for (int t = 0; t < C->initial_vehicle_count - 1; ++t)
+      ix_spawn(&o, R, P, C, &g, base, C->init_longitudinal[t], 1.0, 1.0, C->spawn_probability, 0);
+    for (int f = 0; f < C->warmup_frames; ++f) {
+      act_env(&o, R, P, e);
+      step_env(&o, R, P, e, C->warmup_dt);
+    }
+    ix_spawn(&o, R, P, C, &g, base, C->challenger_longitudinal, C->challenger_position_deviation,
+             C->challenger_speed_deviation, 1.0, 1);
+    /* the ego MDPVehicle, appended after the traffic (:283-312) */
+    const int dest = C->ego_destination >= 0 ? C->ego_destination : 1 + (int)pcg_bounded(&g, 3);
+    const double lon = C->ego_longitudinal + C->ego_deviation * (1.0 + pcg_normal(&g));
+    int n = count_of(&o, base);
+    if (n >= o.N) n = o.N - 1;                   /* no slot left: the last vehicle gives way */
+    const int k = base + n;
+    clear_slot(&o, k);
+    double ex, ey;
+    position(R, C->ego_lane, lon, 0.0, &ex, &ey);
+    o.kind[k] = TTRL_MDP; o.x[k] = ex; o.y[k] = ey; o.h[k] = heading_at(R, C->ego_lane, C->ego_heading_s);
+    o.v[k] = C->ego_speed;
+    o.lane[k] = o.tgt[k] = closest_lane(R, ex, ey, o.h[k]);
+    o.sidx[k] = speed_to_index(P, C->ego_speed);
+    o.ts[k] = P->target_speeds[o.sidx[k]];
+    plan_route(&o, R, C, k, dest);
+    /* "prevent early collisions": list.remove while iterating skips the next vehicle */
+    int lst[256], len = n + 1, keep[256];
+    for (int j = 0; j < len; ++j) { lst[j] = j; keep[j] = 1; }
+    for (int i = 0; i < len; ++i) {
+      const int j = lst[i], kj = base + j;
+      const double dx = o.x[kj] - ex, dy = o.y[kj] - ey;
+      if (j != n && sqrt(dx * dx + dy * dy) < C->ego_clear_distance) {
+        keep[j] = 0;
+        for (int q = i; q < len - 1; ++q) lst[q] = lst[q + 1];
+        len--;
+      }
+    }
+    compact(&o, base, keep);
+    rng_store(&g, o.rng + (size_t)e * TTRL_RNG_WORDS);
+  }
+  return 0;
+}
+
+/* IntersectionEnv.step tail (intersection_env.py:135-139): _clear_vehicles, _spawn_vehicle */
+int oracle_ix_clear_spawn(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                          const ttrl_ix_cfg_t* C, const uint8_t* mask) {
+  if (check(s) || !s->rng || !s->route_n || s->n_veh > 256) return TTRL_E_ARG;
+  S o = view(s);
+#pragma omp parallel for schedule(static)
+  for (int e = 0; e < o.E; ++e) {
+    if (mask && !mask[e]) continue;
+    const int base = e * o.N;
+    ix_clear(&o, R, C, base);
+    pcg_t g; rng_load(&g, o.rng + (size_t)e * TTRL_RNG_WORDS);
+    ix_spawn(&o, R, P, C, &g, base, 0.0, 1.0, 1.0, C->spawn_probability, 0);
+    rng_store(&g, o.rng + (size_t)e * TTRL_RNG_WORDS);
+  }
+  return 0;
+}
+
+/* numpy Generator draws, exposed for tests/test_ix_rng.py: op 0 standard_normal, 1 random,
+ * 2 integers(0, arg), 3 choice(arg, 2, replace=False) (2 outputs), 4 shuffle of arg rows
+ * (arg outputs: the permutation); one output slot per value */
+int oracle_rng_ops(uint64_t* state5, const int32_t* ops, const int32_t* args, int32_t n_ops, double* out) {
+  pcg_t g; rng_load(&g, state5);
+  int w = 0;
+  for (int i = 0; i < n_ops; ++i) {
+    switch (ops[i]) {
+      case 0: out[w++] = pcg_normal(&g); break;
+      case 1: out[w++] = pcg_double(&g); break;
+      case 2: out[w++] = (double)pcg_bounded(&g, (uint32_t)args[i]); break;
+      case 3: { int r[2]; pcg_choice_noreplace(&g, args[i], 2, r); out[w++] = r[0]; out[w++] = r[1]; break; }
+      case 4: {
+        int perm[256]; const int n = args[i];
+        for (int t = 0; t < n; ++t) perm[t] = t;
+        for (int t = n - 1; t >= 1; --t) { const int j = (int)pcg_interval(&g, (uint64_t)t); const int u = perm[t]; perm[t] = perm[j]; perm[j] = u; }
+        for (int t = 0; t < n; ++t) out[w++] = perm[t];
+        break;
+      }
+      default: return TTRL_E_ARG;
+    }
+  }
+  rng_store(&g, state5);
+  return w;
 }
 
 /* ---------------------------------------------------------------------------------------

@@ -1,0 +1,109 @@
+"""VecIntersectionEnv on the MI355X: the device reset (seeding, spawns, 45 warm-up frames,
+challenger, ego, removal), np_random-shuffled observations, rewards, clears and spawns, against
+the golden intersection episodes captured from the reference (oracle/gen_golden_ix.py) and the
+float64 oracle.  Tolerances as tests/test_ix_env_oracle.py; every discrete field exact."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_files, load_golden
+from oracle.oracle import HostState, Oracle
+from test_ix_env_oracle import EPISODE_TOL, KIN, obs_tol, same_state
+from test_ix_oracle import P_IX
+from topotrafficrl_amd import _abi
+from topotrafficrl_amd.intersection import VecIntersectionEnv, intersection_network, ix_cfg, ix_reset
+
+pytestmark = pytest.mark.gpu
+
+GOLD = [load_golden(p) for p in golden_files("ix_*")]
+# scripts/configs/IntersectionEnv/env.json: the default Kinematics observation with order "shuffled"
+ENV_JSON = {"observation": dict(VecIntersectionEnv.default_config()["observation"], order="shuffled")}
+
+
+def env_view(d: dict, e: int) -> dict:
+    return {k: v[e:e + 1] for k, v in d.items()}
+
+
+def test_device_reset_matches_reference_scenes(hip_device):
+    env = VecIntersectionEnv({**ENV_JSON, "num_envs": len(GOLD), "device": hip_device})
+    obs, _ = env.reset(seed=0)   # env e: IntersectionEnv.reset(seed=e)
+    st = env.state.to_numpy()
+    for e, d in enumerate(GOLD):
+        assert int(d["meta"][0]) == e
+        same_state(env_view(st, e), HostState.from_ix(d, "pre", 0, pad_to=32), 1e-9, f"reset {e}")
+        assert np.max(np.abs(obs[e].cpu().numpy() - d["obs0"])) <= 1e-6, e
+
+
+def test_device_episodes_match_reference(hip_device):
+    env = VecIntersectionEnv({**ENV_JSON, "num_envs": len(GOLD), "device": hip_device})
+    env.reset(seed=0)
+    steps = int(GOLD[0]["meta"][1])
+    acts = np.stack([d["actions"] for d in GOLD], 1)  # [steps, E]
+    for p in range(steps):
+        obs, rew, term, trunc, info = env.step(torch.from_numpy(acts[p]).to(hip_device))
+        st = env.state.to_numpy()
+        for e, d in enumerate(GOLD):
+            tol = obs_tol(HostState.from_ix(d, "frame", (p, 14), pad_to=32), EPISODE_TOL)
+            assert np.max(np.abs(obs[e].cpu().numpy() - d["obs"][p])) <= tol, (e, p)
+            assert abs(float(rew[e]) - d["reward"][p]) <= tol, (e, p)
+            assert bool(term[e]) == bool(d["terminated"][p]) and bool(trunc[e]) == bool(d["truncated"][p]), (e, p)
+            same_state(env_view(st, e), HostState.from_ix(d, "post", p, pad_to=32), EPISODE_TOL, f"env {e} step {p}")
+
+
+def test_large_batch_reset_equals_oracle(hip_device):
+    """4096 envs reset on the device; 64 of them replayed on the oracle."""
+    E = 4096
+    env = VecIntersectionEnv({"num_envs": E, "device": hip_device})
+    env.reset(seed=12345)
+    st = env.state.to_numpy()
+    net = intersection_network()
+    o = Oracle(net.table, P_IX)
+    cfg = ix_cfg(net, VecIntersectionEnv.default_config(), P_IX)
+    pick = np.arange(0, E, E // 64)
+    h = HostState(len(pick), 32)
+    o.ix_reset(h, cfg, [12345 + int(e) for e in pick])
+    for i, e in enumerate(pick):
+        same_state(env_view(st, int(e)), {k: v[i:i + 1] for k, v in h.a.items()}, 1e-9, f"env {e}")
+    assert np.array_equal(st["rng"][pick], h["rng"])
+    counts = (st["kind"] > 0).sum(1)
+    assert counts.min() >= 2 and counts.max() <= 32
+
+
+def test_masked_auto_reset(hip_device):
+    """Finished envs restart as default_rng([seed, episode]); the others continue untouched."""
+    E = 64
+    env = VecIntersectionEnv({**ENV_JSON, "num_envs": E, "device": hip_device, "auto_reset": True, "duration": 3})
+    env.reset(seed=7)
+    g = torch.Generator().manual_seed(0)
+    net = intersection_network()
+    o = Oracle(net.table, P_IX)
+    cfg = ix_cfg(net, VecIntersectionEnv.default_config(), P_IX)
+    episodes = np.zeros(E, dtype=np.int64)
+    for p in range(5):
+        before = env.state.to_numpy()
+        a = torch.randint(0, 3, (E,), generator=g).to(hip_device)
+        obs, rew, term, trunc, info = env.step(a)
+        done = (term | trunc).cpu().numpy()
+        episodes += done
+        st = env.state.to_numpy()
+        if done.any():
+            idx = np.nonzero(done)[0]
+            h = HostState(len(idx), 32)
+            o.ix_reset(h, cfg, [[7 + int(e), int(episodes[e])] for e in idx])
+            ob, _ = o.observe_kinematics(h, KIN)
+            for i, e in enumerate(idx):
+                same_state(env_view(st, int(e)), {k: v[i:i + 1] for k, v in h.a.items()}, 1e-9, f"auto-reset {e}")
+                assert np.max(np.abs(obs[e].cpu().numpy() - ob[i])) <= 1e-6
+            assert float(env.time[idx].abs().max()) == 0.0
+        assert not np.array_equal(before["x"], st["x"])
+    assert episodes.sum() > 0
+
+
+def test_f32_episode_runs(hip_device):
+    env = VecIntersectionEnv({"num_envs": 256, "device": hip_device, "dtype": "f32"})
+    obs, _ = env.reset(seed=3)
+    for _ in range(13):
+        obs, rew, term, trunc, info = env.step(torch.ones(256, dtype=torch.int64, device=hip_device))
+    torch.cuda.synchronize()
+    assert torch.isfinite(obs).all() and torch.isfinite(rew).all()
+    assert bool(trunc.all())

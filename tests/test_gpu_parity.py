@@ -38,7 +38,7 @@ def to_dev(h: HostState, device, dtype="f64", pad_to=None):
     b = BatchState(h.E, N, device=device, dtype=dtype)
     arr = {}
     for k, v in h.a.items():
-        if v.ndim == 1:  # per-env fields
+        if k in ("reg_steps", "rng"):  # per-env fields
             arr[k] = v
             continue
         full = np.zeros((h.E, N) + v.shape[2:], dtype=v.dtype)

@@ -13,7 +13,10 @@ import numpy as np
 
 MAX_LANES = 32
 MAX_ROADS = 32
+MAX_NODES = 32
 ROUTE_MAX = 4
+RNG_WORDS = 5
+IX_MAX_INIT = 16
 N_FEATURES = 14
 F32, F64 = 0, 1
 ABSENT, MDP, IDM = 0, 1, 2
@@ -31,7 +34,8 @@ U8_FIELDS = ["kind", "crashed", "has_impact", "lane_change"]
 # network / regulation fields: shapes [E, N, ROUTE_MAX], [E, N], [E]
 ROUTE_FIELDS = ["route_road", "route_lane"]
 NET_FIELDS = ROUTE_FIELDS + ["route_n", "yielding", "reg_steps"]
-ALL_FIELDS = REAL_FIELDS + I32_FIELDS + U8_FIELDS + NET_FIELDS
+# AbstractEnv.np_random per env: [E, RNG_WORDS] uint64 numpy Generator(PCG64) state
+ALL_FIELDS = REAL_FIELDS + I32_FIELDS + U8_FIELDS + NET_FIELDS + ["rng"]
 
 ERRORS = {-1: "TTRL_E_ARG (bad argument)", -2: "TTRL_E_LAUNCH (HIP error)", -3: "TTRL_E_UNSUPPORTED"}
 
@@ -102,7 +106,21 @@ class RewardCfg(C.Structure):
     _fields_ = [("collision_reward", C.c_double), ("high_speed_reward", C.c_double),
                 ("speed_lo", C.c_double), ("speed_hi", C.c_double),
                 ("normalize_reward", C.c_int32), ("offroad_terminal", C.c_int32),
-                ("duration", C.c_double)]
+                ("duration", C.c_double), ("arrived_reward", C.c_double), ("exit_distance", C.c_double)]
+
+
+class IxCfg(C.Structure):
+    _fields_ = [("initial_vehicle_count", C.c_int32), ("warmup_frames", C.c_int32), ("warmup_dt", C.c_double),
+                ("init_longitudinal", C.c_double * IX_MAX_INIT), ("spawn_probability", C.c_double),
+                ("spawn_offset", C.c_double), ("spawn_speed", C.c_double), ("spawn_clear_distance", C.c_double),
+                ("challenger_longitudinal", C.c_double), ("challenger_position_deviation", C.c_double),
+                ("challenger_speed_deviation", C.c_double), ("delta_lo", C.c_double), ("delta_hi", C.c_double),
+                ("n_corners", C.c_int32), ("entry_lane", C.c_int32 * 4), ("exit_node", C.c_int32 * 4),
+                ("ego_lane", C.c_int32), ("ego_destination", C.c_int32),
+                ("ego_longitudinal", C.c_double), ("ego_deviation", C.c_double), ("ego_heading_s", C.c_double),
+                ("ego_speed", C.c_double), ("ego_clear_distance", C.c_double), ("leave_margin", C.c_double),
+                ("path_road", ((C.c_int8 * (ROUTE_MAX - 1)) * 4) * MAX_NODES),
+                ("path_len", (C.c_int8 * 4) * MAX_NODES)]
 
 
 class TtcCfg(C.Structure):
@@ -268,8 +286,10 @@ def _ranges(cfg_ranges, code_arrays):
 def kin_cfg(features=("presence", "x", "y", "vx", "vy"), vehicles_count=5, features_range=None,
             absolute=False, order="sorted", normalize=True, clip=True, see_behind=False,
             lanes_on_road=4, perception_distance=200.0, shuffle_seed=0, shuffle_offset=0,
-            observe_intentions=False, include_obstacles=True, **_ignored) -> KinCfg:
-    """KinematicObservation.__init__ (observation.py:159-196); default ranges observation.py:213-225."""
+            observe_intentions=False, include_obstacles=True, shuffle_rng="philox", **_ignored) -> KinCfg:
+    """KinematicObservation.__init__ (observation.py:159-196); default ranges observation.py:213-225.
+    ``shuffle_rng``: "philox" (counter-based, seed + offset) or "np_random" (the env's numpy
+    Generator in state.rng, exactly as np_random.shuffle(obs[1:]) draws, observation.py:272-273)."""
     if order not in ("sorted", "shuffled"):
         raise ValueError(f"unknown order {order!r}")
     c = KinCfg()
@@ -282,7 +302,9 @@ def kin_cfg(features=("presence", "x", "y", "vx", "vy"), vehicles_count=5, featu
             raise ValueError(f"unsupported Kinematics feature {f!r}")
         c.features[i] = FEATURE_CODE[f]
     c.absolute, c.normalize, c.clip, c.see_behind = int(absolute), int(normalize), int(clip), int(see_behind)
-    c.order_shuffled = int(order == "shuffled")
+    if shuffle_rng not in ("philox", "np_random"):
+        raise ValueError(f"unknown shuffle_rng {shuffle_rng!r}")
+    c.order_shuffled = 0 if order == "sorted" else (2 if shuffle_rng == "np_random" else 1)
     if not features_range:
         features_range = {"x": [-5.0 * 40.0, 5.0 * 40.0], "y": [-4 * lanes_on_road, 4 * lanes_on_road],
                           "vx": [-2 * 40.0, 2 * 40.0], "vy": [-2 * 40.0, 2 * 40.0]}
@@ -337,8 +359,13 @@ def reset_cfg(n_vehicles, lanes: LaneTable, ego_lane=1, ego_x=50.0, ego_speed=25
 
 
 def reward_cfg(collision_reward=-1.0, high_speed_reward=0.4, reward_speed_range=(20.0, 30.0),
-               normalize_reward=False, offroad_terminal=False, duration=40.0) -> RewardCfg:
+               normalize_reward=False, offroad_terminal=False, duration=40.0, arrived_reward=None,
+               exit_distance=25.0) -> RewardCfg:
+    """IntersectionEnv._agent_reward config (intersection_env.py:78-104); arrived_reward None =
+    high_speed_reward (the highway template, which has no exit lanes, normalises to it)."""
     c = RewardCfg()
+    c.arrived_reward = float(high_speed_reward if arrived_reward is None else arrived_reward)
+    c.exit_distance = float(exit_distance)
     c.collision_reward, c.high_speed_reward = float(collision_reward), float(high_speed_reward)
     c.speed_lo, c.speed_hi = float(reward_speed_range[0]), float(reward_speed_range[1])
     c.normalize_reward, c.offroad_terminal = int(normalize_reward), int(offroad_terminal)
@@ -378,9 +405,26 @@ def pcg64_states(seeds) -> np.ndarray:
     return out
 
 
+def rng_states(seeds) -> np.ndarray:
+    """[E, RNG_WORDS] uint64 np_random states of ``np.random.default_rng(seed)`` per env
+    (a seed may be an int or a list of entropy ints), has_uint32 clear."""
+    out = np.zeros((len(seeds), RNG_WORDS), dtype=np.uint64)
+    out[:, :4] = pcg64_states(seeds)
+    return out
+
+
+def rng_from_generator(g: np.random.Generator) -> np.ndarray:
+    """The RNG_WORDS words of a live numpy Generator(PCG64) (test helper)."""
+    st = g.bit_generator.state
+    m = (1 << 64) - 1
+    s, inc = st["state"]["state"], st["state"]["inc"]
+    return np.array([(s >> 64) & m, s & m, (inc >> 64) & m, inc & m,
+                     (int(st["has_uint32"]) << 32) | int(st["uinteger"])], dtype=np.uint64)
+
+
 def state_struct(ptrs: dict, n_envs: int, n_veh: int, dtype: int) -> State:
     s = State()
     s.n_envs, s.n_veh, s.dtype = int(n_envs), int(n_veh), int(dtype)
     for f in ALL_FIELDS:
-        setattr(s, f, ptrs[f])
+        setattr(s, f, ptrs.get(f))
     return s

@@ -23,6 +23,7 @@ _SIGS = {
     "ttrl_simulate": ([_P, _P, _P, _P, C.c_int32, C.c_double, _P], C.c_int),
     "ttrl_neighbours": ([_P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_observe_kinematics": ([_P, _P, _P, _P, _P, _P, _P], C.c_int),
+    "ttrl_observe_kinematics_masked": ([_P, _P, _P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_observe_grid": ([_P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_observe_ttc": ([_P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_observe_lidar": ([_P, _P, _P, _P, _P, _P], C.c_int),
@@ -30,6 +31,8 @@ _SIGS = {
     "ttrl_reset_highway_seeded": ([_P, _P, _P, _P, _P, C.c_int32, _P, _P], C.c_int),
     "ttrl_seed_pcg64": ([_P, C.c_int32, _P], C.c_int),
     "ttrl_rewards": ([_P, _P, _P, _P, _P, _P, _P, _P], C.c_int),
+    "ttrl_ix_reset": ([_P, _P, _P, _P, _P, C.c_int32, _P, _P], C.c_int),
+    "ttrl_ix_clear_spawn": ([_P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_ego_attention_sizes": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P], C.c_int64),
     "ttrl_ego_attention_q": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, C.c_int32, _P, _P, _P], C.c_int),
 }
@@ -59,7 +62,7 @@ def load(path: str | None = None) -> C.CDLL:
             continue  # an older build loaded for comparison (tools/variants.py)
         fn.argtypes = args
         fn.restype = res
-    if lib.ttrl_abi_version() != 3:
+    if lib.ttrl_abi_version() != 4:
         raise ImportError("ABI version mismatch with include/ttrl_mi355x.h")
     if path is None:
         _lib = lib

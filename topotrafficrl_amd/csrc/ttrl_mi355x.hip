@@ -934,7 +934,7 @@ __device__ unsigned long long g_phase[20];
 template <typename T, int NS, int EPW, int NET>
 __global__ void __launch_bounds__(NS* EPW, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES : (sizeof(T) == 8 ? 2 : 4))
 simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int32_t* __restrict__ actions,
-                int frames, double dt_d, int mode, int ablate) {
+                const uint8_t* __restrict__ env_mask, int frames, double dt_d, int mode, int ablate) {
   constexpr bool CV = NET != NET_STRAIGHT;  // curved lane classes possible
   constexpr bool GR = NET == NET_GRAPH;     // roads, routes, RegulatedRoad
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -944,7 +944,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   const int le = tid / NS, i = tid % NS;
   const int N = st.n_veh, nl = R.n_lanes;
   const int env = blockIdx.x * EPW + le;
-  const bool slot = env < st.n_envs && i < N;
+  const bool env_on = env < st.n_envs && (!env_mask || env_mask[env]);  // masked-out envs: untouched
+  const bool slot = env_on && i < N;
   const size_t k = (size_t)env * N + i;
   const int me = le * NS + i;  // this vehicle's LDS slot
   const int eb = le * NS;      // env base in the LDS view
@@ -987,7 +988,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
     }
   }
   int reg = 0;  // RegulatedRoad.steps of this thread's env
-  if constexpr (GR) reg = env < st.n_envs ? st.reg_steps[env] : 0;
+  if constexpr (GR) reg = env_on ? st.reg_steps[env] : 0;
   const int reg_period = GR && R.regulation_frequency > 0 ? (int)(1.0 / dt_d / R.regulation_frequency) : 0;
   PH(15);
   if (i == 0) V.nitem[le] = 0;
@@ -1301,7 +1302,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       if constexpr (GR) {
         if (reg_period > 0) {  // RegulatedRoad.step regulation.py:28-32
           ++reg;
-          const bool doreg = env < st.n_envs && reg % reg_period == 0;
+          const bool doreg = env_on && reg % reg_period == 0;
           if (__syncthreads_or(doreg)) {  // enforce_road_rules regulation.py:34-60, every env of the block in step
             if (doreg && present) {
               const int fl = V.flags[me];
@@ -1568,7 +1569,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
     }
   }
   if constexpr (GR) {
-    if (i == 0 && env < st.n_envs) st.reg_steps[env] = reg;
+    if (i == 0 && env_on) st.reg_steps[env] = reg;
   }
   PH(16);
   PH_FLUSH
@@ -1633,6 +1634,113 @@ __device__ __forceinline__ T feature(const LaneT<T>& L, int f, T x, T y, T h, T 
 }
 
 // Philox4x32-10 (counter-based) for the "shuffled" row order.
+// ------------------------------------------------------------ PCG64 (numpy) scene reset
+struct U128 { unsigned long long hi, lo; };
+__device__ __forceinline__ U128 mul128(U128 a, U128 b) {
+  U128 r;
+  r.lo = a.lo * b.lo;
+  r.hi = __umul64hi(a.lo, b.lo) + a.hi * b.lo + a.lo * b.hi;
+  return r;
+}
+__device__ __forceinline__ U128 add128(U128 a, U128 b) {
+  U128 r;
+  r.lo = a.lo + b.lo;
+  r.hi = a.hi + b.hi + (r.lo < a.lo ? 1ull : 0ull);
+  return r;
+}
+struct Pcg { U128 st, inc; bool has32; unsigned u32; };
+__device__ __forceinline__ unsigned long long pcg_next64(Pcg& g) {
+  const U128 M = {0x2360ED051FC65DA4ull, 0x4385DF649FCCF645ull};
+  g.st = add128(mul128(g.st, M), g.inc);
+  const unsigned long long x = g.st.hi ^ g.st.lo;
+  const unsigned rot = (unsigned)(g.st.hi >> 58);
+  return (x >> rot) | (x << ((64 - rot) & 63));
+}
+__device__ __forceinline__ unsigned pcg_next32(Pcg& g) {
+  if (g.has32) { g.has32 = false; return g.u32; }
+  const unsigned long long n = pcg_next64(g);
+  g.has32 = true; g.u32 = (unsigned)(n >> 32);
+  return (unsigned)n;
+}
+__device__ __forceinline__ double pcg_double(Pcg& g) {
+  return (double)(pcg_next64(g) >> 11) * (1.0 / 9007199254740992.0);
+}
+__device__ __forceinline__ unsigned pcg_bounded(Pcg& g, unsigned n) {  // Generator.integers(0, n)
+  if (n <= 1) return 0;
+  const unsigned rng = n - 1;
+  const unsigned long long rexcl = (unsigned long long)rng + 1;
+  unsigned long long m = (unsigned long long)pcg_next32(g) * rexcl;
+  unsigned left = (unsigned)m;
+  if (left < rexcl) {
+    const unsigned thr = (unsigned)((0xFFFFFFFFull - rng) % rexcl);
+    while (left < thr) { m = (unsigned long long)pcg_next32(g) * rexcl; left = (unsigned)m; }
+  }
+  return (unsigned)(m >> 32);
+}
+
+// numpy.random.Generator over PCG64 (numpy random/src/distributions/distributions.c,
+// _generator.pyx), the env's np_random (gymnasium seeding.np_random): state words
+// {state_hi, state_lo, inc_hi, inc_lo, has_uint32 << 32 | uinteger} in ttrl_state_t.rng.
+__device__ __forceinline__ Pcg rng_load(const uint64_t* w) {
+  Pcg g;
+  g.st = U128{w[0], w[1]};
+  g.inc = U128{w[2], w[3]};
+  g.has32 = (w[4] >> 32) != 0;
+  g.u32 = (unsigned)w[4];
+  return g;
+}
+__device__ __forceinline__ void rng_store(const Pcg& g, uint64_t* w) {
+  w[0] = g.st.hi; w[1] = g.st.lo; w[2] = g.inc.hi; w[3] = g.inc.lo;
+  w[4] = ((uint64_t)(g.has32 ? 1 : 0) << 32) | g.u32;
+}
+// random_interval: uniform on [0, max] by masked rejection (Generator.shuffle)
+__device__ __forceinline__ unsigned pcg_interval(Pcg& g, unsigned max) {
+  if (max == 0) return 0;
+  unsigned mask = max;
+  mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+  unsigned v;
+  while ((v = (pcg_next32(g) & mask)) > max) {}
+  return v;
+}
+#define TTRL_ZIG_QUAL __constant__
+#include "ttrl_ziggurat.h"
+// random_standard_normal: the 256-entry ziggurat of numpy (tables from gen_ziggurat.py)
+__device__ __noinline__ double pcg_normal(Pcg& g) {
+  for (;;) {
+    unsigned long long r = pcg_next64(g);
+    const int idx = (int)(r & 0xff);
+    r >>= 8;
+    const int sign = (int)(r & 0x1);
+    const unsigned long long rabs = (r >> 1) & 0x000fffffffffffffull;
+    double x = (double)rabs * ttrl_zig_wi[idx];
+    if (sign & 0x1) x = -x;
+    if (rabs < ttrl_zig_ki[idx]) return x;
+    if (idx == 0) {
+      for (;;) {
+        const double xx = -TTRL_ZIG_NOR_INV_R * log1p(-pcg_double(g));
+        const double yy = -log1p(-pcg_double(g));
+        if (yy + yy > xx * xx) return ((rabs >> 8) & 0x1) ? -(TTRL_ZIG_NOR_R + xx) : TTRL_ZIG_NOR_R + xx;
+      }
+    } else if (((ttrl_zig_fi[idx - 1] - ttrl_zig_fi[idx]) * pcg_double(g) + ttrl_zig_fi[idx]) < exp(-0.5 * x * x)) {
+      return x;
+    }
+  }
+}
+// Generator.choice(pop, size, replace=False), small population: Floyd's algorithm, then
+// _shuffle_int (random_bounded_uint64 = buffered Lemire draws)
+__device__ __forceinline__ void pcg_choice_noreplace(Pcg& g, int pop, int size, int* out) {
+  for (int j = pop - size; j < pop; ++j) {
+    const int val = (int)pcg_bounded(g, (unsigned)j + 1);
+    bool seen = false;
+    for (int q = 0; q < j - (pop - size); ++q) seen |= out[q] == val;
+    out[j - (pop - size)] = seen ? j : val;
+  }
+  for (int i = size - 1; i >= 1; --i) {
+    const int j = (int)pcg_bounded(g, (unsigned)i + 1);
+    const int t = out[i]; out[i] = out[j]; out[j] = t;
+  }
+}
+
 __device__ __forceinline__ uint4 philox(uint4 c, uint2 key) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
@@ -1645,41 +1753,51 @@ __device__ __forceinline__ uint4 philox(uint4 c, uint2 key) {
 }
 
 // KinematicObservation.observe (observation.py:233-275): ego row + close_objects_to
-// (road.py:418-447) stable-sorted by |lane distance|, normalised (lmap + clip), zero-padded.
+// (road.py:418-447) stable-sorted by |lane distance| (or in list order when shuffled),
+// normalised (lmap + clip), zero-padded.  The ego is the env's first MDP slot (AbstractEnv.vehicle).
+// Shuffled: rows 1..V-1 permuted by np_random.shuffle(obs[1:]) (:272-273) with the env's own
+// numpy Generator (order_shuffled 2, bit-exact) or by a Philox Fisher-Yates (1).
+// env_mask (optional): envs left untouched (rows and np_random) where it is 0.
 template <typename T, int NS, int EPW>
 __global__ void __launch_bounds__(NS* EPW)
 kinematics_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_kin_cfg_t cfg,
-                      float* __restrict__ out, int32_t* __restrict__ ids) {
+                      const uint8_t* __restrict__ env_mask, float* __restrict__ out, int32_t* __restrict__ ids) {
   __shared__ T s_key[EPW * NS];
-  __shared__ int s_cnt[EPW];
+  __shared__ int s_cnt[EPW], s_ego[EPW];
   __shared__ int s_perm[EPW][64];
   __shared__ LaneT<T> s_lanes[LMAX];
   const int tid = threadIdx.x, le = tid / NS, i = tid % NS;
   const int N = st.n_veh;
   const int env = blockIdx.x * EPW + le;
-  const bool env_ok = env < st.n_envs;
+  const bool env_ok = env < st.n_envs && (!env_mask || env_mask[env]);
   const bool slot = env_ok && i < N;
-  const size_t k = (size_t)env * N + i, k0 = (size_t)env * N;
-  {
-    if (tid < R.n_lanes) s_lanes[tid] = make_lane<T>(R, tid);
-    if (i == 0) s_cnt[le] = 0;
-  }
-  const int V = cfg.vehicles_count, F = cfg.n_features;
-  T ex = T(0), ey = T(0), eh = T(0), ev = T(0), x = T(0), y = T(0), h = T(0), v = T(0);
-  int elane = 0, lane = 0;
+  const size_t k = (size_t)env * N + i;
+  if (tid < R.n_lanes) s_lanes[tid] = make_lane<T>(R, tid);
+  if (i == 0) { s_cnt[le] = 0; s_ego[le] = NS; }
+  T x = T(0), y = T(0), h = T(0), v = T(0);
+  int lane = 0;
   bool present = false;
   if (slot) {
-    ex = ((const T*)st.x)[k0]; ey = ((const T*)st.y)[k0]; eh = ((const T*)st.heading)[k0];
-    ev = ((const T*)st.speed)[k0]; elane = st.lane[k0];
     x = ((const T*)st.x)[k]; y = ((const T*)st.y)[k]; h = ((const T*)st.heading)[k];
     v = ((const T*)st.speed)[k]; lane = st.lane[k];
     present = st.kind[k] != TTRL_ABSENT;
   }
   __syncthreads();
+  if (slot && st.kind[k] == TTRL_MDP) atomicMin(&s_ego[le], i);
+  __syncthreads();
+  const int ego = s_ego[le];
+  const bool has_ego = env_ok && ego < N;
+  T ex = T(0), ey = T(0), eh = T(0), ev = T(0);
+  int elane = 0;
+  if (has_ego) {
+    const size_t k0 = (size_t)env * N + ego;
+    ex = ((const T*)st.x)[k0]; ey = ((const T*)st.y)[k0]; eh = ((const T*)st.heading)[k0];
+    ev = ((const T*)st.speed)[k0]; elane = st.lane[k0];
+  }
   // candidate filter (road.py:427-433) and sort key |lane_distance_to| along the ego's lane
   bool cand = false;
   T key = K<T>::inf();
-  if (present && i > 0) {
+  if (has_ego && present && i != ego) {
     const T dx = x - ex, dy = y - ey;
     if (sqrt(dx * dx + dy * dy) < T(cfg.perception_distance)) {
       T s1, r1, s0, r0;
@@ -1704,27 +1822,37 @@ kinematics_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttr
     }
   }
   int nc = env_ok ? s_cnt[le] : 0;
+  const int V = cfg.vehicles_count, F = cfg.n_features;
   if (nc > V - 1) nc = V - 1;
-  // shuffled: rows 1..V-1 permuted (np_random.shuffle(obs[1:]), observation.py:272-273) with
-  // Fisher-Yates driven by Philox(seed, offset, env); the multiset of rows is the reference's.
-  if (cfg.order_shuffled && V - 1 <= 64) {
+  const bool shuf = cfg.order_shuffled && V - 1 <= 64;
+  if (shuf) {
     if (i == 0 && env_ok) {
       int p[64];
       for (int t = 0; t < V - 1; ++t) p[t] = t;
-      const uint2 key2 = make_uint2((unsigned)cfg.shuffle_seed, (unsigned)(cfg.shuffle_seed >> 32));
-      for (int t = V - 2; t > 0; --t) {
-        const uint4 r = philox(make_uint4((unsigned)env, (unsigned)t, (unsigned)cfg.shuffle_offset,
-                                          (unsigned)(cfg.shuffle_offset >> 32)), key2);
-        const int j = (int)(((unsigned long long)r.x * (unsigned)(t + 1)) >> 32);
-        const int tmp = p[t]; p[t] = p[j]; p[j] = tmp;
+      if (cfg.order_shuffled == 2) {  // Generator.shuffle: random_interval swaps, i = n-1 .. 1
+        uint64_t* w = st.rng + (size_t)env * TTRL_RNG_WORDS;
+        Pcg g = rng_load(w);
+        for (int t = V - 2; t > 0; --t) {
+          const int j = (int)pcg_interval(g, (unsigned)t);
+          const int tmp = p[t]; p[t] = p[j]; p[j] = tmp;
+        }
+        rng_store(g, w);
+      } else {  // Philox(seed, offset, env) Fisher-Yates: the multiset of rows is the reference's
+        const uint2 key2 = make_uint2((unsigned)cfg.shuffle_seed, (unsigned)(cfg.shuffle_seed >> 32));
+        for (int t = V - 2; t > 0; --t) {
+          const uint4 r = philox(make_uint4((unsigned)env, (unsigned)t, (unsigned)cfg.shuffle_offset,
+                                            (unsigned)(cfg.shuffle_offset >> 32)), key2);
+          const int j = (int)(((unsigned long long)r.x * (unsigned)(t + 1)) >> 32);
+          const int tmp = p[t]; p[t] = p[j]; p[j] = tmp;
+        }
       }
-      for (int t = 0; t < V - 1; ++t) s_perm[le][p[t]] = t;  // sorted row q -> output slot
+      for (int t = 0; t < V - 1; ++t) s_perm[le][p[t]] = t;  // candidate row q -> output slot
     }
     __syncthreads();
   }
   if (!env_ok) return;
   float* ob = out + (size_t)env * V * F;
-  auto slot_of = [&](int q) { return cfg.order_shuffled && V - 1 <= 64 ? 1 + s_perm[le][q] : 1 + q; };
+  auto slot_of = [&](int q) { return shuf ? 1 + s_perm[le][q] : 1 + q; };
   const T ec = t_cos(eh), es = t_sin(eh);
   auto emit = [&](int row, T px, T py, T phd, T pv, int pl, bool rel) {
     const T c = t_cos(phd), s = t_sin(phd);
@@ -1740,7 +1868,10 @@ kinematics_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttr
       ob[row * F + cidx] = (float)val;
     }
   };
-  if (i == 0 && slot) emit(0, ex, ey, eh, ev, elane, false);
+  if (i == 0) {
+    if (has_ego) emit(0, ex, ey, eh, ev, elane, false);
+    else for (int cidx = 0; cidx < F; ++cidx) ob[cidx] = 0.f;  // no controlled vehicle: zeros
+  }
   if (cand && rank < nc) {
     emit(slot_of(rank), x, y, h, v, lane, true);
     if (ids) ids[(size_t)env * (V - 1) + rank] = i;
@@ -1852,50 +1983,6 @@ grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid
       }
     }
   }
-}
-
-// ------------------------------------------------------------ PCG64 (numpy) scene reset
-struct U128 { unsigned long long hi, lo; };
-__device__ __forceinline__ U128 mul128(U128 a, U128 b) {
-  U128 r;
-  r.lo = a.lo * b.lo;
-  r.hi = __umul64hi(a.lo, b.lo) + a.hi * b.lo + a.lo * b.hi;
-  return r;
-}
-__device__ __forceinline__ U128 add128(U128 a, U128 b) {
-  U128 r;
-  r.lo = a.lo + b.lo;
-  r.hi = a.hi + b.hi + (r.lo < a.lo ? 1ull : 0ull);
-  return r;
-}
-struct Pcg { U128 st, inc; bool has32; unsigned u32; };
-__device__ __forceinline__ unsigned long long pcg_next64(Pcg& g) {
-  const U128 M = {0x2360ED051FC65DA4ull, 0x4385DF649FCCF645ull};
-  g.st = add128(mul128(g.st, M), g.inc);
-  const unsigned long long x = g.st.hi ^ g.st.lo;
-  const unsigned rot = (unsigned)(g.st.hi >> 58);
-  return (x >> rot) | (x << ((64 - rot) & 63));
-}
-__device__ __forceinline__ unsigned pcg_next32(Pcg& g) {
-  if (g.has32) { g.has32 = false; return g.u32; }
-  const unsigned long long n = pcg_next64(g);
-  g.has32 = true; g.u32 = (unsigned)(n >> 32);
-  return (unsigned)n;
-}
-__device__ __forceinline__ double pcg_double(Pcg& g) {
-  return (double)(pcg_next64(g) >> 11) * (1.0 / 9007199254740992.0);
-}
-__device__ __forceinline__ unsigned pcg_bounded(Pcg& g, unsigned n) {  // Generator.integers(0, n)
-  if (n <= 1) return 0;
-  const unsigned rng = n - 1;
-  const unsigned long long rexcl = (unsigned long long)rng + 1;
-  unsigned long long m = (unsigned long long)pcg_next32(g) * rexcl;
-  unsigned left = (unsigned)m;
-  if (left < rexcl) {
-    const unsigned thr = (unsigned)((0xFFFFFFFFull - rng) % rexcl);
-    while (left < thr) { m = (unsigned long long)pcg_next32(g) * rexcl; left = (unsigned)m; }
-  }
-  return (unsigned)(m >> 32);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2225,26 +2312,239 @@ __global__ void reset_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t
   }
 }
 
-// IntersectionEnv._agent_reward / _is_terminated / _is_truncated template (intersection_env.py:78-119)
+// IntersectionEnv._agent_reward / _is_terminated / _is_truncated (intersection_env.py:78-119) and
+// has_arrived (:364-369) for the env's controlled vehicle (its first MDP slot).
 template <typename T>
 __global__ void rewards_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_reward_cfg_t cfg, const double* __restrict__ time,
                                float* __restrict__ reward, uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
   const int env = blockIdx.x * blockDim.x + threadIdx.x;
   if (env >= st.n_envs) return;
-  const size_t k = (size_t)env * st.n_veh;
+  const size_t b = (size_t)env * st.n_veh;
+  int ego = 0;
+  while (ego < st.n_veh && st.kind[b + ego] != TTRL_MDP) ++ego;
+  trunc[env] = (uint8_t)(time[env] >= cfg.duration);
+  if (ego == st.n_veh) { reward[env] = 0.f; term[env] = 0; return; }
+  const size_t k = b + ego;
   const T v = ((const T*)st.speed)[k], x = ((const T*)st.x)[k], y = ((const T*)st.y)[k];
   const int l = st.lane[k];
   const T hs = clip(lmap(v, T(cfg.speed_lo), T(cfg.speed_hi), T(0), T(1)), T(0), T(1));
   T s, r;
   lane_local(make_lane<T>(R, l), x, y, s, r);
   const bool onroad = fabs(r) <= T(R.width[l]) / T(2) + T(0) && -T(5) <= s && s < T(R.length[l]) + T(5);
+  const bool arrived = R.exit_lane[l] && s >= T(cfg.exit_distance);
   const bool crashed = st.crashed[k] != 0;
-  T rw = T(cfg.collision_reward) * T(crashed ? 1 : 0) + T(cfg.high_speed_reward) * hs;
+  T rw = T(cfg.collision_reward) * T(crashed ? 1 : 0) + T(cfg.high_speed_reward) * hs +
+         T(cfg.arrived_reward) * T(arrived ? 1 : 0);
+  if (arrived) rw = T(cfg.arrived_reward);
   rw *= T(onroad ? 1 : 0);
-  if (cfg.normalize_reward) rw = lmap(rw, T(cfg.collision_reward), T(cfg.high_speed_reward), T(0), T(1));
+  if (cfg.normalize_reward) rw = lmap(rw, T(cfg.collision_reward), T(cfg.arrived_reward), T(0), T(1));
   reward[env] = (float)rw;
-  term[env] = (uint8_t)(crashed || (cfg.offroad_terminal && !onroad));
-  trunc[env] = (uint8_t)(time[env] >= cfg.duration);
+  term[env] = (uint8_t)(crashed || arrived || (cfg.offroad_terminal && !onroad));
+}
+
+// ------------------------------------------------------------ the intersection scenario
+// IntersectionEnv (intersection_env.py:131-362) scene management, one thread per env: the
+// vehicle list is inherently sequential (spawns append, clears keep list order, every spawn
+// draws from the env's np_random in turn) and runs once per policy step, next to the fused
+// 15-frame simulate launch that dominates.
+template <typename T>
+__device__ void slot_clear(const ttrl_state_t& st, size_t k) {
+  st.kind[k] = TTRL_ABSENT; st.crashed[k] = 0; st.has_impact[k] = 0; st.lane_change[k] = 0;
+  T* f[] = {(T*)st.x, (T*)st.y, (T*)st.heading, (T*)st.speed, (T*)st.target_speed, (T*)st.timer,
+            (T*)st.steer, (T*)st.acc, (T*)st.impact_x, (T*)st.impact_y};
+  for (T* p : f) p[k] = T(0);
+  ((T*)st.delta)[k] = T(4);
+  st.lane[k] = st.target_lane[k] = 0; st.speed_index[k] = -1;
+  for (int q = 0; q < TTRL_ROUTE_MAX; ++q) st.route_road[k * TTRL_ROUTE_MAX + q] = st.route_lane[k * TTRL_ROUTE_MAX + q] = -1;
+  st.route_n[k] = -1; st.yielding[k] = 0;
+}
+template <typename T>
+__device__ void slot_move(const ttrl_state_t& st, size_t d, size_t k) {
+  T* f[] = {(T*)st.x, (T*)st.y, (T*)st.heading, (T*)st.speed, (T*)st.target_speed, (T*)st.timer, (T*)st.delta,
+            (T*)st.steer, (T*)st.acc, (T*)st.impact_x, (T*)st.impact_y};
+  for (T* p : f) p[d] = p[k];
+  st.kind[d] = st.kind[k]; st.crashed[d] = st.crashed[k]; st.has_impact[d] = st.has_impact[k];
+  st.lane_change[d] = st.lane_change[k];
+  st.lane[d] = st.lane[k]; st.target_lane[d] = st.target_lane[k]; st.speed_index[d] = st.speed_index[k];
+  for (int q = 0; q < TTRL_ROUTE_MAX; ++q) {
+    st.route_road[d * TTRL_ROUTE_MAX + q] = st.route_road[k * TTRL_ROUTE_MAX + q];
+    st.route_lane[d * TTRL_ROUTE_MAX + q] = st.route_lane[k * TTRL_ROUTE_MAX + q];
+  }
+  st.route_n[d] = st.route_n[k]; st.yielding[d] = st.yielding[k];
+}
+// keep bit j of the env's slots; survivors move down in list order, the tail is cleared
+template <typename T>
+__device__ void slots_compact(const ttrl_state_t& st, size_t base, const unsigned* keep) {
+  int w = 0;
+  for (int j = 0; j < st.n_veh; ++j) {
+    if (st.kind[base + j] == TTRL_ABSENT || !((keep[j >> 5] >> (j & 31)) & 1u)) continue;
+    if (w != j) slot_move<T>(st, base + w, base + j);
+    ++w;
+  }
+  for (int j = w; j < st.n_veh; ++j) slot_clear<T>(st, base + j);
+}
+__device__ int slots_count(const ttrl_state_t& st, size_t base) {
+  int n = 0;
+  while (n < st.n_veh && st.kind[base + n] != TTRL_ABSENT) ++n;
+  return n;
+}
+// RoadNetwork.get_closest_lane_index road.py:55-71 with distance_with_heading lane.py:132-147
+__device__ int closest_lane_d(const ttrl_lane_table_t& R, double x, double y, double h) {
+  int best = 0;
+  double bd = 0;
+  for (int l = 0; l < R.n_lanes; ++l) {
+    const LaneT<double> L = make_lane<double>(R, l);
+    double s, r;
+    lane_local(L, x, y, s, r);
+    const double ang = fabs(wrap_to_pi(h - heading_at(L, s)));
+    double a = s - R.length[l]; if (!(a > 0)) a = 0;
+    double c = 0 - s; if (!(c > 0)) c = 0;
+    const double d = fabs(r) + a + c + 1.0 * ang;
+    if (l == 0 || d < bd) { bd = d; best = l; }
+  }
+  return best;
+}
+// ControlledVehicle.plan_route_to controller.py:71-87 (shortest_path precomputed on the host)
+__device__ void plan_route(const ttrl_state_t& st, const ttrl_lane_table_t& R, const ttrl_ix_cfg_t& C, size_t k,
+                           int corner) {
+  const int l = st.lane[k], road = R.road[l], node = R.road_to[road];
+  const int n = C.path_len[node][corner] > 0 ? C.path_len[node][corner] : 0;
+  int8_t* rr = st.route_road + k * TTRL_ROUTE_MAX;
+  int8_t* rl = st.route_lane + k * TTRL_ROUTE_MAX;
+  for (int q = 0; q < TTRL_ROUTE_MAX; ++q) rr[q] = rl[q] = -1;
+  rr[0] = (int8_t)road; rl[0] = (int8_t)R.lane_id[l];
+  for (int q = 0; q < n; ++q) rr[1 + q] = C.path_road[node][corner][q];
+  st.route_n[k] = (int8_t)(1 + n);
+}
+// IntersectionEnv._spawn_vehicle intersection_env.py:320-348 (IDMVehicle.make_on_lane
+// objects.py:68-89, IDMVehicle.__init__ behavior.py:48-64, randomize_behavior :66-69)
+template <typename T>
+__device__ void ix_spawn(const ttrl_state_t& st, const ttrl_lane_table_t& R, const ttrl_params_t& P,
+                         const ttrl_ix_cfg_t& C, Pcg& g, size_t base, double longitudinal, double pos_dev,
+                         double speed_dev, double prob, bool go_straight) {
+  if (pcg_double(g) > prob) return;
+  int route[2];
+  pcg_choice_noreplace(g, 4, 2, route);
+  if (go_straight) route[1] = (route[0] + 2) % 4;
+  const int l = C.entry_lane[route[0]];
+  const double lon = longitudinal + C.spawn_offset + pcg_normal(g) * pos_dev;
+  const double sp = C.spawn_speed + pcg_normal(g) * speed_dev;
+  const LaneT<double> L = make_lane<double>(R, l);
+  double px, py;
+  lane_position(L, lon, 0.0, px, py);
+  const double ph = heading_at(L, lon);
+  for (int j = 0; j < st.n_veh; ++j) {
+    const size_t k = base + j;
+    if (st.kind[k] == TTRL_ABSENT) continue;
+    const double dx = (double)((const T*)st.x)[k] - px, dy = (double)((const T*)st.y)[k] - py;
+    if (sqrt(dx * dx + dy * dy) < C.spawn_clear_distance) return;
+  }
+  const int n = slots_count(st, base);
+  const double delta = C.delta_lo + (C.delta_hi - C.delta_lo) * pcg_double(g);  // drawn even with no slot left
+  if (n >= st.n_veh) return;
+  const size_t k = base + n;
+  slot_clear<T>(st, k);
+  st.kind[k] = TTRL_IDM; st.lane_change[k] = 1;
+  ((T*)st.x)[k] = T(px); ((T*)st.y)[k] = T(py); ((T*)st.heading)[k] = T(ph);
+  ((T*)st.speed)[k] = T(sp); ((T*)st.target_speed)[k] = T(sp);
+  st.lane[k] = st.target_lane[k] = closest_lane_d(R, px, py, ph);
+  ((T*)st.timer)[k] = T(pymod((px + py) * 3.141592653589793, P.lane_change_delay));
+  plan_route(st, R, C, k, route[1]);
+  ((T*)st.delta)[k] = T(delta);
+}
+
+// IntersectionEnv._reset, part 1: np_random = default_rng(SeedSequence(entropy)), _make_road's
+// fresh RegulatedRoad (steps 0, no vehicles), the n-1 initial spawns (intersection_env.py:262-263).
+template <typename T>
+__global__ void ix_begin_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_ix_cfg_t C,
+                                const unsigned* __restrict__ words, int n_words, const uint8_t* __restrict__ mask) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= st.n_envs || (mask && !mask[env])) return;
+  const size_t base = (size_t)env * st.n_veh;
+  unsigned long long s4[4];
+  SeedSeq::pcg64_seed(words + (size_t)env * n_words, n_words, s4);
+  Pcg g;
+  g.st = U128{s4[0], s4[1]}; g.inc = U128{s4[2], s4[3]}; g.has32 = false; g.u32 = 0;
+  for (int j = 0; j < st.n_veh; ++j) slot_clear<T>(st, base + j);
+  st.reg_steps[env] = 0;
+  for (int t = 0; t < C.initial_vehicle_count - 1; ++t)
+    ix_spawn<T>(st, R, P, C, g, base, C.init_longitudinal[t], 1.0, 1.0, C.spawn_probability, false);
+  rng_store(g, st.rng + (size_t)env * TTRL_RNG_WORDS);
+}
+
+// IntersectionEnv._reset, part 2 (after the warm-up frames): the challenger, the ego
+// MDPVehicle appended after the traffic, and the removal of the vehicles within 20 m of it,
+// which skips the vehicle after each removed one (list.remove while iterating, :308-312).
+template <typename T>
+__global__ void ix_finish_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_ix_cfg_t C,
+                                 const uint8_t* __restrict__ mask) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= st.n_envs || (mask && !mask[env])) return;
+  const size_t base = (size_t)env * st.n_veh;
+  uint64_t* w = st.rng + (size_t)env * TTRL_RNG_WORDS;
+  Pcg g = rng_load(w);
+  ix_spawn<T>(st, R, P, C, g, base, C.challenger_longitudinal, C.challenger_position_deviation,
+              C.challenger_speed_deviation, 1.0, true);
+  const int dest = C.ego_destination >= 0 ? C.ego_destination : 1 + (int)pcg_bounded(g, 3);
+  const double lon = C.ego_longitudinal + C.ego_deviation * (1.0 + pcg_normal(g));
+  int n = slots_count(st, base);
+  if (n >= st.n_veh) n = st.n_veh - 1;  // no slot left: the last vehicle gives way to the ego
+  const size_t k = base + n;
+  slot_clear<T>(st, k);
+  const LaneT<double> L = make_lane<double>(R, C.ego_lane);
+  double ex, ey;
+  lane_position(L, lon, 0.0, ex, ey);
+  const double eh = heading_at(L, C.ego_heading_s);
+  st.kind[k] = TTRL_MDP;
+  ((T*)st.x)[k] = T(ex); ((T*)st.y)[k] = T(ey); ((T*)st.heading)[k] = T(eh); ((T*)st.speed)[k] = T(C.ego_speed);
+  st.lane[k] = st.target_lane[k] = closest_lane_d(R, ex, ey, eh);
+  const int si = speed_to_index(P, C.ego_speed);
+  st.speed_index[k] = si;
+  ((T*)st.target_speed)[k] = T(P.target_speeds[si]);
+  plan_route(st, R, C, k, dest);
+  // list.remove while iterating: positions shift left, the iterator index still advances
+  unsigned keep[8] = {~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u};
+  int lst[256];
+  int len = n + 1;
+  for (int j = 0; j < len; ++j) lst[j] = j;
+  for (int i = 0; i < len; ++i) {
+    const int j = lst[i];
+    const double dx = (double)((const T*)st.x)[base + j] - (double)((const T*)st.x)[k];
+    const double dy = (double)((const T*)st.y)[base + j] - (double)((const T*)st.y)[k];
+    if (j != n && sqrt(dx * dx + dy * dy) < C.ego_clear_distance) {
+      keep[j >> 5] &= ~(1u << (j & 31));
+      for (int q = i; q < len - 1; ++q) lst[q] = lst[q + 1];
+      --len;
+    }
+  }
+  slots_compact<T>(st, base, keep);
+  rng_store(g, w);
+}
+
+// IntersectionEnv.step tail (intersection_env.py:135-139): _clear_vehicles (:350-362) keeps the
+// controlled vehicle and every vehicle neither leaving (an "il"->"o" lane within 4 lengths of its
+// end) nor without a route, in list order; then _spawn_vehicle(spawn_probability).
+template <typename T>
+__global__ void ix_clear_spawn_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_ix_cfg_t C,
+                                      const uint8_t* __restrict__ mask) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= st.n_envs || (mask && !mask[env])) return;
+  const size_t base = (size_t)env * st.n_veh;
+  unsigned keep[8] = {~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u};
+  for (int j = 0; j < st.n_veh; ++j) {
+    const size_t k = base + j;
+    if (st.kind[k] != TTRL_IDM) continue;
+    const int l = st.lane[k];
+    T s, r;
+    lane_local(make_lane<T>(R, l), ((const T*)st.x)[k], ((const T*)st.y)[k], s, r);
+    const bool leaving = R.exit_lane[l] && s >= T(R.length[l]) - T(C.leave_margin);
+    if (leaving || st.route_n[k] < 0) keep[j >> 5] &= ~(1u << (j & 31));
+  }
+  slots_compact<T>(st, base, keep);
+  uint64_t* w = st.rng + (size_t)env * TTRL_RNG_WORDS;
+  Pcg g = rng_load(w);
+  ix_spawn<T>(st, R, P, C, g, base, 0.0, 1.0, 1.0, C.spawn_probability, false);
+  rng_store(g, w);
 }
 
 // ------------------------------------------------------------------- launch helpers
@@ -2277,7 +2577,7 @@ int launch_status() { return hipGetLastError() == hipSuccess ? TTRL_OK : TTRL_E_
 
 template <typename T, int NS, int EPW>
 int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const int32_t* actions,
-               int frames, double dt, int mode, int ablate, hipStream_t stream) {
+               const uint8_t* mask, int frames, double dt, int mode, int ablate, hipStream_t stream) {
   const int blocks = (s.n_envs + EPW - 1) / EPW;
   if (blocks == 0) return TTRL_OK;
   const bool graph = is_graph(R);
@@ -2286,35 +2586,35 @@ int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_par
   for (int l = 0; l < R.n_lanes; ++l) curved |= R.type[l] != TTRL_LANE_STRAIGHT;
   if (graph)
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_GRAPH>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, P,
-                       actions, frames, dt, mode, ablate);
+                       actions, mask, frames, dt, mode, ablate);
   else if (curved)
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_CURVED>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R,
-                       P, actions, frames, dt, mode, ablate);
+                       P, actions, mask, frames, dt, mode, ablate);
   else
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_STRAIGHT>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R,
-                       P, actions, frames, dt, mode, ablate);
+                       P, actions, mask, frames, dt, mode, ablate);
   return launch_status();
 }
 
 template <typename T>
 int dispatch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const int32_t* actions,
-                 int frames, double dt, int mode, int ablate, hipStream_t stream) {
+                 const uint8_t* mask, int frames, double dt, int mode, int ablate, hipStream_t stream) {
   switch (slots_for(s.n_veh)) {
-    case 32: return launch_sim<T, 32, 2>(s, R, P, actions, frames, dt, mode, ablate, stream);
-    case 64: return launch_sim<T, 64, 1>(s, R, P, actions, frames, dt, mode, ablate, stream);
-    case 128: return launch_sim<T, 128, 1>(s, R, P, actions, frames, dt, mode, ablate, stream);
-    default: return launch_sim<T, 256, 1>(s, R, P, actions, frames, dt, mode, ablate, stream);
+    case 32: return launch_sim<T, 32, 2>(s, R, P, actions, mask, frames, dt, mode, ablate, stream);
+    case 64: return launch_sim<T, 64, 1>(s, R, P, actions, mask, frames, dt, mode, ablate, stream);
+    case 128: return launch_sim<T, 128, 1>(s, R, P, actions, mask, frames, dt, mode, ablate, stream);
+    default: return launch_sim<T, 256, 1>(s, R, P, actions, mask, frames, dt, mode, ablate, stream);
   }
 }
 
 int run_sim(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P, const int32_t* actions,
-            int frames, double dt, int mode, void* stream, int ablate = 0) {
+            int frames, double dt, int mode, void* stream, int ablate = 0, const uint8_t* mask = nullptr) {
   int rc = check_state(s, R);
   if (rc) return rc;
   if (!P || frames < 0 || P->n_target_speeds < 1 || P->n_target_speeds > 8) return TTRL_E_ARG;
   hipStream_t st = (hipStream_t)stream;
-  return s->dtype == TTRL_F64 ? dispatch_sim<double>(*s, *R, *P, actions, frames, dt, mode, ablate, st)
-                              : dispatch_sim<float>(*s, *R, *P, actions, frames, dt, mode, ablate, st);
+  return s->dtype == TTRL_F64 ? dispatch_sim<double>(*s, *R, *P, actions, mask, frames, dt, mode, ablate, st)
+                              : dispatch_sim<float>(*s, *R, *P, actions, mask, frames, dt, mode, ablate, st);
 }
 
 template <typename T, int NS, int EPW>
@@ -2340,21 +2640,22 @@ int dispatch_nbr(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_p
 
 template <typename T, int NS, int EPW>
 int launch_kin(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const ttrl_kin_cfg_t& c,
-               float* out, int32_t* ids, hipStream_t stream) {
+               const uint8_t* mask, float* out, int32_t* ids, hipStream_t stream) {
   const int blocks = (s.n_envs + EPW - 1) / EPW;
   if (blocks == 0) return TTRL_OK;
-  hipLaunchKernelGGL((kinematics_obs_kernel<T, NS, EPW>), dim3(blocks), dim3(NS * EPW), 0, stream, s, R, P, c, out, ids);
+  hipLaunchKernelGGL((kinematics_obs_kernel<T, NS, EPW>), dim3(blocks), dim3(NS * EPW), 0, stream, s, R, P, c, mask,
+                     out, ids);
   return launch_status();
 }
 
 template <typename T>
 int dispatch_kin(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const ttrl_kin_cfg_t& c,
-                 float* out, int32_t* ids, hipStream_t st) {
+                 const uint8_t* mask, float* out, int32_t* ids, hipStream_t st) {
   switch (slots_for(s.n_veh)) {
-    case 32: return launch_kin<T, 32, 2>(s, R, P, c, out, ids, st);
-    case 64: return launch_kin<T, 64, 1>(s, R, P, c, out, ids, st);
-    case 128: return launch_kin<T, 128, 1>(s, R, P, c, out, ids, st);
-    default: return launch_kin<T, 256, 1>(s, R, P, c, out, ids, st);
+    case 32: return launch_kin<T, 32, 2>(s, R, P, c, mask, out, ids, st);
+    case 64: return launch_kin<T, 64, 1>(s, R, P, c, mask, out, ids, st);
+    case 128: return launch_kin<T, 128, 1>(s, R, P, c, mask, out, ids, st);
+    default: return launch_kin<T, 256, 1>(s, R, P, c, mask, out, ids, st);
   }
 }
 
@@ -2412,17 +2713,25 @@ int ttrl_neighbours(const ttrl_state_t* s, const ttrl_lane_table_t* road, const 
                               : dispatch_nbr<float>(*s, *road, P, query_lane, front, rear, st);
 }
 
-int ttrl_observe_kinematics(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
-                            const ttrl_kin_cfg_t* cfg, float* out, int32_t* ids, void* stream) {
+int ttrl_observe_kinematics_masked(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                                   const ttrl_kin_cfg_t* cfg, const uint8_t* mask, float* out, int32_t* ids,
+                                   void* stream) {
   int rc = check_state(s, road);
   if (rc) return rc;
   if (!p || !cfg || !out || cfg->vehicles_count < 1 || cfg->n_features < 1 || cfg->n_features > TTRL_N_FEATURES)
     return TTRL_E_ARG;
+  if (cfg->order_shuffled < 0 || cfg->order_shuffled > 2) return TTRL_E_ARG;
+  if (cfg->order_shuffled == 2 && (!s->rng || cfg->vehicles_count - 1 > 64)) return TTRL_E_ARG;
   for (int c = 0; c < cfg->n_features; ++c)
     if (cfg->features[c] < 0 || cfg->features[c] >= TTRL_F_ON_ROAD) return TTRL_E_ARG;
   hipStream_t st = (hipStream_t)stream;
-  return s->dtype == TTRL_F64 ? dispatch_kin<double>(*s, *road, *p, *cfg, out, ids, st)
-                              : dispatch_kin<float>(*s, *road, *p, *cfg, out, ids, st);
+  return s->dtype == TTRL_F64 ? dispatch_kin<double>(*s, *road, *p, *cfg, mask, out, ids, st)
+                              : dispatch_kin<float>(*s, *road, *p, *cfg, mask, out, ids, st);
+}
+
+int ttrl_observe_kinematics(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                            const ttrl_kin_cfg_t* cfg, float* out, int32_t* ids, void* stream) {
+  return ttrl_observe_kinematics_masked(s, road, p, cfg, nullptr, out, ids, stream);
 }
 
 int ttrl_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
@@ -2522,6 +2831,69 @@ int ttrl_seed_pcg64(const uint32_t* entropy, int32_t n_words, uint64_t* state4) 
   SeedSeq::pcg64_seed((const unsigned*)entropy, n_words, o);
   for (int k = 0; k < 4; ++k) state4[k] = o[k];
   return TTRL_OK;
+}
+
+static int check_ix(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* p, const ttrl_ix_cfg_t* c) {
+  int rc = check_state(s, R);
+  if (rc) return rc;
+  if (!p || !c || !s->rng || !s->route_road || !s->route_lane || !s->route_n || !s->yielding || !s->reg_steps)
+    return TTRL_E_ARG;
+  if (p->n_target_speeds < 1 || p->n_target_speeds > 8 || c->n_corners != 4) return TTRL_E_ARG;
+  if (c->initial_vehicle_count < 1 || c->initial_vehicle_count > TTRL_IX_MAX_INIT || c->warmup_frames < 0)
+    return TTRL_E_ARG;
+  if (c->ego_lane < 0 || c->ego_lane >= R->n_lanes || c->ego_destination < -1 || c->ego_destination > 3) return TTRL_E_ARG;
+  for (int k = 0; k < 4; ++k)
+    if (c->entry_lane[k] < 0 || c->entry_lane[k] >= R->n_lanes) return TTRL_E_ARG;
+  for (int r = 0; r < R->n_roads; ++r)
+    if (R->road_from[r] < 0 || R->road_from[r] >= TTRL_MAX_NODES || R->road_to[r] < 0 || R->road_to[r] >= TTRL_MAX_NODES)
+      return TTRL_E_ARG;
+  for (int nd = 0; nd < TTRL_MAX_NODES; ++nd)
+    for (int k = 0; k < 4; ++k) {
+      if (c->path_len[nd][k] > TTRL_ROUTE_MAX - 1) return TTRL_E_ARG;
+      for (int q = 0; q < c->path_len[nd][k]; ++q)
+        if (c->path_road[nd][k][q] < 0 || c->path_road[nd][k][q] >= R->n_roads) return TTRL_E_ARG;
+    }
+  return TTRL_OK;
+}
+
+int ttrl_ix_reset(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                  const ttrl_ix_cfg_t* cfg, const uint32_t* entropy, int32_t n_words, const uint8_t* mask,
+                  void* stream) {
+  int rc = check_ix(s, road, p, cfg);
+  if (rc) return rc;
+  if (!entropy || n_words < 1 || n_words > 64) return TTRL_E_ARG;
+  if (s->n_envs == 0) return TTRL_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int blocks = (s->n_envs + 63) / 64;
+  if (s->dtype == TTRL_F64)
+    hipLaunchKernelGGL(ix_begin_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg,
+                       (const unsigned*)entropy, (int)n_words, mask);
+  else
+    hipLaunchKernelGGL(ix_begin_kernel<float>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg,
+                       (const unsigned*)entropy, (int)n_words, mask);
+  if ((rc = launch_status())) return rc;
+  // _make_vehicles' warm-up: 3 s of Road.act / Road.step with no controlled vehicle yet
+  if ((rc = run_sim(s, road, p, nullptr, cfg->warmup_frames, cfg->warmup_dt, MODE_ACT | MODE_STEP, stream, 0, mask)))
+    return rc;
+  if (s->dtype == TTRL_F64)
+    hipLaunchKernelGGL(ix_finish_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg, mask);
+  else
+    hipLaunchKernelGGL(ix_finish_kernel<float>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg, mask);
+  return launch_status();
+}
+
+int ttrl_ix_clear_spawn(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                        const ttrl_ix_cfg_t* cfg, const uint8_t* mask, void* stream) {
+  int rc = check_ix(s, road, p, cfg);
+  if (rc) return rc;
+  if (s->n_envs == 0) return TTRL_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int blocks = (s->n_envs + 63) / 64;
+  if (s->dtype == TTRL_F64)
+    hipLaunchKernelGGL(ix_clear_spawn_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg, mask);
+  else
+    hipLaunchKernelGGL(ix_clear_spawn_kernel<float>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg, mask);
+  return launch_status();
 }
 
 int ttrl_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_reward_cfg_t* cfg,

@@ -159,7 +159,7 @@ class VecHighwayEnv:
     @property
     def vehicle(self):
         """The controlled vehicles: slot 0 of every env (abstract.py:76-79)."""
-        return {k: v[:, 0] for k, v in self.state.t.items() if v.dim() > 1}
+        return {k: v[:, 0] for k, v in self.state.t.items() if k not in ("reg_steps", "rng")}
 
     def define_spaces(self) -> None:
         """abstract.py:123-130"""

@@ -1,0 +1,405 @@
+"""The intersection scenario (intersection-v0, the reference's training scenario) batched on the GPU.
+
+Mirrors ttrl_env/envs/intersection_env.py:
+  * ``intersection_network()``  <- IntersectionEnv._make_road :141-249 (20 lanes, 12 nodes,
+                                   RegulatedRoad priorities), restated with the same numpy
+                                   float64 expressions so the lane table is bit-identical
+  * ``shortest_path()``         <- RoadNetwork.bfs_paths / shortest_path road.py:159-188
+  * ``ix_cfg()``                <- the scene constants of _make_vehicles :251-318 and
+                                   _spawn_vehicle :320-348
+  * ``VecIntersectionEnv``      <- IntersectionEnv (default_config :17-55, step :135-139,
+                                   _reset :131-133, rewards :60-119) over AbstractEnv
+                                   (abstract.py:188-282), ``num_envs`` envs in lockstep.
+
+Every env keeps its own ``np_random`` (numpy Generator(PCG64)) in HBM: the device kernels draw
+spawns and the observation shuffle from it in the reference's order, so an env seeded ``s``
+replays ``IntersectionEnv.reset(seed=s)`` and its steps (tests/test_ix_env.py).
+"""
+from __future__ import annotations
+
+import copy
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _abi, _lib
+from .action import action_factory
+from .observation import observation_factory
+from .road import BatchedRoad, RoadNetwork
+from .state import BatchState
+
+LANE_WIDTH = 4.0  # AbstractLane.DEFAULT_WIDTH lane.py:20
+
+
+class _Graph:
+    """RoadNetwork.graph insertion order: {from: {to: [lane rows]}} (road.py:21-48)."""
+
+    def __init__(self):
+        self.graph: dict = {}
+
+    def add_lane(self, fr: str, to: str, row, priority: int):
+        self.graph.setdefault(fr, {}).setdefault(to, []).append((list(row), int(priority)))
+
+
+def intersection_network(regulation_frequency: int = 2, speed_limit: float = 10.0) -> RoadNetwork:
+    """IntersectionEnv._make_road (intersection_env.py:141-249): the 4-way crossing, horizontal
+    road with right of way; lanes_list() order, node ids in graph order."""
+    lane_width = LANE_WIDTH
+    right_turn_radius = lane_width + 5
+    left_turn_radius = right_turn_radius + lane_width
+    outer_distance = right_turn_radius + lane_width / 2
+    access_length = 50 + 50
+    g = _Graph()
+    straight = lambda s, e: [_abi.LANE_STRAIGHT, s[0], s[1], e[0], e[1], lane_width, speed_limit,  # noqa: E731
+                             0, 0, 0, 0, 0, 0, 0, 0, 0]
+    circular = lambda c, r, a0, a1, cw: [_abi.LANE_CIRCULAR, 0, 0, 0, 0, lane_width, speed_limit,  # noqa: E731
+                                         0, 0, 0, c[0], c[1], r, a0, a1, 1.0 if cw else 0.0]
+    for corner in range(4):
+        angle = np.radians(90 * corner)
+        is_horizontal = corner % 2
+        priority = 3 if is_horizontal else 1
+        rotation = np.array([[np.cos(angle), -np.sin(angle)], [np.sin(angle), np.cos(angle)]])
+        start = rotation @ np.array([lane_width / 2, access_length + outer_distance])
+        end = rotation @ np.array([lane_width / 2, outer_distance])
+        g.add_lane("o" + str(corner), "ir" + str(corner), straight(start, end), priority)
+        r_center = rotation @ (np.array([outer_distance, outer_distance]))
+        g.add_lane("ir" + str(corner), "il" + str((corner - 1) % 4),
+                   circular(r_center, right_turn_radius, angle + np.radians(180), angle + np.radians(270), True),
+                   priority)
+        l_center = rotation @ (np.array([-left_turn_radius + lane_width / 2, left_turn_radius - lane_width / 2]))
+        g.add_lane("ir" + str(corner), "il" + str((corner + 1) % 4),
+                   circular(l_center, left_turn_radius, angle + np.radians(0), angle + np.radians(-90), False),
+                   priority - 1)
+        start = rotation @ np.array([lane_width / 2, outer_distance])
+        end = rotation @ np.array([lane_width / 2, -outer_distance])
+        g.add_lane("ir" + str(corner), "il" + str((corner + 2) % 4), straight(start, end), priority)
+        start = rotation @ np.flip([lane_width / 2, access_length + outer_distance], axis=0)
+        end = rotation @ np.flip([lane_width / 2, outer_distance], axis=0)
+        g.add_lane("il" + str((corner - 1) % 4), "o" + str((corner - 1) % 4), straight(end, start), priority)
+    return network_from_graph(g.graph, regulation_frequency)
+
+
+def network_from_graph(graph: dict, regulation_frequency: int = 0) -> RoadNetwork:
+    """Flatten a {from: {to: [(geometry row, priority)]}} graph into a lane table with topology."""
+    nodes, roads, rows, net = [], [], [], []
+    for fr, tos in graph.items():
+        if fr not in nodes:
+            nodes.append(fr)
+        for to, lanes in tos.items():
+            if to not in nodes:
+                nodes.append(to)
+            r = len(roads)
+            roads.append((fr, to))
+            for i, (row, prio) in enumerate(lanes):
+                rows.append(row)
+                net.append([r, nodes.index(fr), nodes.index(to), prio, int("il" in fr and "o" in to), i])
+    if len(nodes) > _abi.MAX_NODES:
+        raise ValueError(f"at most {_abi.MAX_NODES} nodes")
+    table = _abi.set_network(_abi.lane_table_from_arrays(np.array(rows, dtype=np.float64)),
+                             np.array(net), regulation_frequency=regulation_frequency)
+    network = RoadNetwork(table)
+    network.nodes, network.roads = nodes, roads
+    network.graph = {fr: {to: [k for k, (f, t) in enumerate(roads) if (f, t) == (fr, to)] for to in tos}
+                     for fr, tos in graph.items()}
+    network.lane_rows = np.array(rows, dtype=np.float64)
+    network.lane_net = np.array(net, dtype=np.int32)
+    return network
+
+
+def shortest_path(network: RoadNetwork, start: str, goal: str) -> list:
+    """RoadNetwork.shortest_path = next(bfs_paths(start, goal), []) (road.py:159-188)."""
+    graph = network.graph
+    queue = [(start, [start])]
+    while queue:
+        node, path = queue.pop(0)
+        if node not in graph:
+            return []
+        for nxt in sorted([k for k in graph[node].keys() if k not in path]):
+            if nxt == goal:
+                return path + [nxt]
+            if nxt in graph:
+                queue.append((nxt, path + [nxt]))
+    return []
+
+
+def ix_cfg(network: RoadNetwork, config: dict, params: _abi.Params) -> _abi.IxCfg:
+    """Scene constants of IntersectionEnv._make_vehicles / _spawn_vehicle for the device."""
+    c = _abi.IxCfg()
+    n = int(config["initial_vehicle_count"])
+    if not 1 <= n <= _abi.IX_MAX_INIT:
+        raise ValueError(f"initial_vehicle_count must be in [1, {_abi.IX_MAX_INIT}]")
+    c.initial_vehicle_count = n
+    freq = int(config["simulation_frequency"])
+    c.warmup_frames = 3 * freq                      # simulation_steps = 3 (intersection_env.py:264)
+    c.warmup_dt = 1 / freq
+    for t, v in enumerate(np.linspace(0, 80, n)):
+        c.init_longitudinal[t] = float(v)
+    c.spawn_probability = float(config["spawn_probability"])
+    c.spawn_offset, c.spawn_speed, c.spawn_clear_distance = 5.0, 8.0, 15.0
+    c.challenger_longitudinal, c.challenger_position_deviation, c.challenger_speed_deviation = 60.0, 0.1, 0.0
+    c.delta_lo, c.delta_hi = 3.5, 4.5               # IDMVehicle.DELTA_RANGE behavior.py:39
+    c.n_corners = 4
+    nodes, roads = network.nodes, network.roads
+    lane_of = {}
+    for l in range(network.table.n_lanes):
+        fr, to = roads[network.table.road[l]]
+        lane_of[(fr, to, network.table.lane_id[l])] = l
+    for k in range(4):
+        c.entry_lane[k] = lane_of[(f"o{k}", f"ir{k}", 0)]
+        c.exit_node[k] = nodes.index(f"o{k}")
+    c.ego_lane = lane_of[("o0", "ir0", 0)]          # controlled_vehicles = 1: ego_id 0
+    dest = config["destination"]
+    c.ego_destination = -1 if not dest else int(str(dest)[1:])
+    c.ego_longitudinal, c.ego_deviation, c.ego_heading_s = 60.0, 5.0, 60.0
+    c.ego_speed = float(network.table.speed_limit[c.ego_lane])
+    c.ego_clear_distance = 20.0
+    c.leave_margin = 4 * params.length
+    # routes the scene can plan: a spawn at corner r0 heads for another corner (choice without
+    # replacement), the ego from its lane to the destination; a longer BFS path (a U-turn, 4
+    # roads) would not fit ROUTE_MAX and is marked -1
+    for i, node in enumerate(nodes):
+        for k in range(4):
+            path = shortest_path(network, node, f"o{k}")
+            rds = [roads.index((path[q], path[q + 1])) for q in range(len(path) - 1)]
+            fits = len(rds) <= _abi.ROUTE_MAX - 1
+            c.path_len[i][k] = len(rds) if fits else -1
+            for q in range(_abi.ROUTE_MAX - 1):
+                c.path_road[i][k][q] = rds[q] if fits and q < len(rds) else -1
+    ego_node = nodes.index(roads[network.table.road[c.ego_lane]][1])
+    for k in ([c.ego_destination] if c.ego_destination >= 0 else [1, 2, 3]):
+        if c.path_len[ego_node][k] < 0:
+            raise ValueError(f"destination o{k}: the route exceeds ROUTE_MAX = {_abi.ROUTE_MAX}")
+    return c
+
+
+def _stream(device):
+    if device.type != "cuda":
+        raise RuntimeError("the intersection env runs on a HIP device only (no CPU fallback)")
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ix_reset(state: BatchState, network: RoadNetwork, params: _abi.Params, cfg: _abi.IxCfg,
+             entropy: torch.Tensor, mask: torch.Tensor | None = None) -> None:
+    """IntersectionEnv.reset on the device: env e replays ``default_rng(list(entropy[e]))``."""
+    if entropy.dim() != 2 or entropy.shape[0] != state.n_envs or entropy.dtype != torch.int32:
+        raise ValueError("entropy must be an int32 [n_envs, n_words] tensor of uint32 words")
+    entropy = entropy.to(state.device).contiguous()
+    m = None if mask is None else mask.to(device=state.device, dtype=torch.uint8).contiguous()
+    _lib.call("ttrl_ix_reset", C.byref(state.struct()), C.byref(network.table), C.byref(params), C.byref(cfg),
+              entropy.data_ptr(), int(entropy.shape[1]), None if m is None else m.data_ptr(), _stream(state.device))
+
+
+def ix_clear_spawn(state: BatchState, network: RoadNetwork, params: _abi.Params, cfg: _abi.IxCfg,
+                   mask: torch.Tensor | None = None) -> None:
+    """IntersectionEnv.step tail: _clear_vehicles then _spawn_vehicle, on the device."""
+    m = None if mask is None else mask.to(device=state.device, dtype=torch.uint8).contiguous()
+    _lib.call("ttrl_ix_clear_spawn", C.byref(state.struct()), C.byref(network.table), C.byref(params), C.byref(cfg),
+              None if m is None else m.data_ptr(), _stream(state.device))
+
+
+def seed_words(seeds) -> np.ndarray:
+    """SeedSequence entropy words of int seeds (numpy splits an int into uint32 words, low first)."""
+    out = []
+    for s in seeds:
+        s = int(s)
+        if s < 0:
+            raise ValueError("seeds must be non-negative")
+        w = []
+        while True:
+            w.append(s & 0xFFFFFFFF)
+            s >>= 32
+            if s == 0:
+                break
+        out.append(w)
+    width = max(len(w) for w in out)
+    if any(len(w) != width for w in out):
+        raise ValueError("all seeds of a batch must have the same number of 32-bit words")
+    return np.array(out, dtype=np.uint32)
+
+
+class VecIntersectionEnv:
+    """``num_envs`` intersection-v0 envs; the controlled vehicle of each env is its MDPVehicle."""
+
+    metadata = {"render_modes": []}
+    PERCEPTION_DISTANCE = 5.0 * 40.0  # abstract.py:41
+    SHUFFLE_RNG = "np_random"         # order="shuffled" draws from each env's np_random
+    ACTIONS = {0: "SLOWER", 1: "IDLE", 2: "FASTER"}
+
+    def __init__(self, config: dict | None = None, render_mode: str | None = None) -> None:
+        if render_mode is not None:
+            raise NotImplementedError("rendering is out of scope (SURVEY.md §2)")
+        self.config = self.default_config()
+        self.configure(config)
+        self.road = None
+        self.observation_type = self.action_type = None
+        self.time = None
+        self.steps = 0
+        self.done = False
+        self._build()
+        self.reset()
+
+    @classmethod
+    def default_config(cls) -> dict:
+        """AbstractEnv.default_config (abstract.py:86-109) + IntersectionEnv.default_config
+        (intersection_env.py:17-55) + batching keys."""
+        return {
+            "observation": {"type": "Kinematics", "vehicles_count": 15,
+                            "features": ["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"],
+                            "features_range": {"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]},
+                            "absolute": True, "flatten": False, "observe_intentions": False},
+            "action": {"type": "DiscreteMetaAction", "longitudinal": True, "lateral": False,
+                       "target_speeds": [0, 4.5, 9]},
+            "simulation_frequency": 15,
+            "policy_frequency": 1,
+            "other_vehicles_type": "ttrl_env.vehicle.behavior.IDMVehicle",
+            "duration": 13,
+            "destination": "o1",
+            "controlled_vehicles": 1,
+            "initial_vehicle_count": 10,
+            "spawn_probability": 0.6,
+            "collision_reward": -5,
+            "high_speed_reward": 1,
+            "arrived_reward": 1,
+            "reward_speed_range": [7.0, 9.0],
+            "normalize_reward": False,
+            "offroad_terminal": False,
+            "manual_control": False,
+            # batching
+            "num_envs": 1,
+            "vehicle_slots": 32,       # padded row width; the scene holds ~10-20 vehicles
+            "env_id_offset": 0,
+            "device": "cuda",
+            "dtype": "f64",
+            "auto_reset": False,
+        }
+
+    def configure(self, config: dict | None) -> None:
+        if config:
+            self.config.update(config)
+
+    def _build(self):
+        c = self.config
+        if c["other_vehicles_type"] != "ttrl_env.vehicle.behavior.IDMVehicle":
+            raise NotImplementedError("only IDMVehicle traffic is on the hot path (SURVEY.md §2)")
+        if int(c["controlled_vehicles"]) != 1:
+            raise NotImplementedError("MultiAgentIntersectionEnv (controlled_vehicles > 1) is out of scope")
+        self.num_envs = int(c["num_envs"])
+        self.device = torch.device(c["device"])
+        self.network = intersection_network()
+        # _make_vehicles mutates the IDM class constants (intersection_env.py:258-261)
+        self.params = _abi.default_params(target_speeds=c["action"].get("target_speeds", [0, 4.5, 9]),
+                                          distance_wanted=7.0, comfort_acc_max=6.0, comfort_acc_min=-3.0)
+        self.state = BatchState(self.num_envs, int(c["vehicle_slots"]), device=self.device, dtype=c["dtype"])
+        self.road = BatchedRoad(self.network, self.state, self.params)
+        self.ix = ix_cfg(self.network, c, self.params)
+        self.reward_cfg = _abi.reward_cfg(c["collision_reward"], c["high_speed_reward"], c["reward_speed_range"],
+                                          c["normalize_reward"], c["offroad_terminal"], c["duration"],
+                                          arrived_reward=c["arrived_reward"])
+        self.time = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
+        self._reward = torch.zeros(self.num_envs, dtype=torch.float32, device=self.device)
+        self._term = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
+        self._trunc = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
+        self._entropy = None  # [E, words + 1]: seed words, then the auto-reset episode counter
+        self.define_spaces()
+
+    def define_spaces(self) -> None:
+        """abstract.py:123-130"""
+        self.observation_type = observation_factory(self, self.config["observation"])
+        self.action_type = action_factory(self, self.config["action"])
+        self.observation_space = self.observation_type.space()
+        self.action_space = self.action_type.space()
+
+    def _seeds(self, seed):
+        if seed is None:
+            seed = int(np.random.SeedSequence().generate_state(1)[0])
+        if isinstance(seed, (list, tuple, np.ndarray, torch.Tensor)):
+            s = [int(v) for v in (seed.tolist() if hasattr(seed, "tolist") else seed)]
+            if len(s) != self.num_envs:
+                raise ValueError("per-env seeds must have num_envs entries")
+            return s
+        base = int(seed) + int(self.config["env_id_offset"])
+        return [base + e for e in range(self.num_envs)]
+
+    def reset(self, *, seed=None, options: dict | None = None):
+        """AbstractEnv.reset (abstract.py:188-214) + IntersectionEnv._reset: env e is
+        ``IntersectionEnv.reset(seed=seed + env_id_offset + e)``."""
+        if options and "config" in options:
+            self.configure(options["config"])
+            self._build()
+        words = seed_words(self._seeds(seed))
+        self._entropy = torch.from_numpy(np.concatenate([words, np.zeros((len(words), 1), np.uint32)], 1)
+                                         .view(np.int32)).to(self.device)
+        self.time.zero_()
+        self.steps = 0
+        self.done = False
+        ix_reset(self.state, self.network, self.params, self.ix, self._entropy[:, :-1])
+        obs = self.observation_type.observe()
+        return obs, self._info(obs, None)
+
+    def step(self, action):
+        """IntersectionEnv.step (intersection_env.py:135-139) over AbstractEnv.step (abstract.py:224-250)."""
+        if self.road is None:
+            raise NotImplementedError("The road and vehicle must be initialized in the environment implementation")
+        self.time += 1 / self.config["policy_frequency"]
+        self._simulate(action)
+        obs = self.observation_type.observe()
+        reward, terminated, truncated = self._rewards_and_dones()
+        info = self._info(obs, action)
+        ix_clear_spawn(self.state, self.network, self.params, self.ix)
+        if self.config["auto_reset"]:
+            done = terminated | truncated
+            info["final_observation"], info["final_mask"] = obs, done
+            obs = obs.clone()
+            self._auto_reset(done, obs)
+        return obs, reward, terminated, truncated, info
+
+    def _simulate(self, action=None) -> None:
+        frames = int(self.config["simulation_frequency"] // self.config["policy_frequency"])
+        codes = None
+        if action is not None and not self.config["manual_control"]:
+            codes = self.action_type._codes(action)
+        self.road.simulate(codes, frames, 1 / self.config["simulation_frequency"])
+        self.steps += frames
+
+    def _rewards_and_dones(self):
+        _lib.call("ttrl_rewards", C.byref(self.state.struct()), C.byref(self.network.table), C.byref(self.reward_cfg),
+                  self.time.data_ptr(), self._reward.data_ptr(), self._term.data_ptr(), self._trunc.data_ptr(),
+                  _stream(self.device))
+        return self._reward.clone(), self._term.bool(), self._trunc.bool()
+
+    def _ego(self, field: str) -> torch.Tensor:
+        """Per-env value of the controlled vehicle (the env's first MDP slot)."""
+        kind = self.state["kind"]
+        slot = (kind == _abi.MDP).to(torch.int8).argmax(dim=1, keepdim=True)
+        return self.state[field].gather(1, slot).squeeze(1)
+
+    def _info(self, obs, action) -> dict:
+        """abstract.py:169-186 batched: device tensors [E]."""
+        return {"speed": self._ego("speed").clone(), "crashed": self._ego("crashed").bool(), "action": action}
+
+    def _auto_reset(self, done: torch.Tensor, obs: torch.Tensor) -> None:
+        """Finished envs restart on the device with default_rng([seed words..., episode]) and
+        their first observation is written into ``obs``; the others are untouched."""
+        d = done.to(torch.int32)
+        self._entropy[:, -1] += d
+        ix_reset(self.state, self.network, self.params, self.ix, self._entropy, d)
+        self.time.masked_fill_(done, 0.0)
+        self.observation_type.observe(mask=d, out=obs)
+
+    def get_available_actions(self):
+        return self.action_type.get_available_actions()
+
+    def close(self) -> None:
+        self.done = True
+
+    def render(self):
+        raise NotImplementedError("rendering is out of scope (SURVEY.md §2)")
+
+    def __deepcopy__(self, memo):
+        new = copy.copy(self)
+        new.state = self.state.clone()
+        new.road = BatchedRoad(self.network, new.state, self.params)
+        new.time = self.time.clone()
+        new.define_spaces()
+        return new

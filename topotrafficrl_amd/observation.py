@@ -25,15 +25,25 @@ def _stream(device):
     return torch.cuda.current_stream(device).cuda_stream
 
 
-def kinematics(state, network, params, cfg: _abi.KinCfg, out=None, ids=None):
-    """KinematicObservation.observe for every env: ([E, V, F] float32, [E, V-1] int32 slot ids)."""
+def kinematics(state, network, params, cfg: _abi.KinCfg, out=None, ids=None, mask=None):
+    """KinematicObservation.observe for every env: ([E, V, F] float32, [E, V-1] int32 slot ids).
+    ``mask`` (uint8/bool [E]): only those envs are observed (their np_random advanced); the other
+    rows of ``out`` / ``ids`` are left as they were."""
     E, V, F = state.n_envs, cfg.vehicles_count, cfg.n_features
     if out is None:
         out = torch.empty((E, V, F), dtype=torch.float32, device=state.device)
     if ids is None:
         ids = torch.empty((E, max(V - 1, 1)), dtype=torch.int32, device=state.device)
-    _lib.call("ttrl_observe_kinematics", C.byref(state.struct()), C.byref(network.table), C.byref(params),
-              C.byref(cfg), out.data_ptr(), ids.data_ptr(), _stream(state.device))
+    m = None
+    if mask is not None:
+        m = mask.to(device=state.device, dtype=torch.uint8).contiguous()
+        if m.numel() != E:
+            raise ValueError("mask must have one entry per env")
+    if cfg.order_shuffled == 2 and state["rng"] is None:
+        raise ValueError("np_random-shuffled observation needs the state's rng")
+    _lib.call("ttrl_observe_kinematics_masked", C.byref(state.struct()), C.byref(network.table), C.byref(params),
+              C.byref(cfg), None if m is None else m.data_ptr(), out.data_ptr(), ids.data_ptr(),
+              _stream(state.device))
     return out, ids
 
 
@@ -89,8 +99,11 @@ class BatchedKinematicObservation(BatchedObservationType):
         self.features_range = features_range
         self.absolute, self.order, self.normalize, self.clip = absolute, order, normalize, clip
         self.see_behind, self.observe_intentions = see_behind, observe_intentions
+        # the env's np_random drives the shuffle where the env keeps one on the device
+        # (IntersectionEnv); elsewhere a counter-based Philox stream (seed, call count)
         self.cfg = _abi.kin_cfg(self.features, vehicles_count, features_range, absolute, order, normalize, clip,
-                                see_behind, lanes_on_road=env.road.network.lanes_count)
+                                see_behind, lanes_on_road=env.road.network.lanes_count,
+                                shuffle_rng=getattr(env, "SHUFFLE_RNG", "philox"))
         self._out = self._ids = None
         self._calls = 0
 
@@ -98,15 +111,16 @@ class BatchedKinematicObservation(BatchedObservationType):
         return Box(low=-float("inf"), high=float("inf"), shape=(self.vehicles_count, len(self.features)),
                    dtype="float32")
 
-    def observe(self) -> torch.Tensor:
+    def observe(self, mask: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+        """``mask``: re-observe only these envs into ``out`` (masked auto-reset)."""
         road = self.env.road
-        if self.order == "shuffled":
+        if self.order == "shuffled" and self.cfg.order_shuffled == 1:
             self.cfg.shuffle_seed = int(self.env.shuffle_seed)
             self.cfg.shuffle_offset = self._calls
         self._calls += 1
         # a fresh output per call (the caching allocator makes it free): like the reference's
         # df.values.copy(), a returned observation is never overwritten by a later step
-        self._out, self._ids = kinematics(road.state, road.network, road.params, self.cfg)
+        self._out, self._ids = kinematics(road.state, road.network, road.params, self.cfg, out=out, mask=mask)
         return self._out
 
     @property

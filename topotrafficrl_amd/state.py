@@ -14,6 +14,7 @@ The per-vehicle attributes of the reference objects map to fields as follows:
     crashed, enable_lane_change -> crashed, lane_change
     route (list of lane indexes | None) -> route_road, route_lane [.., ROUTE_MAX], route_n
     RegulatedRoad is_yielding / steps   -> yielding, reg_steps [n_envs]
+    AbstractEnv.np_random (numpy Generator(PCG64)) -> rng [n_envs, 5] (uint64 words as int64)
 """
 from __future__ import annotations
 
@@ -48,6 +49,8 @@ class BatchState:
         self.t["route_n"] = torch.full(shape, -1, dtype=torch.int8, device=self.device)
         self.t["yielding"] = torch.zeros(shape, dtype=torch.uint8, device=self.device)
         self.t["reg_steps"] = torch.zeros(self.n_envs, dtype=torch.int32, device=self.device)
+        # AbstractEnv.np_random of each env (numpy Generator(PCG64) words, see _abi.RNG_WORDS)
+        self.t["rng"] = torch.zeros((self.n_envs, _abi.RNG_WORDS), dtype=torch.int64, device=self.device)
         self._struct = None
 
     def __getitem__(self, k: str) -> torch.Tensor:
@@ -69,11 +72,16 @@ class BatchState:
     def load_numpy(self, arrays: dict) -> "BatchState":
         """Copy host arrays (e.g. oracle.HostState.a) into the device tensors."""
         for k, v in self.t.items():
-            v.copy_(torch.as_tensor(np.ascontiguousarray(arrays[k])).to(v.dtype))
+            a = np.ascontiguousarray(arrays[k])
+            if a.dtype == np.uint64:
+                a = a.view(np.int64)
+            v.copy_(torch.as_tensor(a).to(v.dtype))
         return self
 
     def to_numpy(self) -> dict:
-        return {k: v.cpu().numpy() for k, v in self.t.items()}
+        out = {k: v.cpu().numpy() for k, v in self.t.items()}
+        out["rng"] = out["rng"].view(np.uint64)
+        return out
 
     def clone(self) -> "BatchState":
         b = BatchState.__new__(BatchState)
