@@ -845,8 +845,12 @@ int oracle_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* R, const
   double* grid = (double*)malloc(sizeof(double) * F * W * H);
 #pragma omp for schedule(static)
   for (int e = 0; e < o.E; ++e) {
-    int base = e * o.N, ego = base;
+    int base = e * o.N, ei = ego_of(&o, base), ego = base + ei;
     for (int q = 0; q < F * W * H; ++q) grid[q] = NAN;
+    if (ei < 0) {
+      for (int q = 0; q < F * W * H; ++q) out[(size_t)e * F * W * H + q] = 0.0f;
+      continue;
+    }
     for (int c = 0; c < F; ++c) {
       int f = cfg->features[c];
       if (f == TTRL_F_ON_ROAD) {
@@ -1262,14 +1266,18 @@ int oracle_observe_lidar(const ttrl_state_t* s, const ttrl_lane_table_t* R, cons
   const double range = cfg->maximum_range, step = 2 * PI / C;
 #pragma omp parallel for schedule(static)
   for (int e = 0; e < o.E; ++e) {
-    const int base = e * o.N, ego = base;
+    const int base = e * o.N, ei = ego_of(&o, base), ego = base + ei;
     double grid[64][2];
     for (int c = 0; c < C; ++c) grid[c][0] = grid[c][1] = range;
+    if (ei < 0) {
+      for (int c = 0; c < C; ++c) out[(size_t)e * C * 2 + 2 * c] = out[(size_t)e * C * 2 + 2 * c + 1] = (float)(cfg->normalize ? 1.0 : range);
+      continue;
+    }
     const double ox = o.x[ego], oy = o.y[ego];
     const double ovx = o.v[ego] * cos(o.h[ego]), ovy = o.v[ego] * sin(o.h[ego]);
-    for (int j = 1; j < o.N; ++j) {
+    for (int j = 0; j < o.N; ++j) {
       const int k = base + j;
-      if (o.kind[k] == TTRL_ABSENT) continue;
+      if (j == ei || o.kind[k] == TTRL_ABSENT) continue;
       const double dx = o.x[k] - ox, dy = o.y[k] - oy;
       const double center_distance = sqrt(dx * dx + dy * dy);
       if (center_distance > range) continue;

@@ -107,3 +107,26 @@ def test_f32_episode_runs(hip_device):
     torch.cuda.synchronize()
     assert torch.isfinite(obs).all() and torch.isfinite(rew).all()
     assert bool(trunc.all())
+
+
+def test_grid_and_lidar_observe_the_intersection_ego(hip_device):
+    """OccupancyGrid (env_grid_dense.json) and Lidar of the intersection ego, which sits after the
+    traffic in the vehicle list, on every golden step state: device == oracle."""
+    from observation_helpers import batch_of_ix_states
+    from topotrafficrl_amd.observation import lidar, occupancy_grid
+    from topotrafficrl_amd.road import BatchedRoad
+    from topotrafficrl_amd.state import BatchState
+    h = batch_of_ix_states(GOLD)
+    net = intersection_network()
+    o = Oracle(net.table, P_IX)
+    st = BatchState(h.E, h.N, device=hip_device).load_numpy(h.a)
+    grid = _abi.grid_cfg(["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"], [[-32, 32], [-32, 32]], [2, 2],
+                         {"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]})
+    got = occupancy_grid(st, net, P_IX, grid).cpu().numpy()
+    want = o.observe_grid(h, grid)
+    assert np.max(np.abs(got - want)) <= 1e-6
+    lc = _abi.lidar_cfg()
+    got = lidar(st, net, P_IX, lc).cpu().numpy()
+    want = o.observe_lidar(h, lc)
+    assert np.max(np.abs(got - want)) <= 1e-6
+    BatchedRoad(net, st, P_IX)  # the network table is a valid BatchedRoad network

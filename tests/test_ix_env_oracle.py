@@ -125,3 +125,37 @@ def test_ix_batch_and_mask():
     for e in range(6):
         changed = any(not np.array_equal(big.a[k][e], before.a[k][e]) for k in big.a)
         assert changed == bool(mask[e]), e
+
+
+def test_grid_and_lidar_follow_the_ego_slot():
+    """The observer is the env's first MDP slot: moving the ego to slot 0 of a copy (and the
+    vehicle it displaced to the ego's old slot) leaves the grid and the Lidar unchanged."""
+    from observation_helpers import batch_of_ix_states
+    golds = [load_golden(p) for p in golden_files("ix_*")]
+    h = batch_of_ix_states(golds)
+    net = intersection_network()
+    o = Oracle(net.table, P_IX)
+    grid = _abi.grid_cfg(["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"], [[-32, 32], [-32, 32]], [2, 2],
+                         {"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]})
+    lc = _abi.lidar_cfg()
+    g0, l0 = o.observe_grid(h, grid), o.observe_lidar(h, lc)
+    sw = h.copy()
+    for e in range(h.E):
+        i = int(np.argmax(h["kind"][e] == _abi.MDP))
+        for k, v in sw.a.items():
+            if k not in ("reg_steps", "rng"):
+                v[e, [0, i]] = v[e, [i, 0]]
+    g1, l1 = o.observe_grid(sw, grid), o.observe_lidar(sw, lc)
+    assert np.array_equal(l0, l1)
+    # the grid's lowest-index-wins rule may pick another vehicle in a shared cell: compare the
+    # cells where at most the ego is involved
+    assert np.mean(g0 == g1) > 0.99
+    assert np.any(g0[:, 0] != 0)
+
+
+def test_make_and_register():
+    from topotrafficrl_amd.envs import ENV_IDS, make, register
+    assert "ttrl-intersection-batched-v0" in ENV_IDS
+    with pytest.raises(KeyError):
+        make("merge-v0")
+    assert register() in (True, False)

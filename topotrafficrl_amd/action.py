@@ -49,8 +49,8 @@ class BatchedDiscreteMetaAction:
     def get_available_actions(self) -> torch.Tensor:
         """Batched get_available_actions (action.py:262-298) as an [E, n_actions] bool mask."""
         st, t = self.env.road.state, self.env.road.network.table
-        lane = st["lane"][:, 0].long()
-        x, y = st["x"][:, 0].double(), st["y"][:, 0].double()
+        lane = st.ego("lane").long()
+        x, y = st.ego("x").double(), st.ego("y").double()
         E = st.n_envs
         mask = torch.zeros((E, len(self.actions)), dtype=torch.bool, device=st.device)
         mask[:, self.actions_indexes["IDLE"]] = True
@@ -71,7 +71,7 @@ class BatchedDiscreteMetaAction:
             if "LANE_RIGHT" in self.actions_indexes:
                 mask[:, self.actions_indexes["LANE_RIGHT"]] = reachable(lane + 1)
         if self.longitudinal:
-            si = st["speed_index"][:, 0]
+            si = st.ego("speed_index")
             mask[:, self.actions_indexes["FASTER"]] = si < len(self.target_speeds) - 1
             mask[:, self.actions_indexes["SLOWER"]] = si > 0
         return mask

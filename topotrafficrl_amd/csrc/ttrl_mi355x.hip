@@ -1899,12 +1899,23 @@ grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid
   unsigned* s_road = (unsigned*)(s_win + C);       // [ceil(C/32)] on_road bitmap
   float* s_val = (float*)(s_road + ((C + 31) / 32));  // [F][N] clipped feature values
   const size_t k0 = (size_t)env * N;
+  __shared__ int s_ego;  // the observer: the env's first MDP slot (AbstractEnv.vehicle)
+  if (tid == 0) {
+    int e = 0;
+    while (e < N && st.kind[k0 + e] != TTRL_MDP) ++e;
+    s_ego = e;
+  }
   for (int c = tid; c < C; c += blockDim.x) s_win[c] = 0x7fffffff;
   for (int c = tid; c < (C + 31) / 32; c += blockDim.x) s_road[c] = 0u;
-  const T ex = ((const T*)st.x)[k0], ey = ((const T*)st.y)[k0], eh = ((const T*)st.heading)[k0];
-  const T ev = ((const T*)st.speed)[k0];
-  const int elane = st.lane[k0];
   __syncthreads();
+  if (s_ego >= N) {  // no controlled vehicle: an all-zero grid
+    for (int q = tid; q < F * C; q += blockDim.x) out[(size_t)env * F * C + q] = 0.f;
+    return;
+  }
+  const size_t ke = k0 + s_ego;
+  const T ex = ((const T*)st.x)[ke], ey = ((const T*)st.y)[ke], eh = ((const T*)st.heading)[ke];
+  const T ev = ((const T*)st.speed)[ke];
+  const int elane = st.lane[ke];
   bool has_road = false;
   for (int c = 0; c < F; ++c) has_road |= cfg.features[c] == TTRL_F_ON_ROAD;
   const T rx0 = T(cfg.range_lo[TTRL_F_X]), rx1 = T(cfg.range_hi[TTRL_F_X]);
@@ -2094,17 +2105,33 @@ __global__ void __launch_bounds__(64) lidar_obs_kernel(ttrl_state_t st, ttrl_par
   const T step = T(2) * Tpi<T>() / T(C);
   if (tid < C) { key[tid] = ordered_bits(range); ord[tid] = -1; dist[tid] = range; vel[tid] = range; }
   __syncthreads();
+  __shared__ int s_ego;  // the observer: the env's first MDP slot
+  if (tid == 0) {
+    int e = 0;
+    while (e < N && st.kind[base + e] != TTRL_MDP) ++e;
+    s_ego = e;
+  }
+  __syncthreads();
+  const int ego = s_ego;
+  if (ego >= N) {  // no controlled vehicle: maximum range everywhere
+    for (int c = tid; c < C; c += 64) {
+      out[((size_t)env * C + c) * 2] = (float)(cfg.normalize ? 1.0 : range);
+      out[((size_t)env * C + c) * 2 + 1] = (float)(cfg.normalize ? 1.0 : range);
+    }
+    return;
+  }
   const T* X = (const T*)st.x; const T* Y = (const T*)st.y; const T* H = (const T*)st.heading;
   const T* Vv = (const T*)st.speed;
-  const T ox = X[base], oy = Y[base];
-  const T ovx = Vv[base] * t_cos(H[base]), ovy = Vv[base] * t_sin(H[base]);
+  const size_t ke = base + ego;
+  const T ox = X[ke], oy = Y[ke];
+  const T ovx = Vv[ke] * t_cos(H[ke]), ovy = Vv[ke] * t_sin(H[ke]);
   auto to_index = [&](T a) {  // int(floor(a / step)) % cells, Python modulo
     long k = (long)floor(a / step) % C;
     return (int)(k < 0 ? k + C : k);
   };
   for (int pass = 0; pass < 3; ++pass) {
-    for (int j = 1 + tid; j < N; j += 64) {
-      if (st.kind[base + j] == TTRL_ABSENT) continue;
+    for (int j = tid; j < N; j += 64) {
+      if (j == ego || st.kind[base + j] == TTRL_ABSENT) continue;
       const T dx = X[base + j] - ox, dy = Y[base + j] - oy;
       const T center_distance = sqrt(dx * dx + dy * dy);
       if (center_distance > T(range)) continue;

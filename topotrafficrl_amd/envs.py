@@ -261,11 +261,30 @@ class VecHighwayEnv:
         return new
 
 
-def register(env_id: str = "ttrl-highway-batched-v0") -> bool:
-    """gymnasium.register(id, entry_point) as ttrl_env/__init__.py:28-56 does; no-op without gymnasium."""
+ENV_IDS = {"ttrl-highway-batched-v0": "topotrafficrl_amd.envs:VecHighwayEnv",
+           "ttrl-intersection-batched-v0": "topotrafficrl_amd.intersection:VecIntersectionEnv"}
+
+
+def register(env_id: str | None = None) -> bool:
+    """gymnasium.register(id, entry_point) as ttrl_env/__init__.py:28-56 does (intersection-v0 ->
+    ttrl-intersection-batched-v0); no-op without gymnasium."""
     try:
         import gymnasium
     except ImportError:
         return False
-    gymnasium.register(id=env_id, entry_point="topotrafficrl_amd.envs:VecHighwayEnv")
+    for i, entry in ENV_IDS.items():
+        if env_id is None or i == env_id:
+            gymnasium.register(id=i, entry_point=entry)
     return True
+
+
+def make(env_id: str, config: dict | None = None, **kwargs):
+    """gym.make(id) + env.unwrapped.configure(config) (scripts/utils factory.py:72-91) without
+    gymnasium: the batched env of ``env_id`` ("intersection-v0" / "highway-v0" map to ours)."""
+    aliases = {"intersection-v0": "ttrl-intersection-batched-v0", "highway-v0": "ttrl-highway-batched-v0"}
+    env_id = aliases.get(env_id, env_id)
+    if env_id not in ENV_IDS:
+        raise KeyError(f"unknown env id {env_id!r}")
+    mod, cls = ENV_IDS[env_id].split(":")
+    import importlib
+    return getattr(importlib.import_module(mod), cls)(dict(config or {}, **kwargs))

@@ -368,15 +368,9 @@ class VecIntersectionEnv:
                   _stream(self.device))
         return self._reward.clone(), self._term.bool(), self._trunc.bool()
 
-    def _ego(self, field: str) -> torch.Tensor:
-        """Per-env value of the controlled vehicle (the env's first MDP slot)."""
-        kind = self.state["kind"]
-        slot = (kind == _abi.MDP).to(torch.int8).argmax(dim=1, keepdim=True)
-        return self.state[field].gather(1, slot).squeeze(1)
-
     def _info(self, obs, action) -> dict:
         """abstract.py:169-186 batched: device tensors [E]."""
-        return {"speed": self._ego("speed").clone(), "crashed": self._ego("crashed").bool(), "action": action}
+        return {"speed": self.state.ego("speed"), "crashed": self.state.ego("crashed").bool(), "action": action}
 
     def _auto_reset(self, done: torch.Tensor, obs: torch.Tensor) -> None:
         """Finished envs restart on the device with default_rng([seed words..., episode]) and
@@ -386,6 +380,11 @@ class VecIntersectionEnv:
         ix_reset(self.state, self.network, self.params, self.ix, self._entropy, d)
         self.time.masked_fill_(done, 0.0)
         self.observation_type.observe(mask=d, out=obs)
+
+    @property
+    def vehicle(self):
+        """The controlled vehicles (abstract.py:76-79): each env's MDP slot, field -> [E]."""
+        return {k: self.state.ego(k) for k in _abi.REAL_FIELDS + _abi.I32_FIELDS + _abi.U8_FIELDS}
 
     def get_available_actions(self):
         return self.action_type.get_available_actions()

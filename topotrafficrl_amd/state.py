@@ -66,6 +66,14 @@ class BatchState:
                                              self.n_envs, self.n_veh, self.abi_dtype)
         return self._struct
 
+    def ego_index(self) -> torch.Tensor:
+        """[E] slot of each env's controlled vehicle: its first MDP slot (AbstractEnv.vehicle)."""
+        return (self.t["kind"] == _abi.MDP).to(torch.int8).argmax(dim=1)
+
+    def ego(self, field: str) -> torch.Tensor:
+        """[E] value of ``field`` for each env's controlled vehicle."""
+        return self.t[field].gather(1, self.ego_index().unsqueeze(1)).squeeze(1)
+
     def nbytes(self) -> int:
         return sum(v.numel() * v.element_size() for v in self.t.values())
 
