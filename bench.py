@@ -39,6 +39,10 @@ CONFIGS = {
     3: dict(num_envs=4096, vehicles=128, obs=GRID7, name="4096 envs x 128 vehicles, OccupancyGrid 7x32x32"),
     4: dict(num_envs=4096, vehicles=64, obs=KIN15, name="4096 envs x 64 vehicles per GPU, Kinematics 15x7"),
     5: dict(num_envs=8192, vehicles=64, obs=KIN15, name="8192 envs x 64 vehicles, EgoAttention-2h policy in the loop"),
+    # the reference's training scenario (scripts/configs/IntersectionEnv/env.json): spawns and
+    # clears keep ~10-20 live vehicles in 32 slots; vehicle-steps count live vehicles only
+    6: dict(num_envs=4096, vehicles=32, obs=dict(KIN15, absolute=True, order="shuffled"),
+            name="4096 intersection-v0 envs (env.json: Kinematics 15x7 absolute, shuffled), 32 slots"),
 }
 
 
@@ -97,7 +101,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
-    ap.add_argument("--config", type=int, default=4, choices=[2, 3, 4, 5])
+    ap.add_argument("--config", type=int, default=4, choices=[2, 3, 4, 5, 6])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--graph", action="store_true",
@@ -128,8 +132,14 @@ def main():
     C = CONFIGS[args.config]
     E, N = C["num_envs"], C["vehicles"]
     offset, _ = sharding.weak_shard(E, rank)  # weak scaling: E envs per GPU, global ids [rank*E, (rank+1)*E)
-    env = VecHighwayEnv({"num_envs": E, "vehicles_count": N, "observation": C["obs"], "device": str(dev),
-                         "dtype": args.dtype, "env_id_offset": offset})
+    ix = args.config == 6
+    if ix:
+        from topotrafficrl_amd.intersection import VecIntersectionEnv
+        env = VecIntersectionEnv({"num_envs": E, "vehicle_slots": N, "observation": C["obs"], "device": str(dev),
+                                  "dtype": args.dtype, "env_id_offset": offset, "auto_reset": True})
+    else:
+        env = VecHighwayEnv({"num_envs": E, "vehicles_count": N, "observation": C["obs"], "device": str(dev),
+                             "dtype": args.dtype, "env_id_offset": offset})
     policy = None
     if args.config == 5:
         from topotrafficrl_amd.agent import EgoAttentionPolicy
@@ -137,7 +147,9 @@ def main():
     obs, _ = env.reset(seed=12345)
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
-    acts = torch.randint(0, 5, (args.warmup + args.steps, E), device=dev, generator=g, dtype=torch.int64)
+    n_act = env.action_space.n
+    acts = torch.randint(0, n_act, (args.warmup + args.steps, E), device=dev, generator=g, dtype=torch.int64)
+    live = torch.zeros((), dtype=torch.int64, device=dev)  # live vehicles summed over the timed steps
 
     sg = None
     if args.graph:
@@ -152,6 +164,8 @@ def main():
             sg.replay()
             return
         a = policy.act(obs, t) if policy is not None else acts[t]
+        if ix and t >= args.warmup:
+            live.add_((env.state["kind"] != 0).sum())
         obs, rew, term, trunc, info = env.step(a)
 
     kern_warm = []
@@ -198,6 +212,8 @@ def main():
     elapsed = sharding.max_over_ranks(elapsed, device=None if shared else dev)
 
     veh_steps = world * E * N * 15 * args.steps
+    if ix:  # live vehicles, not slots (the rank's own count scaled by the number of ranks)
+        veh_steps = world * int(live.item()) * 15
     value = veh_steps / elapsed
     rd, wr = state_bytes(args.dtype)
     alg_bytes = E * N * (rd + wr)  # per fused simulate launch
@@ -238,7 +254,10 @@ def main():
                        "simd_cycles": 1024 * clk * 1e9 * kern_ms * 1e-3,
                        "busy_frac_lower_bound": 2 * insts / (1024 * clk * 1e9 * kern_ms * 1e-3),
                        "source": "profiles/pmc_traffic.json (SQ_INSTS_VALU, SQ_WAVES, GRBM clock)"}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if ix:
+        out["config"]["live_vehicles_per_env"] = veh_steps / (world * E * 15 * args.steps)
+        out["config"]["auto_reset"] = True
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not ix:
         out["cpu_baseline"] = cpu_baseline(N, C["obs"] if C["obs"]["type"] == "Kinematics" else GRID7,
                                            args.cpu_seconds)
     if rank == 0:

@@ -193,7 +193,9 @@ typedef struct ttrl_grid_cfg {
 /* TimeToCollisionObservation config (observation.py:114-151, finite_mdp.py:104-167). */
 typedef struct ttrl_ttc_cfg {
   int32_t horizon_bins;           /* int(horizon * policy_frequency) (10)       */
-  int32_t obs_lanes, obs_speeds;  /* 3, 3 (observation.py:139, :146)           */
+  int32_t obs_lanes, obs_speeds;  /* 3, 3 (observation.py:139, :146); 0, 0: the raw
+                                     compute_ttc_grid [speeds][lanes][horizon_bins]
+                                     (AbstractEnv.to_finite_mdp, finite_mdp.py:48)  */
   int32_t _pad;
   double time_quantization;       /* 1 / policy_frequency                       */
 } ttrl_ttc_cfg_t;

@@ -208,7 +208,10 @@ class Oracle:
 
     def observe_ttc(self, h: HostState, cfg: _abi.TtcCfg):
         s = h.struct()
-        out = np.zeros((h.E, cfg.obs_speeds, cfg.obs_lanes, cfg.horizon_bins), dtype=np.float32)
+        if cfg.obs_speeds == 0 and cfg.obs_lanes == 0:  # raw compute_ttc_grid
+            out = np.zeros((h.E, self.params.n_target_speeds, self.lanes.n_lanes, cfg.horizon_bins), dtype=np.float32)
+        else:
+            out = np.zeros((h.E, cfg.obs_speeds, cfg.obs_lanes, cfg.horizon_bins), dtype=np.float32)
         self._ok(self.lib.oracle_observe_ttc(C.byref(s), C.byref(self.lanes), C.byref(self.params), C.byref(cfg),
                                              out.ctypes.data))
         return out

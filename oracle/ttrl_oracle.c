@@ -1213,6 +1213,10 @@ int oracle_observe_ttc(const ttrl_state_t* s, const ttrl_lane_table_t* R, const 
         }
       }
     }
+    if (OS == 0 && OL == 0) {                                     /* raw grid (finite_mdp.py:48) */
+      for (int k = 0; k < NS * NL * T; ++k) out[(size_t)e * NS * NL * T + k] = (float)grid[k];
+      continue;
+    }
     /* observation.py:136-151: pad lanes with ones, window of obs_lanes around the ego's
      * lane; repeat the first / last speed rows (1 + NS) times, window of obs_speeds */
     const int lane = o.lane[ego], sidx = o.sidx[ego];

@@ -17,11 +17,12 @@ def pytest_configure(config):
 
 
 def golden_files(pattern="*.npz"):
-    """Road-frame fixtures of gen_golden.py; the intersection episodes (ix_*, gen_golden_ix.py)
-    have their own layout and are only returned when asked for by name."""
+    """Road-frame fixtures of gen_golden.py; the intersection episodes (ix_*, gen_golden_ix.py) and
+    the finite-MDP tables (mdp_*, gen_golden_mdp.py) have their own layouts and are only returned
+    when asked for by name."""
     files = sorted(glob.glob(os.path.join(GOLDEN, pattern)))
     if pattern == "*.npz":
-        files = [f for f in files if not os.path.basename(f).startswith("ix_")]
+        files = [f for f in files if not os.path.basename(f).startswith(("ix_", "mdp_"))]
     return files
 
 

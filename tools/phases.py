@@ -14,13 +14,18 @@ from topotrafficrl_amd.envs import VecHighwayEnv  # noqa: E402
 
 NAMES = ["meta", "act-setup", "scan", "mobil-bar+verdict", "abort", "steer/acc+bar", "kinematics", "project+bar",
          "candidates+bar", "sat+bar", "fold", "project-init", "idm-free(pow)", "mobil-queue+bar", "mobil-items",
-         "hbm-load+stage", "store", "-", "-", "-"]
+         "hbm-load+stage", "store", "regulation", "-", "-"]
 
 
-def main(dtype="f64", steps=30, frames=15):
+def main(dtype="f64", steps=30, frames=15, ix=False):
     dev = torch.device("cuda:0")
-    env = VecHighwayEnv({"num_envs": 4096, "vehicles_count": 64, "device": "cuda:0", "dtype": dtype})
+    if ix:  # the intersection scenario (NET_GRAPH instance), 32 slots
+        from topotrafficrl_amd.intersection import VecIntersectionEnv
+        env = VecIntersectionEnv({"num_envs": 4096, "device": "cuda:0", "dtype": dtype})
+    else:
+        env = VecHighwayEnv({"num_envs": 4096, "vehicles_count": 64, "device": "cuda:0", "dtype": dtype})
     env.reset(seed=12345)
+    n_act = env.action_space.n
     g = torch.Generator(device=dev).manual_seed(1000)
     lib = _lib.load(os.path.join(ROOT, "tools", "_variants", "lib_timing.so"))
     sim = lib.ttrl_simulate
@@ -31,7 +36,7 @@ def main(dtype="f64", steps=30, frames=15):
     buf = np.zeros(20, dtype=np.uint64)
     tot = np.zeros(20)
     for t in range(steps):
-        a = env.action_type._codes(torch.randint(0, 5, (4096,), device=dev, generator=g))
+        a = env.action_type._codes(torch.randint(0, n_act, (4096,), device=dev, generator=g))
         rd(buf.ctypes.data)
         sim(C.byref(env.state.struct()), C.byref(env.network.table), C.byref(env.params), a.data_ptr(), frames, 1 / 15,
             stream)
@@ -39,7 +44,7 @@ def main(dtype="f64", steps=30, frames=15):
         rd(buf.ctypes.data)
         if t >= 10:
             tot += buf.astype(np.float64)
-    waves = 4096 * (steps - 10)
+    waves = (4096 if not ix else 2048) * (steps - 10)  # ix: two envs per 64-lane workgroup
     per = tot / waves
     print(f"[{dtype}] cycles per wave per {frames}-frame launch (mean over {steps - 10} launches), total {per.sum():.0f}")
     for n, c in zip(NAMES, per):
@@ -47,4 +52,5 @@ def main(dtype="f64", steps=30, frames=15):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "f64", frames=int(sys.argv[2]) if len(sys.argv) > 2 else 15)
+    main(sys.argv[1] if len(sys.argv) > 1 else "f64", frames=int(sys.argv[2]) if len(sys.argv) > 2 else 15,
+         ix="--ix" in sys.argv)

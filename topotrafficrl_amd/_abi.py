@@ -373,11 +373,12 @@ def reward_cfg(collision_reward=-1.0, high_speed_reward=0.4, reward_speed_range=
     return c
 
 
-def ttc_cfg(horizon: float = 10, policy_frequency: float = 1, **_ignored) -> TtcCfg:
-    """TimeToCollisionObservation(horizon) (observation.py:114-151) at the env's policy frequency."""
+def ttc_cfg(horizon: float = 10, policy_frequency: float = 1, raw: bool = False, **_ignored) -> TtcCfg:
+    """TimeToCollisionObservation(horizon) (observation.py:114-151) at the env's policy frequency;
+    ``raw``: the whole compute_ttc_grid (finite_mdp.py:104-167) instead of the 3x3 window."""
     c = TtcCfg()
     c.horizon_bins = int(horizon * policy_frequency)
-    c.obs_lanes, c.obs_speeds = 3, 3
+    c.obs_lanes, c.obs_speeds = (0, 0) if raw else (3, 3)
     c.time_quantization = 1.0 / float(policy_frequency)
     if not 1 <= c.horizon_bins <= 64:
         raise ValueError("TTC horizon * policy_frequency must be in [1, 64]")

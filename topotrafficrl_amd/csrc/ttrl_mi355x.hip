@@ -945,6 +945,14 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   const int N = st.n_veh, nl = R.n_lanes;
   const int env = blockIdx.x * EPW + le;
   const bool env_on = env < st.n_envs && (!env_mask || env_mask[env]);  // masked-out envs: untouched
+  if (env_mask) {  // a workgroup with no active env leaves at once (uniform: before any barrier)
+    bool any = false;
+    for (int q = 0; q < EPW; ++q) {
+      const int e = blockIdx.x * EPW + q;
+      any |= e < st.n_envs && env_mask[e];
+    }
+    if (!any) return;
+  }
   const bool slot = env_on && i < N;
   const size_t k = (size_t)env * N + i;
   const int me = le * NS + i;  // this vehicle's LDS slot
@@ -1353,6 +1361,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
           }
         }
       }
+      PH(17);
       T x = V.x[me], y = V.y[me], h = V.h[me];
       if (present) {
         T v = V.v[me], steer = V.steer[me], acc = V.acc[me];
@@ -2046,6 +2055,11 @@ __global__ void __launch_bounds__(64) ttc_obs_kernel(ttrl_state_t st, ttrl_lane_
     }
   }
   __syncthreads();
+  if (cfg.obs_speeds == 0 && cfg.obs_lanes == 0) {  // the raw compute_ttc_grid (finite_mdp)
+    float* ob = out + (size_t)env * NS * NL * TB;
+    for (int k = tid; k < NS * NL * TB; k += 64) ob[k] = (grid[k] & 2) ? 1.0f : ((grid[k] & 1) ? 0.5f : 0.0f);
+    return;
+  }
   // observation.py:136-151: lane window padded with ones, speed rows repeated at the ends
   const int OS = cfg.obs_speeds, OL = cfg.obs_lanes, sidx = st.speed_index[base];
   float* ob = out + (size_t)env * OS * OL * TB;
@@ -2786,8 +2800,10 @@ int ttrl_observe_ttc(const ttrl_state_t* s, const ttrl_lane_table_t* road, const
                      const ttrl_ttc_cfg_t* cfg, float* out, void* stream) {
   int rc = check_state(s, road);
   if (rc) return rc;
-  if (!p || !cfg || !out || cfg->horizon_bins < 1 || cfg->horizon_bins > 64 || cfg->obs_lanes < 1 ||
-      cfg->obs_speeds < 1 || !(cfg->time_quantization > 0) || p->n_target_speeds < 1 || p->n_target_speeds > 8)
+  const bool raw = cfg && cfg->obs_lanes == 0 && cfg->obs_speeds == 0;
+  if (!p || !cfg || !out || cfg->horizon_bins < 1 || cfg->horizon_bins > 64 || (!raw && cfg->obs_lanes < 1) ||
+      (!raw && cfg->obs_speeds < 1) || !(cfg->time_quantization > 0) || p->n_target_speeds < 1 ||
+      p->n_target_speeds > 8)
     return TTRL_E_ARG;
   if (s->n_envs == 0) return TTRL_OK;
   const size_t lds = sizeof(int) * p->n_target_speeds * road->n_lanes * cfg->horizon_bins;

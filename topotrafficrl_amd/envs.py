@@ -105,6 +105,9 @@ class VecHighwayEnv:
             "reward_speed_range": [20.0, 30.0],
             "normalize_reward": False,
             "offroad_terminal": False,
+            # finite_mdp state reward terms (finite_mdp.py:64-78; highway-env defaults)
+            "right_lane_reward": 0.1,
+            "lane_change_reward": 0.0,
             # batching
             "num_envs": 1,
             "env_id_offset": 0,            # global id of env 0 (sharding: seeds = seed + global id)
@@ -245,6 +248,11 @@ class VecHighwayEnv:
 
     def get_available_actions(self):
         return self.action_type.get_available_actions()
+
+    def to_finite_mdp(self):
+        """abstract.py:416-417: the batched time-to-collision MDP of every env's ego."""
+        from .finite_mdp import finite_mdp
+        return finite_mdp(self, time_quantization=1 / self.config["policy_frequency"])
 
     def close(self) -> None:
         self.done = True

@@ -58,8 +58,12 @@ def occupancy_grid(state, network, params, cfg: _abi.GridCfg, out=None):
 
 
 def time_to_collision(state, network, params, cfg: _abi.TtcCfg, out=None):
-    """TimeToCollisionObservation.observe for every env: [E, 3 speeds, 3 lanes, T] float32."""
-    shape = (state.n_envs, cfg.obs_speeds, cfg.obs_lanes, cfg.horizon_bins)
+    """TimeToCollisionObservation.observe for every env: [E, 3 speeds, 3 lanes, T] float32; with a
+    raw cfg (obs_speeds = obs_lanes = 0) the whole compute_ttc_grid [E, speeds, lanes, T]."""
+    if cfg.obs_speeds == 0 and cfg.obs_lanes == 0:
+        shape = (state.n_envs, params.n_target_speeds, network.table.n_lanes, cfg.horizon_bins)
+    else:
+        shape = (state.n_envs, cfg.obs_speeds, cfg.obs_lanes, cfg.horizon_bins)
     if out is None:
         out = torch.empty(shape, dtype=torch.float32, device=state.device)
     _lib.call("ttrl_observe_ttc", C.byref(state.struct()), C.byref(network.table), C.byref(params),
