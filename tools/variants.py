@@ -53,21 +53,33 @@ def run(dtypes, E=4096, N=64, rounds=7):
         lib = _lib.load(os.path.join(OUT, f"lib_{name}.so"))
         lib.ttrl_simulate.argtypes = [C.c_void_p] * 4 + [C.c_int32, C.c_double, C.c_void_p]
         libs[name] = lib
+    ix = os.environ.get("IX") == "1"  # the intersection scenario (NET_GRAPH instance), 32 slots
     for dtype in dtypes:
-        base = BatchState(E, N, device=dev, dtype=dtype)
-        reset_highway(base, net, P, _abi.reset_cfg(N, net.table), list(range(E)))
-        torch.cuda.synchronize()
         stream = torch.cuda.current_stream(dev).cuda_stream
-        g = torch.Generator(device=dev).manual_seed(1)
-        first = libs[next(iter(libs))]
-        for _ in range(int(os.environ.get("EVOLVE", "20"))):  # time a mid-episode state, not the fresh one
-            a = torch.randint(0, 5, (E,), device=dev, dtype=torch.int32, generator=g)
-            assert first.ttrl_simulate(C.byref(base.struct()), C.byref(net.table), C.byref(P), a.data_ptr(), 15,
-                                       1 / 15, stream) == 0
+        if ix:
+            from topotrafficrl_amd.intersection import VecIntersectionEnv
+            env = VecIntersectionEnv({"num_envs": E, "device": dev, "dtype": dtype})
+            env.reset(seed=12345)
+            g = torch.Generator(device=dev).manual_seed(1)
+            for _ in range(int(os.environ.get("EVOLVE", "6"))):
+                env.step(torch.randint(0, 3, (E,), device=dev, generator=g))
+            base, net, P, N = env.state, env.network, env.params, env.state.n_veh
+            acts = env.action_type._codes(torch.randint(0, 3, (E,), device=dev, generator=g))
+        else:
+            base = BatchState(E, N, device=dev, dtype=dtype)
+            reset_highway(base, net, P, _abi.reset_cfg(N, net.table), list(range(E)))
+            torch.cuda.synchronize()
+            g = torch.Generator(device=dev).manual_seed(1)
+            first = libs[next(iter(libs))]
+            for _ in range(int(os.environ.get("EVOLVE", "20"))):  # time a mid-episode state, not the fresh one
+                a = torch.randint(0, 5, (E,), device=dev, dtype=torch.int32, generator=g)
+                assert first.ttrl_simulate(C.byref(base.struct()), C.byref(net.table), C.byref(P), a.data_ptr(), 15,
+                                           1 / 15, stream) == 0
+            acts = torch.randint(0, 5, (E,), device=dev, dtype=torch.int32,
+                                 generator=torch.Generator(device=dev).manual_seed(0))
         torch.cuda.synchronize()
         ref = None
         work = base.clone()
-        acts = torch.randint(0, 5, (E,), device=dev, dtype=torch.int32, generator=torch.Generator(device=dev).manual_seed(0))
         times = {k: [] for k in VARIANTS}
         for r in range(rounds):
             for name, lib in libs.items():

@@ -2384,85 +2384,140 @@ __global__ void rewards_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_reward
 }
 
 // ------------------------------------------------------------ the intersection scenario
-// IntersectionEnv (intersection_env.py:131-362) scene management, one thread per env: the
-// vehicle list is inherently sequential (spawns append, clears keep list order, every spawn
-// draws from the env's np_random in turn) and runs once per policy step, next to the fused
-// 15-frame simulate launch that dominates.
+// IntersectionEnv (intersection_env.py:131-362) scene management: one wavefront per env, the
+// env's slots on the lanes (chunks of 64 when n_veh > 64).  The vehicle list is sequential by
+// nature (spawns append, clears keep list order, every draw advances the env's np_random), so
+// every lane replays the same numpy Generator in lockstep -- identical state, identical draws,
+// identical (uniform) rejection loops -- while the per-slot work is spread over the lanes:
+// clearing and compacting the rows (coalesced), the spawn's distance test (ballot), the
+// closest-lane search (one road lane per SIMD lane, first-minimum argmin by xor-shuffles).
+
+// Every field of one vehicle row, for compaction in registers.
+template <typename T> struct Row {
+  T f[11];  // x, y, heading, speed, target_speed, timer, delta, steer, acc, impact_x, impact_y
+  int32_t lane, tgt, sidx, route_road, route_lane;  // the 4 int8 route entries packed in one word each
+  uint8_t kind, crashed, has_impact, lane_change, yielding;
+  int8_t route_n;
+};
 template <typename T>
-__device__ void slot_clear(const ttrl_state_t& st, size_t k) {
-  st.kind[k] = TTRL_ABSENT; st.crashed[k] = 0; st.has_impact[k] = 0; st.lane_change[k] = 0;
-  T* f[] = {(T*)st.x, (T*)st.y, (T*)st.heading, (T*)st.speed, (T*)st.target_speed, (T*)st.timer,
-            (T*)st.steer, (T*)st.acc, (T*)st.impact_x, (T*)st.impact_y};
-  for (T* p : f) p[k] = T(0);
-  ((T*)st.delta)[k] = T(4);
-  st.lane[k] = st.target_lane[k] = 0; st.speed_index[k] = -1;
-  for (int q = 0; q < TTRL_ROUTE_MAX; ++q) st.route_road[k * TTRL_ROUTE_MAX + q] = st.route_lane[k * TTRL_ROUTE_MAX + q] = -1;
-  st.route_n[k] = -1; st.yielding[k] = 0;
+__device__ __forceinline__ T* real_field(const ttrl_state_t& st, int q) {
+  void* const p[11] = {st.x, st.y, st.heading, st.speed, st.target_speed, st.timer, st.delta,
+                       st.steer, st.acc, st.impact_x, st.impact_y};
+  return (T*)p[q];
 }
 template <typename T>
-__device__ void slot_move(const ttrl_state_t& st, size_t d, size_t k) {
-  T* f[] = {(T*)st.x, (T*)st.y, (T*)st.heading, (T*)st.speed, (T*)st.target_speed, (T*)st.timer, (T*)st.delta,
-            (T*)st.steer, (T*)st.acc, (T*)st.impact_x, (T*)st.impact_y};
-  for (T* p : f) p[d] = p[k];
-  st.kind[d] = st.kind[k]; st.crashed[d] = st.crashed[k]; st.has_impact[d] = st.has_impact[k];
-  st.lane_change[d] = st.lane_change[k];
-  st.lane[d] = st.lane[k]; st.target_lane[d] = st.target_lane[k]; st.speed_index[d] = st.speed_index[k];
-  for (int q = 0; q < TTRL_ROUTE_MAX; ++q) {
-    st.route_road[d * TTRL_ROUTE_MAX + q] = st.route_road[k * TTRL_ROUTE_MAX + q];
-    st.route_lane[d * TTRL_ROUTE_MAX + q] = st.route_lane[k * TTRL_ROUTE_MAX + q];
-  }
-  st.route_n[d] = st.route_n[k]; st.yielding[d] = st.yielding[k];
+__device__ __forceinline__ Row<T> row_load(const ttrl_state_t& st, size_t k) {
+  Row<T> r;
+#pragma unroll
+  for (int q = 0; q < 11; ++q) r.f[q] = real_field<T>(st, q)[k];
+  r.lane = st.lane[k]; r.tgt = st.target_lane[k]; r.sidx = st.speed_index[k];
+  r.route_road = ((const int32_t*)st.route_road)[k];  // TTRL_ROUTE_MAX == 4 int8 entries
+  r.route_lane = ((const int32_t*)st.route_lane)[k];
+  r.kind = st.kind[k]; r.crashed = st.crashed[k]; r.has_impact = st.has_impact[k];
+  r.lane_change = st.lane_change[k]; r.yielding = st.yielding[k]; r.route_n = st.route_n[k];
+  return r;
 }
-// keep bit j of the env's slots; survivors move down in list order, the tail is cleared
 template <typename T>
-__device__ void slots_compact(const ttrl_state_t& st, size_t base, const unsigned* keep) {
+__device__ __forceinline__ void row_store(const ttrl_state_t& st, size_t k, const Row<T>& r) {
+#pragma unroll
+  for (int q = 0; q < 11; ++q) real_field<T>(st, q)[k] = r.f[q];
+  st.lane[k] = r.lane; st.target_lane[k] = r.tgt; st.speed_index[k] = r.sidx;
+  ((int32_t*)st.route_road)[k] = r.route_road;
+  ((int32_t*)st.route_lane)[k] = r.route_lane;
+  st.kind[k] = r.kind; st.crashed[k] = r.crashed; st.has_impact[k] = r.has_impact;
+  st.lane_change[k] = r.lane_change; st.yielding[k] = r.yielding; st.route_n[k] = r.route_n;
+}
+template <typename T>
+__device__ __forceinline__ Row<T> row_absent() {  // an empty slot, as BatchState initialises it
+  Row<T> r;
+#pragma unroll
+  for (int q = 0; q < 11; ++q) r.f[q] = T(0);
+  r.f[6] = T(4);  // IDMVehicle.DELTA
+  r.lane = r.tgt = 0; r.sidx = -1; r.route_road = r.route_lane = -1;
+  r.kind = TTRL_ABSENT; r.crashed = r.has_impact = r.lane_change = r.yielding = 0; r.route_n = -1;
+  return r;
+}
+// Survivors (present slots whose keep bit is set) move down in list order; the tail is cleared.
+// keep: bit j of word j / 64.  All of a chunk's rows are read before any is written; writes
+// only go to slots <= the one read, so earlier chunks are never read again.
+template <typename T>
+__device__ void wave_compact(const ttrl_state_t& st, size_t base, const unsigned long long* keep, int lane) {
   int w = 0;
-  for (int j = 0; j < st.n_veh; ++j) {
-    if (st.kind[base + j] == TTRL_ABSENT || !((keep[j >> 5] >> (j & 31)) & 1u)) continue;
-    if (w != j) slot_move<T>(st, base + w, base + j);
-    ++w;
+  for (int c0 = 0; c0 < st.n_veh; c0 += 64) {
+    const int j = c0 + lane;
+    const bool in = j < st.n_veh;
+    Row<T> r;
+    bool live = false;
+    if (in) {
+      r = row_load<T>(st, base + j);
+      live = r.kind != TTRL_ABSENT && ((keep[c0 >> 6] >> lane) & 1ull);
+    }
+    const unsigned long long m = __ballot(live);
+    const int dst = w + __popcll(m & ((1ull << lane) - 1ull));
+    __syncthreads();
+    if (live) row_store<T>(st, base + dst, r);
+    w += __popcll(m);
   }
-  for (int j = w; j < st.n_veh; ++j) slot_clear<T>(st, base + j);
+  __syncthreads();
+  for (int j = w + lane; j < st.n_veh; j += 64) row_store<T>(st, base + j, row_absent<T>());
+  __syncthreads();
 }
-__device__ int slots_count(const ttrl_state_t& st, size_t base) {
+__device__ __forceinline__ int wave_count(const ttrl_state_t& st, size_t base, int lane) {
   int n = 0;
-  while (n < st.n_veh && st.kind[base + n] != TTRL_ABSENT) ++n;
+  for (int c0 = 0; c0 < st.n_veh; c0 += 64)
+    n += __popcll(__ballot(c0 + lane < st.n_veh && st.kind[base + c0 + lane] != TTRL_ABSENT));
   return n;
 }
-// RoadNetwork.get_closest_lane_index road.py:55-71 with distance_with_heading lane.py:132-147
-__device__ int closest_lane_d(const ttrl_lane_table_t& R, double x, double y, double h) {
-  int best = 0;
-  double bd = 0;
-  for (int l = 0; l < R.n_lanes; ++l) {
-    const LaneT<double> L = make_lane<double>(R, l);
-    double s, r;
-    lane_local(L, x, y, s, r);
-    const double ang = fabs(wrap_to_pi(h - heading_at(L, s)));
-    double a = s - R.length[l]; if (!(a > 0)) a = 0;
-    double c = 0 - s; if (!(c > 0)) c = 0;
-    const double d = fabs(r) + a + c + 1.0 * ang;
-    if (l == 0 || d < bd) { bd = d; best = l; }
+// RoadNetwork.get_closest_lane_index road.py:55-71 (distance_with_heading lane.py:132-147, first
+// minimum), one network lane per SIMD lane; the result is uniform.
+__device__ int wave_closest_lane(const ttrl_lane_table_t& R, double x, double y, double h, int lane) {
+  double best = K<double>::inf();
+  int bl = 0x7fffffff;
+  for (int l0 = 0; l0 < R.n_lanes; l0 += 64) {
+    const int l = l0 + lane;
+    if (l < R.n_lanes) {
+      const LaneT<double> L = make_lane<double>(R, l);
+      double s, r;
+      lane_local(L, x, y, s, r);
+      const double ang = fabs(wrap_to_pi(h - heading_at(L, s)));
+      double a = s - R.length[l]; if (!(a > 0)) a = 0;
+      double c = 0 - s; if (!(c > 0)) c = 0;
+      const double d = fabs(r) + a + c + 1.0 * ang;
+      if (d < best || (d == best && l < bl)) { best = d; bl = l; }
+    }
   }
-  return best;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double od = __shfl_xor(best, off);
+    const int ol = __shfl_xor(bl, off);
+    if (od < best || (od == best && ol < bl)) { best = od; bl = ol; }
+  }
+  return bl == 0x7fffffff ? 0 : bl;
 }
-// ControlledVehicle.plan_route_to controller.py:71-87 (shortest_path precomputed on the host)
-__device__ void plan_route(const ttrl_state_t& st, const ttrl_lane_table_t& R, const ttrl_ix_cfg_t& C, size_t k,
-                           int corner) {
-  const int l = st.lane[k], road = R.road[l], node = R.road_to[road];
+// ControlledVehicle.plan_route_to controller.py:71-87 (shortest_path precomputed on the host):
+// the packed route words of a vehicle on `lane` heading for corner `corner`.
+__device__ __forceinline__ void plan_route(const ttrl_lane_table_t& R, const ttrl_ix_cfg_t& C, int lane, int corner,
+                                           int32_t& rr, int32_t& rl, int8_t& rn) {
+  const int road = R.road[lane], node = R.road_to[road];
   const int n = C.path_len[node][corner] > 0 ? C.path_len[node][corner] : 0;
-  int8_t* rr = st.route_road + k * TTRL_ROUTE_MAX;
-  int8_t* rl = st.route_lane + k * TTRL_ROUTE_MAX;
-  for (int q = 0; q < TTRL_ROUTE_MAX; ++q) rr[q] = rl[q] = -1;
-  rr[0] = (int8_t)road; rl[0] = (int8_t)R.lane_id[l];
-  for (int q = 0; q < n; ++q) rr[1 + q] = C.path_road[node][corner][q];
-  st.route_n[k] = (int8_t)(1 + n);
+  int8_t a[TTRL_ROUTE_MAX], b[TTRL_ROUTE_MAX];
+  for (int q = 0; q < TTRL_ROUTE_MAX; ++q) a[q] = b[q] = -1;
+  a[0] = (int8_t)road; b[0] = (int8_t)R.lane_id[lane];
+  for (int q = 0; q < n; ++q) a[1 + q] = C.path_road[node][corner][q];
+  rr = rl = 0;
+  for (int q = 0; q < TTRL_ROUTE_MAX; ++q) {
+    rr |= (int32_t)(uint8_t)a[q] << (8 * q);
+    rl |= (int32_t)(uint8_t)b[q] << (8 * q);
+  }
+  rn = (int8_t)(1 + n);
 }
 // IntersectionEnv._spawn_vehicle intersection_env.py:320-348 (IDMVehicle.make_on_lane
-// objects.py:68-89, IDMVehicle.__init__ behavior.py:48-64, randomize_behavior :66-69)
+// objects.py:68-89, IDMVehicle.__init__ behavior.py:48-64, randomize_behavior :66-69).
+// Uniform across the wave: every lane holds the same generator and makes the same draws.
 template <typename T>
-__device__ void ix_spawn(const ttrl_state_t& st, const ttrl_lane_table_t& R, const ttrl_params_t& P,
-                         const ttrl_ix_cfg_t& C, Pcg& g, size_t base, double longitudinal, double pos_dev,
-                         double speed_dev, double prob, bool go_straight) {
+__device__ void wave_spawn(const ttrl_state_t& st, const ttrl_lane_table_t& R, const ttrl_params_t& P,
+                           const ttrl_ix_cfg_t& C, Pcg& g, size_t base, int lane, double longitudinal, double pos_dev,
+                           double speed_dev, double prob, bool go_straight) {
   if (pcg_double(g) > prob) return;
   int route[2];
   pcg_choice_noreplace(g, 4, 2, route);
@@ -2474,118 +2529,147 @@ __device__ void ix_spawn(const ttrl_state_t& st, const ttrl_lane_table_t& R, con
   double px, py;
   lane_position(L, lon, 0.0, px, py);
   const double ph = heading_at(L, lon);
-  for (int j = 0; j < st.n_veh; ++j) {
+  bool near = false;
+  for (int j = lane; j < st.n_veh; j += 64) {
     const size_t k = base + j;
     if (st.kind[k] == TTRL_ABSENT) continue;
     const double dx = (double)((const T*)st.x)[k] - px, dy = (double)((const T*)st.y)[k] - py;
-    if (sqrt(dx * dx + dy * dy) < C.spawn_clear_distance) return;
+    near |= sqrt(dx * dx + dy * dy) < C.spawn_clear_distance;
   }
-  const int n = slots_count(st, base);
+  if (__any(near)) return;
+  const int n = wave_count(st, base, lane);
   const double delta = C.delta_lo + (C.delta_hi - C.delta_lo) * pcg_double(g);  // drawn even with no slot left
   if (n >= st.n_veh) return;
-  const size_t k = base + n;
-  slot_clear<T>(st, k);
-  st.kind[k] = TTRL_IDM; st.lane_change[k] = 1;
-  ((T*)st.x)[k] = T(px); ((T*)st.y)[k] = T(py); ((T*)st.heading)[k] = T(ph);
-  ((T*)st.speed)[k] = T(sp); ((T*)st.target_speed)[k] = T(sp);
-  st.lane[k] = st.target_lane[k] = closest_lane_d(R, px, py, ph);
-  ((T*)st.timer)[k] = T(pymod((px + py) * 3.141592653589793, P.lane_change_delay));
-  plan_route(st, R, C, k, route[1]);
-  ((T*)st.delta)[k] = T(delta);
+  const int cl = wave_closest_lane(R, px, py, ph, lane);
+  if (lane == 0) {
+    Row<T> r = row_absent<T>();
+    r.kind = TTRL_IDM; r.lane_change = 1;
+    r.f[0] = T(px); r.f[1] = T(py); r.f[2] = T(ph); r.f[3] = T(sp); r.f[4] = T(sp);
+    r.f[5] = T(pymod((px + py) * 3.141592653589793, P.lane_change_delay));
+    r.f[6] = T(delta);
+    r.lane = r.tgt = cl;
+    plan_route(R, C, cl, route[1], r.route_road, r.route_lane, r.route_n);
+    row_store<T>(st, base + n, r);
+  }
+  __syncthreads();
 }
 
 // IntersectionEnv._reset, part 1: np_random = default_rng(SeedSequence(entropy)), _make_road's
 // fresh RegulatedRoad (steps 0, no vehicles), the n-1 initial spawns (intersection_env.py:262-263).
 template <typename T>
-__global__ void ix_begin_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_ix_cfg_t C,
-                                const unsigned* __restrict__ words, int n_words, const uint8_t* __restrict__ mask) {
-  const int env = blockIdx.x * blockDim.x + threadIdx.x;
-  if (env >= st.n_envs || (mask && !mask[env])) return;
+__global__ void __launch_bounds__(64) ix_begin_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P,
+                                                      ttrl_ix_cfg_t C, const unsigned* __restrict__ words,
+                                                      int n_words, const uint8_t* __restrict__ mask) {
+  const int env = blockIdx.x, lane = threadIdx.x;
+  if (mask && !mask[env]) return;
   const size_t base = (size_t)env * st.n_veh;
   unsigned long long s4[4];
   SeedSeq::pcg64_seed(words + (size_t)env * n_words, n_words, s4);
   Pcg g;
   g.st = U128{s4[0], s4[1]}; g.inc = U128{s4[2], s4[3]}; g.has32 = false; g.u32 = 0;
-  for (int j = 0; j < st.n_veh; ++j) slot_clear<T>(st, base + j);
-  st.reg_steps[env] = 0;
+  for (int j = lane; j < st.n_veh; j += 64) row_store<T>(st, base + j, row_absent<T>());
+  if (lane == 0) st.reg_steps[env] = 0;
+  __syncthreads();
   for (int t = 0; t < C.initial_vehicle_count - 1; ++t)
-    ix_spawn<T>(st, R, P, C, g, base, C.init_longitudinal[t], 1.0, 1.0, C.spawn_probability, false);
-  rng_store(g, st.rng + (size_t)env * TTRL_RNG_WORDS);
+    wave_spawn<T>(st, R, P, C, g, base, lane, C.init_longitudinal[t], 1.0, 1.0, C.spawn_probability, false);
+  if (lane == 0) rng_store(g, st.rng + (size_t)env * TTRL_RNG_WORDS);
 }
 
 // IntersectionEnv._reset, part 2 (after the warm-up frames): the challenger, the ego
 // MDPVehicle appended after the traffic, and the removal of the vehicles within 20 m of it,
 // which skips the vehicle after each removed one (list.remove while iterating, :308-312).
 template <typename T>
-__global__ void ix_finish_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_ix_cfg_t C,
-                                 const uint8_t* __restrict__ mask) {
-  const int env = blockIdx.x * blockDim.x + threadIdx.x;
-  if (env >= st.n_envs || (mask && !mask[env])) return;
+__global__ void __launch_bounds__(64) ix_finish_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P,
+                                                       ttrl_ix_cfg_t C, const uint8_t* __restrict__ mask) {
+  const int env = blockIdx.x, lane = threadIdx.x;
+  if (mask && !mask[env]) return;
   const size_t base = (size_t)env * st.n_veh;
   uint64_t* w = st.rng + (size_t)env * TTRL_RNG_WORDS;
   Pcg g = rng_load(w);
-  ix_spawn<T>(st, R, P, C, g, base, C.challenger_longitudinal, C.challenger_position_deviation,
-              C.challenger_speed_deviation, 1.0, true);
+  wave_spawn<T>(st, R, P, C, g, base, lane, C.challenger_longitudinal, C.challenger_position_deviation,
+                C.challenger_speed_deviation, 1.0, true);
   const int dest = C.ego_destination >= 0 ? C.ego_destination : 1 + (int)pcg_bounded(g, 3);
   const double lon = C.ego_longitudinal + C.ego_deviation * (1.0 + pcg_normal(g));
-  int n = slots_count(st, base);
+  int n = wave_count(st, base, lane);
   if (n >= st.n_veh) n = st.n_veh - 1;  // no slot left: the last vehicle gives way to the ego
-  const size_t k = base + n;
-  slot_clear<T>(st, k);
   const LaneT<double> L = make_lane<double>(R, C.ego_lane);
   double ex, ey;
   lane_position(L, lon, 0.0, ex, ey);
   const double eh = heading_at(L, C.ego_heading_s);
-  st.kind[k] = TTRL_MDP;
-  ((T*)st.x)[k] = T(ex); ((T*)st.y)[k] = T(ey); ((T*)st.heading)[k] = T(eh); ((T*)st.speed)[k] = T(C.ego_speed);
-  st.lane[k] = st.target_lane[k] = closest_lane_d(R, ex, ey, eh);
-  const int si = speed_to_index(P, C.ego_speed);
-  st.speed_index[k] = si;
-  ((T*)st.target_speed)[k] = T(P.target_speeds[si]);
-  plan_route(st, R, C, k, dest);
-  // list.remove while iterating: positions shift left, the iterator index still advances
-  unsigned keep[8] = {~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u};
-  int lst[256];
-  int len = n + 1;
-  for (int j = 0; j < len; ++j) lst[j] = j;
-  for (int i = 0; i < len; ++i) {
-    const int j = lst[i];
-    const double dx = (double)((const T*)st.x)[base + j] - (double)((const T*)st.x)[k];
-    const double dy = (double)((const T*)st.y)[base + j] - (double)((const T*)st.y)[k];
-    if (j != n && sqrt(dx * dx + dy * dy) < C.ego_clear_distance) {
-      keep[j >> 5] &= ~(1u << (j & 31));
-      for (int q = i; q < len - 1; ++q) lst[q] = lst[q + 1];
-      --len;
+  const int cl = wave_closest_lane(R, ex, ey, eh, lane);
+  if (lane == 0) {
+    Row<T> r = row_absent<T>();
+    r.kind = TTRL_MDP;
+    r.f[0] = T(ex); r.f[1] = T(ey); r.f[2] = T(eh); r.f[3] = T(C.ego_speed);
+    r.lane = r.tgt = cl;
+    r.sidx = speed_to_index(P, C.ego_speed);
+    r.f[4] = T(P.target_speeds[r.sidx]);
+    plan_route(R, C, cl, dest, r.route_road, r.route_lane, r.route_n);
+    row_store<T>(st, base + n, r);
+  }
+  __syncthreads();
+  // which vehicles are within ego_clear_distance (the ego's stored position, as the reference's
+  // np.linalg.norm(v.position - ego_vehicle.position))
+  const T exs = ((const T*)st.x)[base + n], eys = ((const T*)st.y)[base + n];
+  unsigned long long nearw[4] = {0, 0, 0, 0};
+  for (int c0 = 0; c0 < n + 1; c0 += 64) {
+    const int j = c0 + lane;
+    bool nr = false;
+    if (j < n) {
+      const double dx = (double)((const T*)st.x)[base + j] - (double)exs;
+      const double dy = (double)((const T*)st.y)[base + j] - (double)eys;
+      nr = sqrt(dx * dx + dy * dy) < C.ego_clear_distance;
+    }
+    nearw[c0 >> 6] = __ballot(nr);
+  }
+  // list.remove while iterating (uniform on every lane): positions shift left after a removal
+  // while the iterator index still advances, so the vehicle after each removed one is skipped
+  unsigned long long keep[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+  {
+    int i = 0, removed = 0;  // i: iterator index; list position p holds slot p + removed (until then)
+    int j = 0;               // the slot at position i
+    while (true) {
+      j = i + removed;
+      if (j > n) break;
+      if (j != n && ((nearw[j >> 6] >> (j & 63)) & 1ull)) {
+        keep[j >> 6] &= ~(1ull << (j & 63));
+        ++removed;
+      }
+      ++i;
     }
   }
-  slots_compact<T>(st, base, keep);
-  rng_store(g, w);
+  wave_compact<T>(st, base, keep, lane);
+  if (lane == 0) rng_store(g, w);
 }
 
 // IntersectionEnv.step tail (intersection_env.py:135-139): _clear_vehicles (:350-362) keeps the
 // controlled vehicle and every vehicle neither leaving (an "il"->"o" lane within 4 lengths of its
 // end) nor without a route, in list order; then _spawn_vehicle(spawn_probability).
 template <typename T>
-__global__ void ix_clear_spawn_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_ix_cfg_t C,
-                                      const uint8_t* __restrict__ mask) {
-  const int env = blockIdx.x * blockDim.x + threadIdx.x;
-  if (env >= st.n_envs || (mask && !mask[env])) return;
+__global__ void __launch_bounds__(64) ix_clear_spawn_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P,
+                                                            ttrl_ix_cfg_t C, const uint8_t* __restrict__ mask) {
+  const int env = blockIdx.x, lane = threadIdx.x;
+  if (mask && !mask[env]) return;
   const size_t base = (size_t)env * st.n_veh;
-  unsigned keep[8] = {~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u};
-  for (int j = 0; j < st.n_veh; ++j) {
-    const size_t k = base + j;
-    if (st.kind[k] != TTRL_IDM) continue;
-    const int l = st.lane[k];
-    T s, r;
-    lane_local(make_lane<T>(R, l), ((const T*)st.x)[k], ((const T*)st.y)[k], s, r);
-    const bool leaving = R.exit_lane[l] && s >= T(R.length[l]) - T(C.leave_margin);
-    if (leaving || st.route_n[k] < 0) keep[j >> 5] &= ~(1u << (j & 31));
+  unsigned long long keep[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+  for (int c0 = 0; c0 < st.n_veh; c0 += 64) {
+    const int j = c0 + lane;
+    bool drop = false;
+    if (j < st.n_veh && st.kind[base + j] == TTRL_IDM) {
+      const size_t k = base + j;
+      const int l = st.lane[k];
+      T s, r;
+      lane_local(make_lane<T>(R, l), ((const T*)st.x)[k], ((const T*)st.y)[k], s, r);
+      const bool leaving = R.exit_lane[l] && s >= T(R.length[l]) - T(C.leave_margin);
+      drop = leaving || st.route_n[k] < 0;
+    }
+    keep[c0 >> 6] = ~__ballot(drop);
   }
-  slots_compact<T>(st, base, keep);
+  wave_compact<T>(st, base, keep, lane);
   uint64_t* w = st.rng + (size_t)env * TTRL_RNG_WORDS;
   Pcg g = rng_load(w);
-  ix_spawn<T>(st, R, P, C, g, base, 0.0, 1.0, 1.0, C.spawn_probability, false);
-  rng_store(g, w);
+  wave_spawn<T>(st, R, P, C, g, base, lane, 0.0, 1.0, 1.0, C.spawn_probability, false);
+  if (lane == 0) rng_store(g, w);
 }
 
 // ------------------------------------------------------------------- launch helpers
@@ -2907,7 +2991,7 @@ int ttrl_ix_reset(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
   if (!entropy || n_words < 1 || n_words > 64) return TTRL_E_ARG;
   if (s->n_envs == 0) return TTRL_OK;
   hipStream_t st = (hipStream_t)stream;
-  const int blocks = (s->n_envs + 63) / 64;
+  const int blocks = s->n_envs;  // one wavefront per env
   if (s->dtype == TTRL_F64)
     hipLaunchKernelGGL(ix_begin_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg,
                        (const unsigned*)entropy, (int)n_words, mask);
@@ -2931,7 +3015,7 @@ int ttrl_ix_clear_spawn(const ttrl_state_t* s, const ttrl_lane_table_t* road, co
   if (rc) return rc;
   if (s->n_envs == 0) return TTRL_OK;
   hipStream_t st = (hipStream_t)stream;
-  const int blocks = (s->n_envs + 63) / 64;
+  const int blocks = s->n_envs;  // one wavefront per env
   if (s->dtype == TTRL_F64)
     hipLaunchKernelGGL(ix_clear_spawn_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg, mask);
   else
