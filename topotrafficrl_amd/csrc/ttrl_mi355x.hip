@@ -107,11 +107,18 @@ template <typename T> struct LaneT {
   int road, lid, rfirst, rn, prio;  // network: road, id within it, the road's first lane and lane count
 };
 
-// Out of line, with scalar arguments (a struct argument would be materialised in scratch):
-// the curved lanes' trigonometry stays off the straight-road register budget.
+// Scalar arguments (a struct argument would be materialised in scratch); compiled out of the
+// straight-road instance, so the curved lanes' trigonometry stays off its register budget.
 template <typename T> struct Pair { T a, b; };
+// Inlined: the curved-lane geometry runs only in the NET_CURVED / NET_GRAPH instances, where
+// the call overhead cost more than the registers (intersection f64 launch 1.84 -> 1.60 ms).
+#ifdef TTRL_CURVED_NOINLINE
+#define TTRL_CURVED_ATTR __noinline__
+#else
+#define TTRL_CURVED_ATTR __forceinline__
+#endif
 template <typename T>
-__device__ __noinline__ Pair<T> curved_local(int type, T px, T py, T sx, T sy, T ux, T uy, T amp, T puls, T ph,
+__device__ TTRL_CURVED_ATTR Pair<T> curved_local(int type, T px, T py, T sx, T sy, T ux, T uy, T amp, T puls, T ph,
                                              T cx, T cy, T rad, T sph, T dirn) {
   Pair<T> o;
   if (type == TTRL_LANE_SINE) {  // SineLane.local_coordinates lane.py:275-279
@@ -146,7 +153,7 @@ __device__ __forceinline__ void lane_local(const LaneT<T>& L, T px, T py, T& s, 
 }
 
 template <typename T>
-__device__ __noinline__ T curved_heading(int type, T s, T hd, T amp, T puls, T ph, T rad, T sph, T dirn) {
+__device__ TTRL_CURVED_ATTR T curved_heading(int type, T s, T hd, T amp, T puls, T ph, T rad, T sph, T dirn) {
   if (type == TTRL_LANE_SINE)  // SineLane.heading_at lane.py:269-273
     return hd + t_atan(amp * puls * t_cos(puls * s + ph));
   const T phi = dirn * s / rad + sph;  // CircularLane.heading_at lane.py:318-321
