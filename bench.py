@@ -159,6 +159,8 @@ def main():
     def one_step(t):
         nonlocal obs
         if sg is not None:
+            if ix and t >= args.warmup:
+                live.add_((env.state["kind"] != 0).sum())
             if policy is None:
                 sg.set_actions(acts[t])
             sg.replay()

@@ -130,3 +130,23 @@ def test_grid_and_lidar_observe_the_intersection_ego(hip_device):
     want = o.observe_lidar(h, lc)
     assert np.max(np.abs(got - want)) <= 1e-6
     BatchedRoad(net, st, P_IX)  # the network table is a valid BatchedRoad network
+
+
+def test_intersection_step_graph_equals_eager(hip_device):
+    """graph.StepGraph captures the whole intersection step, auto-reset included (device-only
+    masks, counters and masked resets); replays equal eager steps bit for bit."""
+    from topotrafficrl_amd.graph import StepGraph
+    cfg = {**ENV_JSON, "num_envs": 32, "device": hip_device, "auto_reset": True, "duration": 4}
+    eager, graphed = VecIntersectionEnv(cfg), VecIntersectionEnv(cfg)
+    o1, _ = eager.reset(seed=5)
+    o2, _ = graphed.reset(seed=5)
+    sg = StepGraph(graphed, o2, None, warmup=1)
+    g = torch.Generator(device=hip_device).manual_seed(0)
+    for t in range(9):  # two auto-reset rounds (duration 4) plus crashes / arrivals
+        a = torch.randint(0, 3, (32,), device=hip_device, generator=g)
+        o1, r1, te1, tr1, _ = eager.step(a)
+        sg.set_actions(a)
+        o2, r2, te2, tr2 = sg.replay()
+        assert torch.equal(o1, o2) and torch.equal(r1, r2) and torch.equal(te1, te2) and torch.equal(tr1, tr2), t
+    for k in ("x", "kind", "rng", "route_road"):
+        assert torch.equal(eager.state[k], graphed.state[k]), k

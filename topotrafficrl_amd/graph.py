@@ -9,9 +9,10 @@ tracing compiler on this path.
 
 Graph semantics: the tensors a replay returns are static buffers overwritten by the next
 replay (clone what you keep); ``epsilon`` is a device scalar refreshed before each replay,
-so the exploration schedule keeps advancing; the env must not auto-reset (its mask is a
-device op, but the capture would freeze the seed schedule's host side — use
-``VecHighwayEnv(auto_reset=False)`` inside graphs).
+so the exploration schedule keeps advancing.  ``VecHighwayEnv`` must not auto-reset inside a
+graph (use ``auto_reset=False``); ``VecIntersectionEnv`` may (``GRAPH_AUTO_RESET``): its
+done mask, episode counters, seeds and masked resets are all device tensors and launches, so a
+replay resets exactly the envs an eager step would.
 """
 from __future__ import annotations
 
@@ -25,8 +26,8 @@ class StepGraph:
     from a static buffer the caller fills via ``set_actions``)."""
 
     def __init__(self, env, obs: torch.Tensor, policy=None, warmup: int = 2):
-        if env.config.get("auto_reset"):
-            raise ValueError("StepGraph needs auto_reset=False")
+        if env.config.get("auto_reset") and not getattr(env, "GRAPH_AUTO_RESET", False):
+            raise ValueError("StepGraph needs auto_reset=False for this env")
         self.env, self.policy = env, policy
         dev = env.device
         self.obs = obs.clone()
@@ -37,11 +38,15 @@ class StepGraph:
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # warm up allocator pools and lazy initialisation off-graph
             saved = env.state.clone(), env.time.clone(), self.obs.clone()
+            entropy = getattr(env, "_entropy", None)
+            saved_entropy = entropy.clone() if isinstance(entropy, torch.Tensor) else None
             for _ in range(warmup):
                 self._body()
             env.state.copy_(saved[0])
             env.time.copy_(saved[1])
             self.obs.copy_(saved[2])
+            if saved_entropy is not None:
+                entropy.copy_(saved_entropy)
         torch.cuda.current_stream(dev).wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
         if policy is not None:

@@ -224,6 +224,7 @@ class VecIntersectionEnv:
     metadata = {"render_modes": []}
     PERCEPTION_DISTANCE = 5.0 * 40.0  # abstract.py:41
     SHUFFLE_RNG = "np_random"         # order="shuffled" draws from each env's np_random
+    GRAPH_AUTO_RESET = True           # auto-reset is device-only: graph.StepGraph may capture it
     ACTIONS = {0: "SLOWER", 1: "IDLE", 2: "FASTER"}
 
     def __init__(self, config: dict | None = None, render_mode: str | None = None) -> None:
