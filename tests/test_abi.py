@@ -35,7 +35,8 @@ def test_library_loads_and_exports_every_declared_symbol():
 def test_ctypes_mirror_matches_c_layout(tmp_path):
     structs = {"ttrl_lane_table_t": _abi.LaneTable, "ttrl_params_t": _abi.Params, "ttrl_state_t": _abi.State,
                "ttrl_kin_cfg_t": _abi.KinCfg, "ttrl_grid_cfg_t": _abi.GridCfg, "ttrl_reset_cfg_t": _abi.ResetCfg,
-               "ttrl_reward_cfg_t": _abi.RewardCfg, "ttrl_ttc_cfg_t": _abi.TtcCfg, "ttrl_lidar_cfg_t": _abi.LidarCfg}
+               "ttrl_reward_cfg_t": _abi.RewardCfg, "ttrl_ttc_cfg_t": _abi.TtcCfg, "ttrl_lidar_cfg_t": _abi.LidarCfg,
+               "ttrl_ix_cfg_t": _abi.IxCfg}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "ttrl_mi355x.h"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
@@ -68,6 +69,16 @@ def test_argument_errors_need_no_device():
     bad.n_lanes = 99
     s.dtype = _abi.F64
     assert lib.ttrl_neighbours(C.byref(s), C.byref(bad), None, None, None, None) == -1
+    # the intersection entry points need the network fields and np_random (state.rng)
+    from topotrafficrl_amd.intersection import VecIntersectionEnv, intersection_network, ix_cfg
+    net = intersection_network()
+    cfg = ix_cfg(net, VecIntersectionEnv.default_config(), p)
+    words = (C.c_uint32 * 4)(1, 2, 3, 4)
+    assert lib.ttrl_ix_reset(C.byref(s), C.byref(net.table), C.byref(p), C.byref(cfg), words, 1, None, None) == -1
+    assert lib.ttrl_ix_clear_spawn(C.byref(s), C.byref(net.table), C.byref(p), C.byref(cfg), None, None) == -1
+    kin = _abi.kin_cfg(order="shuffled", shuffle_rng="np_random")
+    assert lib.ttrl_observe_kinematics_masked(C.byref(s), C.byref(lanes), C.byref(p), C.byref(kin), None, None,
+                                              None, None) == -1
 
 
 def test_product_refuses_to_run_without_hip_library(tmp_path):

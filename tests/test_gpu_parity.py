@@ -327,3 +327,29 @@ def test_collision_pair_queue_overflow_vs_oracle(hip_device):
         imp = h["has_impact"].astype(bool)
         for k in ("impact_x", "impact_y"):
             assert np.max(np.abs(d[k][imp] - h[k][imp])) < 1e-9, k
+
+
+def test_empty_batch_and_largest_slot_class(hip_device):
+    """n_envs = 0 is a no-op for every entry point; n_veh = 256 (the largest slot class) runs
+    the fused rollout equal to the oracle."""
+    lanes = _abi.straight_lane_table(4)
+    empty = BatchState(0, 64, device=hip_device)
+    road = BatchedRoad(RoadNetwork(lanes), empty, P)
+    road.simulate(torch.zeros(0, dtype=torch.int32), 15, 1 / 15)
+    road.act()
+    road.step(1 / 15)
+    from topotrafficrl_amd.observation import kinematics, occupancy_grid
+    out, _ = kinematics(empty, RoadNetwork(lanes), P, _abi.kin_cfg())
+    assert out.shape[0] == 0
+    assert occupancy_grid(empty, RoadNetwork(lanes), P, _abi.grid_cfg()).shape[0] == 0
+    torch.cuda.synchronize()
+    E, n = 4, 256
+    o = Oracle(lanes, P)
+    h = HostState(E, n)
+    o.reset_highway(h, _abi.reset_cfg(n, lanes), [7, 8, 9, 10])
+    dev = to_dev(h, hip_device)
+    road = BatchedRoad(RoadNetwork(lanes), dev, P)
+    acts = np.array([0, 1, 3, 4], dtype=np.int32)
+    o.simulate(h, acts, 15, 1 / 15)
+    road.simulate(torch.from_numpy(acts), 15, 1 / 15)
+    compare(dev, h, 1e-6)

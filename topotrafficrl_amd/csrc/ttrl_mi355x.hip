@@ -2683,10 +2683,14 @@ __global__ void __launch_bounds__(64) ix_clear_spawn_kernel(ttrl_state_t st, ttr
 // A network beyond one road, or a RegulatedRoad: the simulate kernel's NET_GRAPH instance.
 bool is_graph(const ttrl_lane_table_t& R) { return R.n_roads > 1 || R.regulation_frequency > 0; }
 
+// TTRL_OK, a negative TTRL_E_* code, or EMPTY (> 0: no env, nothing to do -- the entry points
+// then return TTRL_OK before looking at buffers an empty batch need not have)
+constexpr int EMPTY = 1;
 int check_state(const ttrl_state_t* s, const ttrl_lane_table_t* R) {
   if (!s || !R) return TTRL_E_ARG;
   if (s->dtype != TTRL_F32 && s->dtype != TTRL_F64) return TTRL_E_ARG;
   if (s->n_envs < 0 || s->n_veh < 1 || s->n_veh > 256) return TTRL_E_ARG;
+  if (s->n_envs == 0) return EMPTY;
   if (R->n_lanes < 1 || R->n_lanes > LMAX) return TTRL_E_ARG;
   if (R->n_roads < 1 || R->n_roads > TTRL_MAX_ROADS || R->regulation_frequency < 0) return TTRL_E_ARG;
   for (int l = 0; l < R->n_lanes; ++l)  // topology consistent (lanes of a road contiguous, in id order)
@@ -2742,7 +2746,7 @@ int dispatch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_p
 int run_sim(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P, const int32_t* actions,
             int frames, double dt, int mode, void* stream, int ablate = 0, const uint8_t* mask = nullptr) {
   int rc = check_state(s, R);
-  if (rc) return rc;
+  if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!P || frames < 0 || P->n_target_speeds < 1 || P->n_target_speeds > 8) return TTRL_E_ARG;
   hipStream_t st = (hipStream_t)stream;
   return s->dtype == TTRL_F64 ? dispatch_sim<double>(*s, *R, *P, actions, mask, frames, dt, mode, ablate, st)
@@ -2836,7 +2840,7 @@ int ttrl_diag_phase_read(unsigned long long* out) {
 int ttrl_neighbours(const ttrl_state_t* s, const ttrl_lane_table_t* road, const int32_t* query_lane,
                     int32_t* front, int32_t* rear, void* stream) {
   int rc = check_state(s, road);
-  if (rc) return rc;
+  if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!front || !rear) return TTRL_E_ARG;
   ttrl_params_t P{};
   P.lane_vehicle_length = 5.0;  // AbstractLane.VEHICLE_LENGTH
@@ -2849,7 +2853,7 @@ int ttrl_observe_kinematics_masked(const ttrl_state_t* s, const ttrl_lane_table_
                                    const ttrl_kin_cfg_t* cfg, const uint8_t* mask, float* out, int32_t* ids,
                                    void* stream) {
   int rc = check_state(s, road);
-  if (rc) return rc;
+  if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!p || !cfg || !out || cfg->vehicles_count < 1 || cfg->n_features < 1 || cfg->n_features > TTRL_N_FEATURES)
     return TTRL_E_ARG;
   if (cfg->order_shuffled < 0 || cfg->order_shuffled > 2) return TTRL_E_ARG;
@@ -2869,7 +2873,7 @@ int ttrl_observe_kinematics(const ttrl_state_t* s, const ttrl_lane_table_t* road
 int ttrl_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                       const ttrl_grid_cfg_t* cfg, float* out, void* stream) {
   int rc = check_state(s, road);
-  if (rc) return rc;
+  if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!p || !cfg || !out || cfg->n_features < 1 || cfg->n_features > TTRL_N_FEATURES || cfg->shape_x < 1 ||
       cfg->shape_y < 1 || cfg->step_x <= 0 || cfg->step_y <= 0)
     return TTRL_E_ARG;
@@ -2890,7 +2894,7 @@ int ttrl_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
 int ttrl_observe_ttc(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                      const ttrl_ttc_cfg_t* cfg, float* out, void* stream) {
   int rc = check_state(s, road);
-  if (rc) return rc;
+  if (rc) return rc < 0 ? rc : TTRL_OK;
   const bool raw = cfg && cfg->obs_lanes == 0 && cfg->obs_speeds == 0;
   if (!p || !cfg || !out || cfg->horizon_bins < 1 || cfg->horizon_bins > 64 || (!raw && cfg->obs_lanes < 1) ||
       (!raw && cfg->obs_speeds < 1) || !(cfg->time_quantization > 0) || p->n_target_speeds < 1 ||
@@ -2909,7 +2913,7 @@ int ttrl_observe_ttc(const ttrl_state_t* s, const ttrl_lane_table_t* road, const
 int ttrl_observe_lidar(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                        const ttrl_lidar_cfg_t* cfg, float* out, void* stream) {
   int rc = check_state(s, road);
-  if (rc) return rc;
+  if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!p || !cfg || !out || cfg->cells < 1 || cfg->cells > 64 || !(cfg->maximum_range > 0)) return TTRL_E_ARG;
   if (s->n_envs == 0) return TTRL_OK;
   hipStream_t st = (hipStream_t)stream;
@@ -2923,7 +2927,7 @@ int ttrl_observe_lidar(const ttrl_state_t* s, const ttrl_lane_table_t* road, con
 int ttrl_reset_highway(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                        const ttrl_reset_cfg_t* cfg, const uint64_t* pcg, void* stream) {
   int rc = check_state(s, road);
-  if (rc) return rc;
+  if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!p || !cfg || !pcg || cfg->n_vehicles < 1 || cfg->n_vehicles > s->n_veh || cfg->ego_lane < 0 ||
       cfg->ego_lane >= road->n_lanes || p->n_target_speeds < 1 || p->n_target_speeds > 8)
     return TTRL_E_ARG;
@@ -2943,7 +2947,7 @@ int ttrl_reset_highway_seeded(const ttrl_state_t* s, const ttrl_lane_table_t* ro
                               const ttrl_reset_cfg_t* cfg, const uint32_t* entropy, int32_t n_words,
                               const uint8_t* mask, void* stream) {
   int rc = check_state(s, road);
-  if (rc) return rc;
+  if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!p || !cfg || !entropy || n_words < 1 || n_words > 64 || cfg->n_vehicles < 1 || cfg->n_vehicles > s->n_veh ||
       cfg->ego_lane < 0 || cfg->ego_lane >= road->n_lanes || p->n_target_speeds < 1 || p->n_target_speeds > 8)
     return TTRL_E_ARG;
@@ -2969,7 +2973,7 @@ int ttrl_seed_pcg64(const uint32_t* entropy, int32_t n_words, uint64_t* state4) 
 
 static int check_ix(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* p, const ttrl_ix_cfg_t* c) {
   int rc = check_state(s, R);
-  if (rc) return rc;
+  if (rc) return rc;  // EMPTY propagates
   if (!p || !c || !s->rng || !s->route_road || !s->route_lane || !s->route_n || !s->yielding || !s->reg_steps)
     return TTRL_E_ARG;
   if (p->n_target_speeds < 1 || p->n_target_speeds > 8 || c->n_corners != 4) return TTRL_E_ARG;
@@ -2994,7 +2998,7 @@ int ttrl_ix_reset(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
                   const ttrl_ix_cfg_t* cfg, const uint32_t* entropy, int32_t n_words, const uint8_t* mask,
                   void* stream) {
   int rc = check_ix(s, road, p, cfg);
-  if (rc) return rc;
+  if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!entropy || n_words < 1 || n_words > 64) return TTRL_E_ARG;
   if (s->n_envs == 0) return TTRL_OK;
   hipStream_t st = (hipStream_t)stream;
@@ -3019,7 +3023,7 @@ int ttrl_ix_reset(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
 int ttrl_ix_clear_spawn(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                         const ttrl_ix_cfg_t* cfg, const uint8_t* mask, void* stream) {
   int rc = check_ix(s, road, p, cfg);
-  if (rc) return rc;
+  if (rc) return rc < 0 ? rc : TTRL_OK;
   if (s->n_envs == 0) return TTRL_OK;
   hipStream_t st = (hipStream_t)stream;
   const int blocks = s->n_envs;  // one wavefront per env
@@ -3033,7 +3037,7 @@ int ttrl_ix_clear_spawn(const ttrl_state_t* s, const ttrl_lane_table_t* road, co
 int ttrl_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_reward_cfg_t* cfg,
                  const double* time, float* reward, uint8_t* terminated, uint8_t* truncated, void* stream) {
   int rc = check_state(s, road);
-  if (rc) return rc;
+  if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!cfg || !time || !reward || !terminated || !truncated) return TTRL_E_ARG;
   if (s->n_envs == 0) return TTRL_OK;
   hipStream_t st = (hipStream_t)stream;
