@@ -66,6 +66,10 @@ class BatchState:
                                              self.n_envs, self.n_veh, self.abi_dtype)
         return self._struct
 
+    def tensors(self) -> list:
+        """The state tensors in _abi.ALL_FIELDS order (the ``state`` argument of torch.ops.ttrl)."""
+        return [self.t[f] for f in _abi.ALL_FIELDS]
+
     def ego_index(self) -> torch.Tensor:
         """[E] slot of each env's controlled vehicle: its first MDP slot (AbstractEnv.vehicle)."""
         return (self.t["kind"] == _abi.MDP).to(torch.int8).argmax(dim=1)
