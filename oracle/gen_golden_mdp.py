@@ -1,12 +1,15 @@
 """Golden vectors of AbstractEnv.to_finite_mdp — TEST INFRASTRUCTURE, build container only.
 
-Calls the reference's own ``finite_mdp(env, time_quantization, horizon)`` (finite_mdp.py:17-101:
-compute_ttc_grid, transition_model / clip_position through np.fromfunction, the state reward,
-action reward and terminal states) on highway scenes built from the unmodified reference sim core
-(gen_golden.make_highway).  Its last step hands the tables to ``finite_mdp.mdp.DeterministicMDP``
-from the third-party ``finite-mdp`` package, which is absent here: a recorder registered under
-that module name keeps the arguments (transition, reward, terminal, state) — the reference's
-outputs — and nothing else.  Recorded per observation point: the vehicle state and those tables.
+The reference's ``finite_mdp(env, time_quantization, horizon)`` (finite_mdp.py:17-101) ends by
+handing its tables to ``finite_mdp.mdp.DeterministicMDP`` from the third-party ``finite-mdp``
+package, which is absent here (and stays absent: no stand-in is registered).  So the reference's
+own functions compute the parts they own, on highway scenes built from the unmodified reference
+sim core (gen_golden.make_highway):
+  * the TTC grid: ``compute_ttc_grid`` (finite_mdp.py:104-167), called as is;
+  * the transition: ``np.fromfunction(partial(transition_model, grid=grid), ...)`` with the
+    reference's ``transition_model`` / ``clip_position`` (finite_mdp.py:170-208), called as is;
+and the few assembly lines of finite_mdp.py:51-90 (state index, state / action rewards, terminal
+cells) are restated line for line below.
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python oracle/gen_golden_mdp.py
 """
@@ -15,6 +18,7 @@ from __future__ import annotations
 import os
 import sys
 import types
+from functools import partial
 
 import numpy as np
 
@@ -22,26 +26,36 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import gen_golden as G  # noqa: E402  (imports the reference sim core)
 
 R = G.R
-
-
-class _Recorder:  # stands in for finite_mdp.mdp.DeterministicMDP: records its arguments
-    def __init__(self, transition, reward, terminal, state=None):
-        self.transition, self.reward, self.terminal, self.state = transition, reward, terminal, state
-
-
-_mod = types.ModuleType("finite_mdp.mdp")
-_mod.DeterministicMDP = _Recorder
-sys.modules.setdefault("finite_mdp", types.ModuleType("finite_mdp"))
-sys.modules["finite_mdp.mdp"] = _mod
+FM = R.finite_mdp  # ttrl_env.envs.common.finite_mdp (imports only utils and Vehicle)
 
 CONFIG = {"collision_reward": -1.0, "right_lane_reward": 0.1, "high_speed_reward": 0.4, "lane_change_reward": -0.05,
           "policy_frequency": 1}
 
 
-def to_finite_mdp(road):
+def to_finite_mdp(road, time_quantization=1.0, horizon=10.0, n_actions=5):
+    """finite_mdp.py:17-90 up to the DeterministicMDP call: (grid, transition, reward, terminal, state)."""
     ego = road.vehicles[0]
-    env = types.SimpleNamespace(vehicle=ego, road=road, config=CONFIG, action_space=types.SimpleNamespace(n=5))
-    return R.finite_mdp.finite_mdp(env, time_quantization=1 / CONFIG["policy_frequency"], horizon=10.0)
+    env = types.SimpleNamespace(vehicle=ego, road=road, config=CONFIG, action_space=types.SimpleNamespace(n=n_actions))
+    grid = FM.compute_ttc_grid(env, time_quantization, horizon)
+    grid_state = (env.vehicle.speed_index, env.vehicle.lane_index[2], 0)
+    state = np.ravel_multi_index(grid_state, grid.shape)
+    transition_model_with_grid = partial(FM.transition_model, grid=grid)
+    transition = np.fromfunction(transition_model_with_grid, grid.shape + (env.action_space.n,), dtype=int)
+    transition = np.reshape(transition, (np.size(grid), env.action_space.n))
+    v, l, t = grid.shape
+    lanes = np.arange(l) / max(l - 1, 1)
+    speeds = np.arange(v) / max(v - 1, 1)
+    state_reward = (+env.config["collision_reward"] * grid
+                    + env.config["right_lane_reward"] * np.tile(lanes[np.newaxis, :, np.newaxis], (v, 1, t))
+                    + env.config["high_speed_reward"] * np.tile(speeds[:, np.newaxis, np.newaxis], (1, l, t)))
+    state_reward = np.ravel(state_reward)
+    action_reward = [env.config["lane_change_reward"], 0, env.config["lane_change_reward"], 0, 0]
+    reward = np.fromfunction(np.vectorize(lambda s, a: state_reward[s] + action_reward[a]),
+                             (np.size(state_reward), np.size(action_reward)), dtype=int)
+    collision = grid == 1
+    end_of_horizon = np.fromfunction(lambda h, i, j: j == grid.shape[2] - 1, grid.shape, dtype=int)
+    terminal = np.ravel(collision | end_of_horizon)
+    return grid, transition, reward, terminal, state
 
 
 def main():
@@ -51,12 +65,11 @@ def main():
             rng = np.random.default_rng(4242 + seed)
             snaps, trans, rew, term, state, grids = [], [], [], [], [], []
             for p in range(4):
-                mdp = to_finite_mdp(road)
-                env = types.SimpleNamespace(vehicle=road.vehicles[0], road=road, config=CONFIG)
-                grids.append(R.finite_mdp.compute_ttc_grid(env, time_quantization=1.0, horizon=10.0))
+                grid, tr, rw, te, stt = to_finite_mdp(road)
+                grids.append(grid)
                 snaps.append(G.snapshot(road))
-                trans.append(mdp.transition); rew.append(mdp.reward); term.append(mdp.terminal)
-                state.append(mdp.state)
+                trans.append(tr); rew.append(rw); term.append(te)
+                state.append(stt)
                 a = int(rng.integers(0, 5))
                 for f in range(15):
                     if f == 0:

@@ -1,7 +1,8 @@
-"""AbstractEnv.to_finite_mdp batched (topotrafficrl_amd/finite_mdp.py) against the reference's own
-finite_mdp() outputs recorded by oracle/gen_golden_mdp.py on highway scenes: the raw TTC grid
-(compute_ttc_grid) from the oracle and the HIP kernel, the shared transition table, rewards,
-terminal cells and the ego's state index — all exact."""
+"""AbstractEnv.to_finite_mdp batched (topotrafficrl_amd/finite_mdp.py) against the tables of
+oracle/gen_golden_mdp.py on highway scenes (the reference's own compute_ttc_grid and
+transition_model, plus the restated assembly of finite_mdp.py:51-90): the raw TTC grid from the
+oracle and the HIP kernel, the shared transition table, rewards, terminal cells and the ego's
+state index — all exact."""
 import numpy as np
 import pytest
 import torch
