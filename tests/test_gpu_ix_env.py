@@ -150,3 +150,52 @@ def test_intersection_step_graph_equals_eager(hip_device):
         assert torch.equal(o1, o2) and torch.equal(r1, r2) and torch.equal(te1, te2) and torch.equal(tr1, tr2), t
     for k in ("x", "kind", "rng", "route_road"):
         assert torch.equal(eager.state[k], graphed.state[k]), k
+
+
+def test_f32_intersection_steps_vs_golden(hip_device):
+    """fp32 fast path on the intersection: one fused 15-frame step from every golden pre-step
+    state; continuous fields within 1e-2 relative away from standstill (the highway fp32 tests
+    hold 2e-3 over ONE frame; 15 frames through the turns' float atan2 compound it: seen 2.07e-3),
+    discrete flips (lanes, routes, yields, crashes) at most a handful over all 78 steps."""
+    from observation_helpers import batch_of_ix_states
+    from test_gpu_parity import to_dev
+    from test_ix_oracle import LONGI
+    from topotrafficrl_amd.road import BatchedRoad
+    pre = batch_of_ix_states(GOLD, "pre")
+    cases = [(d, p) for d in GOLD for p in range(int(d["meta"][1]))]
+    post = HostState(pre.E, 32)
+    for e, (d, p) in enumerate(cases):
+        g = HostState.from_ix(d, "frame", (p, 14), pad_to=32)
+        for k in post.a:
+            post.a[k][e] = g.a[k][0]
+    net = intersection_network()
+    dev = to_dev(pre, hip_device, dtype="f32")
+    road = BatchedRoad(net, dev, P_IX)
+    road.simulate(torch.tensor([LONGI[int(d["actions"][p])] for d, p in cases]), 15, 1 / 15)
+    out = dev.to_numpy()
+    flips = 0
+    for e in range(pre.E):
+        n = int((post["kind"][e] > 0).sum())
+        same = all(np.array_equal(out[k][e, :n], post[k][e, :n]) for k in
+                   ("lane", "target_lane", "crashed", "yielding", "route_n", "route_road"))
+        if not same:
+            flips += 1
+            continue
+        moving = np.abs(post["speed"][e, :n]) >= 0.1
+        for k in ("x", "y", "heading", "speed"):
+            err = np.abs(out[k][e, :n] - post[k][e, :n]) / (1 + np.abs(post[k][e, :n]))
+            assert np.max(err[moving], initial=0.0) <= 1e-2, (e, k)
+    assert flips <= max(2, pre.E // 10), flips
+
+
+def test_dqn_training_on_the_intersection(hip_device):
+    """Trainer hooks + batched DQN learning on VecIntersectionEnv (3 longitudinal actions,
+    auto-reset, the reference's env.json observation)."""
+    from topotrafficrl_amd.trainer import BatchedDQNAgent, BatchedEvaluation
+    env = VecIntersectionEnv({**ENV_JSON, "num_envs": 64, "device": hip_device, "auto_reset": True})
+    agent = BatchedDQNAgent(hip_device, n_actions=3, config={"batch_size": 64, "memory_capacity": 2048,
+                                                              "target_update": 4})
+    ev = BatchedEvaluation(env, agent, num_episodes=1, sim_seed=0, max_steps=8)
+    ev.run_episodes()
+    L = agent.learner
+    assert len(L.memory) == 512 and L.steps == 8 and torch.isfinite(L.last_loss)
