@@ -343,6 +343,10 @@ int ttrl_ego_attention_q(const float* obs, int32_t batch, int32_t n_entities, in
 int ttrl_ix_reset(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                   const ttrl_ix_cfg_t* cfg, const uint32_t* entropy, int32_t n_words, const uint8_t* mask,
                   void* stream);
+/* Copy every row of the envs with mask[e] != 0 (all fields, per-env route / regulation / rng
+ * words included) from src to dst, which have the same shape and dtype: swapping in scenes reset
+ * ahead of time (the intersection's double-buffered auto-reset). */
+int ttrl_copy_envs(const ttrl_state_t* dst, const ttrl_state_t* src, const uint8_t* mask, void* stream);
 /* IntersectionEnv.step tail after the observation and reward: _clear_vehicles (list order kept),
  * then _spawn_vehicle(spawn_probability) drawing from state.rng; envs with mask[e] != 0. */
 int ttrl_ix_clear_spawn(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,

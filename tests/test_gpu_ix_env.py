@@ -136,7 +136,8 @@ def test_intersection_step_graph_equals_eager(hip_device):
     """graph.StepGraph captures the whole intersection step, auto-reset included (device-only
     masks, counters and masked resets); replays equal eager steps bit for bit."""
     from topotrafficrl_amd.graph import StepGraph
-    cfg = {**ENV_JSON, "num_envs": 32, "device": hip_device, "auto_reset": True, "duration": 4}
+    cfg = {**ENV_JSON, "num_envs": 32, "device": hip_device, "auto_reset": True, "duration": 4,
+           "overlap_resets": False}
     eager, graphed = VecIntersectionEnv(cfg), VecIntersectionEnv(cfg)
     o1, _ = eager.reset(seed=5)
     o2, _ = graphed.reset(seed=5)
@@ -199,3 +200,23 @@ def test_dqn_training_on_the_intersection(hip_device):
     ev.run_episodes()
     L = agent.learner
     assert len(L.memory) == 512 and L.steps == 8 and torch.isfinite(L.last_loss)
+
+
+def test_overlapped_resets_equal_in_place_resets(hip_device):
+    """overlap_resets (next-episode scenes prepared on a side stream, swapped in when an env
+    finishes) gives the same trajectories, bit for bit, as resetting in place."""
+    cfg = {**ENV_JSON, "num_envs": 48, "device": hip_device, "auto_reset": True, "duration": 3}
+    a = VecIntersectionEnv({**cfg, "overlap_resets": True})
+    b = VecIntersectionEnv({**cfg, "overlap_resets": False})
+    oa, _ = a.reset(seed=21)
+    ob, _ = b.reset(seed=21)
+    assert torch.equal(oa, ob)
+    g = torch.Generator(device=hip_device).manual_seed(2)
+    for t in range(8):
+        act = torch.randint(0, 3, (48,), device=hip_device, generator=g)
+        ra = a.step(act)
+        rb = b.step(act)
+        for x, y in zip(ra[:4], rb[:4]):
+            assert torch.equal(x, y), t
+    for k in a.state.t:
+        assert torch.equal(a.state[k], b.state[k]), k

@@ -2679,6 +2679,33 @@ __global__ void __launch_bounds__(64) ix_clear_spawn_kernel(ttrl_state_t st, ttr
   if (lane == 0) rng_store(g, w);
 }
 
+// Masked whole-env copy (double-buffered resets): one workgroup per env, the slots on the lanes.
+template <typename T>
+__global__ void __launch_bounds__(64) copy_envs_kernel(ttrl_state_t dst, ttrl_state_t src,
+                                                       const uint8_t* __restrict__ mask) {
+  const int env = blockIdx.x, lane = threadIdx.x;
+  if (!mask[env]) return;
+  const size_t base = (size_t)env * dst.n_veh;
+  const bool net = dst.route_road && src.route_road;
+  for (int j = lane; j < dst.n_veh; j += 64) {
+    const size_t k = base + j;
+#pragma unroll
+    for (int q = 0; q < 11; ++q) real_field<T>(dst, q)[k] = real_field<T>(src, q)[k];
+    dst.lane[k] = src.lane[k]; dst.target_lane[k] = src.target_lane[k]; dst.speed_index[k] = src.speed_index[k];
+    dst.kind[k] = src.kind[k]; dst.crashed[k] = src.crashed[k]; dst.has_impact[k] = src.has_impact[k];
+    dst.lane_change[k] = src.lane_change[k];
+    if (net) {
+      ((int32_t*)dst.route_road)[k] = ((const int32_t*)src.route_road)[k];
+      ((int32_t*)dst.route_lane)[k] = ((const int32_t*)src.route_lane)[k];
+      dst.route_n[k] = src.route_n[k];
+      dst.yielding[k] = src.yielding[k];
+    }
+  }
+  if (lane == 0 && dst.reg_steps && src.reg_steps) dst.reg_steps[env] = src.reg_steps[env];
+  if (lane < TTRL_RNG_WORDS && dst.rng && src.rng)
+    dst.rng[(size_t)env * TTRL_RNG_WORDS + lane] = src.rng[(size_t)env * TTRL_RNG_WORDS + lane];
+}
+
 // ------------------------------------------------------------------- launch helpers
 // A network beyond one road, or a RegulatedRoad: the simulate kernel's NET_GRAPH instance.
 bool is_graph(const ttrl_lane_table_t& R) { return R.n_roads > 1 || R.regulation_frequency > 0; }
@@ -3017,6 +3044,32 @@ int ttrl_ix_reset(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
     hipLaunchKernelGGL(ix_finish_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg, mask);
   else
     hipLaunchKernelGGL(ix_finish_kernel<float>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg, mask);
+  return launch_status();
+}
+
+int ttrl_copy_envs(const ttrl_state_t* dst, const ttrl_state_t* src, const uint8_t* mask, void* stream) {
+  if (!dst || !src || !mask) return TTRL_E_ARG;
+  if (dst->n_envs != src->n_envs || dst->n_veh != src->n_veh || dst->dtype != src->dtype) return TTRL_E_ARG;
+  if (dst->n_envs < 0 || dst->n_veh < 1 || dst->n_veh > 256 || (dst->dtype != TTRL_F32 && dst->dtype != TTRL_F64))
+    return TTRL_E_ARG;
+  if (dst->n_envs == 0) return TTRL_OK;
+  const void* ptrs[] = {dst->x, dst->y, dst->heading, dst->speed, dst->target_speed, dst->timer, dst->delta, dst->steer,
+                        dst->acc, dst->impact_x, dst->impact_y, dst->lane, dst->target_lane, dst->speed_index,
+                        dst->kind, dst->crashed, dst->has_impact, dst->lane_change, src->x, src->y, src->heading,
+                        src->speed, src->target_speed, src->timer, src->delta, src->steer, src->acc, src->impact_x,
+                        src->impact_y, src->lane, src->target_lane, src->speed_index, src->kind, src->crashed,
+                        src->has_impact, src->lane_change};
+  for (const void* q : ptrs)
+    if (!q) return TTRL_E_ARG;
+  if ((dst->route_road != nullptr) != (src->route_road != nullptr)) return TTRL_E_ARG;
+  if (dst->route_road && (!dst->route_lane || !dst->route_n || !dst->yielding || !src->route_lane || !src->route_n ||
+                          !src->yielding))
+    return TTRL_E_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  if (dst->dtype == TTRL_F64)
+    hipLaunchKernelGGL(copy_envs_kernel<double>, dim3(dst->n_envs), dim3(64), 0, st, *dst, *src, mask);
+  else
+    hipLaunchKernelGGL(copy_envs_kernel<float>, dim3(dst->n_envs), dim3(64), 0, st, *dst, *src, mask);
   return launch_status();
 }
 

@@ -198,6 +198,12 @@ def ix_clear_spawn(state: BatchState, network: RoadNetwork, params: _abi.Params,
               None if m is None else m.data_ptr(), _stream(state.device))
 
 
+def copy_envs(dst: BatchState, src: BatchState, mask: torch.Tensor) -> None:
+    """Copy the whole rows of the masked envs from ``src`` into ``dst`` (same shape and dtype)."""
+    m = mask.to(device=dst.device, dtype=torch.uint8).contiguous()
+    _lib.call("ttrl_copy_envs", C.byref(dst.struct()), C.byref(src.struct()), m.data_ptr(), _stream(dst.device))
+
+
 def seed_words(seeds) -> np.ndarray:
     """SeedSequence entropy words of int seeds (numpy splits an int into uint32 words, low first)."""
     out = []
@@ -224,7 +230,6 @@ class VecIntersectionEnv:
     metadata = {"render_modes": []}
     PERCEPTION_DISTANCE = 5.0 * 40.0  # abstract.py:41
     SHUFFLE_RNG = "np_random"         # order="shuffled" draws from each env's np_random
-    GRAPH_AUTO_RESET = True           # auto-reset is device-only: graph.StepGraph may capture it
     ACTIONS = {0: "SLOWER", 1: "IDLE", 2: "FASTER"}
 
     def __init__(self, config: dict | None = None, render_mode: str | None = None) -> None:
@@ -273,6 +278,10 @@ class VecIntersectionEnv:
             "device": "cuda",
             "dtype": "f64",
             "auto_reset": False,
+            # auto-reset from scenes reset ahead of time on a side HIP stream (double buffer): a
+            # finished env swaps in its next episode's scene, whose 45 warm-up frames ran
+            # overlapped with earlier steps, and the following one is prepared in the background
+            "overlap_resets": True,
         }
 
     def configure(self, config: dict | None) -> None:
@@ -302,7 +311,20 @@ class VecIntersectionEnv:
         self._term = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
         self._trunc = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
         self._entropy = None  # [E, words + 1]: seed words, then the auto-reset episode counter
+        self._spare = None    # next-episode scenes (overlap_resets), prepared on self._side
+        if c["auto_reset"] and c["overlap_resets"]:
+            self._spare = BatchState(self.num_envs, int(c["vehicle_slots"]), device=self.device, dtype=c["dtype"])
+            self._side = torch.cuda.Stream(self.device)
+            self._spare_ready = torch.cuda.Event()
+            self._spare_mask = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
+            self._spare_entropy = None
         self.define_spaces()
+
+    @property
+    def GRAPH_AUTO_RESET(self) -> bool:
+        """graph.StepGraph may capture the auto-reset when it runs on the step's own stream (a
+        capture cannot leave the side stream's background reset pending across replays)."""
+        return self._spare is None
 
     def define_spaces(self) -> None:
         """abstract.py:123-130"""
@@ -335,8 +357,22 @@ class VecIntersectionEnv:
         self.steps = 0
         self.done = False
         ix_reset(self.state, self.network, self.params, self.ix, self._entropy[:, :-1])
+        if self._spare is not None:  # every env's second episode, in the background
+            self._spare_entropy = self._entropy.clone()
+            self._spare_entropy[:, -1] += 1
+            self._prepare_spares(None)
         obs = self.observation_type.observe()
         return obs, self._info(obs, None)
+
+    def _prepare_spares(self, mask: torch.Tensor | None) -> None:
+        """Reset the spare scenes of ``mask`` (all envs: None) to their next episode on the side
+        stream, after the main stream's work so far (the swap that consumed them)."""
+        main = torch.cuda.current_stream(self.device)
+        self._side.wait_stream(main)
+        with torch.cuda.stream(self._side):
+            ix_reset(self._spare, self.network, self.params, self.ix, self._spare_entropy,
+                     None if mask is None else self._spare_mask)
+            self._spare_ready.record(self._side)
 
     def step(self, action):
         """IntersectionEnv.step (intersection_env.py:135-139) over AbstractEnv.step (abstract.py:224-250)."""
@@ -375,10 +411,19 @@ class VecIntersectionEnv:
 
     def _auto_reset(self, done: torch.Tensor, obs: torch.Tensor) -> None:
         """Finished envs restart on the device with default_rng([seed words..., episode]) and
-        their first observation is written into ``obs``; the others are untouched."""
+        their first observation is written into ``obs``; the others are untouched.  With
+        overlap_resets the new scene is swapped in from the spare buffer (reset ahead of time,
+        bit-identical) and the episode after it is prepared in the background."""
         d = done.to(torch.int32)
         self._entropy[:, -1] += d
-        ix_reset(self.state, self.network, self.params, self.ix, self._entropy, d)
+        if self._spare is None:
+            ix_reset(self.state, self.network, self.params, self.ix, self._entropy, d)
+        else:
+            torch.cuda.current_stream(self.device).wait_event(self._spare_ready)
+            copy_envs(self.state, self._spare, d)
+            self._spare_mask.copy_(d)
+            self._spare_entropy[:, -1] += d
+            self._prepare_spares(self._spare_mask)
         self.time.masked_fill_(done, 0.0)
         self.observation_type.observe(mask=d, out=obs)
 
