@@ -83,8 +83,10 @@ def test_dqn_agent_checkpoint_roundtrip(tmp_path):
 def test_ego_attention_masks_absent_rows():
     """Rows with presence < 0.5 must not influence Q (models.py:294-300 mask, -1e9 fill)."""
     net = EgoAttentionNetwork(5).reset(torch.Generator().manual_seed(0))
-    x = torch.rand(2, 15, 7)
+    g = torch.Generator().manual_seed(1)
+    x = torch.rand(2, 15, 7, generator=g)
+    x[:, :5, 0] = 1.0  # present rows (with every row masked the softmax is uniform over all 15)
     x[:, 5:, 0] = 0.0
     y = x.clone()
-    y[:, 5:, 1:] = torch.rand(2, 10, 6) * 9
+    y[:, 5:, 1:] = torch.rand(2, 10, 6, generator=g) * 9
     assert torch.allclose(net(x), net(y), atol=1e-6)
