@@ -220,3 +220,18 @@ def test_overlapped_resets_equal_in_place_resets(hip_device):
             assert torch.equal(x, y), t
     for k in a.state.t:
         assert torch.equal(a.state[k], b.state[k]), k
+
+
+def test_deepcopy_forks_an_independent_env(hip_device):
+    """copy.deepcopy (the reference's what-if simulations, abstract.py:342-429) forks state, seeds
+    and spare scenes: both copies then follow the same trajectory independently."""
+    import copy
+    env = VecIntersectionEnv({**ENV_JSON, "num_envs": 16, "device": hip_device, "auto_reset": True, "duration": 2})
+    env.reset(seed=9)
+    fork = copy.deepcopy(env)
+    a = torch.ones(16, dtype=torch.int64, device=hip_device)
+    for _ in range(4):
+        r1 = env.step(a)
+        r2 = fork.step(a)
+        assert torch.equal(r1[0], r2[0]) and torch.equal(r1[1], r2[1])
+    assert torch.equal(env.state["x"], fork.state["x"]) and env.state["x"].data_ptr() != fork.state["x"].data_ptr()

@@ -446,5 +446,15 @@ class VecIntersectionEnv:
         new.state = self.state.clone()
         new.road = BatchedRoad(self.network, new.state, self.params)
         new.time = self.time.clone()
+        if self._entropy is not None:
+            new._entropy = self._entropy.clone()
+        if self._spare is not None:  # its own spare scenes, side stream and event
+            torch.cuda.current_stream(self.device).wait_event(self._spare_ready)
+            new._spare = self._spare.clone()
+            new._spare_entropy = self._spare_entropy.clone()
+            new._spare_mask = self._spare_mask.clone()
+            new._side = torch.cuda.Stream(self.device)
+            new._spare_ready = torch.cuda.Event()
+            new._spare_ready.record(torch.cuda.current_stream(self.device))
         new.define_spaces()
         return new
