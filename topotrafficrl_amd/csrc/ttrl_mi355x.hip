@@ -47,13 +47,18 @@ __device__ TTRL_TRANSC SinCos<double> t_sincos(double x) {
   ::sincos(x, &r.s, &r.c);
   return r;
 }
-__device__ __forceinline__ float t_sin(float x) { return ::sinf(x); }
-__device__ __forceinline__ float t_cos(float x) { return ::cosf(x); }
-__device__ __forceinline__ float t_tan(float x) { return ::tanf(x); }
-__device__ __forceinline__ float t_atan(float x) { return ::atanf(x); }
-__device__ __forceinline__ float t_asin(float x) { return ::asinf(x); }
-__device__ __forceinline__ float t_pow(float x, float y) { return ::powf(x, y); }
-__device__ __forceinline__ SinCos<float> t_sincos(float x) {
+#ifdef TTRL_F32_TRANSC_NOINLINE
+#define TTRL_TRANSC32 __noinline__
+#else
+#define TTRL_TRANSC32 __forceinline__
+#endif
+__device__ TTRL_TRANSC32 float t_sin(float x) { return ::sinf(x); }
+__device__ TTRL_TRANSC32 float t_cos(float x) { return ::cosf(x); }
+__device__ TTRL_TRANSC32 float t_tan(float x) { return ::tanf(x); }
+__device__ TTRL_TRANSC32 float t_atan(float x) { return ::atanf(x); }
+__device__ TTRL_TRANSC32 float t_asin(float x) { return ::asinf(x); }
+__device__ TTRL_TRANSC32 float t_pow(float x, float y) { return ::powf(x, y); }
+__device__ TTRL_TRANSC32 SinCos<float> t_sincos(float x) {
   SinCos<float> r;
   ::sincosf(x, &r.s, &r.c);
   return r;
