@@ -235,3 +235,32 @@ def test_deepcopy_forks_an_independent_env(hip_device):
         r2 = fork.step(a)
         assert torch.equal(r1[0], r2[0]) and torch.equal(r1[1], r2[1])
     assert torch.equal(env.state["x"], fork.state["x"]) and env.state["x"].data_ptr() != fork.state["x"].data_ptr()
+
+
+@pytest.mark.parametrize("slots", [16, 96])
+def test_slot_classes_match_the_oracle(slots, hip_device):
+    """Other slot widths: 16 (tight: spawns beyond the last slot are dropped after their draws)
+    and 96 (the 128-slot kernels, two 64-lane chunks in the scene kernels); reset and three
+    steps equal the oracle's, which applies the same rules."""
+    E = 8
+    env = VecIntersectionEnv({**ENV_JSON, "num_envs": E, "device": hip_device, "vehicle_slots": slots})
+    obs, _ = env.reset(seed=40)
+    net = intersection_network()
+    o = Oracle(net.table, P_IX)
+    cfg = ix_cfg(net, VecIntersectionEnv.default_config(), P_IX)
+    h = HostState(E, slots)
+    o.ix_reset(h, cfg, [40 + e for e in range(E)])
+    want, _ = o.observe_kinematics(h, KIN)
+    assert np.max(np.abs(obs.cpu().numpy() - want)) <= 1e-6
+    g = torch.Generator(device=hip_device).manual_seed(5)
+    from test_ix_oracle import LONGI
+    for p in range(3):
+        a = torch.randint(0, 3, (E,), device=hip_device, generator=g)
+        obs, rew, term, trunc, _ = env.step(a)
+        o.simulate(h, [LONGI[int(x)] for x in a.cpu().numpy()], 15, 1 / 15)
+        want, _ = o.observe_kinematics(h, KIN)
+        o.ix_clear_spawn(h, cfg)
+        st = env.state.to_numpy()
+        for e in range(E):
+            same_state(env_view(st, e), {k: v[e:e + 1] for k, v in h.a.items()}, EPISODE_TOL, f"{slots} {e} {p}")
+        assert np.max(np.abs(obs.cpu().numpy() - want)) <= 1e-4
