@@ -84,6 +84,56 @@ def cpu_baseline(vehicles: int, obs_cfg: dict, seconds_target: float = 10.0) -> 
                       f"of the reference loop order (oracle/ttrl_oracle.c), OpenMP over envs, {el:.1f} s"}
 
 
+def cpu_baseline_ix(seconds_target: float = 10.0) -> dict:
+    """The intersection episodes on the float64 C restatement (oracle/), OpenMP over envs: env.step
+    = fused frames + shuffled Kinematics + rewards + clear/spawn, with resets (and their 45
+    warm-up frames) where episodes end, as the GPU run does."""
+    from oracle.oracle import HostState, Oracle
+    from topotrafficrl_amd import _abi
+    from topotrafficrl_amd.intersection import VecIntersectionEnv, intersection_network, ix_cfg
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    cfg = VecIntersectionEnv.default_config()
+    net = intersection_network()
+    P = _abi.default_params(target_speeds=[0, 4.5, 9], distance_wanted=7.0, comfort_acc_max=6.0, comfort_acc_min=-3.0)
+    o = Oracle(net.table, P)
+    ix = ix_cfg(net, cfg, P)
+    kin = _abi.kin_cfg(**{k: v for k, v in CONFIGS[6]["obs"].items() if k != "type"}, shuffle_rng="np_random")
+    rew = _abi.reward_cfg(-5, 1, [7.0, 9.0], False, False, 13, arrived_reward=1)
+    E = 1024
+    h = HostState(E, 32)
+    o.ix_reset(h, ix, list(range(E)))
+    o.observe_kinematics(h, kin)
+    t = np.zeros(E)
+    episode = np.zeros(E, dtype=np.int64)
+    rng = np.random.default_rng(0)
+    codes = np.array([_abi.SLOWER, _abi.IDLE, _abi.FASTER], dtype=np.int32)
+    steps, live, t0 = 0, 0, time.perf_counter()
+    while True:
+        live += int((h["kind"] > 0).sum())
+        t += 1
+        o.simulate(h, codes[rng.integers(0, 3, size=E)], 15, 1 / 15)
+        o.observe_kinematics(h, kin)
+        _, term, trunc = o.rewards(h, rew, t)
+        o.ix_clear_spawn(h, ix)
+        done = term | trunc
+        if done.any():
+            episode += done
+            m = done.astype(np.uint8)
+            seeds = [[int(e), int(episode[e])] if done[e] else [int(e), 0] for e in range(E)]
+            o.ix_reset(h, ix, seeds, mask=m)
+            o.observe_kinematics(h, kin, mask=m)
+            t[done] = 0
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds_target or steps >= 100:
+            break
+    return {"value": live * 15 / el, "unit": "vehicle-steps/s (live vehicles)", "cores": threads, "kind": "port",
+            "sample": f"{E} intersection envs x {steps} env.step (15 frames + shuffled Kinematics + rewards + "
+                      f"clear/spawn + auto-resets), float64 C restatement (oracle/ttrl_oracle.c), OpenMP over "
+                      f"envs, {el:.1f} s"}
+
+
 def read_pmc(dtype: str, cfg_id: int) -> dict | None:
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
@@ -268,9 +318,10 @@ def main():
     if ix:
         out["config"]["live_vehicles_per_env"] = veh_steps / (world * E * 15 * args.steps)
         out["config"]["auto_reset"] = True
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not ix:
-        out["cpu_baseline"] = cpu_baseline(N, C["obs"] if C["obs"]["type"] == "Kinematics" else GRID7,
-                                           args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = (cpu_baseline_ix(args.cpu_seconds) if ix else
+                               cpu_baseline(N, C["obs"] if C["obs"]["type"] == "Kinematics" else GRID7,
+                                            args.cpu_seconds))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
