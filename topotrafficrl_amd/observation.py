@@ -98,6 +98,10 @@ class BatchedKinematicObservation(BatchedObservationType):
                  order="sorted", normalize=True, clip=True, see_behind=False, observe_intentions=False,
                  include_obstacles=True, **kwargs):
         super().__init__(env)
+        if observe_intentions and env.road.network.table.n_roads > 1:
+            # with routes, cos_d / sin_d point to each vehicle's destination (kinematics.py:205-226);
+            # the kernels emit the route-less value 0 (exact on a single road only)
+            raise NotImplementedError("observe_intentions on a road network with routes")
         self.features = list(features or self.FEATURES)
         self.vehicles_count = vehicles_count
         self.features_range = features_range
