@@ -467,13 +467,23 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, 
   o.lanes = take(sizeof(LaneT<T>) * n_lanes, 16);
   for (int k = 0; k < 14; ++k) o.reals[k] = take(sizeof(T) * M, 16);
   o.xf = sizeof(T) == 8 ? take(sizeof(float) * M, 16) : o.reals[0];
-  o.key = take(sizeof(T) * (size_t)n_lanes * EPW * (NS + 1), 16);
-  o.pq = take(sizeof(PairRec<T>) * M, 16);
   o.bal = take(16 * sizeof(unsigned long long), 16);
   o.cnt = take(sizeof(int) * EPW * (LMAX + 1), 4);
   o.wcnt = take(sizeof(int) * LMAX * 4, 4);
   o.nitem = take(sizeof(int) * EPW, 4);
   o.pq_n = take(sizeof(int) * EPW, 4);
+  o.kind = take(M, 4);
+  o.flags = take(M, 4);
+  o.sidx = take(M, 4);
+  o.lane = take(M, 4);
+  o.tgt = take(M, 4);
+  // Frame-transient block: the per-lane candidate lists and the act phase's neighbour / MOBIL
+  // scratch (read from the start of a frame's act until its last barrier) and the collision pair
+  // queue (written after the projection).  The RegulatedRoad trajectory predictions live only
+  // between those two (step phase, before the kinematics), so on a road network they share it.
+  const size_t t0 = take(0, 16);
+  o.key = take(sizeof(T) * (size_t)n_lanes * EPW * (NS + 1), 16);
+  o.pq = take(sizeof(PairRec<T>) * M, 16);
   o.mypos = take(sizeof(short) * (size_t)n_lanes * M, 4);
   o.f0 = take(sizeof(short) * M, 4);
   o.r0 = take(sizeof(short) * M, 4);
@@ -481,13 +491,10 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, 
   o.mob = take(sizeof(short) * 2 * M, 4);
   o.item = take(sizeof(short) * 2 * M, 4);
   o.idx = take((size_t)n_lanes * EPW * (NS + 1), 4);
-  o.kind = take(M, 4);
-  o.flags = take(M, 4);
-  o.sidx = take(M, 4);
-  o.lane = take(M, 4);
-  o.tgt = take(M, 4);
   if (graph) {
-    o.pred = take(sizeof(T) * 3 * PRED_T * M, 16);
+    o.pred = t0;
+    const size_t pred_end = t0 + sizeof(T) * 3 * PRED_T * M;
+    if (p < pred_end) p = pred_end;
     o.rroad = take(TTRL_ROUTE_MAX * M, 4);
     o.rlane = take(TTRL_ROUTE_MAX * M, 4);
     o.rn = take(M, 4);
