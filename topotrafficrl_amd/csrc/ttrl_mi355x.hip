@@ -735,7 +735,14 @@ __device__ int next_given(const LaneT<T>* lanes, const RoadTab& R, int cur_road,
 // leaving road whose lane is closest to the projected position.  Out of line: it runs a few
 // times per vehicle and route.  `rr`/`rl`/`rn`: the vehicle's route in LDS.
 template <typename T>
-__device__ __noinline__ int follow_road(const LaneT<T>* lanes, const RoadTab& R, T vl, int tgt, T x, T y, int8_t* rr,
+// Inlined into the NET_GRAPH instance, the only one that calls them (measured: intersection
+// launch f64 1.115 -> 1.072 ms, f32 0.579 -> 0.529 ms against out-of-line calls).
+#ifdef TTRL_NET_NOINLINE
+#define TTRL_NET_ATTR __noinline__
+#else
+#define TTRL_NET_ATTR __forceinline__
+#endif
+__device__ TTRL_NET_ATTR int follow_road(const LaneT<T>* lanes, const RoadTab& R, T vl, int tgt, T x, T y, int8_t* rr,
                                         int8_t* rl, int8_t* rn) {
   const LaneT<T>& L = lanes[tgt];
   T s, r;
@@ -774,7 +781,7 @@ __device__ __noinline__ int follow_road(const LaneT<T>* lanes, const RoadTab& R,
 // RoadNetwork.position_heading_along_route road.py:352-389: the poses at t = 0.25 .. 2.75 s
 // along the route (route None or empty: the current lane), written to p*[0 .. PRED_T).
 template <typename T>
-__device__ __noinline__ void predict_poses(const LaneT<T>* lanes, const RoadTab& R, int cur, T x, T y, T v,
+__device__ TTRL_NET_ATTR void predict_poses(const LaneT<T>* lanes, const RoadTab& R, int cur, T x, T y, T v,
                                            const int8_t* rr, const int8_t* rl, int rn, T* px, T* py, T* ph) {
   T s0, r0;
   lane_local(lanes[cur], x, y, s0, r0);
@@ -801,7 +808,7 @@ __device__ __noinline__ void predict_poses(const LaneT<T>* lanes, const RoadTab&
 // rect_corners points (corners, centre, edge midpoints, :126-155), each tested with
 // point_in_rotated_rectangle :75-91 (which rotates by +angle, as written).
 template <typename T>
-__device__ __noinline__ bool rects_intersect(T ax, T ay, T ah, T bx, T by, T bh, T l, T w) {
+__device__ TTRL_NET_ATTR bool rects_intersect(T ax, T ay, T ah, T bx, T by, T bh, T l, T w) {
   const SinCos<T> ca = t_sincos(ah), cb = t_sincos(bh);
   const T hl = l / T(2), hw = w / T(2);
   const T qx[9] = {-hl, -hl, hl, hl, T(0), -hl, hl, T(0), T(0)};
