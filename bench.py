@@ -126,7 +126,7 @@ def cpu_baseline_ix(seconds_target: float = 10.0) -> dict:
             t[done] = 0
         steps += 1
         el = time.perf_counter() - t0
-        if el >= seconds_target or steps >= 100:
+        if el >= seconds_target or steps >= 2000:
             break
     return {"value": live * 15 / el, "unit": "vehicle-steps/s (live vehicles)", "cores": threads, "kind": "port",
             "sample": f"{E} intersection envs x {steps} env.step (15 frames + shuffled Kinematics + rewards + "

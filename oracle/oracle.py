@@ -182,10 +182,9 @@ class Oracle:
     def ix_reset(self, h: HostState, cfg: _abi.IxCfg, seeds, mask=None):
         """IntersectionEnv.reset(seed) per env: np_random = default_rng(seed), then _reset."""
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
-        st = _abi.rng_states(seeds)
-        for e in range(h.E):
-            if m is None or m[e]:
-                h.a["rng"][e] = st[e]
+        envs = [e for e in range(h.E) if m is None or m[e]]
+        if envs:
+            h.a["rng"][envs] = _abi.rng_states([seeds[e] for e in envs])
         s = h.struct()
         self._ok(self.lib.oracle_ix_reset(C.byref(s), C.byref(self.lanes), C.byref(self.params), C.byref(cfg),
                                           None if m is None else m.ctypes.data))
