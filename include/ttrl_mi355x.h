@@ -356,6 +356,12 @@ int ttrl_ix_clear_spawn(const ttrl_state_t* s, const ttrl_lane_table_t* road, co
 int ttrl_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* road,
                  const ttrl_reward_cfg_t* cfg, const double* time, float* reward,
                  uint8_t* terminated, uint8_t* truncated, void* stream);
+/* As ttrl_rewards, plus the per-objective terms of IntersectionEnv._agent_rewards
+ * (intersection_env.py:95-104) in components [E][4] float32: collision_reward (crashed),
+ * high_speed_reward (clipped lmap of the speed), arrived_reward, on_road_reward. */
+int ttrl_rewards_ex(const ttrl_state_t* s, const ttrl_lane_table_t* road,
+                    const ttrl_reward_cfg_t* cfg, const double* time, float* reward,
+                    uint8_t* terminated, uint8_t* truncated, float* components, void* stream);
 
 #ifdef __cplusplus
 }

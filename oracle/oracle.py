@@ -114,7 +114,7 @@ _SIGS = {
     "oracle_observe_kinematics": [C.c_void_p] * 7,
     "oracle_observe_grid": [C.c_void_p] * 5,
     "oracle_reset_highway": [C.c_void_p] * 5,
-    "oracle_rewards": [C.c_void_p] * 7,
+    "oracle_rewards": [C.c_void_p] * 8,
     "oracle_observe_ttc": [C.c_void_p] * 5,
     "oracle_observe_lidar": [C.c_void_p] * 5,
     "oracle_ix_reset": [C.c_void_p] * 5,
@@ -235,12 +235,16 @@ class Oracle:
         self._ok(self.lib.oracle_reset_highway(C.byref(s), C.byref(self.lanes), C.byref(self.params),
                                                C.byref(cfg), pcg.ctypes.data))
 
-    def rewards(self, h: HostState, cfg: _abi.RewardCfg, time):
+    def rewards(self, h: HostState, cfg: _abi.RewardCfg, time, components: bool = False):
+        """(reward, terminated, truncated) [E]; with ``components`` also the [E, 4] _agent_rewards terms."""
         s = h.struct()
         t = np.ascontiguousarray(np.broadcast_to(np.asarray(time, dtype=np.float64), (h.E,)))
         rew = np.zeros(h.E, dtype=np.float32)
         term = np.zeros(h.E, dtype=np.uint8)
         trunc = np.zeros(h.E, dtype=np.uint8)
+        comp = np.zeros((h.E, 4), dtype=np.float32)
         self._ok(self.lib.oracle_rewards(C.byref(s), C.byref(self.lanes), C.byref(cfg), t.ctypes.data,
-                                         rew.ctypes.data, term.ctypes.data, trunc.ctypes.data))
+                                         rew.ctypes.data, term.ctypes.data, trunc.ctypes.data, comp.ctypes.data))
+        if components:
+            return rew, term.astype(bool), trunc.astype(bool), comp
         return rew, term.astype(bool), trunc.astype(bool)

@@ -957,14 +957,20 @@ int oracle_reset_highway(const ttrl_state_t* s, const ttrl_lane_table_t* R, cons
 
 /* IntersectionEnv._agent_reward / _is_terminated / _is_truncated (intersection_env.py:78-119),
  * has_arrived (:364-369), for the env's controlled vehicle */
+/* components (optional, [E][4]): the _agent_rewards dict (intersection_env.py:95-104) in the order
+ * collision_reward, high_speed_reward, arrived_reward, on_road_reward. */
 int oracle_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_reward_cfg_t* cfg,
-                   const double* time, float* reward, uint8_t* terminated, uint8_t* truncated) {
+                   const double* time, float* reward, uint8_t* terminated, uint8_t* truncated, float* components) {
   if (check(s)) return TTRL_E_ARG;
   S o = view(s);
   ttrl_params_t dummy; memset(&dummy, 0, sizeof dummy); dummy.lane_vehicle_length = 5.0;
   for (int e = 0; e < o.E; ++e) {
     const int ei = ego_of(&o, e * o.N);
-    if (ei < 0) { reward[e] = 0; terminated[e] = 0; truncated[e] = (uint8_t)(time[e] >= cfg->duration); continue; }
+    if (ei < 0) {
+      reward[e] = 0; terminated[e] = 0; truncated[e] = (uint8_t)(time[e] >= cfg->duration);
+      if (components) for (int q = 0; q < 4; ++q) components[e * 4 + q] = 0.f;
+      continue;
+    }
     int k = e * o.N + ei;
     double hs = clipd(lmap(o.v[k], cfg->speed_lo, cfg->speed_hi, 0, 1), 0, 1);
     double sr, rr; local(R, o.lane[k], o.x[k], o.y[k], &sr, &rr);
@@ -978,6 +984,10 @@ int oracle_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl
     reward[e] = (float)r;
     terminated[e] = (uint8_t)(o.crashed[k] || arrived || (cfg->offroad_terminal && !onroad));
     truncated[e] = (uint8_t)(time[e] >= cfg->duration);
+    if (components) {
+      components[e * 4 + 0] = (float)o.crashed[k]; components[e * 4 + 1] = (float)hs;
+      components[e * 4 + 2] = (float)arrived; components[e * 4 + 3] = (float)onroad;
+    }
   }
   return 0;
 }

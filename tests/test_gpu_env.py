@@ -44,11 +44,13 @@ def test_env_step_matches_oracle(road, hip_device):
         obs, rew, term, trunc, info = env.step(torch.from_numpy(a))
         o.simulate(h, a.astype(np.int32), 15, 1 / 15)
         ref_obs, _ = o.observe_kinematics(h, kin)
-        ref_r, ref_term, ref_trunc = o.rewards(h, env.reward_cfg, float(t))
+        ref_r, ref_term, ref_trunc, ref_c = o.rewards(h, env.reward_cfg, float(t), components=True)
         assert np.max(np.abs(obs.cpu().numpy() - ref_obs)) < 1e-6
         assert np.allclose(rew.cpu().numpy(), ref_r, atol=1e-6)
         assert np.array_equal(term.cpu().numpy(), ref_term) and np.array_equal(trunc.cpu().numpy(), ref_trunc)
         assert np.allclose(info["speed"].cpu().numpy(), h["speed"][:, 0])
+        for i, name in enumerate(env.REWARD_TERMS):  # info["rewards"] (abstract.py:182-185)
+            assert np.allclose(info["rewards"][name].cpu().numpy(), ref_c[:, i], atol=1e-6), name
 
 
 def test_truncation_and_auto_reset(hip_device):

@@ -9,6 +9,7 @@ import torch
 from conftest import golden_files, load_golden
 from oracle.oracle import HostState, Oracle
 from test_ix_env_oracle import EPISODE_TOL, KIN, obs_tol, same_state
+from test_host_logic import _reward_from_terms
 from test_ix_oracle import P_IX
 from topotrafficrl_amd import _abi
 from topotrafficrl_amd.intersection import VecIntersectionEnv, intersection_network, ix_cfg, ix_reset
@@ -48,6 +49,12 @@ def test_device_episodes_match_reference(hip_device):
             assert abs(float(rew[e]) - d["reward"][p]) <= tol, (e, p)
             assert bool(term[e]) == bool(d["terminated"][p]) and bool(trunc[e]) == bool(d["truncated"][p]), (e, p)
             same_state(env_view(st, e), HostState.from_ix(d, "post", p, pad_to=32), EPISODE_TOL, f"env {e} step {p}")
+        # IntersectionEnv._info (intersection_env.py:120-128): the terms rebuild the reward
+        terms = np.stack([info["rewards"][n].cpu().numpy() for n in env.REWARD_TERMS], 1)
+        for e in range(len(GOLD)):
+            assert abs(_reward_from_terms(env.reward_cfg, terms[e]) - float(rew[e])) <= 1e-6, (e, p)
+        assert torch.equal(info["agents_rewards"][0], rew)
+        assert torch.equal(info["agents_terminated"][0].cpu(), torch.from_numpy((terms[:, 0] != 0) | (terms[:, 2] != 0)))
 
 
 def test_large_batch_reset_equals_oracle(hip_device):

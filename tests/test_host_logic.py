@@ -163,3 +163,28 @@ def test_rewards_template():
     h.a["crashed"][0, 0] = 1
     r, term, _ = o.rewards(h, cfg, 40.0)
     assert term[0] and abs(r[0] - (-1.0 + 0.2)) < 1e-7
+
+
+def _reward_from_terms(cfg, c):
+    """IntersectionEnv._agent_reward (intersection_env.py:78-93) from the _agent_rewards dict."""
+    r = cfg.collision_reward * c[0] + cfg.high_speed_reward * c[1] + cfg.arrived_reward * c[2]
+    r = cfg.arrived_reward if c[2] else r
+    r *= c[3]
+    if cfg.normalize_reward:
+        r = (r - cfg.collision_reward) / (cfg.arrived_reward - cfg.collision_reward)
+    return r
+
+
+def test_reward_terms_rebuild_the_reward():
+    """info["rewards"] terms: 0/1 flags and the clipped speed term; _agent_reward recombines them."""
+    o, h = _scene(10, [3, 4, 5])
+    h.a["crashed"][1, 0] = 1
+    h.a["y"][2, 0] = 50.0  # off road
+    for norm in (False, True):
+        cfg = _abi.reward_cfg(normalize_reward=norm)
+        r, term, _, comp = o.rewards(h, cfg, 0.0, components=True)
+        assert comp.shape == (3, 4)
+        assert comp[1, 0] == 1 and comp[0, 0] == 0 and comp[2, 3] == 0 and comp[0, 3] == 1
+        assert np.all((comp[:, 1] >= 0) & (comp[:, 1] <= 1))
+        for e in range(3):
+            assert abs(r[e] - _reward_from_terms(cfg, comp[e])) < 1e-6

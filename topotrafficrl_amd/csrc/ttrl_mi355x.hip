@@ -2383,14 +2383,19 @@ __global__ void reset_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t
 // has_arrived (:364-369) for the env's controlled vehicle (its first MDP slot).
 template <typename T>
 __global__ void rewards_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_reward_cfg_t cfg, const double* __restrict__ time,
-                               float* __restrict__ reward, uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
+                               float* __restrict__ reward, uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
+                               float* __restrict__ comp) {
   const int env = blockIdx.x * blockDim.x + threadIdx.x;
   if (env >= st.n_envs) return;
   const size_t b = (size_t)env * st.n_veh;
   int ego = 0;
   while (ego < st.n_veh && st.kind[b + ego] != TTRL_MDP) ++ego;
   trunc[env] = (uint8_t)(time[env] >= cfg.duration);
-  if (ego == st.n_veh) { reward[env] = 0.f; term[env] = 0; return; }
+  if (ego == st.n_veh) {
+    reward[env] = 0.f; term[env] = 0;
+    if (comp) for (int q = 0; q < 4; ++q) comp[(size_t)env * 4 + q] = 0.f;
+    return;
+  }
   const size_t k = b + ego;
   const T v = ((const T*)st.speed)[k], x = ((const T*)st.x)[k], y = ((const T*)st.y)[k];
   const int l = st.lane[k];
@@ -2407,6 +2412,10 @@ __global__ void rewards_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_reward
   if (cfg.normalize_reward) rw = lmap(rw, T(cfg.collision_reward), T(cfg.arrived_reward), T(0), T(1));
   reward[env] = (float)rw;
   term[env] = (uint8_t)(crashed || arrived || (cfg.offroad_terminal && !onroad));
+  if (comp) {
+    float* c = comp + (size_t)env * 4;
+    c[0] = crashed ? 1.f : 0.f; c[1] = (float)hs; c[2] = arrived ? 1.f : 0.f; c[3] = onroad ? 1.f : 0.f;
+  }
 }
 
 // ------------------------------------------------------------ the intersection scenario
@@ -3106,21 +3115,26 @@ int ttrl_ix_clear_spawn(const ttrl_state_t* s, const ttrl_lane_table_t* road, co
   return launch_status();
 }
 
-int ttrl_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_reward_cfg_t* cfg,
-                 const double* time, float* reward, uint8_t* terminated, uint8_t* truncated, void* stream) {
+int ttrl_rewards_ex(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_reward_cfg_t* cfg,
+                    const double* time, float* reward, uint8_t* terminated, uint8_t* truncated, float* components,
+                    void* stream) {
   int rc = check_state(s, road);
   if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!cfg || !time || !reward || !terminated || !truncated) return TTRL_E_ARG;
-  if (s->n_envs == 0) return TTRL_OK;
   hipStream_t st = (hipStream_t)stream;
   const int blocks = (s->n_envs + 255) / 256;
   if (s->dtype == TTRL_F64)
     hipLaunchKernelGGL(rewards_kernel<double>, dim3(blocks), dim3(256), 0, st, *s, *road, *cfg, time, reward,
-                       terminated, truncated);
+                       terminated, truncated, components);
   else
     hipLaunchKernelGGL(rewards_kernel<float>, dim3(blocks), dim3(256), 0, st, *s, *road, *cfg, time, reward,
-                       terminated, truncated);
+                       terminated, truncated, components);
   return launch_status();
+}
+
+int ttrl_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_reward_cfg_t* cfg,
+                 const double* time, float* reward, uint8_t* terminated, uint8_t* truncated, void* stream) {
+  return ttrl_rewards_ex(s, road, cfg, time, reward, terminated, truncated, nullptr, stream);
 }
 
 }  // extern "C"

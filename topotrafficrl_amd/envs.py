@@ -52,6 +52,11 @@ def reset_highway_seeded(state: BatchState, network: RoadNetwork, params: _abi.P
               torch.cuda.current_stream(state.device).cuda_stream)
 
 
+def _reward_terms(names, components: torch.Tensor) -> dict:
+    """[E, 4] component block -> {name: [E] view} (float32; 0/1 for the boolean terms)."""
+    return {n: components[:, i].clone() for i, n in enumerate(names)}
+
+
 class VecHighwayEnv:
     """``num_envs`` synthetic straight highways; vehicle 0 of each env is the controlled ego."""
 
@@ -154,6 +159,7 @@ class VecHighwayEnv:
         self._reward = torch.zeros(self.num_envs, dtype=torch.float32, device=self.device)
         self._term = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
         self._trunc = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
+        self._components = torch.zeros((self.num_envs, 4), dtype=torch.float32, device=self.device)
         # auto-reset entropy per env: [seed lo word, seed hi word, episode]; episode k >= 1 of an env
         # reset with seed s replays np.random.default_rng([s & 0xffffffff, s >> 32, k])
         self._entropy = torch.zeros(self.num_envs, 3, dtype=torch.int32, device=self.device)
@@ -199,6 +205,7 @@ class VecHighwayEnv:
         ent[:, 1] = [(s >> 32) & 0xFFFFFFFF for s in seeds]
         self._entropy.copy_(torch.from_numpy(ent.view(np.int32)))
         obs = self.observation_type.observe()
+        self._rewards_and_dones()  # abstract.py:211 reset's _info evaluates _rewards too
         return obs, self._info(obs, None)
 
     def step(self, action):
@@ -228,16 +235,22 @@ class VecHighwayEnv:
         self.road.simulate(codes, frames, 1 / self.config["simulation_frequency"])
         self.steps += frames
 
+    REWARD_TERMS = ["collision_reward", "high_speed_reward", "arrived_reward", "on_road_reward"]
+
     def _rewards_and_dones(self):
-        _lib.call("ttrl_rewards", C.byref(self.state.struct()), C.byref(self.network.table), C.byref(self.reward_cfg),
-                  self.time.data_ptr(), self._reward.data_ptr(), self._term.data_ptr(), self._trunc.data_ptr(),
+        """reward, terminated, truncated [E]; the per-objective terms (_agent_rewards,
+        intersection_env.py:95-104) go to self._components [E, 4] for info["rewards"]."""
+        _lib.call("ttrl_rewards_ex", C.byref(self.state.struct()), C.byref(self.network.table),
+                  C.byref(self.reward_cfg), self.time.data_ptr(), self._reward.data_ptr(), self._term.data_ptr(),
+                  self._trunc.data_ptr(), self._components.data_ptr(),
                   torch.cuda.current_stream(self.device).cuda_stream)
         return self._reward.clone(), self._term.bool(), self._trunc.bool()
 
     def _info(self, obs, action) -> dict:
-        """abstract.py:169-186 batched: device tensors [E]."""
+        """abstract.py:169-186 batched: device tensors [E]; info["rewards"] holds the per-objective
+        terms of the last _rewards_and_dones (AbstractEnv._rewards)."""
         return {"speed": self.state["speed"][:, 0].clone(), "crashed": self.state["crashed"][:, 0].bool(),
-                "action": action}
+                "action": action, "rewards": _reward_terms(self.REWARD_TERMS, self._components)}
 
     def _auto_reset(self, done: torch.Tensor) -> None:
         """Masked auto-reset of finished envs on the device."""

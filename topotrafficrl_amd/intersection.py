@@ -25,6 +25,7 @@ import torch
 
 from . import _abi, _lib
 from .action import action_factory
+from .envs import _reward_terms
 from .observation import observation_factory
 from .road import BatchedRoad, RoadNetwork
 from .state import BatchState
@@ -310,6 +311,7 @@ class VecIntersectionEnv:
         self._reward = torch.zeros(self.num_envs, dtype=torch.float32, device=self.device)
         self._term = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
         self._trunc = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
+        self._components = torch.zeros((self.num_envs, 4), dtype=torch.float32, device=self.device)
         self._entropy = None  # [E, words + 1]: seed words, then the auto-reset episode counter
         self._spare = None    # next-episode scenes (overlap_resets), prepared on self._side
         if c["auto_reset"] and c["overlap_resets"]:
@@ -362,6 +364,7 @@ class VecIntersectionEnv:
             self._spare_entropy[:, -1] += 1
             self._prepare_spares(None)
         obs = self.observation_type.observe()
+        self._rewards_and_dones()  # abstract.py:211 reset's _info evaluates _rewards too
         return obs, self._info(obs, None)
 
     def _prepare_spares(self, mask: torch.Tensor | None) -> None:
@@ -399,15 +402,26 @@ class VecIntersectionEnv:
         self.road.simulate(codes, frames, 1 / self.config["simulation_frequency"])
         self.steps += frames
 
+    REWARD_TERMS = ["collision_reward", "high_speed_reward", "arrived_reward", "on_road_reward"]
+
     def _rewards_and_dones(self):
-        _lib.call("ttrl_rewards", C.byref(self.state.struct()), C.byref(self.network.table), C.byref(self.reward_cfg),
-                  self.time.data_ptr(), self._reward.data_ptr(), self._term.data_ptr(), self._trunc.data_ptr(),
+        """reward, terminated, truncated [E]; the per-objective terms (_agent_rewards,
+        intersection_env.py:95-104) go to self._components [E, 4] for info["rewards"]."""
+        _lib.call("ttrl_rewards_ex", C.byref(self.state.struct()), C.byref(self.network.table),
+                  C.byref(self.reward_cfg), self.time.data_ptr(), self._reward.data_ptr(), self._term.data_ptr(),
+                  self._trunc.data_ptr(), self._components.data_ptr(),
                   _stream(self.device))
         return self._reward.clone(), self._term.bool(), self._trunc.bool()
 
     def _info(self, obs, action) -> dict:
-        """abstract.py:169-186 batched: device tensors [E]."""
-        return {"speed": self.state.ego("speed"), "crashed": self.state.ego("crashed").bool(), "action": action}
+        """IntersectionEnv._info (intersection_env.py:120-128) over abstract.py:169-186, batched: device
+        tensors [E].  One controlled vehicle per env, so agents_rewards / agents_terminated are
+        1-tuples: its _agent_reward and crashed-or-arrived."""
+        c = self._components
+        return {"speed": self.state.ego("speed"), "crashed": self.state.ego("crashed").bool(), "action": action,
+                "rewards": _reward_terms(self.REWARD_TERMS, c),
+                "agents_rewards": (self._reward.clone(),),
+                "agents_terminated": ((c[:, 0] != 0) | (c[:, 2] != 0),)}
 
     def _auto_reset(self, done: torch.Tensor, obs: torch.Tensor) -> None:
         """Finished envs restart on the device with default_rng([seed words..., episode]) and
