@@ -1,0 +1,107 @@
+"""The single-env view (topotrafficrl_amd/single.py): gymnasium's one-env contract over a batch of
+one.  CPU: the unwrapping over a host stand-in for the batched env.  GPU: SingleEnv over the real
+envs replays the reference's intersection episodes (tests/golden/ix_*.npz)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_files, load_golden
+from topotrafficrl_amd.envs import ENV_IDS, resolve
+from topotrafficrl_amd.single import SingleEnv, SingleHighwayEnv, SingleIntersectionEnv, make_single
+
+
+class _HostBatch:
+    """A one-env batch on the host, shaped like VecIntersectionEnv's outputs."""
+
+    def __init__(self, config, render_mode=None):
+        self.config = dict(config)
+        self.observation_space = self.action_space = None
+        self.time = torch.zeros(1, dtype=torch.float64)
+        self.actions = []
+
+    def _info(self):
+        c = torch.tensor([[0.0, 0.25, 1.0, 1.0]])
+        return {"speed": torch.tensor([8.5]), "crashed": torch.tensor([False]), "action": None,
+                "rewards": {n: c[:, i] for i, n in enumerate(
+                    ["collision_reward", "high_speed_reward", "arrived_reward", "on_road_reward"])},
+                "agents_rewards": (torch.tensor([1.0]),), "agents_terminated": (torch.tensor([True]),)}
+
+    def reset(self, seed=None, options=None):
+        self.seed = seed
+        return torch.arange(14, dtype=torch.float32).reshape(1, 2, 7), self._info()
+
+    def step(self, a):
+        self.actions.append(a.clone())
+        self.time += 1
+        return (torch.ones(1, 2, 7), torch.tensor([1.0]), torch.tensor([True]), torch.tensor([False]),
+                self._info())
+
+    def close(self):
+        pass
+
+
+def test_single_view_unwraps_to_numpy_and_python_scalars():
+    env = SingleEnv(_HostBatch, {"auto_reset": True})
+    assert env.batched.config["num_envs"] == 1 and env.batched.config["auto_reset"] is False
+    obs, info = env.reset(seed=7)
+    assert env.batched.seed == 7
+    assert isinstance(obs, np.ndarray) and obs.shape == (2, 7) and obs.dtype == np.float32
+    obs, r, term, trunc, info = env.step(np.int64(2))
+    assert env.batched.actions[0].tolist() == [2]
+    assert type(r) is float and type(term) is bool and type(trunc) is bool and (term, trunc) == (True, False)
+    assert info["speed"] == 8.5 and info["crashed"] is False and info["action"] == 2
+    # _agent_rewards types: crashed / arrived / on_road bools, the speed term a float
+    assert info["rewards"] == {"collision_reward": False, "high_speed_reward": 0.25,
+                               "arrived_reward": True, "on_road_reward": True}
+    assert type(info["rewards"]["high_speed_reward"]) is float
+    assert info["agents_rewards"] == (1.0,) and info["agents_terminated"] == (True,)
+    assert env.time == 1.0 and env.unwrapped is env
+
+
+def test_single_view_refuses_batches():
+    with pytest.raises(ValueError):
+        SingleEnv(_HostBatch, {"num_envs": 4})
+
+
+def test_single_ids_resolve():
+    assert resolve("ttrl-intersection-single-v0") is SingleIntersectionEnv
+    assert resolve("ttrl-highway-single-v0") is SingleHighwayEnv
+    assert {"ttrl-highway-single-v0", "ttrl-intersection-single-v0"} <= set(ENV_IDS)
+    with pytest.raises(KeyError):
+        resolve("no-such-env-v0")
+
+
+@pytest.mark.gpu
+def test_single_intersection_replays_the_reference(hip_device):
+    from test_ix_env_oracle import EPISODE_TOL, obs_tol
+    from oracle.oracle import HostState
+    from topotrafficrl_amd.intersection import VecIntersectionEnv
+    # scripts/configs/IntersectionEnv/env.json: the default Kinematics observation, order "shuffled"
+    cfg = {"observation": dict(VecIntersectionEnv.default_config()["observation"], order="shuffled"),
+           "device": hip_device}
+    env = make_single("ttrl-intersection-single-v0", cfg)
+    for d in [load_golden(p) for p in golden_files("ix_*")][:3]:
+        obs, info = env.reset(seed=int(d["meta"][0]))
+        assert isinstance(obs, np.ndarray) and np.max(np.abs(obs - d["obs0"])) <= 1e-6
+        for p, a in enumerate(d["actions"]):
+            obs, r, term, trunc, info = env.step(int(a))
+            tol = obs_tol(HostState.from_ix(d, "frame", (p, 14), pad_to=32), EPISODE_TOL)
+            assert np.max(np.abs(obs - d["obs"][p])) <= tol and abs(r - d["reward"][p]) <= tol, p
+            assert term == bool(d["terminated"][p]) and trunc == bool(d["truncated"][p])
+            assert info["agents_rewards"] == (r,) and isinstance(info["rewards"]["collision_reward"], bool)
+
+
+@pytest.mark.gpu
+def test_single_highway_equals_batch_env_zero(hip_device):
+    from topotrafficrl_amd.envs import VecHighwayEnv
+    cfg = {"vehicles_count": 30, "device": hip_device}
+    single = SingleHighwayEnv(cfg)
+    batch = VecHighwayEnv(dict(cfg, num_envs=3))
+    o1, _ = single.reset(seed=11)
+    ob, _ = batch.reset(seed=11)
+    assert np.array_equal(o1, ob[0].cpu().numpy())
+    for a in [3, 1, 0, 4, 2]:
+        o1, r1, t1, _, i1 = single.step(a)
+        ob, rb, tb, _, ib = batch.step(torch.tensor([a, 1, 1]))
+        assert np.array_equal(o1, ob[0].cpu().numpy()) and r1 == float(rb[0]) and t1 == bool(tb[0])
+        assert i1["speed"] == float(ib["speed"][0])

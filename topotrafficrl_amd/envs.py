@@ -283,7 +283,11 @@ class VecHighwayEnv:
 
 
 ENV_IDS = {"ttrl-highway-batched-v0": "topotrafficrl_amd.envs:VecHighwayEnv",
-           "ttrl-intersection-batched-v0": "topotrafficrl_amd.intersection:VecIntersectionEnv"}
+           "ttrl-intersection-batched-v0": "topotrafficrl_amd.intersection:VecIntersectionEnv",
+           # single-env views (numpy out, one env) for gymnasium's checkers: single.py
+           "ttrl-highway-single-v0": "topotrafficrl_amd.single:SingleHighwayEnv",
+           "ttrl-intersection-single-v0": "topotrafficrl_amd.single:SingleIntersectionEnv"}
+ALIASES = {"intersection-v0": "ttrl-intersection-batched-v0", "highway-v0": "ttrl-highway-batched-v0"}
 
 
 def register(env_id: str | None = None) -> bool:
@@ -299,13 +303,17 @@ def register(env_id: str | None = None) -> bool:
     return True
 
 
-def make(env_id: str, config: dict | None = None, **kwargs):
-    """gym.make(id) + env.unwrapped.configure(config) (scripts/utils factory.py:72-91) without
-    gymnasium: the batched env of ``env_id`` ("intersection-v0" / "highway-v0" map to ours)."""
-    aliases = {"intersection-v0": "ttrl-intersection-batched-v0", "highway-v0": "ttrl-highway-batched-v0"}
-    env_id = aliases.get(env_id, env_id)
+def resolve(env_id: str):
+    """The env class registered under ``env_id`` (reference ids through ALIASES)."""
+    env_id = ALIASES.get(env_id, env_id)
     if env_id not in ENV_IDS:
         raise KeyError(f"unknown env id {env_id!r}")
     mod, cls = ENV_IDS[env_id].split(":")
     import importlib
-    return getattr(importlib.import_module(mod), cls)(dict(config or {}, **kwargs))
+    return getattr(importlib.import_module(mod), cls)
+
+
+def make(env_id: str, config: dict | None = None, **kwargs):
+    """gym.make(id) + env.unwrapped.configure(config) (scripts/utils factory.py:72-91) without
+    gymnasium: the batched env of ``env_id`` ("intersection-v0" / "highway-v0" map to ours)."""
+    return resolve(env_id)(dict(config or {}, **kwargs))
