@@ -87,7 +87,16 @@ template <typename T> __device__ __forceinline__ T not_zero(T x) {
 }
 // numpy float remainder (result has the divisor's sign)
 template <typename T> __device__ __forceinline__ T pymod(T a, T b) {
-  if (a >= T(0) && a < b) return a;  // fmod(a, b) == a exactly; skips the generic fmod
+  // One period either side needs no generic fmod: fmod(a, b) is a for 0 <= a < b, a - b for
+  // b <= a < 2b (exact by Sterbenz, as fmod's result is), and a for -b < a < 0, which numpy then
+  // moves into the divisor's sign with one rounded a + b.
+  if (b > T(0)) {
+    if (a >= T(0) && a < b) return a;
+#ifndef TTRL_NO_PYMOD_FAST
+    if (a >= b && a < T(2) * b) return a - b;
+    if (a < T(0) && a > -b) return a + b;
+#endif
+  }
   T m = fmod(a, b);
   if (m != T(0)) { if ((b < T(0)) != (m < T(0))) m += b; }
   else m = copysign(T(0), b);
@@ -444,13 +453,18 @@ template <typename T> struct View {
   uint8_t* ynew;                 // [EPW*NS] RegulatedRoad: yields decided this enforcement
   RoadTab* rt;                   // road topology
   T *px, *py, *ph;               // [EPW*NS][PRED_T] predicted poses (is_conflict_possible)
+  unsigned long long* onm;       // [LMAX] (vehicle, lane) projection: on-lane slot masks
+  uint8_t* live;                 // [EPW*NS] present slots in slot order
+  int8_t* lperm;                 // [LMAX] lanes, straight ones first
+  T* pd;                         // [EPW*NS] per-item-thread closest distance so far
+  int8_t* pl;                    // [EPW*NS] ... and its lane (-1 none)
 };
 constexpr int PRED_T = 11;       // np.arange(0.25, 3, 0.25) (regulation.py:86)
 
 // Byte offsets of the view's arrays in the dynamic LDS block (host: sizing; device: carve).
 struct ViewLayout {
   size_t lanes, reals[14], xf, key, pq, bal, cnt, wcnt, nitem, pq_n, mypos, f0, r0, ft, mob, item, idx, kind,
-      flags, sidx, lane, tgt, pred, rroad, rlane, rn, ynew, rt, total;
+      flags, sidx, lane, tgt, pred, rroad, rlane, rn, ynew, rt, onm, live, lperm, pd, pl, total;
 };
 
 template <typename T>
@@ -500,6 +514,11 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, 
     o.rn = take(M, 4);
     o.ynew = take(M, 4);
     o.rt = take(sizeof(RoadTab), 4);
+    o.onm = take(sizeof(unsigned long long) * LMAX, 8);
+    o.pd = take(sizeof(T) * M, 16);
+    o.live = take(M, 4);
+    o.lperm = take(LMAX, 4);
+    o.pl = take(M, 4);
   }
   o.total = take(0, 16);
   return o;
@@ -545,6 +564,11 @@ __device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lane
     V.rn = (int8_t*)(smem + o.rn);
     V.ynew = (uint8_t*)(smem + o.ynew);
     V.rt = (RoadTab*)(smem + o.rt);
+    V.onm = (unsigned long long*)(smem + o.onm);
+    V.pd = (T*)(smem + o.pd);
+    V.live = (uint8_t*)(smem + o.live);
+    V.lperm = (int8_t*)(smem + o.lperm);
+    V.pl = (int8_t*)(smem + o.pl);
   }
   return V;
 }
@@ -625,11 +649,37 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
   if constexpr (NS <= 64) {
     const int sh = (tid & 63) / NS * NS;
     const unsigned long long seg = NS == 64 ? ~0ull : ((1ull << NS) - 1);
+    bool have = false;  // bd / best hold a lane
     for (int l = 0; l < nl; ++l) {
       const LaneT<T> L = V.lanes[l];
       T s, r;
-      lane_local<CV>(L, x, y, s, r);
-      const bool on = present && fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl;
+      bool full = true;  // s computed (always, on a straight lane)
+#ifndef TTRL_NO_RING
+      if constexpr (CV) {
+#else
+      if constexpr (false) {
+#endif
+        if (L.type == TTRL_LANE_CIRCULAR) {
+          // CircularLane.local_coordinates (lane.py:327-334) lateral part first: the atan2 of s is
+          // needed only inside the on_lane band, or below the closest distance so far -- every term
+          // of distance_with_heading is >= 0, so d >= |r| and a lane with |r| >= bd cannot win.
+          const T dx = x - L.cx, dy = y - L.cy;
+          const T rr = sqrt(dx * dx + dy * dy);
+          r = L.dirn * (L.rad - rr);
+          full = present && (fabs(r) <= L.w / T(2) + T(1) || (want_closest && (!have || fabs(r) < bd)));
+          s = T(0);
+          if (full) {
+            T phi = atan2(dy, dx);
+            phi = L.sph + wrap_to_pi(phi - L.sph);
+            s = L.dirn * (phi - L.sph) * L.rad;
+          }
+        } else {
+          lane_local<CV>(L, x, y, s, r);
+        }
+      } else {
+        lane_local<CV>(L, x, y, s, r);
+      }
+      const bool on = full && present && fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl;
       const unsigned long long m = (__ballot(on) >> sh) & seg;
       const int pos = on ? __popcll(m & ((1ull << i) - 1)) : -1;
       if (on) {
@@ -640,14 +690,15 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
       const int c = __popcll(m);
       mx = c > mx ? c : mx;
       if (i == 0) cnt[l] = c;
-      if (want_closest) {
+      if (want_closest && full) {
         const T hdl = heading_at<CV>(L, s);  // distance_with_heading lane.py:132-147
-        if (l == 0 || hdl != prev_hd) ang = fabs(wrap_to_pi(h - hdl));
+        if (!have || hdl != prev_hd) ang = fabs(wrap_to_pi(h - hdl));
         prev_hd = hdl;
         T a = s - L.len; if (!(a > T(0))) a = T(0);
         T b = T(0) - s; if (!(b > T(0))) b = T(0);
         const T d = fabs(r) + a + b + T(1) * ang;
-        if (l == 0 || d < bd) { bd = d; best = l; }
+        if (!have || d < bd) { bd = d; best = l; }
+        have = true;
       }
     }
   } else {
@@ -696,6 +747,148 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
   }
   if (i == 0) cnt[LMAX] = mx;
   return best;
+}
+
+#ifdef TTRL_CHECK_ITEMS
+__device__ int g_dbg_count = 0;
+#endif
+// project_all for the road-network instance (one wavefront per workgroup), over (vehicle, lane)
+// items: a scene holds ~8 live vehicles in its 32 slots, so one vehicle per SIMD lane left 3/4 of
+// the lanes idle through the frame's longest phase (every vehicle on all 20 lanes, atan2 on the
+// turns).  The live vehicles are split across the wavefront, each group of `total` lanes taking
+// every G-th lane of V.lperm (straight lanes first, so an iteration rarely mixes lane classes).
+// The results equal project_all's: the on-lane lists are rebuilt per lane in slot order from the
+// on-lane masks, and the closest lane is the lexicographic (d, lane) minimum -- the first minimum
+// of get_closest_lane_index.  All threads must call it.
+// (With the float32 road-network instance at a 128-VGPR budget -- 102 VGPRs and 132 SGPRs spilled
+// -- this phase produced non-finite states or hung; at the 2-wave budget nothing spills.)
+#ifndef TTRL_ITEMS_NOINLINE
+#define TTRL_ITEMS_ATTR __forceinline__
+#else
+#define TTRL_ITEMS_ATTR __noinline__
+#endif
+template <typename T, int NS, int EPW>
+__device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const ttrl_params_t& P, int nl, int tid, int le, int i,
+                             bool present, bool want_closest) {
+  static_assert(NS * EPW == 64, "one wavefront per workgroup");
+  constexpr int NSP = NS + 1;
+  const T vl = T(P.lane_vehicle_length);
+  const unsigned long long below = (1ull << tid) - 1;
+  const unsigned long long live = __ballot(present);
+  const int total = __popcll(live);
+  if (present) V.live[__popcll(live & below)] = (uint8_t)tid;
+  if (tid < nl) V.onm[tid] = 0ull;
+  __syncthreads();
+  const int G = total > 0 ? 64 / total : 1;  // lane groups per vehicle
+  const int g = total > 0 ? tid / total : 1;
+  T bd = T(0), prev_hd = T(0), ang = T(0);
+  int best = -1;
+  if (g < G) {
+    const int v = V.live[tid - g * total];
+    const int vbase = (v / NS) * NSP + v % NS;
+    const T x = V.x[v], y = V.y[v], h = V.h[v];
+    for (int kk = g; kk < nl; kk += G) {
+      int l = V.lperm[kk];
+#ifdef TTRL_CHECK_ITEMS
+      if (l < 0 || l >= nl) {
+        if (atomicAdd(&g_dbg_count, 1) < 20) printf("items: blk %d tid %d lperm[%d] = %d\n", (int)blockIdx.x, tid, kk, l);
+        l = kk;
+      }
+#endif
+      const LaneT<T> L = V.lanes[l];
+      T s, r;
+      lane_local<true>(L, x, y, s, r);
+      if (fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl) {  // AbstractLane.on_lane margin 1
+        atomicOr(&V.onm[l], 1ull << v);
+        V.key[(size_t)l * EPW * NSP + vbase] = s;  // at the slot; compacted below
+      }
+      if (want_closest) {
+        const T hdl = heading_at<true>(L, s);  // distance_with_heading lane.py:132-147
+        if (best < 0 || hdl != prev_hd) ang = fabs(wrap_to_pi(h - hdl));
+        prev_hd = hdl;
+        T a = s - L.len; if (!(a > T(0))) a = T(0);
+        T b = T(0) - s; if (!(b > T(0))) b = T(0);
+        const T d = fabs(r) + a + b + T(1) * ang;
+        if (best < 0 || d < bd || (d == bd && l < best)) { bd = d; best = l; }
+      }
+    }
+  }
+  if (want_closest) { V.pd[tid] = bd; V.pl[tid] = (int8_t)best; }
+  __syncthreads();
+  int cl = 0;
+  if (want_closest && present) {  // the vehicle's groups, combined as (d, lane)
+    const int q = __popcll(live & below);
+    T cd = T(0);
+    cl = -1;
+    for (int gg = 0; gg < G; ++gg) {
+      const int u = gg * total + q, lu = V.pl[u];
+      if (lu < 0) continue;
+      const T du = V.pd[u];
+      if (cl < 0 || du < cd || (du == cd && lu < cl)) { cd = du; cl = lu; }
+    }
+  }
+  // per lane, in slot order: positions, compacted keys (read at the slot before any write; one
+  // wavefront, so every lane's read precedes every lane's write), slots and counts
+  const int sh = le * NS;
+  const unsigned long long seg = NS == 64 ? ~0ull : ((1ull << NS) - 1);
+  int* cnt = V.cnt + le * (LMAX + 1);
+  int mx = 0;
+  for (int l = 0; l < nl; ++l) {
+    const unsigned long long m = (V.onm[l] >> sh) & seg;
+    const bool on = (m >> i) & 1ull;
+    const int pos = on ? __popcll(m & ((1ull << i) - 1)) : -1;
+    const size_t base = ((size_t)l * EPW + le) * NSP;
+    if (on) {
+      const T sv = V.key[base + i];
+      V.key[base + pos] = sv;
+      V.idx[base + pos] = (uint8_t)i;
+    }
+    V.mypos[(size_t)l * EPW * NS + le * NS + i] = (short)pos;
+    const int c = __popcll(m);
+    mx = c > mx ? c : mx;
+    if (i == 0) cnt[l] = c;
+  }
+  if (i == 0) cnt[LMAX] = mx;
+#ifdef TTRL_CHECK_ITEMS
+  __syncthreads();
+  if (present) {  // the per-vehicle projection, compared
+    const T x = V.x[tid], y = V.y[tid], h = V.h[tid];
+    T bd2 = T(0), ang2 = T(0);
+    int best2 = 0;
+    for (int l = 0; l < nl; ++l) {
+      const LaneT<T> L = V.lanes[l];
+      T s, r;
+      lane_local<true>(L, x, y, s, r);
+      const bool on = fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl;
+      const unsigned long long m = (V.onm[l] >> sh) & seg;
+      const bool on1 = (m >> i) & 1ull;
+      const int pos = __popcll(m & ((1ull << i) - 1));
+      const size_t base = ((size_t)l * EPW + le) * NSP;
+      if (on != on1 || (on && (V.key[base + pos] != s || V.idx[base + pos] != i)))
+        if (atomicAdd(&g_dbg_count, 1) < 20)
+          printf("items: blk %d tid %d lane %d on %d/%d pos %d key %g/%g idx %d total %d\n", (int)blockIdx.x, tid,
+                 l, (int)on, (int)on1, pos, (double)V.key[base + pos], (double)s, (int)V.idx[base + pos], total);
+      if (want_closest) {
+        const T hdl = heading_at<true>(L, s);
+        ang2 = fabs(wrap_to_pi(h - hdl));
+        T a = s - L.len; if (!(a > T(0))) a = T(0);
+        T b = T(0) - s; if (!(b > T(0))) b = T(0);
+        const T d = fabs(r) + a + b + T(1) * ang2;
+        if (l == 0 || d < bd2) { bd2 = d; best2 = l; }
+      }
+    }
+    if (want_closest && best2 != cl && atomicAdd(&g_dbg_count, 1) < 20)
+      printf("items: blk %d tid %d closest %d/%d total %d G %d\n", (int)blockIdx.x, tid, cl, best2, total, G);
+  }
+  if (tid == 0)
+    for (int a = 0; a < nl; ++a) {
+      bool found = false;
+      for (int b = 0; b < nl; ++b) found |= V.lperm[b] == a;
+      if (!found && atomicAdd(&g_dbg_count, 1) < 20) printf("items: blk %d lperm lacks %d\n", (int)blockIdx.x, a);
+    }
+  __syncthreads();
+#endif
+  return cl;
 }
 
 // ------------------------------------------------------------------ road network / routes
@@ -958,7 +1151,11 @@ __device__ unsigned long long g_phase[20];
 // and written once); each phase loads the few fields it needs into registers, so no state is
 // live across phases and the kernel runs at high occupancy without spilling.
 template <typename T, int NS, int EPW, int NET>
-__global__ void __launch_bounds__(NS* EPW, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES : (sizeof(T) == 8 ? 2 : 4))
+// Waves per SIMD the register budget is sized for: 2 in float64 and on a road network (whose
+// LDS view allows ~1.25-2.5 waves per SIMD anyway; at 4 the float32 instance spilled heavily), 4
+// for the float32 highway.
+__global__ void __launch_bounds__(NS* EPW, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES
+                                                               : (sizeof(T) == 8 || NET == NET_GRAPH ? 2 : 4))
 simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int32_t* __restrict__ actions,
                 const uint8_t* __restrict__ env_mask, int frames, double dt_d, int mode, int ablate) {
   constexpr bool CV = NET != NET_STRAIGHT;  // curved lane classes possible
@@ -992,6 +1189,11 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       V.rt->first[tid] = R.road_first[tid]; V.rt->n[tid] = R.road_n[tid];
     }
     if (tid == 0) V.rt->n_roads = R.n_roads;
+    // project_items' lane order: straight lanes first, then the curved ones (list order within)
+    const bool cur = tid < nl && V.lanes[tid].type != TTRL_LANE_STRAIGHT;
+    const unsigned long long below = (1ull << (tid & 63)) - 1;
+    const unsigned long long cm = __ballot(cur), sm = __ballot(tid < nl && !cur);
+    if (tid < nl) V.lperm[cur ? __popcll(sm) + __popcll(cm & below) : __popcll(sm & below)] = (int8_t)tid;
   }
   const T dt = T(dt_d);
 
@@ -1423,7 +1625,15 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         if constexpr (sizeof(T) == 8) V.xf[me] = (float)x;
       }
       PH(6);
-      const int cl = project_all<T, NS, EPW, CV>(V, P, nl, tid, le, i, present, x, y, h, !(ablate & A_NO_LANE));
+      int cl;
+#ifndef TTRL_NO_ITEMS
+      if constexpr (GR && NS * EPW == 64)
+#else
+      if constexpr (false)
+#endif
+        cl = project_items<T, NS, EPW>(V, P, nl, tid, le, i, present, !(ablate & A_NO_LANE));
+      else
+        cl = project_all<T, NS, EPW, CV>(V, P, nl, tid, le, i, present, x, y, h, !(ablate & A_NO_LANE));
       if (present && !(ablate & A_NO_LANE)) V.lane[me] = (int8_t)cl;  // on_state_update kinematics.py:170-177
       if (i == 0) V.pq_n[le] = 0;
       __syncthreads();
