@@ -148,8 +148,8 @@ def read_pmc(dtype: str, cfg_id: int) -> dict | None:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None, help="default 20 (config 6: 100)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 3 (config 6: 10)")
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     ap.add_argument("--config", type=int, default=4, choices=[2, 3, 4, 5, 6])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -157,6 +157,12 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="replay each step as one captured HIP graph (policy + env.step for config 5)")
     args = ap.parse_args()
+    # intersection steps are short (~2 ms) and their background resets settle over a few steps:
+    # a longer timed window keeps the number stable from run to run
+    if args.steps is None:
+        args.steps = 100 if args.config == 6 else 20
+    if args.warmup is None:
+        args.warmup = 10 if args.config == 6 else 3
 
     import torch
     import torch.distributed as dist

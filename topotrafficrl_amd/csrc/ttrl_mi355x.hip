@@ -1552,33 +1552,62 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             }
             V.ynew[me] = 0;
             __syncthreads();
-            if (doreg) {  // every pair (a < b) once: thread i takes (i, i + d mod NS), d = 1 .. NS/2
+            PH(18);
+            // is_conflict_possible (regulation.py:80-103) then respect_priorities (:62-77) for the pair
+            // (a < b) of the env at LDS base ebp; a yield only ever sets ynew, so pairs commute
+            auto reg_pair = [&](int ebp, int a, int b) {
+              bool conflict = false;
+              for (int t = 0; t < PRED_T && !conflict; ++t) {
+                const int pa = (ebp + a) * PRED_T + t, pb = (ebp + b) * PRED_T + t;
+                const T dx = V.px[pb] - V.px[pa], dy = V.py[pb] - V.py[pa];
+                if (sqrt(dx * dx + dy * dy) > T(P.length)) continue;
+                conflict = rects_intersect(V.px[pa], V.py[pa], V.ph[pa], V.px[pb], V.py[pb], V.ph[pb],
+                                           T(1.5) * T(P.length), T(0.9) * T(P.width));
+              }
+              if (!conflict) return;
+              const int qa = V.lanes[V.lane[ebp + a]].prio, qb = V.lanes[V.lane[ebp + b]].prio;
+              int yv;
+              if (qa > qb) yv = b;
+              else if (qa < qb) yv = a;
+              else {
+                const int ka = ebp + a, kb = ebp + b;
+                const T fab = V.ch[ka] * (V.x[kb] - V.x[ka]) + V.sh[ka] * (V.y[kb] - V.y[ka]);
+                const T fba = V.ch[kb] * (V.x[ka] - V.x[kb]) + V.sh[kb] * (V.y[ka] - V.y[kb]);
+                yv = fab > fba ? a : b;
+              }
+              if (V.kind[ebp + yv] == TTRL_IDM) V.ynew[ebp + yv] = 1;  // ControlledVehicle, not MDPVehicle
+            };
+            if constexpr (NS * EPW == 64) {
+              // One wavefront: the live pairs of the enforcing envs are spread over all its lanes
+              // (a scene has ~8 live vehicles in 32 slots: slot-owned pairs left most lanes idle)
+              const bool alive = V.kind[me] != TTRL_ABSENT;
+              const unsigned long long am = __ballot(alive), dm = __ballot(doreg);
+              constexpr unsigned long long SEG = NS == 64 ? ~0ull : ((1ull << NS) - 1);
+              if (alive) V.live[eb + __popcll(((am >> eb) & SEG) & ((1ull << i) - 1))] = (uint8_t)i;
+              int np[EPW], tot = 0;
+#pragma unroll
+              for (int e = 0; e < EPW; ++e) {
+                const int n = ((dm >> (e * NS)) & 1ull) ? __popcll((am >> (e * NS)) & SEG) : 0;
+                np[e] = n * (n - 1) / 2;
+                tot += np[e];
+              }
+              __syncthreads();
+              for (int k = tid; k < tot; k += 64) {
+                int e = 0, kk = k;
+                while (kk >= np[e]) { kk -= np[e]; ++e; }
+                int rb = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)kk)) * 0.5f);  // pairs ordered by rb
+                while (rb * (rb - 1) / 2 > kk) --rb;
+                while ((rb + 1) * rb / 2 <= kk) ++rb;
+                const int ra = kk - rb * (rb - 1) / 2;
+                reg_pair(e * NS, V.live[e * NS + ra], V.live[e * NS + rb]);
+              }
+            } else if (doreg) {  // every pair (a < b) once: thread i takes (i, i + d mod NS), d = 1 .. NS/2
               for (int d = 1; d <= NS / 2; ++d) {
                 if (d == NS / 2 && i >= NS / 2) break;
                 const int j = (i + d) & (NS - 1);
                 const int a = i < j ? i : j, b = i < j ? j : i;
                 if (V.kind[eb + a] == TTRL_ABSENT || V.kind[eb + b] == TTRL_ABSENT) continue;
-                bool conflict = false;  // is_conflict_possible regulation.py:80-103
-                for (int t = 0; t < PRED_T && !conflict; ++t) {
-                  const int pa = (eb + a) * PRED_T + t, pb = (eb + b) * PRED_T + t;
-                  const T dx = V.px[pb] - V.px[pa], dy = V.py[pb] - V.py[pa];
-                  if (sqrt(dx * dx + dy * dy) > T(P.length)) continue;
-                  conflict = rects_intersect(V.px[pa], V.py[pa], V.ph[pa], V.px[pb], V.py[pb], V.ph[pb],
-                                             T(1.5) * T(P.length), T(0.9) * T(P.width));
-                }
-                if (!conflict) continue;
-                // respect_priorities regulation.py:62-77
-                const int qa = V.lanes[V.lane[eb + a]].prio, qb = V.lanes[V.lane[eb + b]].prio;
-                int yv;
-                if (qa > qb) yv = b;
-                else if (qa < qb) yv = a;
-                else {
-                  const int ka = eb + a, kb = eb + b;
-                  const T fab = V.ch[ka] * (V.x[kb] - V.x[ka]) + V.sh[ka] * (V.y[kb] - V.y[ka]);
-                  const T fba = V.ch[kb] * (V.x[ka] - V.x[kb]) + V.sh[kb] * (V.y[ka] - V.y[kb]);
-                  yv = fab > fba ? a : b;
-                }
-                if (V.kind[eb + yv] == TTRL_IDM) V.ynew[eb + yv] = 1;  // ControlledVehicle, not MDPVehicle
+                reg_pair(eb, a, b);
               }
             }
             __syncthreads();
