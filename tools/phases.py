@@ -14,7 +14,7 @@ from topotrafficrl_amd.envs import VecHighwayEnv  # noqa: E402
 
 NAMES = ["meta", "act-setup", "scan", "mobil-bar+verdict", "abort", "steer/acc+bar", "kinematics", "project+bar",
          "candidates+bar", "sat+bar", "fold", "project-init", "idm-free(pow)", "mobil-queue+bar", "mobil-items",
-         "hbm-load+stage", "store", "regulation-pairs", "regulation-predict", "-"]
+         "hbm-load+stage", "store", "regulation-pairs", "regulation-predict", "follow_road"]
 
 
 def main(dtype="f64", steps=30, frames=15, ix=False):

@@ -778,6 +778,8 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const ttrl_params
   const int total = __popcll(live);
   if (present) V.live[__popcll(live & below)] = (uint8_t)tid;
   if (tid < nl) V.onm[tid] = 0ull;
+  for (int k = tid; k < nl * EPW * NS / 2; k += 64) ((int*)V.mypos)[k] = -1;  // not on the lane
+  if (tid < EPW) V.cnt[tid * (LMAX + 1) + LMAX] = 0;
   __syncthreads();
   const int G = total > 0 ? 64 / total : 1;  // lane groups per vehicle
   const int g = total > 0 ? tid / total : 1;
@@ -827,31 +829,27 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const ttrl_params
       if (cl < 0 || du < cd || (du == cd && lu < cl)) { cd = du; cl = lu; }
     }
   }
-  // per lane, in slot order: positions, compacted keys (read at the slot before any write; one
-  // wavefront, so every lane's read precedes every lane's write), slots and counts
-  const int sh = le * NS;
-  const unsigned long long seg = NS == 64 ? ~0ull : ((1ull << NS) - 1);
-  int* cnt = V.cnt + le * (LMAX + 1);
-  int mx = 0;
-  for (int l = 0; l < nl; ++l) {
-    const unsigned long long m = (V.onm[l] >> sh) & seg;
-    const bool on = (m >> i) & 1ull;
-    const int pos = on ? __popcll(m & ((1ull << i) - 1)) : -1;
-    const size_t base = ((size_t)l * EPW + le) * NSP;
-    if (on) {
-      const T sv = V.key[base + i];
-      V.key[base + pos] = sv;
-      V.idx[base + pos] = (uint8_t)i;
+  // one thread per (lane, env) list: its on-lane slots in slot order, keys compacted in place
+  // (position <= slot), slots, each vehicle's position and the list lengths
+  if (tid < nl * EPW) {
+    const int l = tid / EPW, e = tid - l * EPW;
+    constexpr unsigned long long SEG = NS == 64 ? ~0ull : ((1ull << NS) - 1);
+    const size_t base = ((size_t)l * EPW + e) * NSP;
+    int pos = 0;
+    for (unsigned long long m = (V.onm[l] >> (e * NS)) & SEG; m; m &= m - 1, ++pos) {
+      const int v = __builtin_ctzll(m);
+      V.key[base + pos] = V.key[base + v];
+      V.idx[base + pos] = (uint8_t)v;
+      V.mypos[(size_t)l * EPW * NS + e * NS + v] = (short)pos;
     }
-    V.mypos[(size_t)l * EPW * NS + le * NS + i] = (short)pos;
-    const int c = __popcll(m);
-    mx = c > mx ? c : mx;
-    if (i == 0) cnt[l] = c;
+    V.cnt[e * (LMAX + 1) + l] = pos;
+    atomicMax(&V.cnt[e * (LMAX + 1) + LMAX], pos);
   }
-  if (i == 0) cnt[LMAX] = mx;
 #ifdef TTRL_CHECK_ITEMS
   __syncthreads();
   if (present) {  // the per-vehicle projection, compared
+    const int sh = le * NS;
+    const unsigned long long seg = NS == 64 ? ~0ull : ((1ull << NS) - 1);
     const T x = V.x[tid], y = V.y[tid], h = V.h[tid];
     T bd2 = T(0), ang2 = T(0);
     int best2 = 0;
@@ -889,6 +887,18 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const ttrl_params
   __syncthreads();
 #endif
   return cl;
+}
+
+// The vehicle's longitudinal position along lane l: from the lane's candidate list when the vehicle
+// is on it (the projection after the last kinematics stored exactly lane_local's s for the same
+// position), else lane_local itself -- saves the turns' atan2 in the act phase.
+template <typename T, int NS, int EPW>
+__device__ __forceinline__ T lane_s(const View<T>& V, int l, int le, int i, T x, T y) {
+  const int pos = V.mypos[(size_t)l * EPW * NS + le * NS + i];
+  if (pos >= 0) return V.key[((size_t)l * EPW + le) * (NS + 1) + pos];
+  T s, r;
+  lane_local(V.lanes[l], x, y, s, r);
+  return s;
 }
 
 // ------------------------------------------------------------------ road network / routes
@@ -936,10 +946,8 @@ template <typename T>
 #define TTRL_NET_ATTR __forceinline__
 #endif
 __device__ TTRL_NET_ATTR int follow_road(const LaneT<T>* lanes, const RoadTab& R, T vl, int tgt, T x, T y, int8_t* rr,
-                                        int8_t* rl, int8_t* rn) {
+                                        int8_t* rl, int8_t* rn, T s) {  // s: the position along lanes[tgt]
   const LaneT<T>& L = lanes[tgt];
-  T s, r;
-  lane_local(L, x, y, s, r);
   if (!(s > L.len - vl / T(2))) return tgt;  // AbstractLane.after_end lane.py:120-125
   const int rd = L.road, id = L.lid, to = R.to[rd];
   int nroad = -1, nid = -1;
@@ -1242,7 +1250,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       int tgt = V.tgt[me];
       if constexpr (GR)  // ControlledVehicle.act starts with follow_road (controller.py:98)
         tgt = follow_road(V.lanes, *V.rt, T(P.lane_vehicle_length), tgt, x, y, V.rroad + me * TTRL_ROUTE_MAX,
-                          V.rlane + me * TTRL_ROUTE_MAX, V.rn + me);
+                          V.rlane + me * TTRL_ROUTE_MAX, V.rn + me, lane_s<T, NS, EPW>(V, tgt, le, i, x, y));
       if (act == TTRL_FASTER || act == TTRL_SLOWER) {  // MDPVehicle.act controller.py:304-315
         int si = speed_to_index(P, v) + (act == TTRL_FASTER ? 1 : -1);
         si = si < 0 ? 0 : (si > P.n_target_speeds - 1 ? P.n_target_speeds - 1 : si);
@@ -1278,10 +1286,12 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         if constexpr (GR) {  // follow_road opens IDMVehicle.act (not crashed) and ControlledVehicle.act
           if (present && (kind == TTRL_MDP || !(V.flags[me] & FL_CRASHED))) {
             tgt_new = follow_road(V.lanes, *V.rt, T(P.lane_vehicle_length), tgt_new, V.x[me], V.y[me],
-                                  V.rroad + me * TTRL_ROUTE_MAX, V.rlane + me * TTRL_ROUTE_MAX, V.rn + me);
+                                  V.rroad + me * TTRL_ROUTE_MAX, V.rlane + me * TTRL_ROUTE_MAX, V.rn + me,
+                                  lane_s<T, NS, EPW>(V, tgt_new, le, i, V.x[me], V.y[me]));
             V.tgt[me] = (int8_t)tgt_new;
           }
         }
+        PH(19);
         const int lane = V.lane[me], tgt = V.tgt[me];
         const int fl = V.flags[me];
         const bool idm = present && kind == TTRL_IDM && !(fl & FL_CRASHED);
@@ -1312,8 +1322,12 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         T s2[2];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          T rr;
-          lane_local<CV>(V.lanes[ql[q] < 0 ? 0 : ql[q]], x, y, s2[q], rr);
+          if constexpr (GR) {
+            s2[q] = lane_s<T, NS, EPW>(V, ql[q] < 0 ? 0 : ql[q], le, i, x, y);
+          } else {
+            T rr;
+            lane_local<CV>(V.lanes[ql[q] < 0 ? 0 : ql[q]], x, y, s2[q], rr);
+          }
         }
         int f2[2] = {-1, -1}, r2[2] = {-1, -1};
         PH(1);
