@@ -52,9 +52,24 @@ def reset_highway_seeded(state: BatchState, network: RoadNetwork, params: _abi.P
               torch.cuda.current_stream(state.device).cuda_stream)
 
 
+def rewards_and_dones(env, stream: int):
+    """One rewards_kernel launch into fresh outputs: reward [E] f32, terminated / truncated [E] bool
+    and the per-objective block env._components [E, 4].  The kernel writes every element (bool
+    storage is one byte), so the returned tensors need no clone / cast launches of their own."""
+    E, dev = env.num_envs, env.device
+    reward = torch.empty(E, dtype=torch.float32, device=dev)
+    term = torch.empty(E, dtype=torch.bool, device=dev)
+    trunc = torch.empty(E, dtype=torch.bool, device=dev)
+    comp = torch.empty((E, 4), dtype=torch.float32, device=dev)
+    _lib.call("ttrl_rewards_ex", C.byref(env.state.struct()), C.byref(env.network.table), C.byref(env.reward_cfg),
+              env.time.data_ptr(), reward.data_ptr(), term.data_ptr(), trunc.data_ptr(), comp.data_ptr(), stream)
+    env._reward, env._term, env._trunc, env._components = reward, term, trunc, comp
+    return reward, term, trunc
+
+
 def _reward_terms(names, components: torch.Tensor) -> dict:
     """[E, 4] component block -> {name: [E] view} (float32; 0/1 for the boolean terms)."""
-    return {n: components[:, i].clone() for i, n in enumerate(names)}
+    return {n: components[:, i] for i, n in enumerate(names)}  # views of this step's fresh [E, 4]
 
 
 class VecHighwayEnv:
@@ -240,11 +255,7 @@ class VecHighwayEnv:
     def _rewards_and_dones(self):
         """reward, terminated, truncated [E]; the per-objective terms (_agent_rewards,
         intersection_env.py:95-104) go to self._components [E, 4] for info["rewards"]."""
-        _lib.call("ttrl_rewards_ex", C.byref(self.state.struct()), C.byref(self.network.table),
-                  C.byref(self.reward_cfg), self.time.data_ptr(), self._reward.data_ptr(), self._term.data_ptr(),
-                  self._trunc.data_ptr(), self._components.data_ptr(),
-                  torch.cuda.current_stream(self.device).cuda_stream)
-        return self._reward.clone(), self._term.bool(), self._trunc.bool()
+        return rewards_and_dones(self, torch.cuda.current_stream(self.device).cuda_stream)
 
     def _info(self, obs, action) -> dict:
         """abstract.py:169-186 batched: device tensors [E]; info["rewards"] holds the per-objective

@@ -25,7 +25,7 @@ import torch
 
 from . import _abi, _lib
 from .action import action_factory
-from .envs import _reward_terms
+from .envs import _reward_terms, rewards_and_dones
 from .observation import observation_factory
 from .road import BatchedRoad, RoadNetwork
 from .state import BatchState
@@ -407,11 +407,7 @@ class VecIntersectionEnv:
     def _rewards_and_dones(self):
         """reward, terminated, truncated [E]; the per-objective terms (_agent_rewards,
         intersection_env.py:95-104) go to self._components [E, 4] for info["rewards"]."""
-        _lib.call("ttrl_rewards_ex", C.byref(self.state.struct()), C.byref(self.network.table),
-                  C.byref(self.reward_cfg), self.time.data_ptr(), self._reward.data_ptr(), self._term.data_ptr(),
-                  self._trunc.data_ptr(), self._components.data_ptr(),
-                  _stream(self.device))
-        return self._reward.clone(), self._term.bool(), self._trunc.bool()
+        return rewards_and_dones(self, _stream(self.device))
 
     def _info(self, obs, action) -> dict:
         """IntersectionEnv._info (intersection_env.py:120-128) over abstract.py:169-186, batched: device
