@@ -23,6 +23,7 @@
  *   ttrl_reset_highway       scene init: Vehicle.create_random kinematics.py:50-104,
  *                            IDMVehicle.__init__/randomize_behavior behavior.py:48-69
  *   ttrl_rewards             reward/termination template  ttrl_env/envs/intersection_env.py:78-119
+ *   ttrl_rewards_step        + the step's time / info     ttrl_env/envs/common/abstract.py:169-186, :239
  *   ttrl_ix_reset            IntersectionEnv._reset        ttrl_env/envs/intersection_env.py:135-318
  *                            (_make_vehicles :251-318, _spawn_vehicle :320-348, AbstractEnv.reset abstract.py:188-214)
  *   ttrl_ix_clear_spawn      IntersectionEnv.step tail     ttrl_env/envs/intersection_env.py:135-139
@@ -362,6 +363,14 @@ int ttrl_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* road,
 int ttrl_rewards_ex(const ttrl_state_t* s, const ttrl_lane_table_t* road,
                     const ttrl_reward_cfg_t* cfg, const double* time, float* reward,
                     uint8_t* terminated, uint8_t* truncated, float* components, void* stream);
+/* The env.step tail in one launch: time[E] += time_inc (AbstractEnv.step abstract.py:239; 0 leaves
+ * time untouched), then ttrl_rewards_ex, and -- when ego_speed / ego_crashed are given (both or
+ * neither) -- the info's speed [E] (the state's dtype) and crashed [E] uint8 of the controlled
+ * vehicle (abstract.py:169-186; slot 0 for an env without one). */
+int ttrl_rewards_step(const ttrl_state_t* s, const ttrl_lane_table_t* road,
+                      const ttrl_reward_cfg_t* cfg, double* time, double time_inc, float* reward,
+                      uint8_t* terminated, uint8_t* truncated, float* components, void* ego_speed,
+                      uint8_t* ego_crashed, void* stream);
 
 #ifdef __cplusplus
 }

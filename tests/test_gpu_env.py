@@ -49,6 +49,8 @@ def test_env_step_matches_oracle(road, hip_device):
         assert np.allclose(rew.cpu().numpy(), ref_r, atol=1e-6)
         assert np.array_equal(term.cpu().numpy(), ref_term) and np.array_equal(trunc.cpu().numpy(), ref_trunc)
         assert np.allclose(info["speed"].cpu().numpy(), h["speed"][:, 0])
+        assert np.array_equal(info["crashed"].cpu().numpy(), h["crashed"][:, 0] != 0)
+        assert np.all(env.time.cpu().numpy() == float(t))  # time += 1 runs in the rewards launch
         for i, name in enumerate(env.REWARD_TERMS):  # info["rewards"] (abstract.py:182-185)
             assert np.allclose(info["rewards"][name].cpu().numpy(), ref_c[:, i], atol=1e-6), name
 

@@ -54,6 +54,10 @@ def test_device_episodes_match_reference(hip_device):
         for e in range(len(GOLD)):
             assert abs(_reward_from_terms(env.reward_cfg, terms[e]) - float(rew[e])) <= 1e-6, (e, p)
         assert torch.equal(info["agents_rewards"][0], rew)
+        # info speed / crashed come from the rewards launch; the step tail's clears leave the ego as it was
+        assert torch.equal(info["speed"], env.state.ego("speed"))
+        assert torch.equal(info["crashed"], env.state.ego("crashed").bool())
+        assert np.all(env.time.cpu().numpy() == float(p + 1))
         assert torch.equal(info["agents_terminated"][0].cpu(), torch.from_numpy((terms[:, 0] != 0) | (terms[:, 2] != 0)))
 
 

@@ -32,6 +32,7 @@ _SIGS = {
     "ttrl_seed_pcg64": ([_P, C.c_int32, _P], C.c_int),
     "ttrl_rewards": ([_P, _P, _P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_rewards_ex": ([_P, _P, _P, _P, _P, _P, _P, _P, _P], C.c_int),
+    "ttrl_rewards_step": ([_P, _P, _P, _P, C.c_double, _P, _P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_ix_reset": ([_P, _P, _P, _P, _P, C.c_int32, _P, _P], C.c_int),
     "ttrl_ix_clear_spawn": ([_P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_copy_envs": ([_P, _P, _P, _P], C.c_int),

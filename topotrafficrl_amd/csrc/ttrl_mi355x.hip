@@ -2635,15 +2635,26 @@ __global__ void reset_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t
 // IntersectionEnv._agent_reward / _is_terminated / _is_truncated (intersection_env.py:78-119) and
 // has_arrived (:364-369) for the env's controlled vehicle (its first MDP slot).
 template <typename T>
-__global__ void rewards_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_reward_cfg_t cfg, const double* __restrict__ time,
-                               float* __restrict__ reward, uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
-                               float* __restrict__ comp) {
+__global__ void rewards_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_reward_cfg_t cfg, double* __restrict__ time,
+                               double time_inc, float* __restrict__ reward, uint8_t* __restrict__ term,
+                               uint8_t* __restrict__ trunc, float* __restrict__ comp, T* __restrict__ ego_speed,
+                               uint8_t* __restrict__ ego_crashed) {
   const int env = blockIdx.x * blockDim.x + threadIdx.x;
   if (env >= st.n_envs) return;
   const size_t b = (size_t)env * st.n_veh;
   int ego = 0;
   while (ego < st.n_veh && st.kind[b + ego] != TTRL_MDP) ++ego;
-  trunc[env] = (uint8_t)(time[env] >= cfg.duration);
+  double t = time[env];
+  if (time_inc != 0.0) {  // AbstractEnv.step's `self.time += 1 / policy_frequency` (abstract.py:239)
+    t += time_inc;
+    time[env] = t;
+  }
+  if (ego_speed) {  // info speed / crashed (abstract.py:169-186) of the controlled vehicle, slot 0 if none
+    const size_t k0 = b + (ego == st.n_veh ? 0 : ego);
+    ego_speed[env] = ((const T*)st.speed)[k0];
+    ego_crashed[env] = st.crashed[k0] != 0;
+  }
+  trunc[env] = (uint8_t)(t >= cfg.duration);
   if (ego == st.n_veh) {
     reward[env] = 0.f; term[env] = 0;
     if (comp) for (int q = 0; q < 4; ++q) comp[(size_t)env * 4 + q] = 0.f;
@@ -3368,21 +3379,29 @@ int ttrl_ix_clear_spawn(const ttrl_state_t* s, const ttrl_lane_table_t* road, co
   return launch_status();
 }
 
-int ttrl_rewards_ex(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_reward_cfg_t* cfg,
-                    const double* time, float* reward, uint8_t* terminated, uint8_t* truncated, float* components,
-                    void* stream) {
+int ttrl_rewards_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_reward_cfg_t* cfg,
+                      double* time, double time_inc, float* reward, uint8_t* terminated, uint8_t* truncated,
+                      float* components, void* ego_speed, uint8_t* ego_crashed, void* stream) {
   int rc = check_state(s, road);
   if (rc) return rc < 0 ? rc : TTRL_OK;
-  if (!cfg || !time || !reward || !terminated || !truncated) return TTRL_E_ARG;
+  if (!cfg || !time || !reward || !terminated || !truncated || (!ego_speed) != (!ego_crashed)) return TTRL_E_ARG;
   hipStream_t st = (hipStream_t)stream;
   const int blocks = (s->n_envs + 255) / 256;
   if (s->dtype == TTRL_F64)
-    hipLaunchKernelGGL(rewards_kernel<double>, dim3(blocks), dim3(256), 0, st, *s, *road, *cfg, time, reward,
-                       terminated, truncated, components);
+    hipLaunchKernelGGL(rewards_kernel<double>, dim3(blocks), dim3(256), 0, st, *s, *road, *cfg, time, time_inc,
+                       reward, terminated, truncated, components, (double*)ego_speed, ego_crashed);
   else
-    hipLaunchKernelGGL(rewards_kernel<float>, dim3(blocks), dim3(256), 0, st, *s, *road, *cfg, time, reward,
-                       terminated, truncated, components);
+    hipLaunchKernelGGL(rewards_kernel<float>, dim3(blocks), dim3(256), 0, st, *s, *road, *cfg, time, time_inc,
+                       reward, terminated, truncated, components, (float*)ego_speed, ego_crashed);
   return launch_status();
+}
+
+int ttrl_rewards_ex(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_reward_cfg_t* cfg,
+                    const double* time, float* reward, uint8_t* terminated, uint8_t* truncated, float* components,
+                    void* stream) {
+  // time_inc 0: the kernel only reads time
+  return ttrl_rewards_step(s, road, cfg, const_cast<double*>(time), 0.0, reward, terminated, truncated, components,
+                           nullptr, nullptr, stream);
 }
 
 int ttrl_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_reward_cfg_t* cfg,

@@ -52,20 +52,24 @@ def reset_highway_seeded(state: BatchState, network: RoadNetwork, params: _abi.P
               torch.cuda.current_stream(state.device).cuda_stream)
 
 
-def rewards_and_dones(env, stream: int):
-    """One rewards_kernel launch into fresh outputs: reward [E] f32, terminated / truncated [E] bool
-    and the per-objective block env._components [E, 4].  The kernel writes every element (bool
-    storage is one byte), so the returned tensors need no clone / cast launches of their own."""
+def rewards_and_dones(env, stream: int, time_inc: float = 0.0):
+    """The step tail in one launch (ttrl_rewards_step): env.time += time_inc, then reward [E] f32,
+    terminated / truncated [E] bool, the per-objective block env._components [E, 4] and the info's
+    ego speed / crashed (env._ego_speed, env._ego_crashed), all into fresh tensors.  The kernel
+    writes every element (bool storage is one byte), so nothing needs a clone / cast launch."""
     E, dev = env.num_envs, env.device
     reward = torch.empty(E, dtype=torch.float32, device=dev)
     term = torch.empty(E, dtype=torch.bool, device=dev)
     trunc = torch.empty(E, dtype=torch.bool, device=dev)
     comp = torch.empty((E, 4), dtype=torch.float32, device=dev)
-    _lib.call("ttrl_rewards_ex", C.byref(env.state.struct()), C.byref(env.network.table), C.byref(env.reward_cfg),
-              env.time.data_ptr(), reward.data_ptr(), term.data_ptr(), trunc.data_ptr(), comp.data_ptr(), stream)
+    speed = torch.empty(E, dtype=env.state["speed"].dtype, device=dev)
+    crashed = torch.empty(E, dtype=torch.bool, device=dev)
+    _lib.call("ttrl_rewards_step", C.byref(env.state.struct()), C.byref(env.network.table), C.byref(env.reward_cfg),
+              env.time.data_ptr(), float(time_inc), reward.data_ptr(), term.data_ptr(), trunc.data_ptr(),
+              comp.data_ptr(), speed.data_ptr(), crashed.data_ptr(), stream)
     env._reward, env._term, env._trunc, env._components = reward, term, trunc, comp
+    env._ego_speed, env._ego_crashed = speed, crashed
     return reward, term, trunc
-
 
 def _reward_terms(names, components: torch.Tensor) -> dict:
     """[E, 4] component block -> {name: [E] view} (float32; 0/1 for the boolean terms)."""
@@ -227,10 +231,11 @@ class VecHighwayEnv:
         """abstract.py:224-250: (obs, reward[E], terminated[E], truncated[E], info)."""
         if self.road is None:
             raise NotImplementedError("The road and vehicle must be initialized in the environment implementation")
-        self.time += 1 / self.config["policy_frequency"]
         self._simulate(action)
         obs = self.observation_type.observe()
-        reward, terminated, truncated = self._rewards_and_dones()
+        # time += 1 / policy_frequency (abstract.py:239) runs in the rewards launch: nothing in
+        # between reads it
+        reward, terminated, truncated = self._rewards_and_dones(1 / self.config["policy_frequency"])
         info = self._info(obs, action)
         if self.config["auto_reset"]:
             # finished envs restart on the device; obs is the new episode's first observation and
@@ -252,15 +257,15 @@ class VecHighwayEnv:
 
     REWARD_TERMS = ["collision_reward", "high_speed_reward", "arrived_reward", "on_road_reward"]
 
-    def _rewards_and_dones(self):
+    def _rewards_and_dones(self, time_inc: float = 0.0):
         """reward, terminated, truncated [E]; the per-objective terms (_agent_rewards,
         intersection_env.py:95-104) go to self._components [E, 4] for info["rewards"]."""
-        return rewards_and_dones(self, torch.cuda.current_stream(self.device).cuda_stream)
+        return rewards_and_dones(self, torch.cuda.current_stream(self.device).cuda_stream, time_inc)
 
     def _info(self, obs, action) -> dict:
         """abstract.py:169-186 batched: device tensors [E]; info["rewards"] holds the per-objective
         terms of the last _rewards_and_dones (AbstractEnv._rewards)."""
-        return {"speed": self.state["speed"][:, 0].clone(), "crashed": self.state["crashed"][:, 0].bool(),
+        return {"speed": self._ego_speed, "crashed": self._ego_crashed,
                 "action": action, "rewards": _reward_terms(self.REWARD_TERMS, self._components)}
 
     def _auto_reset(self, done: torch.Tensor) -> None:

@@ -381,10 +381,10 @@ class VecIntersectionEnv:
         """IntersectionEnv.step (intersection_env.py:135-139) over AbstractEnv.step (abstract.py:224-250)."""
         if self.road is None:
             raise NotImplementedError("The road and vehicle must be initialized in the environment implementation")
-        self.time += 1 / self.config["policy_frequency"]
         self._simulate(action)
         obs = self.observation_type.observe()
-        reward, terminated, truncated = self._rewards_and_dones()
+        # time += 1 / policy_frequency (abstract.py:239) runs in the rewards launch
+        reward, terminated, truncated = self._rewards_and_dones(1 / self.config["policy_frequency"])
         info = self._info(obs, action)
         ix_clear_spawn(self.state, self.network, self.params, self.ix)
         if self.config["auto_reset"]:
@@ -404,17 +404,17 @@ class VecIntersectionEnv:
 
     REWARD_TERMS = ["collision_reward", "high_speed_reward", "arrived_reward", "on_road_reward"]
 
-    def _rewards_and_dones(self):
+    def _rewards_and_dones(self, time_inc: float = 0.0):
         """reward, terminated, truncated [E]; the per-objective terms (_agent_rewards,
         intersection_env.py:95-104) go to self._components [E, 4] for info["rewards"]."""
-        return rewards_and_dones(self, _stream(self.device))
+        return rewards_and_dones(self, _stream(self.device), time_inc)
 
     def _info(self, obs, action) -> dict:
         """IntersectionEnv._info (intersection_env.py:120-128) over abstract.py:169-186, batched: device
         tensors [E].  One controlled vehicle per env, so agents_rewards / agents_terminated are
         1-tuples: its _agent_reward and crashed-or-arrived."""
         c = self._components
-        return {"speed": self.state.ego("speed"), "crashed": self.state.ego("crashed").bool(), "action": action,
+        return {"speed": self._ego_speed, "crashed": self._ego_crashed, "action": action,
                 "rewards": _reward_terms(self.REWARD_TERMS, c),
                 "agents_rewards": (self._reward.clone(),),
                 "agents_terminated": ((c[:, 0] != 0) | (c[:, 2] != 0),)}
