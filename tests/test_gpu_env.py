@@ -162,6 +162,22 @@ def test_auto_reset_in_step_returns_new_first_observation(hip_device):
     assert torch.equal(obs, fresh.observation_type.observe())
 
 
+def test_deepcopy_forks_an_independent_highway_env(hip_device):
+    """copy.deepcopy forks state, time and the auto-reset seed words / episode counters: both
+    copies follow the same trajectory through their auto-resets independently, and the fork's
+    resets do not change which episode the original replays next."""
+    import copy
+    env = make(8, 20, duration=2, auto_reset=True)
+    env.reset(seed=6)
+    env.step(torch.ones(8, dtype=torch.int64))
+    fork = copy.deepcopy(env)
+    assert fork._entropy.data_ptr() != env._entropy.data_ptr()
+    a = torch.full((8,), 3, dtype=torch.int64)
+    for _ in range(4):  # lockstep through two auto-resets (shared counters would advance twice)
+        r1, r2 = env.step(a), fork.step(a)
+        assert torch.equal(r1[0], r2[0]) and torch.equal(r1[1], r2[1])
+
+
 def test_returned_observations_are_not_overwritten(hip_device):
     """Like the reference's df.values.copy(), an obs kept by the caller survives later steps
     (a trainer records (s, a, r, s') pairs across steps)."""

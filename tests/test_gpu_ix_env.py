@@ -275,3 +275,39 @@ def test_slot_classes_match_the_oracle(slots, hip_device):
         for e in range(E):
             same_state(env_view(st, e), {k: v[e:e + 1] for k, v in h.a.items()}, EPISODE_TOL, f"{slots} {e} {p}")
         assert np.max(np.abs(obs.cpu().numpy() - want)) <= 1e-4
+
+
+def test_reset_right_after_step_joins_the_background_resets(hip_device):
+    """reset() straight after a step, while the side stream may still be resetting the spare
+    scenes: it waits for them before replacing the spare buffers (or rebuilding with a new config),
+    so the result equals a fresh env's."""
+    cfg = {**ENV_JSON, "num_envs": 32, "device": hip_device, "auto_reset": True, "duration": 2}
+    env = VecIntersectionEnv(cfg)
+    env.reset(seed=3)
+    a = torch.ones(32, dtype=torch.int64, device=hip_device)
+    env.step(a)
+    obs, _ = env.reset(seed=11, options={"config": {"initial_vehicle_count": 8}})
+    fresh = VecIntersectionEnv({**cfg, "initial_vehicle_count": 8})
+    want, _ = fresh.reset(seed=11)
+    assert torch.equal(obs, want)
+    for _ in range(3):
+        r1, r2 = env.step(a), fresh.step(a)
+        assert torch.equal(r1[0], r2[0]) and torch.equal(r1[1], r2[1])
+    obs, _ = env.reset(seed=11)  # same config, buffers kept: the spare reset is joined too
+    want, _ = fresh.reset(seed=11)
+    assert torch.equal(obs, want)
+
+
+def test_masked_observation_keeps_the_other_envs_ids(hip_device):
+    """An auto-reset step re-observes only the finished envs: observed_ids of the others stay those
+    of their last full observation."""
+    env = VecIntersectionEnv({**ENV_JSON, "num_envs": 16, "device": hip_device})
+    env.reset(seed=4)
+    ot = env.observation_type
+    ot.observe()
+    full = ot.observed_ids.clone()
+    mask = torch.zeros(16, dtype=torch.int32, device=hip_device)
+    mask[3] = 1
+    ot.observe(mask=mask, out=torch.empty((16, ot.vehicles_count, len(ot.features)), device=hip_device))
+    keep = torch.arange(16, device=hip_device) != 3
+    assert torch.equal(ot.observed_ids[keep], full[keep])

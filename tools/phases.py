@@ -17,13 +17,13 @@ NAMES = ["meta", "act-setup", "scan", "mobil-bar+verdict", "abort", "steer/acc+b
          "hbm-load+stage", "store", "regulation-pairs", "regulation-predict", "follow_road"]
 
 
-def main(dtype="f64", steps=30, frames=15, ix=False):
+def main(dtype="f64", steps=30, frames=15, ix=False, E=4096):
     dev = torch.device("cuda:0")
     if ix:  # the intersection scenario (NET_GRAPH instance), 32 slots
         from topotrafficrl_amd.intersection import VecIntersectionEnv
         env = VecIntersectionEnv({"num_envs": 4096, "device": "cuda:0", "dtype": dtype})
     else:
-        env = VecHighwayEnv({"num_envs": 4096, "vehicles_count": 64, "device": "cuda:0", "dtype": dtype})
+        env = VecHighwayEnv({"num_envs": E, "vehicles_count": 64, "device": "cuda:0", "dtype": dtype})
     env.reset(seed=12345)
     n_act = env.action_space.n
     g = torch.Generator(device=dev).manual_seed(1000)
@@ -36,7 +36,7 @@ def main(dtype="f64", steps=30, frames=15, ix=False):
     buf = np.zeros(20, dtype=np.uint64)
     tot = np.zeros(20)
     for t in range(steps):
-        a = env.action_type._codes(torch.randint(0, n_act, (4096,), device=dev, generator=g))
+        a = env.action_type._codes(torch.randint(0, n_act, (E,), device=dev, generator=g))
         rd(buf.ctypes.data)
         sim(C.byref(env.state.struct()), C.byref(env.network.table), C.byref(env.params), a.data_ptr(), frames, 1 / 15,
             stream)
@@ -44,13 +44,13 @@ def main(dtype="f64", steps=30, frames=15, ix=False):
         rd(buf.ctypes.data)
         if t >= 10:
             tot += buf.astype(np.float64)
-    waves = (4096 if not ix else 2048) * (steps - 10)  # ix: two envs per 64-lane workgroup
+    waves = (E if not ix else 2048) * (steps - 10)  # ix: two envs per 64-lane workgroup
     per = tot / waves
-    print(f"[{dtype}] cycles per wave per {frames}-frame launch (mean over {steps - 10} launches), total {per.sum():.0f}")
+    print(f"[{dtype}] E={E} cycles per wave per {frames}-frame launch (mean over {steps - 10} launches), total {per.sum():.0f}")
     for n, c in zip(NAMES, per):
         print(f"  {n:16s} {c:10.0f}  {100 * c / per.sum():5.1f}%  ({c / frames:8.0f} per frame)")
 
 
 if __name__ == "__main__":
     main(sys.argv[1] if len(sys.argv) > 1 else "f64", frames=int(sys.argv[2]) if len(sys.argv) > 2 else 15,
-         ix="--ix" in sys.argv)
+         ix="--ix" in sys.argv, E=int(os.environ.get("ENVS", "4096")))

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Print VGPR / SGPR / scratch / occupancy of the simulate kernels (compile-time resource usage).
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -I include "$@" -o /tmp/regs.so \
+hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -mllvm -disable-machine-licm -fPIC -shared -I include "$@" -o /tmp/regs.so \
   topotrafficrl_amd/csrc/ttrl_mi355x.hip -Rpass-analysis=kernel-resource-usage 2>&1 \
   | awk '/Function Name/{n=$NF; sub(/\[.*/,"",n); name=$0; sub(/.*Function Name: /,"",name); sub(/ \[.*/,"",name)}
          /VGPRs:/{v=$0; sub(/.*VGPRs: /,"",v); sub(/ .*/,"",v)}

@@ -31,7 +31,7 @@ def build():
                                check=True, capture_output=True, text=True).stdout)
     for name, flags in {**VARIANTS, **TIMING}.items():
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
-               "-shared", "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "topotrafficrl_amd", "csrc"), *flags, "-o", os.path.join(OUT, f"lib_{name}.so"),
+               "-shared", "-mllvm", "-disable-machine-licm", "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "topotrafficrl_amd", "csrc"), *flags, "-o", os.path.join(OUT, f"lib_{name}.so"),
                head if name.startswith("head") else src]
         procs.append(subprocess.Popen(cmd))
     for p in procs:

@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include "ttrl_mi355x.h"
+#include "ttrl_math.h"
 
 namespace {
 
@@ -28,6 +29,23 @@ namespace {
 #else
 #define TTRL_TRANSC __noinline__
 #endif
+#ifdef TTRL_FAKE_TRANSC
+// Diagnostic timing build only (tools/variants.py): float32 hardware approximations stand in
+// for the float64 transcendentals, so the results are NOT the reference's.
+__device__ __forceinline__ double t_sin(double x) { return __sinf((float)x); }
+__device__ __forceinline__ double t_cos(double x) { return __cosf((float)x); }
+__device__ __forceinline__ double t_tan(double x) { return __tanf((float)x); }
+__device__ __forceinline__ double t_atan(double x) { return atanf((float)x); }
+__device__ __forceinline__ double t_asin(double x) { return asinf((float)x); }
+__device__ __forceinline__ double t_pow(double x, double y) { return __expf((float)y * __logf((float)x)); }
+template <typename T> struct SinCos { T s, c; };
+__device__ __forceinline__ SinCos<double> t_sincos(double x) {
+  SinCos<double> r;
+  r.s = __sinf((float)x);
+  r.c = __cosf((float)x);
+  return r;
+}
+#else
 __device__ TTRL_TRANSC double t_sin(double x) { return ::sin(x); }
 __device__ TTRL_TRANSC double t_cos(double x) { return ::cos(x); }
 __device__ TTRL_TRANSC double t_tan(double x) { return ::tan(x); }
@@ -47,6 +65,7 @@ __device__ TTRL_TRANSC SinCos<double> t_sincos(double x) {
   ::sincos(x, &r.s, &r.c);
   return r;
 }
+#endif
 #ifdef TTRL_F32_TRANSC_NOINLINE
 #define TTRL_TRANSC32 __noinline__
 #else
@@ -63,6 +82,28 @@ __device__ TTRL_TRANSC32 SinCos<float> t_sincos(float x) {
   ::sincosf(x, &r.s, &r.c);
   return r;
 }
+
+// Elementary functions of the simulate kernel's vehicle model (steering, bicycle model, IDM):
+// float64 through the short inline fdlibm restatements of ttrl_math.h, float32 through ocml.
+#ifdef TTRL_FAKE_TRANSC
+__device__ __forceinline__ SinCos<double> k_sincos(double x) { return t_sincos(x); }
+__device__ __forceinline__ double k_atan(double x) { return t_atan(x); }
+__device__ __forceinline__ double k_asin(double x) { return t_asin(x); }
+__device__ __forceinline__ double k_pow(double x, double y) { return t_pow(x, y); }
+#else
+__device__ __forceinline__ SinCos<double> k_sincos(double x) {
+  SinCos<double> r;
+  ttrl_math::sincos_d(x, r.s, r.c);
+  return r;
+}
+__device__ __forceinline__ double k_atan(double x) { return ttrl_math::atan_d(x); }
+__device__ __forceinline__ double k_asin(double x) { return ttrl_math::asin_d(x); }
+__device__ __forceinline__ double k_pow(double x, double y) { return ttrl_math::pow_d(x, y); }
+#endif
+__device__ __forceinline__ SinCos<float> k_sincos(float x) { return t_sincos(x); }
+__device__ __forceinline__ float k_atan(float x) { return t_atan(x); }
+__device__ __forceinline__ float k_asin(float x) { return t_asin(x); }
+__device__ __forceinline__ float k_pow(float x, float y) { return t_pow(x, y); }
 
 constexpr int LMAX = TTRL_MAX_LANES;
 constexpr float FAR = 1e30f;  // x of absent slots in the LDS view: never within a collision window
@@ -224,13 +265,13 @@ __device__ __forceinline__ T steering_control(const LaneT<T>& L, const ttrl_para
   lane_local<CV>(L, x, y, s, r);
   const T lfh = heading_at<CV>(L, s + v * T(P.tau_pursuit));  // lane_future_heading
   const T lat_cmd = -T(P.kp_lateral) * r;
-  const T hcmd = t_asin(clip(lat_cmd / not_zero(v), T(-1), T(1)));
+  const T hcmd = k_asin(clip(lat_cmd / not_zero(v), T(-1), T(1)));
   const T href = lfh + clip(hcmd, -Tpi<T>() / T(4), Tpi<T>() / T(4));
   const T hrate = T(P.kp_heading) * wrap_to_pi(href - h);
   // slip = asin(c); tan(slip) = c / sqrt((1 - c)(1 + c)) (= +-inf at |c| = 1, where the
   // reference's tan(+-pi/2) = +-1.6e16 and atan of either is +-pi/2): one call instead of two
   const T c = clip(T(P.length) / T(2) / not_zero(v) * hrate, T(-1), T(1));
-  const T st = t_atan(T(2) * (c / sqrt((T(1) - c) * (T(1) + c))));
+  const T st = k_atan(T(2) * (c / sqrt((T(1) - c) * (T(1) + c))));
   return clip(st, -T(P.max_steering), T(P.max_steering));
 }
 
@@ -418,19 +459,16 @@ struct RoadTab {
   int n_roads;
 };
 
-// A close pair (i < j) queued for the SAT test, and its result.
-template <typename T> struct PairRec {
-  T tx, ty;
-  short i, j;
-  int res;  // bit0 intersecting, bit1 will_intersect
-};
+// The collision queue holds close pairs (i < j) for the SAT test as three arrays: the translation
+// (tx, ty) and ij = i | j << 8 | result << 16 (bit 0 intersecting, bit 1 will_intersect).
+__device__ __forceinline__ int pair_pack(int i, int j, int res) { return i | (j << 8) | (res << 16); }
 
 // LDS "road view" of one workgroup (EPW envs x NS slots).
 template <typename T> struct View {
   LaneT<T>* lanes;   // [LMAX]
   T *x, *y, *v, *ch, *sh, *ts;  // [EPW*NS] shared road view (read by other vehicles)
   float* xf;                     // [EPW*NS] float copy of x for the collision window prefilter (== x for f32)
-  T *h, *timer, *delta, *steer, *acc, *ix, *iy;  // [EPW*NS] per-vehicle state resident in LDS
+  T *h, *delta;                  // [EPW*NS] heading (project_items reads it across lanes), IDM DELTA (MOBIL items)
   T* afree;                      // [EPW*NS] IDM free-road term of the frame (MOBIL items read it)
   uint8_t *kind, *flags;         // [EPW*NS] flags: 1 crashed, 2 has_impact, 4 enable_lane_change
   int8_t* sidx;                  // [EPW*NS] MDPVehicle.speed_index
@@ -445,7 +483,8 @@ template <typename T> struct View {
   int* nitem;        // [EPW] MOBIL items queued this frame
   int8_t *lane, *tgt;            // [EPW*NS] lane (-1 absent), target (old, for the act phase)
   unsigned long long* bal;       // [2][8] cross-wave ballots (NS > 64)
-  PairRec<T>* pq;                // [EPW][NS] close vehicle pairs of the frame (collision queue)
+  T *pq_tx, *pq_ty;              // [EPW][NS] close vehicle pairs of the frame (collision queue) ...
+  int* pq_ij;                    // ... over the act phase's scratch (afree .. item), dead by then
   int* pq_n;                     // [EPW] queue lengths (> NS: overflow)
   // NET_GRAPH only (null otherwise)
   int8_t *rroad, *rlane;         // [EPW*NS][TTRL_ROUTE_MAX] routes
@@ -462,9 +501,10 @@ template <typename T> struct View {
 constexpr int PRED_T = 11;       // np.arange(0.25, 3, 0.25) (regulation.py:86)
 
 // Byte offsets of the view's arrays in the dynamic LDS block (host: sizing; device: carve).
+constexpr int N_REALS = 8;  // x, y, v, ch, sh, ts, h, delta
 struct ViewLayout {
-  size_t lanes, reals[14], xf, key, pq, bal, cnt, wcnt, nitem, pq_n, mypos, f0, r0, ft, mob, item, idx, kind,
-      flags, sidx, lane, tgt, pred, rroad, rlane, rn, ynew, rt, onm, live, lperm, pd, pl, total;
+  size_t lanes, reals[N_REALS], xf, key, afree, pq_tx, pq_ty, pq_ij, bal, cnt, wcnt, nitem, pq_n, mypos, f0, r0, ft,
+      mob, item, idx, kind, flags, sidx, lane, tgt, pred, rroad, rlane, rn, ynew, rt, onm, live, lperm, pd, pl, total;
 };
 
 template <typename T>
@@ -479,11 +519,11 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, 
     return r;
   };
   o.lanes = take(sizeof(LaneT<T>) * n_lanes, 16);
-  for (int k = 0; k < 14; ++k) o.reals[k] = take(sizeof(T) * M, 16);
+  for (int k = 0; k < N_REALS; ++k) o.reals[k] = take(sizeof(T) * M, 16);
   o.xf = sizeof(T) == 8 ? take(sizeof(float) * M, 16) : o.reals[0];
-  o.bal = take(16 * sizeof(unsigned long long), 16);
+  o.bal = take(NS > 64 ? 16 * sizeof(unsigned long long) : 0, 16);  // cross-wave ballots
   o.cnt = take(sizeof(int) * EPW * (LMAX + 1), 4);
-  o.wcnt = take(sizeof(int) * LMAX * 4, 4);
+  o.wcnt = take(NS > 64 ? sizeof(int) * LMAX * 4 : 0, 4);
   o.nitem = take(sizeof(int) * EPW, 4);
   o.pq_n = take(sizeof(int) * EPW, 4);
   o.kind = take(M, 4);
@@ -491,20 +531,28 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, 
   o.sidx = take(M, 4);
   o.lane = take(M, 4);
   o.tgt = take(M, 4);
-  // Frame-transient block: the per-lane candidate lists and the act phase's neighbour / MOBIL
-  // scratch (read from the start of a frame's act until its last barrier) and the collision pair
-  // queue (written after the projection).  The RegulatedRoad trajectory predictions live only
-  // between those two (step phase, before the kinematics), so on a road network they share it.
+  // Frame-transient block: the per-lane candidate lists (written by the projection at the end of
+  // a frame's step, read by the next frame's act), the act phase's neighbour / MOBIL scratch (read
+  // from the start of a frame's act until its last barrier) and, over that scratch, the collision
+  // pair queue (written after the projection).  The RegulatedRoad trajectory predictions live only
+  // between the act and the kinematics, so on a road network they share the whole block.
   const size_t t0 = take(0, 16);
   o.key = take(sizeof(T) * (size_t)n_lanes * EPW * (NS + 1), 16);
-  o.pq = take(sizeof(PairRec<T>) * M, 16);
   o.mypos = take(sizeof(short) * (size_t)n_lanes * M, 4);
+  o.idx = take((size_t)n_lanes * EPW * (NS + 1), 4);
+  const size_t u0 = take(0, 16);
+  o.afree = take(sizeof(T) * M, 16);
   o.f0 = take(sizeof(short) * M, 4);
   o.r0 = take(sizeof(short) * M, 4);
   o.ft = take(sizeof(short) * M, 4);
   o.mob = take(sizeof(short) * 2 * M, 4);
   o.item = take(sizeof(short) * 2 * M, 4);
-  o.idx = take((size_t)n_lanes * EPW * (NS + 1), 4);
+  const size_t u1 = take(0, 16);
+  p = u0;
+  o.pq_tx = take(sizeof(T) * M, 16);
+  o.pq_ty = take(sizeof(T) * M, 16);
+  o.pq_ij = take(sizeof(int) * M, 4);
+  if (p < u1) p = u1;
   if (graph) {
     o.pred = t0;
     const size_t pred_end = t0 + sizeof(T) * 3 * PRED_T * M;
@@ -531,12 +579,14 @@ __device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lane
   const ViewLayout o = view_layout<T>(EPW, NS, n_lanes, graph);
   View<T> V;
   V.lanes = (LaneT<T>*)(smem + o.lanes);
-  T** reals[] = {&V.x, &V.y, &V.v, &V.ch, &V.sh, &V.ts, &V.h, &V.timer, &V.delta, &V.steer, &V.acc,
-                 &V.ix, &V.iy, &V.afree};
-  for (int k = 0; k < 14; ++k) *reals[k] = (T*)(smem + o.reals[k]);
+  T** reals[N_REALS] = {&V.x, &V.y, &V.v, &V.ch, &V.sh, &V.ts, &V.h, &V.delta};
+  for (int k = 0; k < N_REALS; ++k) *reals[k] = (T*)(smem + o.reals[k]);
   V.xf = (float*)(smem + o.xf);
   V.key = (T*)(smem + o.key);
-  V.pq = (PairRec<T>*)(smem + o.pq);
+  V.afree = (T*)(smem + o.afree);
+  V.pq_tx = (T*)(smem + o.pq_tx);
+  V.pq_ty = (T*)(smem + o.pq_ty);
+  V.pq_ij = (int*)(smem + o.pq_ij);
   V.bal = (unsigned long long*)(smem + o.bal);
   V.cnt = (int*)(smem + o.cnt);
   V.wcnt = (int*)(smem + o.wcnt);
@@ -905,6 +955,9 @@ __device__ __forceinline__ T lane_s(const View<T>& V, int l, int le, int i, T x,
 // Network mode of the simulate kernel: one straight road (the highway), one road of curved
 // lanes, or a graph of roads with routes and RegulatedRoad priorities (the intersection).
 enum { NET_STRAIGHT = 0, NET_CURVED = 1, NET_GRAPH = 2 };
+// Lanes the straight-road instance's LDS layout is sized for; a road with more lanes runs the
+// NET_CURVED instance (which handles straight lanes too, with a layout sized at run time).
+constexpr int STRAIGHT_LANE_CAP = 4;
 
 // AbstractLane.distance lane.py:127-130
 template <typename T>
@@ -1010,7 +1063,7 @@ __device__ TTRL_NET_ATTR void predict_poses(const LaneT<T>* lanes, const RoadTab
 // point_in_rotated_rectangle :75-91 (which rotates by +angle, as written).
 template <typename T>
 __device__ TTRL_NET_ATTR bool rects_intersect(T ax, T ay, T ah, T bx, T by, T bh, T l, T w) {
-  const SinCos<T> ca = t_sincos(ah), cb = t_sincos(bh);
+  const SinCos<T> ca = k_sincos(ah), cb = k_sincos(bh);
   const T hl = l / T(2), hw = w / T(2);
   const T qx[9] = {-hl, -hl, hl, hl, T(0), -hl, hl, T(0), T(0)};
   const T qy[9] = {-hw, hw, hw, -hw, T(0), T(0), T(0), -hw, hw};
@@ -1038,7 +1091,7 @@ __device__ __forceinline__ T idm_ratio(T v, T ts, T lim) {
 }
 template <typename T>
 __device__ __forceinline__ T idm_free(const ttrl_params_t& P, T v, T ts, T lim, T delta) {
-  return T(P.comfort_acc_max) * (T(1) - t_pow(idm_ratio(v, ts, lim), delta));
+  return T(P.comfort_acc_max) * (T(1) - k_pow(idm_ratio(v, ts, lim), delta));
 }
 
 // IDM interaction term  COMFORT_ACC_MAX * (desired_gap(e, f) / not_zero(d))^2 (behavior.py:185-189,
@@ -1159,11 +1212,14 @@ __device__ unsigned long long g_phase[20];
 // and written once); each phase loads the few fields it needs into registers, so no state is
 // live across phases and the kernel runs at high occupancy without spilling.
 template <typename T, int NS, int EPW, int NET>
-// Waves per SIMD the register budget is sized for: 2 in float64 and on a road network (whose
-// LDS view allows ~1.25-2.5 waves per SIMD anyway; at 4 the float32 instance spilled heavily), 4
-// for the float32 highway.
+// Waves per SIMD the register budget is sized for: 4 on the straight highway (its compile-time
+// LDS view, <= 10 KB per 64-slot env in float64, fits 4 workgroups per SIMD, so a 4096-env batch
+// runs in one round instead of two: 0.455 -> 0.356 ms per float64 launch with machine LICM off,
+// see build flags), 2 on curved roads in float64 and on a road network (whose LDS view allows
+// ~1.25-2.5 waves per SIMD anyway).
 __global__ void __launch_bounds__(NS* EPW, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES
-                                                               : (sizeof(T) == 8 || NET == NET_GRAPH ? 2 : 4))
+                                                               : (NET == NET_STRAIGHT ? 4
+                                                                  : (sizeof(T) == 8 || NET == NET_GRAPH ? 2 : 4)))
 simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int32_t* __restrict__ actions,
                 const uint8_t* __restrict__ env_mask, int frames, double dt_d, int mode, int ablate) {
   constexpr bool CV = NET != NET_STRAIGHT;  // curved lane classes possible
@@ -1188,7 +1244,9 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   const size_t k = (size_t)env * N + i;
   const int me = le * NS + i;  // this vehicle's LDS slot
   const int eb = le * NS;      // env base in the LDS view
-  View<T> V = carve<T>(smem, EPW, NS, nl, GR);
+  // The straight-road instance carves a compile-time layout (LANE_CAP lanes): every view array
+  // is then the LDS base plus an immediate offset, so no base addresses occupy registers.
+  View<T> V = carve<T>(smem, EPW, NS, NET == NET_STRAIGHT ? STRAIGHT_LANE_CAP : nl, GR);
   PH_INIT
   stage_lanes(V, R, tid);
   if constexpr (GR) {
@@ -1206,6 +1264,9 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   const T dt = T(dt_d);
 
   bool present;
+  // Vehicle state only this thread reads (IDM timer, the action, the pending impact) stays in
+  // registers for the launch; what other vehicles read is staged in the LDS view.
+  T my_timer, my_steer, my_acc, my_ix, my_iy;
   {  // HBM -> LDS, once per launch (coalesced SoA rows)
     Veh<T> a;
     if (slot) load_veh(a, st, k);
@@ -1213,10 +1274,10 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
     present = slot && a.kind != TTRL_ABSENT;
     V.x[me] = present ? a.x : T(FAR); V.y[me] = a.y;
     if constexpr (sizeof(T) == 8) V.xf[me] = present ? (float)a.x : FAR; V.v[me] = a.v; V.ts[me] = a.ts;
-    const SinCos<T> sc = t_sincos(a.h);
+    const SinCos<T> sc = k_sincos(a.h);
     V.ch[me] = sc.c; V.sh[me] = sc.s;
-    V.h[me] = a.h; V.timer[me] = a.timer; V.delta[me] = a.delta; V.steer[me] = a.steer; V.acc[me] = a.acc;
-    V.ix[me] = a.ix; V.iy[me] = a.iy;
+    V.h[me] = a.h; V.delta[me] = a.delta;
+    my_timer = a.timer; my_steer = a.steer; my_acc = a.acc; my_ix = a.ix; my_iy = a.iy;
     V.kind[me] = (uint8_t)(present ? a.kind : TTRL_ABSENT);
     V.flags[me] = (uint8_t)((a.crashed ? FL_CRASHED : 0) | (a.hasimp ? FL_IMPACT : 0) | (a.lc ? FL_LC : 0));
     V.sidx[me] = (int8_t)a.sidx;
@@ -1268,8 +1329,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       }
       // ControlledVehicle.act low-level control (controller.py:126-133); Road.act recomputes
       // the same values this frame, the standalone ttrl_meta_action returns them.
-      V.steer[me] = steering_control<CV>(V.lanes[tgt], P, x, y, h, v);
-      V.acc[me] = T(P.kp_a) * (ts - v);
+      my_steer = steering_control<CV>(V.lanes[tgt], P, x, y, h, v);
+      my_acc = T(P.kp_a) * (ts - v);
       V.ts[me] = ts;
       V.tgt[me] = (int8_t)tgt;
     }
@@ -1299,9 +1360,9 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         const bool changing = idm && lane != tgt;
         const T x = V.x[me], y = V.y[me], v = V.v[me];
         bool fire = false;
-        if (idm && lc && !changing && T(P.lane_change_delay) < V.timer[me] && !(ablate & A_NO_MOBIL)) {
+        if (idm && lc && !changing && T(P.lane_change_delay) < my_timer && !(ablate & A_NO_MOBIL)) {
           fire = true;  // utils.do_every
-          V.timer[me] = T(0);
+          my_timer = T(0);
         }
         // side lanes (RoadNetwork.side_lanes road.py:200-211), gated as behavior.py:252-260
         bool left = false, right = false;
@@ -1523,8 +1584,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       // steering + IDM longitudinal (behavior.py:109-135); ego: ControlledVehicle.act (controller.py:126-133)
       const bool mdp = present && kind == TTRL_MDP;
       if (idm || mdp) {  // one steering pass for both kinds (the ego steers to its own target)
-        V.steer[me] = (idm && (ablate & A_NO_STEER)) ? T(0)
-                                                    : steering_control<CV>(V.lanes[idm ? tgt_new : tgt], P, x, y, V.h[me], v);
+        my_steer = (idm && (ablate & A_NO_STEER)) ? T(0)
+                                                 : steering_control<CV>(V.lanes[idm ? tgt_new : tgt], P, x, y, V.h[me], v);
       }
       if (idm) {
         const T a_free = V.afree[me];
@@ -1537,9 +1598,9 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
           if (ft >= 0) a2 -= idm_interact<CV>(V, P, eb, i, ft);
           if (a2 < acc) acc = a2;
         }
-        V.acc[me] = clip(acc, -T(P.acc_max), T(P.acc_max));
+        my_acc = clip(acc, -T(P.acc_max), T(P.acc_max));
       } else if (mdp) {
-        V.acc[me] = T(P.kp_a) * (V.ts[me] - v);
+        my_acc = T(P.kp_a) * (V.ts[me] - v);
       }
     }
 
@@ -1635,32 +1696,34 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       PH(17);
       T x = V.x[me], y = V.y[me], h = V.h[me];
       if (present) {
-        T v = V.v[me], steer = V.steer[me], acc = V.acc[me];
+        T v = V.v[me], steer = my_steer, acc = my_acc;
         int fl = V.flags[me];
-        if (kind == TTRL_IDM) V.timer[me] += dt;  // IDMVehicle.step behavior.py:147
+        if (kind == TTRL_IDM) my_timer += dt;  // IDMVehicle.step behavior.py:147
         // Vehicle.clip_actions kinematics.py:155-168
         if (fl & FL_CRASHED) { steer = T(0); acc = T(-1) * v; }
         if (v > T(P.max_speed)) { const T c = T(1) * (T(P.max_speed) - v); if (c < acc) acc = c; }
         else if (v < T(P.min_speed)) { const T c = T(1) * (T(P.min_speed) - v); if (c > acc) acc = c; }
-        V.steer[me] = steer;
-        V.acc[me] = acc;
+        my_steer = steer;
+        my_acc = acc;
         // kinematic bicycle, Vehicle.step kinematics.py:140-153
         if (ablate & A_NO_KIN) {
           x += v * V.ch[me] * dt; y += v * V.sh[me] * dt; v += acc * dt;
         } else {
-          // beta = atan(tan(steer) / 2) enters only through cos / sin of beta and of h + beta:
-          // cos(beta) = 1 / sqrt(1 + tb^2), sin(beta) = tb cos(beta), and h + beta by the
-          // angle sum on the resident cos / sin of h (a few ulp from the reference's direct
+          // beta = atan(tan(steer) / 2) enters only through cos / sin of beta and of h + beta.
+          // With (sd, cd) = sincos(steer), tan(beta) = sd / (2 cd), so cos(beta) =
+          // 2 |cd| / sqrt(4 cd^2 + sd^2) and sin(beta) = sign(cd) sd / sqrt(4 cd^2 + sd^2); h + beta
+          // by the angle sum on the resident cos / sin of h (a few ulp from the reference's direct
           // cos(h + beta), far inside the stated tolerances)
-          const T tb = T(1) / T(2) * t_tan(steer);
-          const T cb = T(1) / sqrt(T(1) + tb * tb), sb = tb * cb;
+          const SinCos<T> sd = k_sincos(steer);
+          const T inv = T(1) / sqrt(T(4) * (sd.c * sd.c) + sd.s * sd.s);
+          const T cb = T(2) * fabs(sd.c) * inv, sb = (sd.c < T(0) ? -sd.s : sd.s) * inv;
           const T c0 = V.ch[me], s0 = V.sh[me];
           const T vx = v * (c0 * cb - s0 * sb), vy = v * (s0 * cb + c0 * sb);
           x += vx * dt; y += vy * dt;
-          if (fl & FL_IMPACT) { x += V.ix[me]; y += V.iy[me]; fl = (fl | FL_CRASHED) & ~FL_IMPACT; }
+          if (fl & FL_IMPACT) { x += my_ix; y += my_iy; fl = (fl | FL_CRASHED) & ~FL_IMPACT; }
           h += v * sb / (T(P.length) / T(2)) * dt;
           v += acc * dt;
-          const SinCos<T> sc = t_sincos(h);
+          const SinCos<T> sc = k_sincos(h);
           V.ch[me] = sc.c; V.sh[me] = sc.s;
         }
         V.flags[me] = (uint8_t)fl;
@@ -1728,7 +1791,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
                               V.v[eb + j], dt))
               continue;  // provably (false, false): contributes nothing
             const int q = atomicAdd(&V.pq_n[le], 1);
-            if (q < NS) { V.pq[le * NS + q].i = (short)i; V.pq[le * NS + q].j = (short)j; }
+            if (q < NS) V.pq_ij[le * NS + q] = pair_pack(i, j, 0);
           }
         }
       }
@@ -1745,8 +1808,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
           const int t = t0 + i;
           if (t < npairs * 8) {
             const int q = t >> 3, kx = t & 7;
-            PairRec<T>& r = V.pq[le * NS + q];
-            const int a = eb + r.i, b = eb + r.j;
+            const int ij = V.pq_ij[le * NS + q];
+            const int a = eb + (ij & 0xff), b = eb + ((ij >> 8) & 0xff);
             T dd, dist, axx, axy;
             sat_axis(P, kx, V.x[a], V.y[a], V.ch[a], V.sh[a], V.v[a], V.x[b], V.y[b], V.ch[b], V.sh[b], V.v[b], dt,
                      dd, dist, axx, axy);
@@ -1764,21 +1827,23 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
               if (om < bm || (om == bm && ok < bk)) { bm = om; bk = ok; axx = ox; axy = oy; }
             }
             if (kx == 0) {
-              r.tx = will ? bm * axx : T(0);
-              r.ty = will ? bm * axy : T(0);
-              r.res = (inter ? 1 : 0) | (will ? 2 : 0);
+              V.pq_tx[le * NS + q] = will ? bm * axx : T(0);
+              V.pq_ty[le * NS + q] = will ? bm * axy : T(0);
+              V.pq_ij[le * NS + q] = pair_pack(ij & 0xff, (ij >> 8) & 0xff, (inter ? 1 : 0) | (will ? 2 : 0));
             }
           }
         }
       } else if (npairs <= NS && !(ablate & A_NO_SAT)) {
         for (int q = i; q < npairs; q += NS) {
-          PairRec<T>& r = V.pq[le * NS + q];
-          const int a = eb + r.i, b = eb + r.j;
+          const int ij = V.pq_ij[le * NS + q], pi_ = ij & 0xff, pj_ = (ij >> 8) & 0xff;
+          const int a = eb + pi_, b = eb + pj_;
           bool inter, will;
           T tx, ty;
           sat_pair(P, V.x[a], V.y[a], V.ch[a], V.sh[a], V.v[a], V.x[b], V.y[b], V.ch[b], V.sh[b], V.v[b], dt,
                    inter, will, tx, ty);
-          r.tx = tx; r.ty = ty; r.res = (inter ? 1 : 0) | (will ? 2 : 0);
+          V.pq_tx[le * NS + q] = tx;
+          V.pq_ty[le * NS + q] = ty;
+          V.pq_ij[le * NS + q] = pair_pack(pi_, pj_, (inter ? 1 : 0) | (will ? 2 : 0));
         }
       }
       __syncthreads();
@@ -1789,13 +1854,13 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         T gx = T(0), gy = T(0), lx = T(0), ly = T(0);
         if (npairs <= NS) {
           for (int q = 0; q < npairs; ++q) {
-            const PairRec<T> r = V.pq[le * NS + q];
-            if (r.i == i) {
-              if (r.res & 1) crash = true;
-              if ((r.res & 2) && r.j > best_gt) { best_gt = r.j; gx = r.tx / T(2); gy = r.ty / T(2); }
-            } else if (r.j == i) {
-              if (r.res & 1) crash = true;
-              if ((r.res & 2) && r.i > best_lt) { best_lt = r.i; lx = -r.tx / T(2); ly = -r.ty / T(2); }
+            const int ij = V.pq_ij[le * NS + q], ri = ij & 0xff, rj = (ij >> 8) & 0xff, res = ij >> 16;
+            if (ri == i) {
+              if (res & 1) crash = true;
+              if ((res & 2) && rj > best_gt) { best_gt = rj; gx = V.pq_tx[le * NS + q] / T(2); gy = V.pq_ty[le * NS + q] / T(2); }
+            } else if (rj == i) {
+              if (res & 1) crash = true;
+              if ((res & 2) && ri > best_lt) { best_lt = ri; lx = -V.pq_tx[le * NS + q] / T(2); ly = -V.pq_ty[le * NS + q] / T(2); }
             }
           }
         } else {  // overflow: every vehicle sweeps all its partners in index order
@@ -1828,8 +1893,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         }
         int fl = V.flags[me];
         if (crash) fl |= FL_CRASHED;
-        if (best_gt >= 0) { fl |= FL_IMPACT; V.ix[me] = gx; V.iy[me] = gy; }
-        else if (best_lt >= 0) { fl |= FL_IMPACT; V.ix[me] = lx; V.iy[me] = ly; }
+        if (best_gt >= 0) { fl |= FL_IMPACT; my_ix = gx; my_iy = gy; }
+        else if (best_lt >= 0) { fl |= FL_IMPACT; my_ix = lx; my_iy = ly; }
         V.flags[me] = (uint8_t)fl;
       }
     }
@@ -1838,8 +1903,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   __syncthreads();
   if (slot) {  // LDS -> HBM, once per launch
     Veh<T> a;
-    a.x = V.x[me]; a.y = V.y[me]; a.h = V.h[me]; a.v = V.v[me]; a.ts = V.ts[me]; a.timer = V.timer[me];
-    a.steer = V.steer[me]; a.acc = V.acc[me]; a.ix = V.ix[me]; a.iy = V.iy[me];
+    a.x = V.x[me]; a.y = V.y[me]; a.h = V.h[me]; a.v = V.v[me]; a.ts = V.ts[me]; a.timer = my_timer;
+    a.steer = my_steer; a.acc = my_acc; a.ix = my_ix; a.iy = my_iy;
     a.lane = V.lane[me]; a.tgt = V.tgt[me]; a.sidx = V.sidx[me];
     const int fl = V.flags[me];
     a.crashed = (fl & FL_CRASHED) != 0; a.hasimp = (fl & FL_IMPACT) != 0;
@@ -3004,6 +3069,7 @@ bool is_graph(const ttrl_lane_table_t& R) { return R.n_roads > 1 || R.regulation
 
 // TTRL_OK, a negative TTRL_E_* code, or EMPTY (> 0: no env, nothing to do -- the entry points
 // then return TTRL_OK before looking at buffers an empty batch need not have)
+#ifndef TTRL_KERNEL_ONLY  // host launchers
 constexpr int EMPTY = 1;
 int check_state(const ttrl_state_t* s, const ttrl_lane_table_t* R) {
   if (!s || !R) return TTRL_E_ARG;
@@ -3036,9 +3102,10 @@ int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_par
   const int blocks = (s.n_envs + EPW - 1) / EPW;
   if (blocks == 0) return TTRL_OK;
   const bool graph = is_graph(R);
-  const size_t lds = host_view_bytes(sizeof(T) == 8 ? TTRL_F64 : TTRL_F32, EPW, NS, R.n_lanes, graph);
-  bool curved = false;
+  bool curved = R.n_lanes > STRAIGHT_LANE_CAP;  // wider straight roads: the run-time layout instance
   for (int l = 0; l < R.n_lanes; ++l) curved |= R.type[l] != TTRL_LANE_STRAIGHT;
+  const size_t lds = host_view_bytes(sizeof(T) == 8 ? TTRL_F64 : TTRL_F32, EPW, NS,
+                                     graph || curved ? R.n_lanes : STRAIGHT_LANE_CAP, graph);
   if (graph)
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_GRAPH>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, P,
                        actions, mask, frames, dt, mode, ablate);
@@ -3114,7 +3181,14 @@ int dispatch_kin(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_p
   }
 }
 
+#endif  // TTRL_KERNEL_ONLY
+#ifdef TTRL_KERNEL_ONLY  // kernel-development builds (tools/asmstat.py): the highway instances only
+void* const kernel_only_refs[] = {(void*)&simulate_kernel<double, 64, 1, NET_STRAIGHT>,
+                                  (void*)&simulate_kernel<float, 64, 1, NET_STRAIGHT>};
+#endif
 }  // namespace
+
+#ifndef TTRL_KERNEL_ONLY
 
 // ===================================================================== C ABI
 extern "C" {
@@ -3410,3 +3484,4 @@ int ttrl_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttr
 }
 
 }  // extern "C"
+#endif  // TTRL_KERNEL_ONLY

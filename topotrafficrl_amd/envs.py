@@ -294,6 +294,8 @@ class VecHighwayEnv:
         new.state = self.state.clone()
         new.road = BatchedRoad(self.network, new.state, self.params)
         new.time = self.time.clone()
+        if self._entropy is not None:  # the fork's auto-resets must not advance our episode counters
+            new._entropy = self._entropy.clone()
         new.define_spaces()
         return new
 

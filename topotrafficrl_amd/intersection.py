@@ -349,6 +349,10 @@ class VecIntersectionEnv:
     def reset(self, *, seed=None, options: dict | None = None):
         """AbstractEnv.reset (abstract.py:188-214) + IntersectionEnv._reset: env e is
         ``IntersectionEnv.reset(seed=seed + env_id_offset + e)``."""
+        if self._spare is not None:
+            # the side stream may still be resetting the spares (it writes _spare and reads
+            # _spare_entropy): join it before either buffer is replaced or freed below
+            torch.cuda.current_stream(self.device).wait_event(self._spare_ready)
         if options and "config" in options:
             self.configure(options["config"])
             self._build()
