@@ -27,7 +27,7 @@ def main(dtype="f64", steps=30, frames=15, ix=False, E=4096):
     env.reset(seed=12345)
     n_act = env.action_space.n
     g = torch.Generator(device=dev).manual_seed(1000)
-    lib = _lib.load(os.path.join(ROOT, "tools", "_variants", "lib_timing.so"))
+    lib = _lib.load(os.path.join(ROOT, "tools", "_variants", os.environ.get("TIMING_LIB", "lib_timing.so")))
     sim = lib.ttrl_simulate
     sim.argtypes = [C.c_void_p] * 4 + [C.c_int32, C.c_double, C.c_void_p]
     rd = lib.ttrl_diag_phase_read
@@ -49,6 +49,33 @@ def main(dtype="f64", steps=30, frames=15, ix=False, E=4096):
     print(f"[{dtype}] E={E} cycles per wave per {frames}-frame launch (mean over {steps - 10} launches), total {per.sum():.0f}")
     for n, c in zip(NAMES, per):
         print(f"  {n:16s} {c:10.0f}  {100 * c / per.sum():5.1f}%  ({c / frames:8.0f} per frame)")
+    # the last launch, wave by wave: start / end spread and the per-SIMD finish (load balance)
+    nw = E if not ix else 2048
+    tr = np.zeros((nw, 3), dtype=np.uint64)
+    lib.ttrl_diag_wave_read.argtypes = [C.c_void_p, C.c_int]
+    lib.ttrl_diag_wave_read(tr.ctypes.data, nw)
+    hw = tr[:, 2]
+    xcc = (hw >> np.uint64(32)).astype(np.int64)
+    t0, t1 = tr[:, 0].astype(np.int64), tr[:, 1].astype(np.int64)
+    for x in np.unique(xcc):  # each XCD has its own shader clock: times relative to its first wave
+        b = t0[xcc == x].min()
+        t0[xcc == x] -= b
+        t1[xcc == x] -= b
+    base = 0
+    dur = t1 - t0
+    simd = (hw >> np.uint64(32)) * np.uint64(1 << 16) + ((hw & np.uint64(0xffff)) >> np.uint64(4))
+    print(f"waves {nw}: duration mean {dur.mean():.0f} min {dur.min()} max {dur.max()} p90 {np.percentile(dur, 90):.0f}; "
+          f"start spread {t0.max() - base}, last end {t1.max() - base}")
+    keys, inv = np.unique(simd, return_inverse=True)
+    lo = np.full(len(keys), np.iinfo(np.int64).max); hi = np.zeros(len(keys), dtype=np.int64)
+    np.minimum.at(lo, inv, t0); np.maximum.at(hi, inv, t1)
+    span = hi - lo
+    cnt = np.bincount(inv)
+    print(f"SIMDs used {len(keys)}, waves per SIMD {dict(zip(*np.unique(cnt, return_counts=True)))}; per-SIMD span "
+          f"(last end - first start, one clock) mean {span.mean():.0f} p10 {np.percentile(span, 10):.0f} "
+          f"p50 {np.percentile(span, 50):.0f} p90 {np.percentile(span, 90):.0f} max {span.max()}")
+    st = t0 - lo[inv]
+    print(f"wave start offset within its SIMD: mean {st.mean():.0f} max {st.max()}")
 
 
 if __name__ == "__main__":

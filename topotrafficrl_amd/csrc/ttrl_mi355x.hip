@@ -191,11 +191,17 @@ __device__ TTRL_CURVED_ATTR Pair<T> curved_local(int type, T px, T py, T sx, T s
   return o;
 }
 
-// CV = false: the caller's road is straight-only (the hot simulate kernel is instantiated
-// both ways), so the curved call sites -- and the registers they pin -- are compiled out.
+// CV = false: the caller's road is the straight highway (the NET_STRAIGHT simulate instance, which
+// the launcher picks only when every lane is a StraightLane along +x, direction exactly (1, 0), as
+// RoadNetwork.straight_road_network builds them), so the curved call sites -- and the registers
+// they pin -- are compiled out, and local_coordinates reduces to two subtractions:
+// s = dx * 1 + dy * 0 = dx and r = dx * -0 + dy * 1 = dy, the same values up to the sign of a zero.
 template <bool CV = true, typename T>
 __device__ __forceinline__ void lane_local(const LaneT<T>& L, T px, T py, T& s, T& r) {
-  if (!CV || L.type == TTRL_LANE_STRAIGHT) {  // StraightLane.local_coordinates lane.py:209-213
+  if (!CV) {
+    s = px - L.sx;
+    r = py - L.sy;
+  } else if (L.type == TTRL_LANE_STRAIGHT) {  // StraightLane.local_coordinates lane.py:209-213
     T dx = px - L.sx, dy = py - L.sy;
     s = dx * L.dx + dy * L.dy;
     r = dx * (-L.dy) + dy * L.dx;
@@ -470,6 +476,7 @@ template <typename T> struct View {
   float* xf;                     // [EPW*NS] float copy of x for the collision window prefilter (== x for f32)
   T *h, *delta;                  // [EPW*NS] heading (project_items reads it across lanes), IDM DELTA (MOBIL items)
   T* afree;                      // [EPW*NS] IDM free-road term of the frame (MOBIL items read it)
+  T* powb;                       // [EPW*NS] its power's base (pow_base), any vehicle's (MOBIL items)
   uint8_t *kind, *flags;         // [EPW*NS] flags: 1 crashed, 2 has_impact, 4 enable_lane_change
   int8_t* sidx;                  // [EPW*NS] MDPVehicle.speed_index
   T* key;            // [n_lanes][EPW][NS+1] s of the vehicles on each lane (AbstractLane.on_lane margin 1)
@@ -503,7 +510,7 @@ constexpr int PRED_T = 11;       // np.arange(0.25, 3, 0.25) (regulation.py:86)
 // Byte offsets of the view's arrays in the dynamic LDS block (host: sizing; device: carve).
 constexpr int N_REALS = 8;  // x, y, v, ch, sh, ts, h, delta
 struct ViewLayout {
-  size_t lanes, reals[N_REALS], xf, key, afree, pq_tx, pq_ty, pq_ij, bal, cnt, wcnt, nitem, pq_n, mypos, f0, r0, ft,
+  size_t lanes, reals[N_REALS], xf, key, afree, powb, pq_tx, pq_ty, pq_ij, bal, cnt, wcnt, nitem, pq_n, mypos, f0, r0, ft,
       mob, item, idx, kind, flags, sidx, lane, tgt, pred, rroad, rlane, rn, ynew, rt, onm, live, lperm, pd, pl, total;
 };
 
@@ -542,6 +549,7 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, 
   o.idx = take((size_t)n_lanes * EPW * (NS + 1), 4);
   const size_t u0 = take(0, 16);
   o.afree = take(sizeof(T) * M, 16);
+  o.powb = take(sizeof(T) * M, 16);
   o.f0 = take(sizeof(short) * M, 4);
   o.r0 = take(sizeof(short) * M, 4);
   o.ft = take(sizeof(short) * M, 4);
@@ -584,6 +592,7 @@ __device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lane
   V.xf = (float*)(smem + o.xf);
   V.key = (T*)(smem + o.key);
   V.afree = (T*)(smem + o.afree);
+  V.powb = (T*)(smem + o.powb);
   V.pq_tx = (T*)(smem + o.pq_tx);
   V.pq_ty = (T*)(smem + o.pq_ty);
   V.pq_ij = (int*)(smem + o.pq_ij);
@@ -1093,6 +1102,13 @@ template <typename T>
 __device__ __forceinline__ T idm_free(const ttrl_params_t& P, T v, T ts, T lim, T delta) {
   return T(P.comfort_acc_max) * (T(1) - k_pow(idm_ratio(v, ts, lim), delta));
 }
+// The power split in two, so a vehicle's base can be shared: the act phase stores every vehicle's
+// pow_base (float64: log of the ratio, as k_pow = exp(DELTA log ratio) computes it; float32: the
+// ratio) and MOBIL's new-follower term raises it to the caller's DELTA with the same bits.
+__device__ __forceinline__ double pow_base(double ratio) { return ttrl_math::log_d(ratio); }
+__device__ __forceinline__ float pow_base(float ratio) { return ratio; }
+__device__ __forceinline__ double pow_from_base(double b, double delta) { return ttrl_math::exp_d(delta * b); }
+__device__ __forceinline__ float pow_from_base(float b, float delta) { return t_pow(b, delta); }
 
 // IDM interaction term  COMFORT_ACC_MAX * (desired_gap(e, f) / not_zero(d))^2 (behavior.py:185-189,
 // desired_gap :192-217, lane_distance_to objects.py:182-197 along e's current lane).
@@ -1185,22 +1201,47 @@ enum { A_NO_COLL = 1, A_NO_MOBIL = 2, A_NO_ABORT = 4, A_NO_SCAN = 8, A_NO_STEER 
 
 enum { FL_CRASHED = 1, FL_IMPACT = 2, FL_LC = 4, FL_YIELD = 8 };
 
-// Diagnostic build only (-DTTRL_PHASE_TIMING): per-phase shader-clock cycles of every wave,
-// summed into g_phase (tools/phases.py).  The production kernel carries no stamps.
-#ifdef TTRL_PHASE_TIMING
+// Diagnostic builds only.  -DTTRL_PHASE_TIMING: per-phase shader-clock cycles of every wave,
+// summed into g_phase (tools/phases.py); the accumulators live in LDS (32-bit, one row per wave),
+// so the stamps leave the kernel's register allocation as it is (a register array of 20 counters
+// cost 40 VGPRs and spilled) -- but they add 320 B of LDS per workgroup.  -DTTRL_WAVE_TRACE: every
+// wave's (start, end) shader clock with its HW_ID / XCC_ID, no LDS (tools/phases.py --waves).
+// The production kernel carries neither.
+#if defined(TTRL_PHASE_TIMING) || defined(TTRL_WAVE_TRACE)
 __device__ unsigned long long g_phase[20];
-#define PH_INIT                                    \
-  unsigned long long ph_acc[20] = {};              \
-  unsigned long long ph_t = __builtin_readcyclecounter();
-#define PH(k)                                               \
-  do {                                                      \
-    const unsigned long long ph_n = __builtin_readcyclecounter(); \
-    ph_acc[k] += ph_n - ph_t;                               \
-    ph_t = ph_n;                                            \
+constexpr int WTRACE_MAX = 16384;
+__device__ unsigned long long g_wtrace[WTRACE_MAX][3];
+#define WT_INIT const unsigned long long ph_t0 = __builtin_readcyclecounter();
+#define WT_FLUSH                                                       \
+  {                                                                    \
+    const unsigned ph_w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); \
+    if ((threadIdx.x & 63) == 0 && ph_w < WTRACE_MAX) {                \
+      g_wtrace[ph_w][0] = ph_t0;                                       \
+      g_wtrace[ph_w][1] = __builtin_readcyclecounter();                \
+      g_wtrace[ph_w][2] = ((unsigned long long)__builtin_amdgcn_s_getreg(63508) << 32) | __builtin_amdgcn_s_getreg(63492); \
+    }                                                                  \
+  }
+#endif
+#ifdef TTRL_PHASE_TIMING
+#define PH_INIT                                                        \
+  WT_INIT                                                              \
+  __shared__ unsigned ph_acc[4][20];                                   \
+  if ((threadIdx.x & 63) < 20) ph_acc[threadIdx.x >> 6][threadIdx.x & 63] = 0; \
+  unsigned long long ph_t = ph_t0;
+#define PH(k)                                                          \
+  do {                                                                 \
+    const unsigned long long ph_n = __builtin_readcyclecounter();      \
+    if ((threadIdx.x & 63) == 0) ph_acc[threadIdx.x >> 6][k] += (unsigned)(ph_n - ph_t); \
+    ph_t = ph_n;                                                       \
   } while (0)
 #define PH_FLUSH                                                       \
-  if ((threadIdx.x & 63) == 0)                                         \
-    for (int ph_k = 0; ph_k < 20; ++ph_k) atomicAdd(&g_phase[ph_k], ph_acc[ph_k]);
+  if ((threadIdx.x & 63) < 20)                                         \
+    atomicAdd(&g_phase[threadIdx.x & 63], (unsigned long long)ph_acc[threadIdx.x >> 6][threadIdx.x & 63]); \
+  WT_FLUSH
+#elif defined(TTRL_WAVE_TRACE)
+#define PH_INIT WT_INIT
+#define PH(k)
+#define PH_FLUSH WT_FLUSH
 #else
 #define PH_INIT
 #define PH(k)
@@ -1407,7 +1448,11 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         }
         PH(2);
         T a_free = T(0);
-        if (idm && !(ablate & A_NO_IDM)) a_free = idm_free(P, v, V.ts[me], V.lanes[lane].lim, V.delta[me]);
+        // IDM free-road term (behavior.py:172-183); the power's base of every present vehicle goes
+        // to LDS for the MOBIL items (a new follower may be any vehicle, the caller's DELTA)
+        const T pb = pow_base(idm_ratio(v, V.ts[me], V.lanes[lane < 0 ? 0 : lane].lim));
+        V.powb[me] = pb;
+        if (idm && !(ablate & A_NO_IDM)) a_free = T(P.comfort_acc_max) * (T(1) - pow_from_base(pb, V.delta[me]));
         PH(12);
         V.afree[me] = a_free;
         V.f0[me] = (short)f2[0];
@@ -1471,7 +1516,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             T term = T(0);
             if (e_ >= 0 && f_ >= 0) term = idm_interact<CV>(V, P, eb, e_, f_);
             T fr = T(0);
-            if (g == 0 && nf >= 0) fr = idm_free(P, V.v[eb + nf], V.ts[eb + nf], V.lanes[V.lane[eb + nf]].lim, delta);
+            if (g == 0 && nf >= 0) fr = T(P.comfort_acc_max) * (T(1) - pow_from_base(V.powb[eb + nf], delta));
             const T t_np = __shfl_xor(term, 1, G), t_op = __shfl_xor(term, 2, G);
             if (g == 0) {
               const T af = V.afree[ve];
@@ -1786,7 +1831,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             const T dx = V.x[eb + j] - xi, dy = V.y[eb + j] - yi;
             const T d2 = dx * dx + dy * dy;
             if (d2 > (thr + T(1)) * (thr + T(1))) continue;  // far: skip the exact test
-            if (sqrt(d2) > thr) continue;                     // objects.py:123-133 exact
+            // objects.py:123-133 exact: norm > thr; inside thr - 1 it provably is not (no sqrt)
+            if (!(thr > T(1) && d2 < (thr - T(1)) * (thr - T(1))) && sqrt(d2) > thr) continue;
             if (sat_separated(P, xi, yi, V.ch[me], V.sh[me], vi, V.x[eb + j], V.y[eb + j], V.ch[eb + j], V.sh[eb + j],
                               V.v[eb + j], dt))
               continue;  // provably (false, false): contributes nothing
@@ -3102,8 +3148,11 @@ int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_par
   const int blocks = (s.n_envs + EPW - 1) / EPW;
   if (blocks == 0) return TTRL_OK;
   const bool graph = is_graph(R);
-  bool curved = R.n_lanes > STRAIGHT_LANE_CAP;  // wider straight roads: the run-time layout instance
-  for (int l = 0; l < R.n_lanes; ++l) curved |= R.type[l] != TTRL_LANE_STRAIGHT;
+  // the NET_STRAIGHT instance: at most STRAIGHT_LANE_CAP straight lanes along +x; any other road
+  // (curved, rotated or wider) runs the NET_CURVED instance, which handles every lane class
+  bool curved = R.n_lanes > STRAIGHT_LANE_CAP;
+  for (int l = 0; l < R.n_lanes; ++l)
+    curved |= R.type[l] != TTRL_LANE_STRAIGHT || R.dir_x[l] != 1.0 || R.dir_y[l] != 0.0;
   const size_t lds = host_view_bytes(sizeof(T) == 8 ? TTRL_F64 : TTRL_F32, EPW, NS,
                                      graph || curved ? R.n_lanes : STRAIGHT_LANE_CAP, graph);
   if (graph)
@@ -3221,12 +3270,18 @@ int ttrl_diag_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road, con
   return run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream, ablate);
 }
 
-#ifdef TTRL_PHASE_TIMING
-// Diagnostic build only: read and clear the per-phase cycle sums (12 u64).
+#if defined(TTRL_PHASE_TIMING) || defined(TTRL_WAVE_TRACE)
+// Diagnostic build only: read and clear the per-phase cycle sums (20 u64).
 int ttrl_diag_phase_read(unsigned long long* out) {
   unsigned long long z[20] = {};
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 20) != hipSuccess) return TTRL_E_LAUNCH;
   return hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) == hipSuccess ? TTRL_OK : TTRL_E_LAUNCH;
+}
+// ... and the per-wave trace of the last launch: n x (start, end, hw_id | xcc_id << 32)
+int ttrl_diag_wave_read(unsigned long long* out, int n) {
+  if (n > WTRACE_MAX) n = WTRACE_MAX;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wtrace), sizeof(unsigned long long) * 3 * n) == hipSuccess
+             ? TTRL_OK : TTRL_E_LAUNCH;
 }
 #endif
 
