@@ -311,16 +311,20 @@ def main():
         "env_steps_per_s": world * E * args.steps / elapsed,
     }
     if pmc and pmc.get("valu_insts_per_wave") and pmc.get("sq_waves"):
-        # Secondary roofline: the path is VALU/LDS-latency bound.  VALU wave-
-        # instructions per launch (SQ_INSTS_VALU from the committed profile of this kernel) at the
-        # 2-cycle wave64 issue of a 32-lane SIMD, against every SIMD's issue cycles in the live
-        # kernel time (a lower bound on VALU busy time: f64 ops issue at half that rate).
-        insts = pmc["valu_insts_per_wave"] * pmc["sq_waves"]
+        # The bound that applies: the fused kernel is VALU-issue bound, not HBM
+        # bound.  From the committed PMC profile of this kernel (profiles/pmc_traffic.json):
+        # SQ_ACTIVE_INST_VALU (quad-cycles, x4) summed over the launch's waves against every SIMD's
+        # cycles in the live kernel time (1024 SIMDs x the GRBM clock) -- the measured VALU-busy
+        # fraction; the instruction count is SQ_INSTS_VALU.
+        waves = pmc["sq_waves"]
         clk = pmc.get("effective_clock_ghz") or 2.4
-        out["valu"] = {"insts_per_launch": insts, "issue_cycles_lower_bound": 2 * insts,
-                       "simd_cycles": 1024 * clk * 1e9 * kern_ms * 1e-3,
-                       "busy_frac_lower_bound": 2 * insts / (1024 * clk * 1e9 * kern_ms * 1e-3),
-                       "source": "profiles/pmc_traffic.json (SQ_INSTS_VALU, SQ_WAVES, GRBM clock)"}
+        simd_cycles = 1024 * clk * 1e9 * kern_ms * 1e-3
+        out["valu"] = {"insts_per_launch": pmc["valu_insts_per_wave"] * waves, "simd_cycles": simd_cycles,
+                       "source": "profiles/pmc_traffic.json (SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU, SQ_WAVES, GRBM clock)"}
+        if pmc.get("valu_active_cycles_per_wave"):
+            active = pmc["valu_active_cycles_per_wave"] * waves
+            out["valu"].update({"active_cycles_per_launch": active, "busy_frac": active / simd_cycles})
+            out["roofline"]["limiter"] = "valu" if active / simd_cycles > out["roofline"]["frac"] else "hbm"
     if ix:
         out["config"]["live_vehicles_per_env"] = veh_steps / (world * E * 15 * args.steps)
         out["config"]["auto_reset"] = True

@@ -80,6 +80,8 @@ for dt in ("f64", "f32"):
         "note": "hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024; FETCH_SIZE doubled per the gfx950 calibration",
         "sq_waves": waves, "valu_insts_per_wave": valu / waves, "lds_insts_per_wave": lds / waves,
         "salu_insts_per_wave": salu / waves, "effective_clock_ghz": clk,
+        # SQ_ACTIVE_INST_VALU counts quad-cycles (4 shader cycles) per wave
+        "valu_active_cycles_per_wave": 4 * act_valu / waves,
         "kernel_ns_trace_avg": sim_avg}
     md += ["", f"Fused `{simk}`: trace avg {sim_avg / 1e3:.1f} us per 15-frame launch "
                f"(bench line under rocprof: {e['value']:.3e} veh-steps/s).",
