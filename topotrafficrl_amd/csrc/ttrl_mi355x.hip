@@ -106,6 +106,25 @@ __device__ __forceinline__ float k_asin(float x) { return t_asin(x); }
 __device__ __forceinline__ float k_pow(float x, float y) { return t_pow(x, y); }
 
 constexpr int LMAX = TTRL_MAX_LANES;
+// Lanes the straight-road instance's LDS layout is sized for; a road with more lanes runs the
+// NET_CURVED instance (which handles straight lanes too, with a layout sized at run time).
+constexpr int STRAIGHT_LANE_CAP = 4;
+
+// Lane exchange inside 8-lane groups on the DPP network (a VALU move, a few cycles) instead of
+// ds_bpermute (an LDS round trip): K = 1 and 2 swap with lane g ^ K (quad_perm), K = 4 pairs lane
+// g with 7 - g (row_half_mirror), joining the group's two quads -- all the symmetric (commutative,
+// associative) group reductions below need.  Every lane of a group must be active.
+template <int K> __device__ __forceinline__ int grp8_swap(int v) {
+  static_assert(K == 1 || K == 2 || K == 4, "8-lane group exchange");
+  return __builtin_amdgcn_mov_dpp(v, K == 1 ? 0xB1 : (K == 2 ? 0x4E : 0x141), 0xf, 0xf, false);
+}
+template <int K> __device__ __forceinline__ double grp8_swap(double v) {
+  const int lo = grp8_swap<K>(__double2loint(v)), hi = grp8_swap<K>(__double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+template <int K> __device__ __forceinline__ float grp8_swap(float v) {
+  return __int_as_float(grp8_swap<K>(__float_as_int(v)));
+}
 constexpr float FAR = 1e30f;  // x of absent slots in the LDS view: never within a collision window
 
 template <typename T> struct K;
@@ -478,7 +497,6 @@ template <typename T> struct View {
   T* afree;                      // [EPW*NS] IDM free-road term of the frame (MOBIL items read it)
   T* powb;                       // [EPW*NS] its power's base (pow_base), any vehicle's (MOBIL items)
   uint8_t *kind, *flags;         // [EPW*NS] flags: 1 crashed, 2 has_impact, 4 enable_lane_change
-  int8_t* sidx;                  // [EPW*NS] MDPVehicle.speed_index
   T* key;            // [n_lanes][EPW][NS+1] s of the vehicles on each lane (AbstractLane.on_lane margin 1)
   uint8_t* idx;      // [n_lanes][EPW][NS+1] their slots, slot order
   short* mypos;      // [n_lanes][EPW*NS] each vehicle's position in the list, -1 if not on the lane
@@ -511,7 +529,7 @@ constexpr int PRED_T = 11;       // np.arange(0.25, 3, 0.25) (regulation.py:86)
 constexpr int N_REALS = 8;  // x, y, v, ch, sh, ts, h, delta
 struct ViewLayout {
   size_t lanes, reals[N_REALS], xf, key, afree, powb, pq_tx, pq_ty, pq_ij, bal, cnt, wcnt, nitem, pq_n, mypos, f0, r0, ft,
-      mob, item, idx, kind, flags, sidx, lane, tgt, pred, rroad, rlane, rn, ynew, rt, onm, live, lperm, pd, pl, total;
+      mob, item, idx, kind, flags, lane, tgt, pred, rroad, rlane, rn, ynew, rt, onm, live, lperm, pd, pl, total;
 };
 
 template <typename T>
@@ -535,7 +553,6 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, 
   o.pq_n = take(sizeof(int) * EPW, 4);
   o.kind = take(M, 4);
   o.flags = take(M, 4);
-  o.sidx = take(M, 4);
   o.lane = take(M, 4);
   o.tgt = take(M, 4);
   // Frame-transient block: the per-lane candidate lists (written by the projection at the end of
@@ -610,7 +627,6 @@ __device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lane
   V.idx = (uint8_t*)(smem + o.idx);
   V.kind = (uint8_t*)(smem + o.kind);
   V.flags = (uint8_t*)(smem + o.flags);
-  V.sidx = (int8_t*)(smem + o.sidx);
   V.lane = (int8_t*)(smem + o.lane);
   V.tgt = (int8_t*)(smem + o.tgt);
   if (graph) {
@@ -709,7 +725,7 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
     const int sh = (tid & 63) / NS * NS;
     const unsigned long long seg = NS == 64 ? ~0ull : ((1ull << NS) - 1);
     bool have = false;  // bd / best hold a lane
-    for (int l = 0; l < nl; ++l) {
+    auto lane_l = [&](int l) {
       const LaneT<T> L = V.lanes[l];
       T s, r;
       bool full = true;  // s computed (always, on a straight lane)
@@ -759,6 +775,13 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
         if (!have || d < bd) { bd = d; best = l; }
         have = true;
       }
+    };
+    if constexpr (CV) {
+      for (int l = 0; l < nl; ++l) lane_l(l);
+    } else {  // the straight instance's lanes have a compile-time bound: unrolled, their projections overlap
+#pragma unroll
+      for (int l = 0; l < STRAIGHT_LANE_CAP; ++l)
+        if (l < nl) lane_l(l);
     }
   } else {
     constexpr int W = NS / 64;
@@ -964,9 +987,6 @@ __device__ __forceinline__ T lane_s(const View<T>& V, int l, int le, int i, T x,
 // Network mode of the simulate kernel: one straight road (the highway), one road of curved
 // lanes, or a graph of roads with routes and RegulatedRoad priorities (the intersection).
 enum { NET_STRAIGHT = 0, NET_CURVED = 1, NET_GRAPH = 2 };
-// Lanes the straight-road instance's LDS layout is sized for; a road with more lanes runs the
-// NET_CURVED instance (which handles straight lanes too, with a layout sized at run time).
-constexpr int STRAIGHT_LANE_CAP = 4;
 
 // AbstractLane.distance lane.py:127-130
 template <typename T>
@@ -1201,6 +1221,7 @@ enum { A_NO_COLL = 1, A_NO_MOBIL = 2, A_NO_ABORT = 4, A_NO_SCAN = 8, A_NO_STEER 
 
 enum { FL_CRASHED = 1, FL_IMPACT = 2, FL_LC = 4, FL_YIELD = 8 };
 
+
 // Diagnostic builds only.  -DTTRL_PHASE_TIMING: per-phase shader-clock cycles of every wave,
 // summed into g_phase (tools/phases.py); the accumulators live in LDS (32-bit, one row per wave),
 // so the stamps leave the kernel's register allocation as it is (a register array of 20 counters
@@ -1308,6 +1329,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   // Vehicle state only this thread reads (IDM timer, the action, the pending impact) stays in
   // registers for the launch; what other vehicles read is staged in the LDS view.
   T my_timer, my_steer, my_acc, my_ix, my_iy;
+  int my_sidx;
   {  // HBM -> LDS, once per launch (coalesced SoA rows)
     Veh<T> a;
     if (slot) load_veh(a, st, k);
@@ -1321,7 +1343,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
     my_timer = a.timer; my_steer = a.steer; my_acc = a.acc; my_ix = a.ix; my_iy = a.iy;
     V.kind[me] = (uint8_t)(present ? a.kind : TTRL_ABSENT);
     V.flags[me] = (uint8_t)((a.crashed ? FL_CRASHED : 0) | (a.hasimp ? FL_IMPACT : 0) | (a.lc ? FL_LC : 0));
-    V.sidx[me] = (int8_t)a.sidx;
+    my_sidx = a.sidx;
     V.lane[me] = (int8_t)(present ? a.lane : -1);
     V.tgt[me] = (int8_t)(present ? a.tgt : -1);
     if constexpr (GR) {
@@ -1356,7 +1378,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       if (act == TTRL_FASTER || act == TTRL_SLOWER) {  // MDPVehicle.act controller.py:304-315
         int si = speed_to_index(P, v) + (act == TTRL_FASTER ? 1 : -1);
         si = si < 0 ? 0 : (si > P.n_target_speeds - 1 ? P.n_target_speeds - 1 : si);
-        V.sidx[me] = (int8_t)si;
+        my_sidx = si;
         ts = T(P.target_speeds[si]);
       } else if (act == TTRL_LANE_LEFT || act == TTRL_LANE_RIGHT) {  // controller.py:103-124
         int id, lo = 0, hi = nl - 1;
@@ -1463,8 +1485,19 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         // MOBIL (IDMVehicle.mobil behavior.py:265-324, route None) as work items, one per
         // (firing vehicle, candidate side lane): a frame has a handful of firing vehicles, so
         // the side-lane queries and IDM terms of all of them cost one pass.
-        if (left) V.item[le * 2 * NS + atomicAdd(&V.nitem[le], 1)] = (short)i;
-        if (right) V.item[le * 2 * NS + atomicAdd(&V.nitem[le], 1)] = (short)(i | 0x4000);
+        if constexpr (NS <= 64) {  // one wavefront: queue slots from ballots, no LDS atomics
+          const int sh = (tid & 63) / NS * NS;
+          const unsigned long long seg = NS == 64 ? ~0ull : ((1ull << NS) - 1) << sh;
+          const unsigned long long below = (1ull << (tid & 63)) - 1;
+          const unsigned long long bl = __ballot(left) & seg, br = __ballot(right) & seg;
+          const int pos = __popcll(bl & below) + __popcll(br & below);
+          if (left) V.item[le * 2 * NS + pos] = (short)i;
+          if (right) V.item[le * 2 * NS + pos + (left ? 1 : 0)] = (short)(i | 0x4000);
+          if (i == 0) V.nitem[le] = __popcll(bl) + __popcll(br);
+        } else {
+          if (left) V.item[le * 2 * NS + atomicAdd(&V.nitem[le], 1)] = (short)i;
+          if (right) V.item[le * 2 * NS + atomicAdd(&V.nitem[le], 1)] = (short)(i | 0x4000);
+        }
       }
       __syncthreads();
       PH(13);
@@ -1499,13 +1532,15 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
                 sr = ur ? xk : sr;
                 rp = ur ? kk : rp;
               }
-  #pragma unroll
-              for (int off = 1; off < G; off <<= 1) {
-                const T osf = __shfl_xor(sf, off, G), osr = __shfl_xor(sr, off, G);
-                const int ofp = __shfl_xor(fp, off, G), orp = __shfl_xor(rp, off, G);
+              // combine the group's 8 partial scans (front: min s, ties to the later position; rear:
+              // max s, ties to the earlier), lane g with g ^ 1, g ^ 2, then 7 - g
+              auto merge = [&](T osf, int ofp, T osr, int orp) {
                 if (osf < sf || (osf == sf && ofp > fp)) { sf = osf; fp = ofp; }
                 if (osr > sr || (osr == sr && orp >= 0 && (rp < 0 || orp < rp))) { sr = osr; rp = orp; }
-              }
+              };
+              merge(grp8_swap<1>(sf), grp8_swap<1>(fp), grp8_swap<1>(sr), grp8_swap<1>(rp));
+              merge(grp8_swap<2>(sf), grp8_swap<2>(fp), grp8_swap<2>(sr), grp8_swap<2>(rp));
+              merge(grp8_swap<4>(sf), grp8_swap<4>(fp), grp8_swap<4>(sr), grp8_swap<4>(rp));
             }
             const int np_ = fp >= 0 ? (int)V.idx[rowb + fp] : -1, nf = rp >= 0 ? (int)V.idx[rowb + rp] : -1;
             const int op = V.f0[ve], of = V.r0[ve];
@@ -1517,7 +1552,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             if (e_ >= 0 && f_ >= 0) term = idm_interact<CV>(V, P, eb, e_, f_);
             T fr = T(0);
             if (g == 0 && nf >= 0) fr = T(P.comfort_acc_max) * (T(1) - pow_from_base(V.powb[eb + nf], delta));
-            const T t_np = __shfl_xor(term, 1, G), t_op = __shfl_xor(term, 2, G);
+            const T t_np = grp8_swap<1>(term), t_op = grp8_swap<2>(term);
             if (g == 0) {
               const T af = V.afree[ve];
               const T nfpa = nf >= 0 ? fr - term : T(0);
@@ -1804,7 +1839,56 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       // the pair (i, j > i) is tested against thr0 + v_i dt: i's own speed bounds its window
       const T Rw = thr0 + fabs(V.v[me]) * dt + T(1);
       constexpr int CH = NS < 64 ? NS : 64;
-      if (present && do_coll) {
+      if constexpr (NS <= 64) {
+        // One wavefront: each vehicle i tests its partners j > i in a float window (its own speed
+        // bounds the reference's asymmetric threshold), then the exact tests run one candidate per
+        // lane per round, queue slots coming from the round's ballot (no LDS atomics).
+        unsigned long long m = 0;
+        if (present && do_coll) {
+          const float xfi = V.xf[me];
+          // float window: |xf_j - xf_i| in float errs by < 1.2e-7 (|x_i| + |x_j|), far below the slack
+          const float Rwf = (float)Rw * 1.0001f + 1e-5f * fabsf(xfi) + 1e-3f;
+#pragma unroll
+          for (int j1 = 0; j1 < NS; j1 += 8) {
+            float xs[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) xs[u] = V.xf[eb + j1 + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+              if (!(fabsf(xs[u] - xfi) > Rwf)) m |= 1ull << (j1 + u);
+          }
+          m &= ~((2ull << i) - 1);  // keep j > i
+          if (ablate & A_NO_PREF) m = 0;
+        }
+        const T xi = V.x[me], yi = V.y[me], vi = V.v[me];
+        const T thr = thr0 + vi * dt;
+        const unsigned long long seg = NS == 64 ? ~0ull : ((1ull << NS) - 1) << ((tid & 63) / NS * NS);
+        const unsigned long long below = (1ull << (tid & 63)) - 1;
+        int base = 0;  // pairs of this env queued so far
+        while (__any(m != 0)) {
+          bool push = false;
+          int j = 0;
+          if (m) {
+            j = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const T dx = V.x[eb + j] - xi, dy = V.y[eb + j] - yi;
+            const T d2 = dx * dx + dy * dy;
+            // objects.py:123-133 exact: norm > thr (far pairs skip it; inside thr - 1 no sqrt needed),
+            // then pairs the SAT provably separates contribute nothing
+            push = !(d2 > (thr + T(1)) * (thr + T(1))) &&
+                   !(!(thr > T(1) && d2 < (thr - T(1)) * (thr - T(1))) && sqrt(d2) > thr) &&
+                   !sat_separated(P, xi, yi, V.ch[me], V.sh[me], vi, V.x[eb + j], V.y[eb + j], V.ch[eb + j],
+                                  V.sh[eb + j], V.v[eb + j], dt);
+          }
+          const unsigned long long bal = __ballot(push) & seg;
+          if (push) {
+            const int q = base + __popcll(bal & below);
+            if (q < NS) V.pq_ij[le * NS + q] = pair_pack(i, j, 0);
+          }
+          base += __popcll(bal);
+        }
+        if (i == 0) V.pq_n[le] = base;
+      } else if (present && do_coll) {
         const T xi = V.x[me], yi = V.y[me], vi = V.v[me];
         const T thr = thr0 + vi * dt;
         // float window: |xf_j - xf_i| in float errs by < 1.2e-7 (|x_i| + |x_j|), far below the slack
@@ -1865,13 +1949,12 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             T bm = fabs(dist);
             if (bm != bm) bm = K<T>::inf();  // abs(nan) < min_distance is false: never chosen
             int bk = kx;
-#pragma unroll
-            for (int off = 1; off < 8; off <<= 1) {
-              const T om = __shfl_xor(bm, off, 8);
-              const int ok = __shfl_xor(bk, off, 8);
-              const T ox = __shfl_xor(axx, off, 8), oy = __shfl_xor(axy, off, 8);
+            auto merge = [&](T om, int ok, T ox, T oy) {
               if (om < bm || (om == bm && ok < bk)) { bm = om; bk = ok; axx = ox; axy = oy; }
-            }
+            };
+            merge(grp8_swap<1>(bm), grp8_swap<1>(bk), grp8_swap<1>(axx), grp8_swap<1>(axy));
+            merge(grp8_swap<2>(bm), grp8_swap<2>(bk), grp8_swap<2>(axx), grp8_swap<2>(axy));
+            merge(grp8_swap<4>(bm), grp8_swap<4>(bk), grp8_swap<4>(axx), grp8_swap<4>(axy));
             if (kx == 0) {
               V.pq_tx[le * NS + q] = will ? bm * axx : T(0);
               V.pq_ty[le * NS + q] = will ? bm * axy : T(0);
@@ -1951,7 +2034,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
     Veh<T> a;
     a.x = V.x[me]; a.y = V.y[me]; a.h = V.h[me]; a.v = V.v[me]; a.ts = V.ts[me]; a.timer = my_timer;
     a.steer = my_steer; a.acc = my_acc; a.ix = my_ix; a.iy = my_iy;
-    a.lane = V.lane[me]; a.tgt = V.tgt[me]; a.sidx = V.sidx[me];
+    a.lane = V.lane[me]; a.tgt = V.tgt[me]; a.sidx = my_sidx;
     const int fl = V.flags[me];
     a.crashed = (fl & FL_CRASHED) != 0; a.hasimp = (fl & FL_IMPACT) != 0;
     if (!present) {  // absent rows pass through untouched
