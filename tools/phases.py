@@ -76,6 +76,17 @@ def main(dtype="f64", steps=30, frames=15, ix=False, E=4096):
           f"p50 {np.percentile(span, 50):.0f} p90 {np.percentile(span, 90):.0f} max {span.max()}")
     st = t0 - lo[inv]
     print(f"wave start offset within its SIMD: mean {st.mean():.0f} max {st.max()}")
+    if os.environ.get("TIMING_LIB", "lib_timing.so") == "lib_timing.so":  # per-wave phase cycles
+        wp = np.zeros((nw, 20), dtype=np.uint32)
+        lib.ttrl_diag_wave_phases.argtypes = [C.c_void_p, C.c_int]
+        lib.ttrl_diag_wave_phases(wp.ctypes.data, nw)
+        tot = wp.sum(1).astype(np.float64)
+        slow = tot >= np.percentile(tot, 95)
+        mid = (tot >= np.percentile(tot, 40)) & (tot <= np.percentile(tot, 60))
+        print(f"the slowest 5% of waves (phase sum {tot[slow].mean():.0f}) vs the median ones ({tot[mid].mean():.0f}), "
+              f"cycles per launch:")
+        for k in np.argsort(-(wp[slow].mean(0) - wp[mid].mean(0)))[:10]:
+            print(f"  {NAMES[k]:16s} slow {wp[slow, k].mean():9.0f}  median {wp[mid, k].mean():9.0f}")
 
 
 if __name__ == "__main__":
