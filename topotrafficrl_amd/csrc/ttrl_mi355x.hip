@@ -1232,6 +1232,7 @@ enum { FL_CRASHED = 1, FL_IMPACT = 2, FL_LC = 4, FL_YIELD = 8 };
 __device__ unsigned long long g_phase[20];
 constexpr int WTRACE_MAX = 16384;
 __device__ unsigned long long g_wtrace[WTRACE_MAX][3];
+__device__ unsigned g_wphase[WTRACE_MAX][20];  // PHASE_TIMING: each wave's phase cycles of the last launch
 #define WT_INIT const unsigned long long ph_t0 = __builtin_readcyclecounter();
 #define WT_FLUSH                                                       \
   {                                                                    \
@@ -1256,8 +1257,11 @@ __device__ unsigned long long g_wtrace[WTRACE_MAX][3];
     ph_t = ph_n;                                                       \
   } while (0)
 #define PH_FLUSH                                                       \
-  if ((threadIdx.x & 63) < 20)                                         \
+  if ((threadIdx.x & 63) < 20) {                                       \
     atomicAdd(&g_phase[threadIdx.x & 63], (unsigned long long)ph_acc[threadIdx.x >> 6][threadIdx.x & 63]); \
+    const unsigned ph_w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); \
+    if (ph_w < WTRACE_MAX) g_wphase[ph_w][threadIdx.x & 63] = ph_acc[threadIdx.x >> 6][threadIdx.x & 63]; \
+  }                                                                    \
   WT_FLUSH
 #elif defined(TTRL_WAVE_TRACE)
 #define PH_INIT WT_INIT
@@ -3359,6 +3363,12 @@ int ttrl_diag_phase_read(unsigned long long* out) {
   unsigned long long z[20] = {};
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 20) != hipSuccess) return TTRL_E_LAUNCH;
   return hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) == hipSuccess ? TTRL_OK : TTRL_E_LAUNCH;
+}
+// ... each wave's phase cycles of the last launch (PHASE_TIMING builds): n x 20 u32
+int ttrl_diag_wave_phases(unsigned* out, int n) {
+  if (n > WTRACE_MAX) n = WTRACE_MAX;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wphase), sizeof(unsigned) * 20 * n) == hipSuccess ? TTRL_OK
+                                                                                                  : TTRL_E_LAUNCH;
 }
 // ... and the per-wave trace of the last launch: n x (start, end, hw_id | xcc_id << 32)
 int ttrl_diag_wave_read(unsigned long long* out, int n) {
