@@ -4,16 +4,9 @@
 // (:157-194), EgoAttentionNetwork.forward (:237-312), attention (:370-388) for
 // ego_attention_2h.json (embeddings 7->64->64 ReLU, 2 heads of 32, output 64->64->64->A).
 //
-// Two launches, no intermediate round trip through torch:
-//   rows_kernel  one lane per entity row (ego rows and other rows in separate blocks, so every
-//                block reads one weight set and the weights are wave-uniform scalar loads):
-//                embedding MLP, then the row's key and value; K^T, V^T [64][rows] and the ego
-//                embeddings E^T [64][B] are written feature-major (coalesced across lanes).
-//   env_kernel   one wave per 4 envs, lane o = feature o: query, masked softmax over the
-//                entities per head, the value mix, the combine + residual, the output MLP.
-// The forward is a dense contraction, but on gfx950 float32 MFMA issues at the float32
-// vector rate, so the rows are plain FMAs fed by scalar-cached weights; the win over the torch
-// graph is fusion (no HBM round trips of the [B*15, 64] activations) and launch count.
+// One launch (ego_attention_kernel below): a wave per 4 envs, lane k = feature k, the key and
+// value projections moved out of the entity loop by linearity, the per-entity scores summed over
+// the lanes by one transposing butterfly; only the Q-values reach HBM.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -40,216 +33,331 @@ __host__ __device__ inline PolicyLayout policy_layout(int F, int A) {
   return L;
 }
 
-constexpr int RB = 256;  // rows (lanes) per rows_kernel block
+constexpr int EPWV = 4;  // envs per wave of ego_attention_kernel
 
-// acc[o] += sum_k Wt[k][o] * in[k] in outer-product order: each k step is 64 independent FMAs
-// (no serial accumulation chain) fed by broadcast float4 reads of the [in][out] weights.
-__device__ __forceinline__ void dense64(const float4* __restrict__ wt, const float (&in)[HD], float (&acc)[HD]) {
+#ifdef TTRL_POL_CLOCKS  // diagnostic build: shader-clock stamps at the phase boundaries of each wave
+constexpr int POL_CLK_BLOCKS = 4096;
+__device__ long long g_pol_clk[POL_CLK_BLOCKS * 9];
+#define POL_T(n) (pol_clk[n] = clock64())
+#else
+#define POL_T(n) ((void)0)
+#endif
+
+// acc[u] += sum_k W[k][o] * v[k].u for the wave's EPWV vectors staged in LDS as one float4 per
+// feature (env u in component u). Lane o's whole weight column (the [in][out] rows are coalesced
+// across lanes) is requested before the first FMA, so one memory latency covers the 64 loads;
+// each weight is used EPWV times.
+__device__ __forceinline__ void matvec4(const float* __restrict__ w, const float4* v, int o, float (&acc)[EPWV]) {
+  float col[HD];
+#pragma unroll
+  for (int k = 0; k < HD; ++k) col[k] = w[k * HD + o];
 #pragma unroll
   for (int k = 0; k < HD; ++k) {
-#pragma unroll
-    for (int o = 0; o < HD; o += 4) {
-      const float4 w = wt[(k * HD + o) / 4];
-      acc[o] = fmaf(w.x, in[k], acc[o]);
-      acc[o + 1] = fmaf(w.y, in[k], acc[o + 1]);
-      acc[o + 2] = fmaf(w.z, in[k], acc[o + 2]);
-      acc[o + 3] = fmaf(w.w, in[k], acc[o + 3]);
-    }
+    const float4 x = v[k];
+    acc[0] = fmaf(col[k], x.x, acc[0]);
+    acc[1] = fmaf(col[k], x.y, acc[1]);
+    acc[2] = fmaf(col[k], x.z, acc[2]);
+    acc[3] = fmaf(col[k], x.w, acc[3]);
   }
 }
 
-template <int F>
-__global__ void __launch_bounds__(RB) rows_kernel(const float* __restrict__ obs, int B, int NE,
-                                                  const float* __restrict__ W, int A, float* __restrict__ KT,
-                                                  float* __restrict__ VT, float* __restrict__ ET) {
-  // the block's weights (embedding W1, b1, W2, b2, then key / value), transposed to [in][out]
-  // in LDS once; every lane of the block multiplies by the same weights (broadcast reads)
-  __shared__ float4 w2t[HD * HD / 4], wkt[HD * HD / 4], wvt[HD * HD / 4];
-  __shared__ float w1t[F * HD], b1s[HD], b2s[HD];
-  const PolicyLayout L = policy_layout(F, A);
-  const int ego_blocks = (B + RB - 1) / RB;
-  const bool ego = (int)blockIdx.x < ego_blocks;
-  const float* w1 = W + (ego ? L.e1w : L.o1w);
-  const float* b1 = W + (ego ? L.e1b : L.o1b);
-  const float* w2 = W + (ego ? L.e2w : L.o2w);
-  const float* b2 = W + (ego ? L.e2b : L.o2b);
-  const int tid = threadIdx.x;
-  float* w2f = reinterpret_cast<float*>(w2t);
-  float* wkf = reinterpret_cast<float*>(wkt);
-  float* wvf = reinterpret_cast<float*>(wvt);
-  for (int i = tid; i < HD * HD; i += RB) {  // packed matrices are [in][out] already
-    w2f[i] = w2[i];
-    wkf[i] = W[L.wk + i];
-    wvf[i] = W[L.wv + i];
-  }
-  for (int i = tid; i < HD * F; i += RB) w1t[i] = w1[i];
-  if (tid < HD) { b1s[tid] = b1[tid]; b2s[tid] = b2[tid]; }
-  __syncthreads();
-  const long t = ego ? (long)blockIdx.x * RB + tid : (long)(blockIdx.x - ego_blocks) * RB + tid;
-  const long n_rows = ego ? B : (long)B * (NE - 1);
-  if (t >= n_rows) return;
-  const long env = ego ? t : t / (NE - 1);
-  const int j = ego ? 0 : 1 + (int)(t % (NE - 1));
-  const long row = env * NE + j;
-  const long R = (long)B * NE;
-  float x[F];
-#pragma unroll
-  for (int k = 0; k < F; ++k) x[k] = obs[row * F + k];
-  float h1[HD], acc[HD];
-#pragma unroll
-  for (int o = 0; o < HD; ++o) h1[o] = b1s[o];
-#pragma unroll
-  for (int k = 0; k < F; ++k)
-#pragma unroll
-    for (int o = 0; o < HD; ++o) h1[o] = fmaf(w1t[k * HD + o], x[k], h1[o]);
-#pragma unroll
-  for (int o = 0; o < HD; ++o) { h1[o] = h1[o] > 0.0f ? h1[o] : 0.0f; acc[o] = b2s[o]; }
-  dense64(w2t, h1, acc);
-  float h2[HD];
-#pragma unroll
-  for (int o = 0; o < HD; ++o) h2[o] = acc[o] > 0.0f ? acc[o] : 0.0f;
-  if (ego)
-#pragma unroll
-    for (int o = 0; o < HD; ++o) ET[(long)o * B + env] = h2[o];
-#pragma unroll
-  for (int o = 0; o < HD; ++o) acc[o] = 0.0f;
-  dense64(wkt, h2, acc);
-#pragma unroll
-  for (int o = 0; o < HD; ++o) { KT[(long)o * R + row] = acc[o]; acc[o] = 0.0f; }
-  dense64(wvt, h2, acc);
-#pragma unroll
-  for (int o = 0; o < HD; ++o) VT[(long)o * R + row] = acc[o];
+__device__ __forceinline__ float4 f4(const float (&a)[EPWV]) { return make_float4(a[0], a[1], a[2], a[3]); }
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 
-constexpr int EPB = 8;  // envs per wave in env_kernel
+// v from the lane whose index differs in bit B (quad_perm / ds_swizzle / row_ror:8 / bpermute)
+template <int B>
+__device__ __forceinline__ float lane_xor(float v) {
+  if constexpr (B == 0) return dpp_f<0xB1>(v);
+  else if constexpr (B == 1) return dpp_f<0x4E>(v);
+  else if constexpr (B == 2) return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x101F));
+  else if constexpr (B == 3) return dpp_f<0x128>(v);
+  else if constexpr (B == 4) return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401F));
+  else return __int_as_float(__builtin_amdgcn_ds_bpermute((int)((threadIdx.x ^ 32) << 2), __float_as_int(v)));
+}
 
-template <int F>
-__global__ void __launch_bounds__(64) env_kernel(const float* __restrict__ obs, int B, int NE, int heads,
-                                                 const float* __restrict__ W, int A, const float* __restrict__ KT,
-                                                 const float* __restrict__ VT, const float* __restrict__ ET,
-                                                 float* __restrict__ Q) {
-  const PolicyLayout L = policy_layout(F, A);
-  __shared__ float vec[EPB][HD];       // the vector being multiplied (q input, value mix, ...)
-  __shared__ float prob[EPB][8][32];   // softmax weights [head][entity] (heads * NE <= 64)
-  const int o = threadIdx.x;
-  const int dph = HD / heads;
-  const long R = (long)B * NE;
-  const float scale = 1.0f / sqrtf((float)dph);
-  float e[EPB];
+// Sums over the wave's 64 lanes of N values at once (a transposing butterfly): at lane bit B the
+// lanes with the bit set keep the upper half of their values and send the lower half, so N values
+// take N - 1 + (6 - log2 N) exchanges instead of 6 N. Afterwards v[0] of lane L is the sum of value
+// fold_index<N>(L); lanes 0 .. N-1 hold every index once.
+template <int B, int N>
+__device__ __forceinline__ void fold(float* v, int lane) {
+  if constexpr (N > 1) {
+    const bool hi = (lane >> B) & 1;
 #pragma unroll
-  for (int u = 0; u < EPB; ++u) {
-    const long b = (long)blockIdx.x * EPB + u;
-    e[u] = b < B ? ET[(long)o * B + b] : 0.0f;
-    vec[u][o] = e[u];
-  }
-  __syncthreads();
-  // query_ego: q[o] = Wq[o] . e
-  float q[EPB];
-#pragma unroll
-  for (int u = 0; u < EPB; ++u) q[u] = 0.0f;
-  for (int k = 0; k < HD; ++k) {
-    const float w = W[L.wq + k * HD + o];  // [in][out]: coalesced across lanes
-#pragma unroll
-    for (int u = 0; u < EPB; ++u) q[u] = fmaf(w, vec[u][k], q[u]);
-  }
-  __syncthreads();
-  // scores per (head, entity): lane o < heads*NE takes one; masked_fill(presence < 0.5, -1e9)
-  const int h = o / NE, jj = o % NE;
-#pragma unroll
-  for (int u = 0; u < EPB; ++u) {
-    vec[u][o] = q[u];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int u = 0; u < EPB; ++u) {
-    const long b = (long)blockIdx.x * EPB + u;
-    if (o < heads * NE && b < B) {
-      float s = 0.0f;
-      for (int d = 0; d < dph; ++d) s = fmaf(vec[u][h * dph + d], KT[(long)(h * dph + d) * R + b * NE + jj], s);
-      s = s * scale;
-      if (obs[(b * NE + jj) * F + 0] < 0.5f) s = -1e9f;
-      prob[u][h][jj] = s;
+    for (int i = 0; i < N / 2; ++i) {
+      const float keep = hi ? v[i + N / 2] : v[i];
+      const float send = hi ? v[i] : v[i + N / 2];
+      v[i] = keep + lane_xor<B>(send);
     }
+    fold<B + 1, N / 2>(v, lane);
+  } else if constexpr (B < 6) {
+    v[0] += lane_xor<B>(v[0]);
+    fold<B + 1, 1>(v, lane);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ int fold_index(int lane) {
+  int idx = 0;
+#pragma unroll
+  for (int b = 0, n = N; n > 1; ++b, n >>= 1) idx += ((lane >> b) & 1) * (n / 2);
+  return idx;
+}
+
+// LDS of one wave (floats): the broadcast vectors, the wave's observations, every entity's
+// embedding (float4 over the envs; reused for the per-head weighted sums), the scores / weights
+struct PolLds {
+  int ob, xs, ps, total;
+};
+__host__ __device__ inline PolLds pol_lds(int NE, int F, int H) {
+  PolLds P;
+  P.ob = HD * 4;
+  P.xs = P.ob + ((EPWV * NE * F + 3) & ~3);
+  P.ps = P.xs + (NE > H ? NE : H) * HD * 4;
+  P.total = P.ps + NE * EPWV * H;
+  return P;
+}
+
+// One wave per EPWV envs, lane k = feature k. Linearity moves the key and value projections
+// out of the entity loop: with x_j the 64-wide embedding of entity j,
+//   score_hj = q_h . (Wk x_j)_h / sqrt(d) = x_j . qk_h,      qk_h = Wk_h^T q_h / sqrt(d)
+//   mix_h    = sum_j p_hj (Wv x_j)_h      = (Wv (sum_j p_hj x_j))_h
+// so an entity costs its embedding (F + 64 FMAs per lane per env) and a share of one butterfly
+// reduction; the value projection runs once per env on the weighted embedding sum.
+//   1. ego embeddings, queries, qk_h (env-level weights loaded once per wave, used EPWV times)
+//   2. entities j (j = 0: the ego's own embedding): embedding to LDS, scores with
+//      masked_fill(presence < 0.5, -1e9) (models.py:383); softmax over j per (env, head)
+//      (models.py:384); the weighted sums of the embeddings
+//   3. the value projection, attention_combine + residual (att + ego) / 2, output MLP, predict
+// Dense algebra, but float32 MFMA issues at the float32 vector rate on gfx950: the win is fusion
+// and the reassociation (no [B*NE, 64] activations through HBM, one launch).
+template <int F, int H>
+__global__ void __launch_bounds__(64, 2) ego_attention_kernel(const float* __restrict__ obs, int B, int NE,
+                                                              const float* __restrict__ W, int A,
+                                                              float* __restrict__ Q) {
+  constexpr int DPH = HD / H, NV = EPWV * H;
+  const PolicyLayout L = policy_layout(F, A);
+  const PolLds P = pol_lds(NE, F, H);
+#ifdef TTRL_POL_CLOCKS
+  long long pol_clk[9];
+  pol_clk[0] = clock64();
+#endif
+  extern __shared__ float4 lds4[];
+  float* lds = reinterpret_cast<float*>(lds4);
+  float4* bc = lds4;                                 // [HD] vectors broadcast to the wave
+  const float* ob = lds + P.ob;                      // [EPWV][NE][F]
+  float4* xs = reinterpret_cast<float4*>(lds + P.xs);  // [NE][HD]; then [H][HD] weighted sums
+  float* ps = lds + P.ps;                            // [NE][NV] scores, then softmax weights
+  const int k = threadIdx.x;
+  const long b0 = (long)blockIdx.x * EPWV;
+  {  // one coalesced copy of the wave's EPWV consecutive [NE][F] observations
+    const long avail = ((long)B - b0) * NE * F;  // a partial last wave repeats env b0 (never stored)
+    const int n = EPWV * NE * F;
+    for (int i = k; i < n; i += HD) lds[P.ob + i] = obs[b0 * NE * F + (i < avail ? i : i % (NE * F))];
   }
   __syncthreads();
-  if (o < heads * EPB) {  // softmax over the entities of one (env, head)
-    const int u = o / heads, hh = o % heads;
-    float m = -3.4e38f;
-    for (int k = 0; k < NE; ++k) m = fmaxf(m, prob[u][hh][k]);
+  // 1. ego embeddings (MultiLayerPerceptron, ReLU after both layers), queries, qk_h
+  POL_T(1);
+  float e[EPWV], t[EPWV];
+#pragma unroll
+  for (int u = 0; u < EPWV; ++u) {
+    float h = W[L.e1b + k];
+#pragma unroll
+    for (int f = 0; f < F; ++f) h = fmaf(W[L.e1w + f * HD + k], ob[u * NE * F + f], h);
+    t[u] = h > 0.0f ? h : 0.0f;
+    e[u] = W[L.e2b + k];
+  }
+  bc[k] = f4(t);
+  __syncthreads();
+  matvec4(W + L.e2w, bc, k, e);
+  POL_T(2);
+#pragma unroll
+  for (int u = 0; u < EPWV; ++u) {
+    e[u] = e[u] > 0.0f ? e[u] : 0.0f;
+    t[u] = 0.0f;
+  }
+  __syncthreads();
+  bc[k] = f4(e);
+  __syncthreads();
+  matvec4(W + L.wq, bc, k, t);  // t = q (lane o = query feature o)
+  POL_T(3);
+  __syncthreads();
+  bc[k] = f4(t);
+  __syncthreads();
+  float qk[EPWV][H];
+#pragma unroll
+  for (int u = 0; u < EPWV; ++u)
+#pragma unroll
+    for (int h = 0; h < H; ++h) qk[u][h] = 0.0f;
+  const float4* wrow = reinterpret_cast<const float4*>(W + L.wk + k * HD);  // Wk[k][.]: row k
+#pragma unroll
+  for (int o4 = 0; o4 < HD / 4; ++o4) {
+    const float4 w = wrow[o4];
+    const int h = o4 * 4 / DPH;
+    const float4 q0 = bc[o4 * 4], q1 = bc[o4 * 4 + 1], q2 = bc[o4 * 4 + 2], q3 = bc[o4 * 4 + 3];
+    qk[0][h] = fmaf(w.w, q3.x, fmaf(w.z, q2.x, fmaf(w.y, q1.x, fmaf(w.x, q0.x, qk[0][h]))));
+    qk[1][h] = fmaf(w.w, q3.y, fmaf(w.z, q2.y, fmaf(w.y, q1.y, fmaf(w.x, q0.y, qk[1][h]))));
+    qk[2][h] = fmaf(w.w, q3.z, fmaf(w.z, q2.z, fmaf(w.y, q1.z, fmaf(w.x, q0.z, qk[2][h]))));
+    qk[3][h] = fmaf(w.w, q3.w, fmaf(w.z, q2.w, fmaf(w.y, q1.w, fmaf(w.x, q0.w, qk[3][h]))));
+  }
+  const float scale = 1.0f / sqrtf((float)DPH);
+#pragma unroll
+  for (int u = 0; u < EPWV; ++u)
+#pragma unroll
+    for (int h = 0; h < H; ++h) qk[u][h] *= scale;
+  // 2. the entities, all EPWV envs at once
+  POL_T(4);
+  float w2o[HD];  // lane k's column of the others' second embedding layer
+#pragma unroll
+  for (int i = 0; i < HD; ++i) w2o[i] = W[L.o2w + i * HD + k];
+  float w1o[F];
+#pragma unroll
+  for (int f = 0; f < F; ++f) w1o[f] = W[L.o1w + f * HD + k];
+  const float b1o = W[L.o1b + k], b2o = W[L.o2b + k];
+  const int my_idx = fold_index<NV>(k);  // the (env, head) whose score lane k < NV ends up with
+  POL_T(5);
+  for (int j = 0; j < NE; ++j) {
+    float x[EPWV];
+    if (j == 0) {
+#pragma unroll
+      for (int u = 0; u < EPWV; ++u) x[u] = e[u];
+    } else {  // the others' embedding of entity j
+#pragma unroll
+      for (int u = 0; u < EPWV; ++u) {
+        float h = b1o;
+#pragma unroll
+        for (int f = 0; f < F; ++f) h = fmaf(w1o[f], ob[(u * NE + j) * F + f], h);
+        t[u] = h > 0.0f ? h : 0.0f;
+        x[u] = b2o;
+      }
+      __syncthreads();
+      bc[k] = f4(t);
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < HD; ++i) {
+        const float4 v = bc[i];
+        x[0] = fmaf(w2o[i], v.x, x[0]);
+        x[1] = fmaf(w2o[i], v.y, x[1]);
+        x[2] = fmaf(w2o[i], v.z, x[2]);
+        x[3] = fmaf(w2o[i], v.w, x[3]);
+      }
+#pragma unroll
+      for (int u = 0; u < EPWV; ++u) x[u] = x[u] > 0.0f ? x[u] : 0.0f;
+    }
+    xs[j * HD + k] = f4(x);
+    float v[NV];
+#pragma unroll
+    for (int u = 0; u < EPWV; ++u)
+#pragma unroll
+      for (int h = 0; h < H; ++h) v[u * H + h] = x[u] * qk[u][h];
+    fold<0, NV>(v, k);
+    if (k < NV) ps[j * NV + my_idx] = ob[((my_idx / H) * NE + j) * F] < 0.5f ? -1e9f : v[0];
+  }
+  __syncthreads();
+  if (k < NV) {  // softmax over the entities of (env, head) = k
+    float m = -__builtin_inff();
+    for (int j = 0; j < NE; ++j) m = fmaxf(m, ps[j * NV + k]);
     float sum = 0.0f;
-    for (int k = 0; k < NE; ++k) {
-      const float p = expf(prob[u][hh][k] - m);
-      prob[u][hh][k] = p;
+    for (int j = 0; j < NE; ++j) {
+      const float p = expf(ps[j * NV + k] - m);
+      ps[j * NV + k] = p;
       sum += p;
     }
-    for (int k = 0; k < NE; ++k) prob[u][hh][k] /= sum;
+    for (int j = 0; j < NE; ++j) ps[j * NV + k] /= sum;
   }
   __syncthreads();
-  // value mix: out[o] = sum_j p[head(o)][j] V[j][o]
-  float mix[EPB];
+  float acc[EPWV][H];
 #pragma unroll
-  for (int u = 0; u < EPB; ++u) {
-    const long b = (long)blockIdx.x * EPB + u;
-    float a = 0.0f;
-    if (b < B)
-      for (int k = 0; k < NE; ++k) a = fmaf(prob[u][o / dph][k], VT[(long)o * R + b * NE + k], a);
-    mix[u] = a;
+  for (int u = 0; u < EPWV; ++u)
+#pragma unroll
+    for (int h = 0; h < H; ++h) acc[u][h] = 0.0f;
+  for (int j = 0; j < NE; ++j) {
+    const float4 xv = xs[j * HD + k];
+    const float xu[EPWV] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+    for (int u = 0; u < EPWV; ++u)
+#pragma unroll
+      for (int h = 0; h < H; ++h) acc[u][h] = fmaf(ps[j * NV + u * H + h], xu[u], acc[u][h]);
   }
-#pragma unroll
-  for (int u = 0; u < EPB; ++u) vec[u][o] = mix[u];
-  __syncthreads();
-  // attention_combine + residual: (Wc . out + ego) / 2
-  float att[EPB];
-#pragma unroll
-  for (int u = 0; u < EPB; ++u) att[u] = 0.0f;
-  for (int k = 0; k < HD; ++k) {
-    const float w = W[L.wc + k * HD + o];
-#pragma unroll
-    for (int u = 0; u < EPB; ++u) att[u] = fmaf(w, vec[u][k], att[u]);
-  }
+  // 3. value projection per head, attention_combine, residual, output MLP, predict
+  POL_T(6);
   __syncthreads();
 #pragma unroll
-  for (int u = 0; u < EPB; ++u) vec[u][o] = (att[u] + e[u]) / 2.0f;
+  for (int h = 0; h < H; ++h) xs[h * HD + k] = make_float4(acc[0][h], acc[1][h], acc[2][h], acc[3][h]);
+#pragma unroll
+  for (int u = 0; u < EPWV; ++u) t[u] = 0.0f;
   __syncthreads();
-  // output MLP 64 -> 64 -> 64 (ReLU) -> A
+  matvec4(W + L.wv, xs + (k / DPH) * HD, k, t);  // output feature k belongs to head k / DPH
+  __syncthreads();
+  float y[EPWV];
+#pragma unroll
+  for (int u = 0; u < EPWV; ++u) y[u] = 0.0f;
+  bc[k] = f4(t);
+  __syncthreads();
+  matvec4(W + L.wc, bc, k, y);
+  POL_T(7);
+#pragma unroll
+  for (int u = 0; u < EPWV; ++u) y[u] = (y[u] + e[u]) / 2.0f;
   const int offs_w[2] = {L.h1w, L.h2w}, offs_b[2] = {L.h1b, L.h2b};
+#pragma unroll
   for (int layer = 0; layer < 2; ++layer) {
-    float a[EPB];
-#pragma unroll
-    for (int u = 0; u < EPB; ++u) a[u] = W[offs_b[layer] + o];
-    for (int k = 0; k < HD; ++k) {
-      const float w = W[offs_w[layer] + k * HD + o];
-#pragma unroll
-      for (int u = 0; u < EPB; ++u) a[u] = fmaf(w, vec[u][k], a[u]);
-    }
     __syncthreads();
+    bc[k] = f4(y);
 #pragma unroll
-    for (int u = 0; u < EPB; ++u) vec[u][o] = a[u] > 0.0f ? a[u] : 0.0f;
+    for (int u = 0; u < EPWV; ++u) y[u] = W[offs_b[layer] + k];
     __syncthreads();
+    matvec4(W + offs_w[layer], bc, k, y);
+#pragma unroll
+    for (int u = 0; u < EPWV; ++u) y[u] = y[u] > 0.0f ? y[u] : 0.0f;
   }
-  if (o < A * EPB) {
-    const int u = o / A, act = o % A;
-    const long b = (long)blockIdx.x * EPB + u;
-    if (b < B) {
-      float a = W[L.pb + act];
-      for (int k = 0; k < HD; ++k) a = fmaf(W[L.pw + k * A + act], vec[u][k], a);
-      Q[b * A + act] = a;
+  __syncthreads();
+  bc[k] = f4(y);
+  __syncthreads();
+  if (k < A) {
+    float a[EPWV];
+#pragma unroll
+    for (int u = 0; u < EPWV; ++u) a[u] = W[L.pb + k];
+#pragma unroll 16
+    for (int i = 0; i < HD; ++i) {
+      const float w = W[L.pw + i * A + k];
+      const float4 v = bc[i];
+      a[0] = fmaf(w, v.x, a[0]);
+      a[1] = fmaf(w, v.y, a[1]);
+      a[2] = fmaf(w, v.z, a[2]);
+      a[3] = fmaf(w, v.w, a[3]);
     }
+#pragma unroll
+    for (int u = 0; u < EPWV; ++u)
+      if (b0 + u < B) Q[(b0 + u) * A + k] = a[u];
   }
+  POL_T(8);
+#ifdef TTRL_POL_CLOCKS
+  if (k == 0 && blockIdx.x < POL_CLK_BLOCKS)
+    for (int n = 0; n < 9; ++n) g_pol_clk[blockIdx.x * 9 + n] = pol_clk[n] - pol_clk[0];
+#endif
+}
+
+template <int F, int H>
+int launch(const float* obs, int B, int NE, const float* W, int A, float* Q, hipStream_t st) {
+  const size_t lds = pol_lds(NE, F, H).total * sizeof(float);
+  hipLaunchKernelGGL((ego_attention_kernel<F, H>), dim3((B + EPWV - 1) / EPWV), dim3(64), lds, st, obs, B, NE,
+                     W, A, Q);
+  return hipGetLastError() == hipSuccess ? TTRL_OK : TTRL_E_LAUNCH;
 }
 
 template <int F>
-int launch(const float* obs, int B, int NE, int heads, const float* W, int A, float* scratch, float* Q,
-           hipStream_t st) {
-  const long R = (long)B * NE;
-  float* KT = scratch;
-  float* VT = KT + HD * R;
-  float* ET = VT + HD * R;
-  const int blocks1 = (B + RB - 1) / RB + (int)((B * (long)(NE - 1) + RB - 1) / RB);
-  hipLaunchKernelGGL(rows_kernel<F>, dim3(blocks1), dim3(RB), 0, st, obs, B, NE, W, A, KT, VT, ET);
-  hipLaunchKernelGGL(env_kernel<F>, dim3((B + EPB - 1) / EPB), dim3(64), 0, st, obs, B, NE, heads, W, A, KT, VT,
-                     ET, Q);
-  return hipGetLastError() == hipSuccess ? TTRL_OK : TTRL_E_LAUNCH;
+int launch_heads(const float* obs, int B, int NE, int heads, const float* W, int A, float* Q, hipStream_t st) {
+  switch (heads) {
+    case 1: return launch<F, 1>(obs, B, NE, W, A, Q, st);
+    case 2: return launch<F, 2>(obs, B, NE, W, A, Q, st);
+    case 4: return launch<F, 4>(obs, B, NE, W, A, Q, st);
+    case 8: return launch<F, 8>(obs, B, NE, W, A, Q, st);
+    default: return TTRL_E_ARG;
+  }
 }
 
 }  // namespace
@@ -259,7 +367,7 @@ extern "C" {
 int64_t ttrl_ego_attention_sizes(int32_t n_features, int32_t n_actions, int32_t batch, int32_t n_entities,
                                  int64_t* scratch_floats) {
   if (n_features < 1 || n_features > 16 || n_actions < 1 || n_actions > 16) return TTRL_E_ARG;
-  if (scratch_floats) *scratch_floats = (int64_t)HD * batch * (2 * (int64_t)n_entities + 1);
+  if (scratch_floats) *scratch_floats = 1;  // the fused kernel keeps every activation on chip
   return policy_layout(n_features, n_actions).total;
 }
 
@@ -271,11 +379,19 @@ int ttrl_ego_attention_q(const float* obs, int32_t batch, int32_t n_entities, in
   if (batch == 0) return TTRL_OK;
   hipStream_t st = (hipStream_t)stream;
   switch (n_features) {
-    case 5: return launch<5>(obs, batch, n_entities, heads, weights, n_actions, scratch, q, st);
-    case 7: return launch<7>(obs, batch, n_entities, heads, weights, n_actions, scratch, q, st);
-    case 8: return launch<8>(obs, batch, n_entities, heads, weights, n_actions, scratch, q, st);
+    case 5: return launch_heads<5>(obs, batch, n_entities, heads, weights, n_actions, q, st);
+    case 7: return launch_heads<7>(obs, batch, n_entities, heads, weights, n_actions, q, st);
+    case 8: return launch_heads<8>(obs, batch, n_entities, heads, weights, n_actions, q, st);
     default: return TTRL_E_UNSUPPORTED;
   }
 }
+
+#ifdef TTRL_POL_CLOCKS
+int ttrl_diag_policy_clocks(long long* out, int32_t n) {
+  if (n > POL_CLK_BLOCKS * 9) n = POL_CLK_BLOCKS * 9;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pol_clk), n * sizeof(long long)) == hipSuccess ? TTRL_OK
+                                                                                              : TTRL_E_LAUNCH;
+}
+#endif
 
 }  // extern "C"
