@@ -242,3 +242,29 @@ def test_fused_ego_attention_matches_torch_forward(B, hip_device):
     with torch.no_grad():
         net.output_layer.predict.bias.add_(1.0)
     assert torch.allclose(net.fused_q(x), net(x), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("heads,F_,NE,A,B", [(1, 7, 15, 5, 37), (2, 5, 2, 3, 9), (2, 7, 5, 5, 130), (2, 8, 32, 4, 66),
+                                             (4, 7, 16, 5, 21), (8, 7, 8, 5, 13)])
+def test_fused_ego_attention_shapes_and_biases(heads, F_, NE, A, B, hip_device):
+    """Every supported head count / feature count / entity count (partial entity batches, partial
+    last wave), with random nonzero biases in every layer."""
+    import copy
+    from topotrafficrl_amd.agent import EGO_ATTENTION_2H, EgoAttentionNetwork
+    cfg = copy.deepcopy(EGO_ATTENTION_2H)
+    cfg["embedding_layer"]["in"] = cfg["others_embedding_layer"]["in"] = F_
+    cfg["attention_layer"]["heads"] = heads
+    gen = torch.Generator().manual_seed(heads * 100 + NE)
+    net = EgoAttentionNetwork(A, cfg).reset(gen)
+    with torch.no_grad():
+        for m in net.modules():
+            if isinstance(m, torch.nn.Linear) and m.bias is not None:
+                m.bias.uniform_(-0.3, 0.3, generator=gen)
+    net = net.to(hip_device)
+    g = torch.Generator(device=hip_device).manual_seed(NE)
+    x = torch.rand(B, NE, F_, device=hip_device, generator=g) * 2 - 1
+    x[:, :, 0] = (torch.rand(B, NE, device=hip_device, generator=g) < 0.6).float()
+    x[0, 0, 0] = 0.0  # a masked ego
+    ref = net(x)
+    got = net.fused_q(x)
+    assert torch.allclose(got, ref, rtol=1e-4, atol=1e-5), float((got - ref).abs().max())

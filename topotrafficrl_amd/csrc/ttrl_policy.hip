@@ -108,33 +108,46 @@ __device__ __forceinline__ int fold_index(int lane) {
   return idx;
 }
 
-// LDS of one wave (floats): the broadcast vectors, the wave's observations, every entity's
-// embedding (float4 over the envs; reused for the per-head weighted sums), the scores / weights
+// LDS of one wave (floats): the broadcast vectors, the wave's observations, the ego embeddings,
+// qk_h (then the per-head weighted embedding sums), the ego scores
 struct PolLds {
-  int ob, xs, ps, total;
+  int ob, es, qk, s0, total;
 };
 __host__ __device__ inline PolLds pol_lds(int NE, int F, int H) {
   PolLds P;
   P.ob = HD * 4;
-  P.xs = P.ob + ((EPWV * NE * F + 3) & ~3);
-  P.ps = P.xs + (NE > H ? NE : H) * HD * 4;
-  P.total = P.ps + NE * EPWV * H;
+  P.es = P.ob + ((EPWV * NE * F + 3) & ~3);
+  P.qk = P.es + HD * 4;
+  P.s0 = P.qk + H * HD * 4;
+  P.total = P.s0 + EPWV * H;
   return P;
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// D = A B + C on a 16 x 16 x 4 float32 tile (exact fmaf chain over k). Lane l holds A[l & 15][l >> 4],
+// B[l >> 4][l & 15] and D[4 (l >> 4) + r][l & 15] in register r.
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
 // One wave per EPWV envs, lane k = feature k. Linearity moves the key and value projections
 // out of the entity loop: with x_j the 64-wide embedding of entity j,
 //   score_hj = q_h . (Wk x_j)_h / sqrt(d) = x_j . qk_h,      qk_h = Wk_h^T q_h / sqrt(d)
 //   mix_h    = sum_j p_hj (Wv x_j)_h      = (Wv (sum_j p_hj x_j))_h
-// so an entity costs its embedding (F + 64 FMAs per lane per env) and a share of one butterfly
-// reduction; the value projection runs once per env on the weighted embedding sum.
-//   1. ego embeddings, queries, qk_h (env-level weights loaded once per wave, used EPWV times)
-//   2. entities j (j = 0: the ego's own embedding): embedding to LDS, scores with
-//      masked_fill(presence < 0.5, -1e9) (models.py:383); softmax over j per (env, head)
-//      (models.py:384); the weighted sums of the embeddings
+// so an entity costs only its embedding, and the value projection runs once per env on the
+// weighted embedding sum.
+//   1. ego embeddings, queries, qk_h, the ego's scores (VALU, lane k = feature k; env-level
+//      weights loaded once per wave, used EPWV times)
+//   2. the other entities, 4 at a time for the wave's 4 envs: a 16-column tile (column c = entity
+//      c >> 2, env c & 3) through both embedding layers on float32 MFMA 16x16x4 (the first
+//      layer's output tile is the second's B operand in place: its k order is permuted, and the
+//      register-resident weight fragments follow that order), scores from the tile rows each
+//      lane holds, masked_fill(presence < 0.5, -1e9) (models.py:383), and an online softmax over
+//      the entities (models.py:384): running max / sum / weighted embedding sum per (env, head)
 //   3. the value projection, attention_combine + residual (att + ego) / 2, output MLP, predict
-// Dense algebra, but float32 MFMA issues at the float32 vector rate on gfx950: the win is fusion
-// and the reassociation (no [B*NE, 64] activations through HBM, one launch).
+// No [B*NE, 64] activation reaches HBM; f32 MFMA is exact f32 (an fmaf chain) at the f32 vector
+// rate, but it needs no LDS broadcast of the activations, which bounded the VALU form.
 template <int F, int H>
 __global__ void __launch_bounds__(64, 2) ego_attention_kernel(const float* __restrict__ obs, int B, int NE,
                                                               const float* __restrict__ W, int A,
@@ -150,8 +163,9 @@ __global__ void __launch_bounds__(64, 2) ego_attention_kernel(const float* __res
   float* lds = reinterpret_cast<float*>(lds4);
   float4* bc = lds4;                                 // [HD] vectors broadcast to the wave
   const float* ob = lds + P.ob;                      // [EPWV][NE][F]
-  float4* xs = reinterpret_cast<float4*>(lds + P.xs);  // [NE][HD]; then [H][HD] weighted sums
-  float* ps = lds + P.ps;                            // [NE][NV] scores, then softmax weights
+  float4* es = reinterpret_cast<float4*>(lds + P.es);  // [HD] ego embeddings
+  float4* qks = reinterpret_cast<float4*>(lds + P.qk);  // [H][HD] qk_h; then the weighted sums
+  float* s0s = lds + P.s0;                           // [EPWV][H] the ego's scores
   const int k = threadIdx.x;
   const long b0 = (long)blockIdx.x * EPWV;
   {  // one coalesced copy of the wave's EPWV consecutive [NE][F] observations
@@ -209,89 +223,140 @@ __global__ void __launch_bounds__(64, 2) ego_attention_kernel(const float* __res
   for (int u = 0; u < EPWV; ++u)
 #pragma unroll
     for (int h = 0; h < H; ++h) qk[u][h] *= scale;
-  // 2. the entities, all EPWV envs at once
+  // the ego (entity 0): its score x_0 . qk_h summed over the lanes, masked like the others
   POL_T(4);
-  float w2o[HD];  // lane k's column of the others' second embedding layer
-#pragma unroll
-  for (int i = 0; i < HD; ++i) w2o[i] = W[L.o2w + i * HD + k];
-  float w1o[F];
-#pragma unroll
-  for (int f = 0; f < F; ++f) w1o[f] = W[L.o1w + f * HD + k];
-  const float b1o = W[L.o1b + k], b2o = W[L.o2b + k];
-  const int my_idx = fold_index<NV>(k);  // the (env, head) whose score lane k < NV ends up with
-  POL_T(5);
-  for (int j = 0; j < NE; ++j) {
-    float x[EPWV];
-    if (j == 0) {
-#pragma unroll
-      for (int u = 0; u < EPWV; ++u) x[u] = e[u];
-    } else {  // the others' embedding of entity j
-#pragma unroll
-      for (int u = 0; u < EPWV; ++u) {
-        float h = b1o;
-#pragma unroll
-        for (int f = 0; f < F; ++f) h = fmaf(w1o[f], ob[(u * NE + j) * F + f], h);
-        t[u] = h > 0.0f ? h : 0.0f;
-        x[u] = b2o;
-      }
-      __syncthreads();
-      bc[k] = f4(t);
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < HD; ++i) {
-        const float4 v = bc[i];
-        x[0] = fmaf(w2o[i], v.x, x[0]);
-        x[1] = fmaf(w2o[i], v.y, x[1]);
-        x[2] = fmaf(w2o[i], v.z, x[2]);
-        x[3] = fmaf(w2o[i], v.w, x[3]);
-      }
-#pragma unroll
-      for (int u = 0; u < EPWV; ++u) x[u] = x[u] > 0.0f ? x[u] : 0.0f;
-    }
-    xs[j * HD + k] = f4(x);
+  {
     float v[NV];
 #pragma unroll
     for (int u = 0; u < EPWV; ++u)
 #pragma unroll
-      for (int h = 0; h < H; ++h) v[u * H + h] = x[u] * qk[u][h];
+      for (int h = 0; h < H; ++h) v[u * H + h] = e[u] * qk[u][h];
     fold<0, NV>(v, k);
-    if (k < NV) ps[j * NV + my_idx] = ob[((my_idx / H) * NE + j) * F] < 0.5f ? -1e9f : v[0];
+    const int idx = fold_index<NV>(k);
+    if (k < NV) s0s[idx] = ob[(idx / H) * NE * F] < 0.5f ? -1e9f : v[0];
+    es[k] = f4(e);
+#pragma unroll
+    for (int h = 0; h < H; ++h) qks[h * HD + k] = make_float4(qk[0][h], qk[1][h], qk[2][h], qk[3][h]);
   }
-  __syncthreads();
-  if (k < NV) {  // softmax over the entities of (env, head) = k
-    float m = -__builtin_inff();
-    for (int j = 0; j < NE; ++j) m = fmaxf(m, ps[j * NV + k]);
-    float sum = 0.0f;
-    for (int j = 0; j < NE; ++j) {
-      const float p = expf(ps[j * NV + k] - m);
-      ps[j * NV + k] = p;
-      sum += p;
+  // 2. the other entities on MFMA. Lane l: column c = l & 15 (entity jj = c >> 2 of the batch,
+  // env u = c & 3), row group g = l >> 4; it holds tile rows 16 M + 4 g + r (M, r = 0..3).
+  const int g = k >> 4, c = k & 15, jj = c >> 2, u = c & 3;
+  constexpr int KS1 = (F + 1 + 3) / 4;  // first-layer k steps: F inputs, then the bias (input = 1)
+  float a1[KS1][4], a2[4][4][4], b2[4][4];
+#pragma unroll
+  for (int st = 0; st < KS1; ++st)
+#pragma unroll
+    for (int M = 0; M < 4; ++M) {
+      const int in = 4 * st + g;
+      a1[st][M] = in < F ? W[L.o1w + in * HD + 16 * M + c] : (in == F ? W[L.o1b + 16 * M + c] : 0.0f);
     }
-    for (int j = 0; j < NE; ++j) ps[j * NV + k] /= sum;
-  }
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a2[M][m][r] = W[L.o2w + (16 * m + 4 * g + r) * HD + 16 * M + c];
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b2[M][r] = W[L.o2b + 16 * M + 4 * g + r];
   __syncthreads();
-  float acc[EPWV][H];
+  float qf[H][4][4], acc[H][4][4], mx[H], sm[H];
+  {
+    const float* qkf = reinterpret_cast<const float*>(qks);
+    const float* ef = reinterpret_cast<const float*>(es);
 #pragma unroll
-  for (int u = 0; u < EPWV; ++u)
+    for (int M = 0; M < 4; ++M)
 #pragma unroll
-    for (int h = 0; h < H; ++h) acc[u][h] = 0.0f;
-  for (int j = 0; j < NE; ++j) {
-    const float4 xv = xs[j * HD + k];
-    const float xu[EPWV] = {xv.x, xv.y, xv.z, xv.w};
+      for (int r = 0; r < 4; ++r) {
+        const int f = 16 * M + 4 * g + r;
+        const float x0 = jj == 0 ? ef[f * 4 + u] : 0.0f;  // the ego's term, counted once per env
 #pragma unroll
-    for (int u = 0; u < EPWV; ++u)
+        for (int h = 0; h < H; ++h) {
+          qf[h][M][r] = qkf[(h * HD + f) * 4 + u];
+          acc[h][M][r] = x0;
+        }
+      }
 #pragma unroll
-      for (int h = 0; h < H; ++h) acc[u][h] = fmaf(ps[j * NV + u * H + h], xu[u], acc[u][h]);
+    for (int h = 0; h < H; ++h) {
+      mx[h] = s0s[u * H + h];
+      sm[h] = 1.0f;
+    }
   }
+  POL_T(5);
+  for (int j0 = 1; j0 < NE; j0 += 4) {
+    const int j = j0 + jj;
+    const bool live = j < NE;
+    const float* oj = ob + (u * NE + (live ? j : 0)) * F;
+    f32x4 t1[4];
+#pragma unroll
+    for (int M = 0; M < 4; ++M) t1[M] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int st = 0; st < KS1; ++st) {
+      const int in = 4 * st + g;
+      const float bv = !live ? 0.0f : (in < F ? oj[in < F ? in : 0] : (in == F ? 1.0f : 0.0f));
+#pragma unroll
+      for (int M = 0; M < 4; ++M) t1[M] = mfma4(a1[st][M], bv, t1[M]);
+    }
+    f32x4 t2[4];
+#pragma unroll
+    for (int M = 0; M < 4; ++M) t2[M] = f32x4{b2[M][0], b2[M][1], b2[M][2], b2[M][3]};
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float x1 = t1[m][r] > 0.0f ? t1[m][r] : 0.0f;  // ReLU; k step (m, r) = rows 16 m + 4 g + r
+#pragma unroll
+        for (int M = 0; M < 4; ++M) t2[M] = mfma4(a2[M][m][r], x1, t2[M]);
+      }
+    float x[4][4];
+#pragma unroll
+    for (int M = 0; M < 4; ++M)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) x[M][r] = t2[M][r] > 0.0f ? t2[M][r] : 0.0f;
+    const float presence = oj[0];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      float sc = 0.0f;
+#pragma unroll
+      for (int M = 0; M < 4; ++M)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc = fmaf(x[M][r], qf[h][M][r], sc);
+      sc += lane_xor<4>(sc);  // the other row groups of the column
+      sc += lane_xor<5>(sc);
+      sc = !live ? -__builtin_inff() : (presence < 0.5f ? -1e9f : sc);
+      float bm = fmaxf(sc, lane_xor<2>(sc));  // the batch's entities of env u
+      bm = fmaxf(bm, lane_xor<3>(bm));
+      const float mn = fmaxf(mx[h], bm), corr = expf(mx[h] - mn), p = expf(sc - mn);
+      float ps = p + lane_xor<2>(p);
+      ps += lane_xor<3>(ps);
+      sm[h] = fmaf(sm[h], corr, ps);
+      mx[h] = mn;
+#pragma unroll
+      for (int M = 0; M < 4; ++M)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[h][M][r] = fmaf(acc[h][M][r], corr, p * x[M][r]);
+    }
+  }
+  // the weighted sums of env u over the batch columns (lanes differing in bits 2, 3), to LDS
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < H; ++h)
+#pragma unroll
+    for (int M = 0; M < 4; ++M)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float a = acc[h][M][r];
+        a += lane_xor<2>(a);
+        a += lane_xor<3>(a);
+        if (jj == 0) reinterpret_cast<float*>(qks)[(h * HD + 16 * M + 4 * g + r) * 4 + u] = a / sm[h];
+      }
   // 3. value projection per head, attention_combine, residual, output MLP, predict
   POL_T(6);
-  __syncthreads();
 #pragma unroll
-  for (int h = 0; h < H; ++h) xs[h * HD + k] = make_float4(acc[0][h], acc[1][h], acc[2][h], acc[3][h]);
-#pragma unroll
-  for (int u = 0; u < EPWV; ++u) t[u] = 0.0f;
+  for (int v = 0; v < EPWV; ++v) t[v] = 0.0f;
   __syncthreads();
-  matvec4(W + L.wv, xs + (k / DPH) * HD, k, t);  // output feature k belongs to head k / DPH
+  matvec4(W + L.wv, qks + (k / DPH) * HD, k, t);  // output feature k belongs to head k / DPH
   __syncthreads();
   float y[EPWV];
 #pragma unroll
