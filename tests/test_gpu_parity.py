@@ -218,6 +218,35 @@ def test_random_batch_rollout_vs_oracle(n, hip_device):
         compare(dev, h, 1e-6)
 
 
+@pytest.mark.parametrize("n", [24, 64])
+def test_tied_positions_vs_oracle(n, hip_device):
+    """Vehicles sharing x exactly (the ego included, same and different lanes): the sorted-order
+    neighbour lookups of the straight instance cannot rank them, so those envs take the slot-order
+    scans with the reference's tie rules (front: later slot, rear: earlier slot)."""
+    E = 32
+    lanes = _abi.straight_lane_table(4)
+    o = Oracle(lanes, P)
+    h = HostState(E, n)
+    o.reset_highway(h, _abi.reset_cfg(n, lanes), list(range(300, 300 + E)))
+    rng = np.random.default_rng(5)
+    for e in range(E):
+        for _ in range(1 + e % 4):
+            a, b = rng.choice(n, 2, replace=False)
+            h["x"][e, a] = h["x"][e, b]
+    h["x"][:, 3] = h["x"][:, 0]  # a tie with the ego in every env
+    dev = to_dev(h, hip_device)
+    road = BatchedRoad(RoadNetwork(lanes), dev, P)
+    acts = rng.integers(0, 5, size=E).astype(np.int32)
+    o.simulate(h, acts, 1, 1 / 15)
+    road.simulate(torch.from_numpy(acts), 1, 1 / 15)
+    compare(dev, h, 1e-9)
+    for _ in range(2):
+        acts = rng.integers(0, 5, size=E).astype(np.int32)
+        o.simulate(h, acts, 15, 1 / 15)
+        road.simulate(torch.from_numpy(acts), 15, 1 / 15)
+        compare(dev, h, 1e-6)
+
+
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
 def test_close_pairs_collisions_vs_oracle(dtype, hip_device):
     """Clusters of vehicles at random close poses (many pairs touching, near-touching or

@@ -522,6 +522,13 @@ template <typename T> struct View {
   int8_t* lperm;                 // [LMAX] lanes, straight ones first
   T* pd;                         // [EPW*NS] per-item-thread closest distance so far
   int8_t* pl;                    // [EPW*NS] ... and its lane (-1 none)
+  // Straight instance, one wavefront (sorted_view): the env's vehicles in (x, slot) order instead
+  // of the per-lane lists (key / idx / mypos are not allocated)
+  uint8_t* onb;                  // [EPW*NS] lanes the vehicle is on (bit l: AbstractLane.on_lane margin 1)
+  uint8_t *sord, *spos;          // [EPW*NS] slot at each sorted position / sorted position of each slot
+  float* sxf;                    // [EPW*NS] xf at each sorted position (collision window walk)
+  unsigned long long* lmask;     // [EPW][lanes] per lane: sorted positions of the vehicles on it
+  int* stie;                     // [EPW] the order has ties in some lane's s (use the slot scans)
 };
 constexpr int PRED_T = 11;       // np.arange(0.25, 3, 0.25) (regulation.py:86)
 
@@ -529,11 +536,13 @@ constexpr int PRED_T = 11;       // np.arange(0.25, 3, 0.25) (regulation.py:86)
 constexpr int N_REALS = 8;  // x, y, v, ch, sh, ts, h, delta
 struct ViewLayout {
   size_t lanes, reals[N_REALS], xf, key, afree, powb, pq_tx, pq_ty, pq_ij, bal, cnt, wcnt, nitem, pq_n, mypos, f0, r0, ft,
-      mob, item, idx, kind, flags, lane, tgt, pred, rroad, rlane, rn, ynew, rt, onm, live, lperm, pd, pl, total;
+      mob, item, idx, kind, flags, lane, tgt, pred, rroad, rlane, rn, ynew, rt, onm, live, lperm, pd, pl, onb, sord,
+      spos, sxf, lmask, stie, total;
 };
 
 template <typename T>
-__host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, bool graph = false) {
+__host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, bool graph = false,
+                                                  bool sorted = false) {
   ViewLayout o{};
   size_t p = 0;
   const size_t M = (size_t)EPW * NS;
@@ -561,9 +570,18 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, 
   // pair queue (written after the projection).  The RegulatedRoad trajectory predictions live only
   // between the act and the kinematics, so on a road network they share the whole block.
   const size_t t0 = take(0, 16);
-  o.key = take(sizeof(T) * (size_t)n_lanes * EPW * (NS + 1), 16);
-  o.mypos = take(sizeof(short) * (size_t)n_lanes * M, 4);
-  o.idx = take((size_t)n_lanes * EPW * (NS + 1), 4);
+  if (sorted) {  // the sorted order replaces the lists (the projection writes it, the act reads it)
+    o.sxf = take(sizeof(float) * M, 16);
+    o.lmask = take(sizeof(unsigned long long) * EPW * n_lanes, 8);
+    o.stie = take(sizeof(int) * EPW, 4);
+    o.onb = take(M, 4);
+    o.sord = take(M, 4);
+    o.spos = take(M, 4);
+  } else {
+    o.key = take(sizeof(T) * (size_t)n_lanes * EPW * (NS + 1), 16);
+    o.mypos = take(sizeof(short) * (size_t)n_lanes * M, 4);
+    o.idx = take((size_t)n_lanes * EPW * (NS + 1), 4);
+  }
   const size_t u0 = take(0, 16);
   o.afree = take(sizeof(T) * M, 16);
   o.powb = take(sizeof(T) * M, 16);
@@ -600,8 +618,9 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, 
 // Pointer arithmetic stays on the __shared__ base, so every access is a ds_* instruction
 // with a 32-bit LDS address.
 template <typename T>
-__device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lanes, bool graph = false) {
-  const ViewLayout o = view_layout<T>(EPW, NS, n_lanes, graph);
+__device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lanes, bool graph = false,
+                                         bool sorted = false) {
+  const ViewLayout o = view_layout<T>(EPW, NS, n_lanes, graph, sorted);
   View<T> V;
   V.lanes = (LaneT<T>*)(smem + o.lanes);
   T** reals[N_REALS] = {&V.x, &V.y, &V.v, &V.ch, &V.sh, &V.ts, &V.h, &V.delta};
@@ -645,12 +664,20 @@ __device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lane
     V.lperm = (int8_t*)(smem + o.lperm);
     V.pl = (int8_t*)(smem + o.pl);
   }
+  if (sorted) {
+    V.onb = (uint8_t*)(smem + o.onb);
+    V.sord = (uint8_t*)(smem + o.sord);
+    V.spos = (uint8_t*)(smem + o.spos);
+    V.sxf = (float*)(smem + o.sxf);
+    V.lmask = (unsigned long long*)(smem + o.lmask);
+    V.stie = (int*)(smem + o.stie);
+  }
   return V;
 }
 
-size_t host_view_bytes(int dtype, int EPW, int NS, int n_lanes, bool graph = false) {
-  return dtype == TTRL_F64 ? view_layout<double>(EPW, NS, n_lanes, graph).total
-                           : view_layout<float>(EPW, NS, n_lanes, graph).total;
+size_t host_view_bytes(int dtype, int EPW, int NS, int n_lanes, bool graph = false, bool sorted = false) {
+  return dtype == TTRL_F64 ? view_layout<double>(EPW, NS, n_lanes, graph, sorted).total
+                           : view_layout<float>(EPW, NS, n_lanes, graph, sorted).total;
 }
 
 template <typename T>
@@ -713,7 +740,7 @@ __device__ __forceinline__ void store_veh(const Veh<T>& a, const ttrl_state_t& s
 // slot order (ballot + popcount prefix), so neighbour scans visit only real candidates in
 // the reference's list order; returns the closest lane (RoadNetwork.get_closest_lane_index
 // road.py:55-71, distance_with_heading lane.py:132-147).  All threads must call it.
-template <typename T, int NS, int EPW, bool CV = true>
+template <typename T, int NS, int EPW, bool CV = true, bool LISTS = true>
 __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t& P, int nl, int tid, int le, int i,
                                            bool present, T x, T y, T h, bool want_closest) {
   constexpr int NSP = NS + 1;
@@ -725,6 +752,7 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
     const int sh = (tid & 63) / NS * NS;
     const unsigned long long seg = NS == 64 ? ~0ull : ((1ull << NS) - 1);
     bool have = false;  // bd / best hold a lane
+    int onbits = 0;     // !LISTS: the lanes this vehicle is on
     auto lane_l = [&](int l) {
       const LaneT<T> L = V.lanes[l];
       T s, r;
@@ -755,16 +783,20 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
         lane_local<CV>(L, x, y, s, r);
       }
       const bool on = full && present && fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl;
-      const unsigned long long m = (__ballot(on) >> sh) & seg;
-      const int pos = on ? __popcll(m & ((1ull << i) - 1)) : -1;
-      if (on) {
-        V.key[((size_t)l * EPW + le) * NSP + pos] = s;
-        V.idx[((size_t)l * EPW + le) * NSP + pos] = (uint8_t)i;
+      if constexpr (LISTS) {
+        const unsigned long long m = (__ballot(on) >> sh) & seg;
+        const int pos = on ? __popcll(m & ((1ull << i) - 1)) : -1;
+        if (on) {
+          V.key[((size_t)l * EPW + le) * NSP + pos] = s;
+          V.idx[((size_t)l * EPW + le) * NSP + pos] = (uint8_t)i;
+        }
+        V.mypos[(size_t)l * EPW * NS + le * NS + i] = (short)pos;
+        const int c = __popcll(m);
+        mx = c > mx ? c : mx;
+        if (i == 0) cnt[l] = c;
+      } else {
+        onbits |= on ? 1 << l : 0;
       }
-      V.mypos[(size_t)l * EPW * NS + le * NS + i] = (short)pos;
-      const int c = __popcll(m);
-      mx = c > mx ? c : mx;
-      if (i == 0) cnt[l] = c;
       if (want_closest && full) {
         const T hdl = heading_at<CV>(L, s);  // distance_with_heading lane.py:132-147
         if (!have || hdl != prev_hd) ang = fabs(wrap_to_pi(h - hdl));
@@ -783,6 +815,7 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
       for (int l = 0; l < STRAIGHT_LANE_CAP; ++l)
         if (l < nl) lane_l(l);
     }
+    if constexpr (!LISTS) V.onb[le * NS + i] = (uint8_t)onbits;
   } else {
     constexpr int W = NS / 64;
     const int wave = tid >> 6, lane = tid & 63;
@@ -827,8 +860,103 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
       }
     }
   }
-  if (i == 0) cnt[LMAX] = mx;
+  if constexpr (LISTS)
+    if (i == 0) cnt[LMAX] = mx;
   return best;
+}
+
+// The env's vehicles in (x, slot) order (sorted_view instances: one wavefront, NS lanes per env).
+// Sorted position p lives in lane p of the env's segment; the order of the previous frame is
+// restored by odd-even transposition (vehicles pass each other rarely within a frame, so this is
+// usually the check alone), a launch's first order by ranks.  Results: sord / spos, the float x
+// in sorted order, per lane the sorted positions of the vehicles on it, and a tie flag: when two
+// present vehicles have equal s on some lane (or x is NaN) the sorted order cannot stand for the
+// reference's list-order tie rules, and the callers fall back to slot-order scans.
+template <typename T, int NS, int EPW>
+__device__ __forceinline__ void sort_order(const View<T>& V, int nl, int tid, int le, int i, bool init) {
+  const int eb = le * NS;
+  if (init) {
+    const T xi = V.x[eb + i];
+    int rk = 0;
+    for (int j = 0; j < NS; ++j) {
+      const T xj = V.x[eb + j];
+      rk += (xj < xi || (xj == xi && j < i) || (xi != xi && xj == xj) || (xi != xi && xj != xj && j < i)) ? 1 : 0;
+    }
+    V.sord[eb + rk] = (uint8_t)i;
+    __syncthreads();
+  }
+  const int s0 = V.sord[eb + i];
+  T key = V.x[eb + s0];
+  bool nan = key != key;
+  if (nan) key = K<T>::inf();  // sorted last; the tie flag sends the env to the slot scans
+  int pay = s0 | (int)V.onb[eb + s0] << 8;
+  auto less = [](T ka, int pa, T kb, int pb) { return ka < kb || (ka == kb && (pa & 0xff) < (pb & 0xff)); };
+  const int base = tid - i;  // the segment's first lane
+  auto cmpx = [&](int pt, bool valid) {  // lower lane of the pair keeps the smaller element
+    const T pk = __shfl(key, base + pt);
+    const int pp = __shfl(pay, base + pt);
+    const bool pl = less(pk, pp, key, pay);
+    const bool take = valid && (i < pt ? pl : !pl);
+    key = take ? pk : key;
+    pay = take ? pp : pay;
+  };
+  T nk;
+  int np;
+  for (int pass = 0;; ++pass) {
+    nk = __shfl(key, base + (i + 1 < NS ? i + 1 : i));
+    np = __shfl(pay, base + (i + 1 < NS ? i + 1 : i));
+    const bool ok = i + 1 >= NS || less(key, pay, nk, np);
+    if (__all(ok) || pass == NS) break;
+    cmpx(i ^ 1, true);
+    const int po = (i & 1) ? i + 1 : i - 1;
+    cmpx(po >= 0 && po < NS ? po : i, po >= 0 && po < NS);
+  }
+  const int sl = pay & 0xff;
+  V.sord[eb + i] = (uint8_t)sl;
+  V.spos[eb + sl] = (uint8_t)i;
+  V.sxf[eb + i] = (float)key;
+  const int sh = (tid & 63) - i;
+  const unsigned long long seg = NS == 64 ? ~0ull : ((1ull << NS) - 1);
+#pragma unroll
+  for (int l = 0; l < STRAIGHT_LANE_CAP; ++l) {
+    const unsigned long long m = (__ballot((pay >> (8 + l)) & 1) >> sh) & seg;
+    if (i == 0 && l < nl) V.lmask[le * STRAIGHT_LANE_CAP + l] = m;
+  }
+  bool tie = nan;
+  if (i + 1 < NS && key < T(FAR) && nk < T(FAR)) {
+    tie |= !less(key, pay, nk, np) || nk == key;  // not sorted (pass cap) / equal x
+#pragma unroll
+    for (int l = 0; l < STRAIGHT_LANE_CAP; ++l)
+      if (l < nl) tie |= (key - V.lanes[l].sx) == (nk - V.lanes[l].sx);
+  }
+  const unsigned long long tb = (__ballot(tie) >> sh) & seg;
+  if (i == 0) V.stie[le] = tb != 0;
+}
+
+// Road.neighbour_vehicles (road.py:480-513) on lane l for the vehicle at sorted position p, from
+// the lane's position mask (no ties: positions order the keys strictly); slots, -1 for none.
+template <typename T, int NS>
+__device__ __forceinline__ void sorted_nbrs(const View<T>& V, int le, int l, int p, int& f, int& r) {
+  const unsigned long long m = V.lmask[le * STRAIGHT_LANE_CAP + l] & ~(1ull << p);
+  const unsigned long long up = m & ~((2ull << p) - 1), dn = m & ((1ull << p) - 1);
+  f = up ? (int)V.sord[le * NS + __ffsll((long long)up) - 1] : -1;
+  r = dn ? (int)V.sord[le * NS + 63 - __clzll((long long)dn)] : -1;
+}
+
+// The same in the reference's list (slot) order, for envs whose sorted order has ties: front =
+// min s_v >= s (ties: later slot), rear = max s_v < s (ties: earlier slot).
+template <typename T, int NS>
+__device__ __forceinline__ void slot_nbrs(const View<T>& V, int le, int self, int l, T s, int& f, int& r) {
+  const T sx = V.lanes[l].sx;
+  T sf = K<T>::inf(), sr = -K<T>::inf();
+  f = -1;
+  r = -1;
+  for (int j = 0; j < NS; ++j) {
+    if (j == self || !((V.onb[le * NS + j] >> l) & 1)) continue;
+    const T xk = V.x[le * NS + j] - sx;  // lane_local's s on a straight +x lane
+    if (s <= xk && xk <= sf) { sf = xk; f = j; }
+    if (xk < s && xk > sr) { sr = xk; r = j; }
+  }
 }
 
 #ifdef TTRL_CHECK_ITEMS
@@ -987,6 +1115,10 @@ __device__ __forceinline__ T lane_s(const View<T>& V, int l, int le, int i, T x,
 // Network mode of the simulate kernel: one straight road (the highway), one road of curved
 // lanes, or a graph of roads with routes and RegulatedRoad priorities (the intersection).
 enum { NET_STRAIGHT = 0, NET_CURVED = 1, NET_GRAPH = 2 };
+// The straight instance on one wavefront per workgroup keeps each env's vehicles in (x, slot) order
+// (sort_order) instead of per-lane candidate lists: on lanes along +x every lane's s is x minus a
+// constant, so that one order ranks the candidates of every lane.
+constexpr bool sorted_view(int NS, int EPW, int NET) { return NET == NET_STRAIGHT && NS * EPW == 64; }
 
 // AbstractLane.distance lane.py:127-130
 template <typename T>
@@ -1312,7 +1444,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   const int eb = le * NS;      // env base in the LDS view
   // The straight-road instance carves a compile-time layout (LANE_CAP lanes): every view array
   // is then the LDS base plus an immediate offset, so no base addresses occupy registers.
-  View<T> V = carve<T>(smem, EPW, NS, NET == NET_STRAIGHT ? STRAIGHT_LANE_CAP : nl, GR);
+  constexpr bool SO = sorted_view(NS, EPW, NET);
+  View<T> V = carve<T>(smem, EPW, NS, NET == NET_STRAIGHT ? STRAIGHT_LANE_CAP : nl, GR, SO);
   PH_INIT
   stage_lanes(V, R, tid);
   if constexpr (GR) {
@@ -1365,7 +1498,11 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   PH(15);
   if (i == 0) V.nitem[le] = 0;
   __syncthreads();  // lane table + view staged
-  project_all<T, NS, EPW, CV>(V, P, nl, tid, le, i, present, V.x[me], V.y[me], T(0), false);
+  project_all<T, NS, EPW, CV, !SO>(V, P, nl, tid, le, i, present, V.x[me], V.y[me], T(0), false);
+  if constexpr (SO) {
+    __syncthreads();
+    sort_order<T, NS, EPW>(V, nl, tid, le, i, true);
+  }
   const int kind = V.kind[me];
 
   PH(11);
@@ -1459,7 +1596,18 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         }
         int f2[2] = {-1, -1}, r2[2] = {-1, -1};
         PH(1);
-        if (!(ablate & A_NO_SCAN)) {
+        if constexpr (SO) {
+          if (!(ablate & A_NO_SCAN)) {
+            const bool tie = V.stie[le] != 0;
+            const int p = V.spos[me];
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+              if (ql[q] >= 0) {
+                if (!tie) sorted_nbrs<T, NS>(V, le, ql[q], p, f2[q], r2[q]);
+                else slot_nbrs<T, NS>(V, le, i, ql[q], s2[q], f2[q], r2[q]);
+              }
+          }
+        } else if (!(ablate & A_NO_SCAN)) {
           if (__any(ql[1] >= 0)) {
             if (polite) scan_neighbours<T, 2, NS, EPW, 1u>(V, le, i, ql, s2, f2, r2);
             else scan_neighbours<T, 2, NS, EPW, 0u>(V, le, i, ql, s2, f2, r2);
@@ -1522,8 +1670,14 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             lane_local<CV>(V.lanes[ln], V.x[ve], V.y[ve], sq, rr);
             T sf = K<T>::inf(), sr = -K<T>::inf();
             int fp = -1, rp = -1;
-            const size_t rowb = ((size_t)ln * EPW + le) * (NS + 1);
-            if (!(ablate & A_NO_SCAN)) {
+            int np_ = -1, nf = -1;  // the side lane's front / rear of the item's vehicle
+            const size_t rowb = SO ? 0 : ((size_t)ln * EPW + le) * (NS + 1);
+            if constexpr (SO) {
+              if (!(ablate & A_NO_SCAN)) {
+                if (V.stie[le] == 0) sorted_nbrs<T, NS>(V, le, ln, V.spos[ve], np_, nf);
+                else slot_nbrs<T, NS>(V, le, vi, ln, sq, np_, nf);
+              }
+            } else if (!(ablate & A_NO_SCAN)) {
               const T* row = V.key + rowb;
               const int n = V.cnt[le * (LMAX + 1) + ln];
               const int mep = V.mypos[(size_t)ln * EPW * NS + le * NS + vi];  // the item's vehicle is skipped
@@ -1546,7 +1700,10 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
               merge(grp8_swap<2>(sf), grp8_swap<2>(fp), grp8_swap<2>(sr), grp8_swap<2>(rp));
               merge(grp8_swap<4>(sf), grp8_swap<4>(fp), grp8_swap<4>(sr), grp8_swap<4>(rp));
             }
-            const int np_ = fp >= 0 ? (int)V.idx[rowb + fp] : -1, nf = rp >= 0 ? (int)V.idx[rowb + rp] : -1;
+            if constexpr (!SO) {
+              np_ = fp >= 0 ? (int)V.idx[rowb + fp] : -1;
+              nf = rp >= 0 ? (int)V.idx[rowb + rp] : -1;
+            }
             const int op = V.f0[ve], of = V.r0[ve];
             const T delta = V.delta[ve];
             // IDM_self(new follower, front = self), a(self | new front), a(self | old front): DELTA is the caller's
@@ -1823,10 +1980,14 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
 #endif
         cl = project_items<T, NS, EPW>(V, P, nl, tid, le, i, present, !(ablate & A_NO_LANE));
       else
-        cl = project_all<T, NS, EPW, CV>(V, P, nl, tid, le, i, present, x, y, h, !(ablate & A_NO_LANE));
+        cl = project_all<T, NS, EPW, CV, !SO>(V, P, nl, tid, le, i, present, x, y, h, !(ablate & A_NO_LANE));
       if (present && !(ablate & A_NO_LANE)) V.lane[me] = (int8_t)cl;  // on_state_update kinematics.py:170-177
       if (i == 0) V.pq_n[le] = 0;
       __syncthreads();
+      if constexpr (SO) {  // this frame's order: the collision window below, the next frame's act
+        sort_order<T, NS, EPW>(V, nl, tid, le, i, false);
+        __syncthreads();
+      }
       PH(7);
 
       // collisions for all pairs (road.py:474-476, objects.py:91-137), impact: last writer.
@@ -1848,7 +2009,17 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         // bounds the reference's asymmetric threshold), then the exact tests run one candidate per
         // lane per round, queue slots coming from the round's ballot (no LDS atomics).
         unsigned long long m = 0;
-        if (present && do_coll) {
+        if (SO && present && do_coll && V.stie[le] == 0) {
+          // the window is a run of sorted positions (the float x is monotone in x): walk out from
+          // this vehicle's position both ways while inside it
+          const float xfi = V.xf[me];
+          const float Rwf = (float)Rw * 1.0001f + 1e-5f * fabsf(xfi) + 1e-3f;
+          const int p = V.spos[me];
+          for (int q = p + 1; q < NS && !(V.sxf[eb + q] - xfi > Rwf); ++q) m |= 1ull << V.sord[eb + q];
+          for (int q = p - 1; q >= 0 && !(xfi - V.sxf[eb + q] > Rwf); --q) m |= 1ull << V.sord[eb + q];
+          m &= ~((2ull << i) - 1);  // keep j > i
+          if (ablate & A_NO_PREF) m = 0;
+        } else if (present && do_coll) {
           const float xfi = V.xf[me];
           // float window: |xf_j - xf_i| in float errs by < 1.2e-7 (|x_i| + |x_j|), far below the slack
           const float Rwf = (float)Rw * 1.0001f + 1e-5f * fabsf(xfi) + 1e-3f;
@@ -3241,7 +3412,8 @@ int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_par
   for (int l = 0; l < R.n_lanes; ++l)
     curved |= R.type[l] != TTRL_LANE_STRAIGHT || R.dir_x[l] != 1.0 || R.dir_y[l] != 0.0;
   const size_t lds = host_view_bytes(sizeof(T) == 8 ? TTRL_F64 : TTRL_F32, EPW, NS,
-                                     graph || curved ? R.n_lanes : STRAIGHT_LANE_CAP, graph);
+                                     graph || curved ? R.n_lanes : STRAIGHT_LANE_CAP, graph,
+                                     !graph && !curved && sorted_view(NS, EPW, NET_STRAIGHT));
   if (graph)
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_GRAPH>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, P,
                        actions, mask, frames, dt, mode, ablate);
