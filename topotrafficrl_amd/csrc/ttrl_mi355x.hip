@@ -742,7 +742,7 @@ __device__ __forceinline__ void store_veh(const Veh<T>& a, const ttrl_state_t& s
 // road.py:55-71, distance_with_heading lane.py:132-147).  All threads must call it.
 template <typename T, int NS, int EPW, bool CV = true, bool LISTS = true>
 __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t& P, int nl, int tid, int le, int i,
-                                           bool present, T x, T y, T h, bool want_closest) {
+                                           bool present, T x, T y, T h, bool want_closest, int* onb_out = nullptr) {
   constexpr int NSP = NS + 1;
   const T vl = T(P.lane_vehicle_length);
   int best = 0, mx = 0;
@@ -815,7 +815,10 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
       for (int l = 0; l < STRAIGHT_LANE_CAP; ++l)
         if (l < nl) lane_l(l);
     }
-    if constexpr (!LISTS) V.onb[le * NS + i] = (uint8_t)onbits;
+    if constexpr (!LISTS) {
+      V.onb[le * NS + i] = (uint8_t)onbits;
+      if (onb_out) *onb_out = onbits;
+    }
   } else {
     constexpr int W = NS / 64;
     const int wave = tid >> 6, lane = tid & 63;
@@ -868,50 +871,51 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
 // The env's vehicles in (x, slot) order (sorted_view instances: one wavefront, NS lanes per env).
 // Sorted position p lives in lane p of the env's segment; the order of the previous frame is
 // restored by odd-even transposition (vehicles pass each other rarely within a frame, so this is
-// usually the check alone), a launch's first order by ranks.  Results: sord / spos, the float x
+// usually the check alone), a launch's first order by a bitonic sort.  my_slot (a register of the
+// lane at sorted position p) carries the slot at p from frame to frame.  Results: sord / spos, the float x
 // in sorted order, per lane the sorted positions of the vehicles on it, and a tie flag: when two
 // present vehicles have equal s on some lane (or x is NaN) the sorted order cannot stand for the
 // reference's list-order tie rules, and the callers fall back to slot-order scans.
 template <typename T, int NS, int EPW>
-__device__ __forceinline__ void sort_order(const View<T>& V, int nl, int tid, int le, int i, bool init) {
+__device__ __forceinline__ void sort_order(const View<T>& V, int nl, int tid, int le, int i, bool init, int& my_slot,
+                                           T xo, int obo) {
   const int eb = le * NS;
-  if (init) {
-    const T xi = V.x[eb + i];
-    int rk = 0;
-    for (int j = 0; j < NS; ++j) {
-      const T xj = V.x[eb + j];
-      rk += (xj < xi || (xj == xi && j < i) || (xi != xi && xj == xj) || (xi != xi && xj != xj && j < i)) ? 1 : 0;
-    }
-    V.sord[eb + rk] = (uint8_t)i;
-    __syncthreads();
-  }
-  const int s0 = V.sord[eb + i];
-  T key = V.x[eb + s0];
-  bool nan = key != key;
-  if (nan) key = K<T>::inf();  // sorted last; the tie flag sends the env to the slot scans
-  int pay = s0 | (int)V.onb[eb + s0] << 8;
-  auto less = [](T ka, int pa, T kb, int pb) { return ka < kb || (ka == kb && (pa & 0xff) < (pb & 0xff)); };
   const int base = tid - i;  // the segment's first lane
-  auto cmpx = [&](int pt, bool valid) {  // lower lane of the pair keeps the smaller element
+  if (init) my_slot = i;  // a launch's first order: bitonic from slot order
+  // gathered from the lane of the slot (x and lane bits are still in its registers: no barrier)
+  T key = __shfl(xo, base + my_slot);
+  const int ob = __shfl(obo, base + my_slot);
+  const bool nan = key != key;
+  if (nan) key = K<T>::inf();  // sorted last; the tie flag sends the env to the slot scans
+  int pay = my_slot | ob << 8;
+  auto less = [](T ka, int pa, T kb, int pb) { return ka < kb || (ka == kb && (pa & 0xff) < (pb & 0xff)); };
+  auto cmpx = [&](int pt, bool valid, bool up) {  // the pair's lower lane keeps the smaller element if up
     const T pk = __shfl(key, base + pt);
     const int pp = __shfl(pay, base + pt);
     const bool pl = less(pk, pp, key, pay);
-    const bool take = valid && (i < pt ? pl : !pl);
+    const bool take = valid && ((i < pt) == up ? pl : !pl);
     key = take ? pk : key;
     pay = take ? pp : pay;
   };
+  if (init) {
+#pragma unroll
+    for (int k = 2; k <= NS; k <<= 1)
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) cmpx(i ^ j, true, (i & k) == 0);
+  }
   T nk;
   int np;
-  for (int pass = 0;; ++pass) {
+  for (int pass = 0;; ++pass) {  // the previous frame's order, restored by odd-even transposition
     nk = __shfl(key, base + (i + 1 < NS ? i + 1 : i));
     np = __shfl(pay, base + (i + 1 < NS ? i + 1 : i));
     const bool ok = i + 1 >= NS || less(key, pay, nk, np);
     if (__all(ok) || pass == NS) break;
-    cmpx(i ^ 1, true);
+    cmpx(i ^ 1, true, true);
     const int po = (i & 1) ? i + 1 : i - 1;
-    cmpx(po >= 0 && po < NS ? po : i, po >= 0 && po < NS);
+    cmpx(po >= 0 && po < NS ? po : i, po >= 0 && po < NS, true);
   }
   const int sl = pay & 0xff;
+  my_slot = sl;
   V.sord[eb + i] = (uint8_t)sl;
   V.spos[eb + sl] = (uint8_t)i;
   V.sxf[eb + i] = (float)key;
@@ -924,7 +928,7 @@ __device__ __forceinline__ void sort_order(const View<T>& V, int nl, int tid, in
   }
   bool tie = nan;
   if (i + 1 < NS && key < T(FAR) && nk < T(FAR)) {
-    tie |= !less(key, pay, nk, np) || nk == key;  // not sorted (pass cap) / equal x
+    tie |= !less(key, pay, nk, np) || nk == key;  // unsorted at the pass cap (not expected) / equal x
 #pragma unroll
     for (int l = 0; l < STRAIGHT_LANE_CAP; ++l)
       if (l < nl) tie |= (key - V.lanes[l].sx) == (nk - V.lanes[l].sx);
@@ -1467,6 +1471,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   // registers for the launch; what other vehicles read is staged in the LDS view.
   T my_timer, my_steer, my_acc, my_ix, my_iy;
   int my_sidx;
+  int my_sorted = 0;  // SO: the slot at this lane's sorted position
   {  // HBM -> LDS, once per launch (coalesced SoA rows)
     Veh<T> a;
     if (slot) load_veh(a, st, k);
@@ -1498,10 +1503,11 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   PH(15);
   if (i == 0) V.nitem[le] = 0;
   __syncthreads();  // lane table + view staged
-  project_all<T, NS, EPW, CV, !SO>(V, P, nl, tid, le, i, present, V.x[me], V.y[me], T(0), false);
-  if constexpr (SO) {
-    __syncthreads();
-    sort_order<T, NS, EPW>(V, nl, tid, le, i, true);
+  {
+    int ob = 0;
+    const T x0 = V.x[me];
+    project_all<T, NS, EPW, CV, !SO>(V, P, nl, tid, le, i, present, x0, V.y[me], T(0), false, &ob);
+    if constexpr (SO) sort_order<T, NS, EPW>(V, nl, tid, le, i, true, my_sorted, x0, ob);
   }
   const int kind = V.kind[me];
 
@@ -1979,15 +1985,15 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       if constexpr (false)
 #endif
         cl = project_items<T, NS, EPW>(V, P, nl, tid, le, i, present, !(ablate & A_NO_LANE));
-      else
-        cl = project_all<T, NS, EPW, CV, !SO>(V, P, nl, tid, le, i, present, x, y, h, !(ablate & A_NO_LANE));
+      else {
+        int ob = 0;
+        cl = project_all<T, NS, EPW, CV, !SO>(V, P, nl, tid, le, i, present, x, y, h, !(ablate & A_NO_LANE), &ob);
+        // this frame's order: the collision window below, the next frame's act
+        if constexpr (SO) sort_order<T, NS, EPW>(V, nl, tid, le, i, false, my_sorted, x, ob);
+      }
       if (present && !(ablate & A_NO_LANE)) V.lane[me] = (int8_t)cl;  // on_state_update kinematics.py:170-177
       if (i == 0) V.pq_n[le] = 0;
       __syncthreads();
-      if constexpr (SO) {  // this frame's order: the collision window below, the next frame's act
-        sort_order<T, NS, EPW>(V, nl, tid, le, i, false);
-        __syncthreads();
-      }
       PH(7);
 
       // collisions for all pairs (road.py:474-476, objects.py:91-137), impact: last writer.
