@@ -204,7 +204,7 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
     n_act = env.action_space.n
-    acts = torch.randint(0, n_act, (args.warmup + args.steps, E), device=dev, generator=g, dtype=torch.int64)
+    acts = torch.randint(0, n_act, (args.warmup + args.steps, E), device=dev, generator=g, dtype=torch.int32)
     live = torch.zeros((), dtype=torch.int64, device=dev)  # live vehicles summed over the timed steps
 
     sg = None
@@ -284,6 +284,11 @@ def main():
     value = veh_steps / elapsed
     rd, wr = state_bytes(args.dtype)
     alg_bytes = E * N * (rd + wr)  # per fused simulate launch
+    kernel = "simulate_kernel (fused 15-frame Road.act+Road.step)"
+    if C["obs"]["type"] == "Kinematics" and not ix:  # the launch also writes the observation (ttrl_simulate_observe)
+        V, F = C["obs"]["vehicles_count"], len(C["obs"]["features"])
+        alg_bytes += E * (V * F * 4 + (V - 1) * 4)
+        kernel = "simulate_kernel (fused 15-frame Road.act+Road.step + Kinematics observation)"
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     pmc = read_pmc(args.dtype, args.config)
     out = {
@@ -305,9 +310,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
-                     "kernel": "simulate_kernel (fused 15-frame Road.act+Road.step)",
+                     "kernel": kernel,
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
-                     "alg_bytes_per_vehicle_step": (rd + wr) / 15.0},
+                     "alg_bytes_per_vehicle_step": alg_bytes / (E * N * 15.0)},
         "env_steps_per_s": world * E * args.steps / elapsed,
     }
     if pmc and pmc.get("valu_insts_per_wave") and pmc.get("sq_waves"):

@@ -278,6 +278,14 @@ int ttrl_road_step(const ttrl_state_t* s, const ttrl_lane_table_t* road,
 int ttrl_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road,
                   const ttrl_params_t* p, const int32_t* actions, int32_t frames,
                   double dt, void* stream);
+/* ttrl_simulate followed by ttrl_observe_kinematics of the final state, in the same launch (the
+ * observation is computed from the on-chip state after the last frame; AbstractEnv.step's
+ * _simulate + observation_type.observe, abstract.py:234-242).  Same outputs as the two calls;
+ * not for road networks with routes (TTRL_E_ARG). */
+int ttrl_simulate_observe(const ttrl_state_t* s, const ttrl_lane_table_t* road,
+                          const ttrl_params_t* p, const int32_t* actions, int32_t frames,
+                          double dt, const ttrl_kin_cfg_t* cfg, float* out, int32_t* ids,
+                          void* stream);
 /* Road.neighbour_vehicles(v, lane) for every vehicle; query_lane [E*N] int32
  * (-1 = the vehicle's own lane).  front/rear [E*N] int32 vehicle index or -1. */
 int ttrl_neighbours(const ttrl_state_t* s, const ttrl_lane_table_t* road,

@@ -268,3 +268,25 @@ def test_fused_ego_attention_shapes_and_biases(heads, F_, NE, A, B, hip_device):
     ref = net(x)
     got = net.fused_q(x)
     assert torch.allclose(got, ref, rtol=1e-4, atol=1e-5), float((got - ref).abs().max())
+
+
+@pytest.mark.parametrize("road,N,dtype,order", [("straight", 64, "f64", "sorted"), ("straight", 24, "f32", "sorted"),
+                                                ("straight", 100, "f64", "shuffled"), ("sine", 40, "f64", "sorted")])
+def test_fused_step_observation_equals_separate_observe(road, N, dtype, order, hip_device):
+    """env.step's observation written by the simulate launch itself (ttrl_simulate_observe) ==
+    ttrl_simulate followed by ttrl_observe_kinematics, bit for bit (rows and observed slot ids)."""
+    obs_cfg = dict(KIN15, order=order)
+    kw = dict(road=road, lanes_count=4 if road == "straight" else 3)
+    a, b = make(16, N, obs=obs_cfg, dtype=dtype, **kw), make(16, N, obs=obs_cfg, dtype=dtype, **kw)
+    a.reset(seed=21)
+    b.reset(seed=21)
+    rng = np.random.default_rng(4)
+    for _ in range(4):
+        act = torch.from_numpy(rng.integers(0, 5, size=16))
+        oa, *_ = a.step(act)
+        b._simulate(act)
+        ob = b.observation_type.observe()
+        assert torch.equal(oa, ob)
+        assert torch.equal(a.observation_type.observed_ids, b.observation_type.observed_ids)
+        assert torch.equal(a.state["x"], b.state["x"])
+        b._rewards_and_dones(1.0)

@@ -35,11 +35,15 @@ class BatchedDiscreteMetaAction:
         if self._lut is None or self._lut.device != dev:
             self._lut = torch.tensor([self._CODE[self.actions[i]] for i in range(len(self.actions))],
                                      dtype=torch.int32, device=dev)
+            # the default action set maps index i to code i: no lookup launch then
+            self._identity = bool(torch.equal(self._lut.cpu(), torch.arange(len(self.actions), dtype=torch.int32)))
         a = torch.as_tensor(actions)
         if a.device.type == "cpu":
             an = a.numpy()
             if an.size and (an.min() < 0 or an.max() >= len(self.actions)):
                 raise KeyError(f"action out of range [0, {len(self.actions)})")  # self.actions[int(a)] raises
+        if self._identity:
+            return a.to(device=dev, dtype=torch.int32).reshape(-1)
         return self._lut[a.to(dev).long().reshape(-1)]
 
     def act(self, actions) -> None:

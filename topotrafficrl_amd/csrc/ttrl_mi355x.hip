@@ -1409,6 +1409,13 @@ __device__ unsigned g_wphase[WTRACE_MAX][20];  // PHASE_TIMING: each wave's phas
 #define PH_FLUSH
 #endif
 
+template <typename T, int NS, int EPW, typename EgoFn>
+__device__ __forceinline__ void kin_observe(const ttrl_state_t& st, const LaneT<T>* lanes, const ttrl_params_t& P,
+                                            const ttrl_kin_cfg_t& cfg, bool env_ok, int env, T x, T y, T h, T v,
+                                            T hc, T hs, int lane, bool present, bool mdp, EgoFn ego_of, T* s_key,
+                                            int* s_cnt, int* s_ego, int (*s_perm)[64], float* __restrict__ out,
+                                            int32_t* __restrict__ ids);
+
 // Fused frame loop.  EPW envs per workgroup, NS slots per env, blockDim = EPW*NS.  The whole
 // vehicle state of the workgroup's envs is resident in LDS for the launch (HBM is read once
 // and written once); each phase loads the few fields it needs into registers, so no state is
@@ -1423,7 +1430,8 @@ __global__ void __launch_bounds__(NS* EPW, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES
                                                                : (NET == NET_STRAIGHT ? 4
                                                                   : (sizeof(T) == 8 || NET == NET_GRAPH ? 2 : 4)))
 simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int32_t* __restrict__ actions,
-                const uint8_t* __restrict__ env_mask, int frames, double dt_d, int mode, int ablate) {
+                const uint8_t* __restrict__ env_mask, int frames, double dt_d, int mode, int ablate, ttrl_kin_cfg_t kcfg,
+                float* __restrict__ obs_out, int32_t* __restrict__ obs_ids) {
   constexpr bool CV = NET != NET_STRAIGHT;  // curved lane classes possible
   constexpr bool GR = NET == NET_GRAPH;     // roads, routes, RegulatedRoad
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2235,6 +2243,25 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
     if (i == 0 && env_on) st.reg_steps[env] = reg;
   }
   PH(16);
+  if constexpr (!GR) {
+    if (obs_out) {  // ttrl_simulate_observe: the Kinematics observation of the final state, from LDS
+      // scratch over the act phase's (dead) block
+      constexpr int M = EPW * NS;
+      char* scr = (char*)V.afree;
+      T* s_key = (T*)scr;
+      int(*s_perm)[64] = (int(*)[64])(scr + ((sizeof(T) * M + 15) & ~(size_t)15));
+      int* s_cnt = (int*)(s_perm + EPW);
+      int* s_ego = s_cnt + EPW;
+      __syncthreads();
+      auto ego_of = [&](int ego, T& ex, T& ey, T& eh, T& ev, T& ec, T& es, int& elane) {
+        ex = V.x[eb + ego]; ey = V.y[eb + ego]; eh = V.h[eb + ego]; ev = V.v[eb + ego]; elane = V.lane[eb + ego];
+        ec = V.ch[eb + ego]; es = V.sh[eb + ego];
+      };
+      kin_observe<T, NS, EPW>(st, V.lanes, P, kcfg, env_on, env, V.x[me], V.y[me], V.h[me], V.v[me], V.ch[me],
+                              V.sh[me], (int)V.lane[me], present, present && kind == TTRL_MDP, ego_of, s_key, s_cnt,
+                              s_ego, s_perm, obs_out, obs_ids);
+    }
+  }
   PH_FLUSH
 }
 
@@ -2420,43 +2447,29 @@ __device__ __forceinline__ uint4 philox(uint4 c, uint2 key) {
 // normalised (lmap + clip), zero-padded.  The ego is the env's first MDP slot (AbstractEnv.vehicle).
 // Shuffled: rows 1..V-1 permuted by np_random.shuffle(obs[1:]) (:272-273) with the env's own
 // numpy Generator (order_shuffled 2, bit-exact) or by a Philox Fisher-Yates (1).
-// env_mask (optional): envs left untouched (rows and np_random) where it is 0.
-template <typename T, int NS, int EPW>
-__global__ void __launch_bounds__(NS* EPW)
-kinematics_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_kin_cfg_t cfg,
-                      const uint8_t* __restrict__ env_mask, float* __restrict__ out, int32_t* __restrict__ ids) {
-  __shared__ T s_key[EPW * NS];
-  __shared__ int s_cnt[EPW], s_ego[EPW];
-  __shared__ int s_perm[EPW][64];
-  __shared__ LaneT<T> s_lanes[LMAX];
+// Every thread of the workgroup calls it with its own vehicle's values (it synchronises the
+// workgroup) -- hc, hs: cos / sin of its heading, k_sincos as the simulate kernel keeps them --
+// and ego_of(ego, ex, ey, eh, ev, ec, es, elane) fetches the ego's.  The scratch arrays are
+// s_key[EPW * NS], s_cnt[EPW], s_ego[EPW], s_perm[EPW][64].  Used by kinematics_obs_kernel and,
+// fused after the last frame, by simulate_kernel (ttrl_simulate_observe).
+template <typename T, int NS, int EPW, typename EgoFn>
+__device__ __forceinline__ void kin_observe(const ttrl_state_t& st, const LaneT<T>* lanes, const ttrl_params_t& P,
+                                            const ttrl_kin_cfg_t& cfg, bool env_ok, int env, T x, T y, T h, T v,
+                                            T hc, T hs, int lane, bool present, bool mdp, EgoFn ego_of, T* s_key,
+                                            int* s_cnt, int* s_ego, int (*s_perm)[64], float* __restrict__ out,
+                                            int32_t* __restrict__ ids) {
   const int tid = threadIdx.x, le = tid / NS, i = tid % NS;
   const int N = st.n_veh;
-  const int env = blockIdx.x * EPW + le;
-  const bool env_ok = env < st.n_envs && (!env_mask || env_mask[env]);
   const bool slot = env_ok && i < N;
-  const size_t k = (size_t)env * N + i;
-  if (tid < R.n_lanes) s_lanes[tid] = make_lane<T>(R, tid);
   if (i == 0) { s_cnt[le] = 0; s_ego[le] = NS; }
-  T x = T(0), y = T(0), h = T(0), v = T(0);
-  int lane = 0;
-  bool present = false;
-  if (slot) {
-    x = ((const T*)st.x)[k]; y = ((const T*)st.y)[k]; h = ((const T*)st.heading)[k];
-    v = ((const T*)st.speed)[k]; lane = st.lane[k];
-    present = st.kind[k] != TTRL_ABSENT;
-  }
   __syncthreads();
-  if (slot && st.kind[k] == TTRL_MDP) atomicMin(&s_ego[le], i);
+  if (slot && mdp) atomicMin(&s_ego[le], i);
   __syncthreads();
   const int ego = s_ego[le];
   const bool has_ego = env_ok && ego < N;
-  T ex = T(0), ey = T(0), eh = T(0), ev = T(0);
+  T ex = T(0), ey = T(0), eh = T(0), ev = T(0), ec = T(1), es = T(0);
   int elane = 0;
-  if (has_ego) {
-    const size_t k0 = (size_t)env * N + ego;
-    ex = ((const T*)st.x)[k0]; ey = ((const T*)st.y)[k0]; eh = ((const T*)st.heading)[k0];
-    ev = ((const T*)st.speed)[k0]; elane = st.lane[k0];
-  }
+  if (has_ego) ego_of(ego, ex, ey, eh, ev, ec, es, elane);
   // candidate filter (road.py:427-433) and sort key |lane_distance_to| along the ego's lane
   bool cand = false;
   T key = K<T>::inf();
@@ -2464,8 +2477,8 @@ kinematics_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttr
     const T dx = x - ex, dy = y - ey;
     if (sqrt(dx * dx + dy * dy) < T(cfg.perception_distance)) {
       T s1, r1, s0, r0;
-      lane_local(s_lanes[elane], x, y, s1, r1);
-      lane_local(s_lanes[elane], ex, ey, s0, r0);
+      lane_local(lanes[elane], x, y, s1, r1);
+      lane_local(lanes[elane], ex, ey, s0, r0);
       const T ld = s1 - s0;
       if (cfg.see_behind || -T(2) * T(P.length) < ld) { cand = true; key = fabs(ld); }
     }
@@ -2516,14 +2529,12 @@ kinematics_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttr
   if (!env_ok) return;
   float* ob = out + (size_t)env * V * F;
   auto slot_of = [&](int q) { return shuf ? 1 + s_perm[le][q] : 1 + q; };
-  const T ec = t_cos(eh), es = t_sin(eh);
-  auto emit = [&](int row, T px, T py, T phd, T pv, int pl, bool rel) {
-    const T c = t_cos(phd), s = t_sin(phd);
+  auto emit = [&](int row, T px, T py, T phd, T pv, T c, T s, int pl, bool rel) {
     for (int cidx = 0; cidx < F; ++cidx) {
       const int f = cfg.features[cidx];
-      T val = feature(s_lanes[pl], f, px, py, phd, pv, c, s);
+      T val = feature(lanes[pl], f, px, py, phd, pv, c, s);
       if (rel && !cfg.absolute && (f == TTRL_F_X || f == TTRL_F_Y || f == TTRL_F_VX || f == TTRL_F_VY))
-        val -= feature(s_lanes[elane], f, ex, ey, eh, ev, ec, es);
+        val -= feature(lanes[elane], f, ex, ey, eh, ev, ec, es);
       if (cfg.normalize && cfg.has_range[f]) {
         val = lmap(val, T(cfg.range_lo[f]), T(cfg.range_hi[f]), T(-1), T(1));
         if (cfg.clip) val = clip(val, T(-1), T(1));
@@ -2532,11 +2543,11 @@ kinematics_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttr
     }
   };
   if (i == 0) {
-    if (has_ego) emit(0, ex, ey, eh, ev, elane, false);
+    if (has_ego) emit(0, ex, ey, eh, ev, ec, es, elane, false);
     else for (int cidx = 0; cidx < F; ++cidx) ob[cidx] = 0.f;  // no controlled vehicle: zeros
   }
   if (cand && rank < nc) {
-    emit(slot_of(rank), x, y, h, v, lane, true);
+    emit(slot_of(rank), x, y, h, v, hc, hs, lane, true);
     if (ids) ids[(size_t)env * (V - 1) + rank] = i;
   }
   for (int q = nc + i; q < V - 1; q += NS) {  // zero rows
@@ -2544,6 +2555,43 @@ kinematics_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttr
     for (int cidx = 0; cidx < F; ++cidx) ob[row * F + cidx] = 0.f;
     if (ids) ids[(size_t)env * (V - 1) + q] = -1;
   }
+}
+
+// env_mask (optional): envs left untouched (rows and np_random) where it is 0.
+template <typename T, int NS, int EPW>
+__global__ void __launch_bounds__(NS* EPW)
+kinematics_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_kin_cfg_t cfg,
+                      const uint8_t* __restrict__ env_mask, float* __restrict__ out, int32_t* __restrict__ ids) {
+  __shared__ T s_key[EPW * NS];
+  __shared__ int s_cnt[EPW], s_ego[EPW];
+  __shared__ int s_perm[EPW][64];
+  __shared__ LaneT<T> s_lanes[LMAX];
+  const int tid = threadIdx.x, le = tid / NS, i = tid % NS;
+  const int N = st.n_veh;
+  const int env = blockIdx.x * EPW + le;
+  const bool env_ok = env < st.n_envs && (!env_mask || env_mask[env]);
+  const bool slot = env_ok && i < N;
+  const size_t k = (size_t)env * N + i;
+  if (tid < R.n_lanes) s_lanes[tid] = make_lane<T>(R, tid);
+  T x = T(0), y = T(0), h = T(0), v = T(0);
+  int lane = 0;
+  bool present = false, mdp = false;
+  if (slot) {
+    x = ((const T*)st.x)[k]; y = ((const T*)st.y)[k]; h = ((const T*)st.heading)[k];
+    v = ((const T*)st.speed)[k]; lane = st.lane[k];
+    present = st.kind[k] != TTRL_ABSENT;
+    mdp = st.kind[k] == TTRL_MDP;
+  }
+  auto ego_of = [&](int ego, T& ex, T& ey, T& eh, T& ev, T& ec, T& es, int& elane) {
+    const size_t k0 = (size_t)env * N + ego;
+    ex = ((const T*)st.x)[k0]; ey = ((const T*)st.y)[k0]; eh = ((const T*)st.heading)[k0];
+    ev = ((const T*)st.speed)[k0]; elane = st.lane[k0];
+    const SinCos<T> sc = k_sincos(eh);
+    ec = sc.c; es = sc.s;
+  };
+  const SinCos<T> sc = k_sincos(h);
+  kin_observe<T, NS, EPW>(st, s_lanes, P, cfg, env_ok, env, x, y, h, v, sc.c, sc.s, lane, present, mdp, ego_of, s_key,
+                          s_cnt, s_ego, s_perm, out, ids);
 }
 
 // OccupancyGridObservation.observe (observation.py:353-434) + fill_road_layer_by_lanes
@@ -3406,9 +3454,17 @@ int slots_for(int n) { return n <= 32 ? 32 : n <= 64 ? 64 : n <= 128 ? 128 : 256
 
 int launch_status() { return hipGetLastError() == hipSuccess ? TTRL_OK : TTRL_E_LAUNCH; }
 
+// The Kinematics observation fused after the last frame (ttrl_simulate_observe); out == nullptr: none.
+struct SimObs {
+  ttrl_kin_cfg_t cfg;
+  float* out;
+  int32_t* ids;
+};
+
 template <typename T, int NS, int EPW>
 int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const int32_t* actions,
-               const uint8_t* mask, int frames, double dt, int mode, int ablate, hipStream_t stream) {
+               const uint8_t* mask, int frames, double dt, int mode, int ablate, hipStream_t stream,
+               const SimObs& ob) {
   const int blocks = (s.n_envs + EPW - 1) / EPW;
   if (blocks == 0) return TTRL_OK;
   const bool graph = is_graph(R);
@@ -3422,35 +3478,48 @@ int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_par
                                      !graph && !curved && sorted_view(NS, EPW, NET_STRAIGHT));
   if (graph)
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_GRAPH>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, P,
-                       actions, mask, frames, dt, mode, ablate);
+                       actions, mask, frames, dt, mode, ablate, ob.cfg, (float*)nullptr, (int32_t*)nullptr);
   else if (curved)
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_CURVED>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R,
-                       P, actions, mask, frames, dt, mode, ablate);
+                       P, actions, mask, frames, dt, mode, ablate, ob.cfg, ob.out, ob.ids);
   else
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_STRAIGHT>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R,
-                       P, actions, mask, frames, dt, mode, ablate);
+                       P, actions, mask, frames, dt, mode, ablate, ob.cfg, ob.out, ob.ids);
   return launch_status();
 }
 
 template <typename T>
 int dispatch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const int32_t* actions,
-                 const uint8_t* mask, int frames, double dt, int mode, int ablate, hipStream_t stream) {
+                 const uint8_t* mask, int frames, double dt, int mode, int ablate, hipStream_t stream,
+                 const SimObs& ob) {
   switch (slots_for(s.n_veh)) {
-    case 32: return launch_sim<T, 32, 2>(s, R, P, actions, mask, frames, dt, mode, ablate, stream);
-    case 64: return launch_sim<T, 64, 1>(s, R, P, actions, mask, frames, dt, mode, ablate, stream);
-    case 128: return launch_sim<T, 128, 1>(s, R, P, actions, mask, frames, dt, mode, ablate, stream);
-    default: return launch_sim<T, 256, 1>(s, R, P, actions, mask, frames, dt, mode, ablate, stream);
+    case 32: return launch_sim<T, 32, 2>(s, R, P, actions, mask, frames, dt, mode, ablate, stream, ob);
+    case 64: return launch_sim<T, 64, 1>(s, R, P, actions, mask, frames, dt, mode, ablate, stream, ob);
+    case 128: return launch_sim<T, 128, 1>(s, R, P, actions, mask, frames, dt, mode, ablate, stream, ob);
+    default: return launch_sim<T, 256, 1>(s, R, P, actions, mask, frames, dt, mode, ablate, stream, ob);
   }
 }
 
 int run_sim(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P, const int32_t* actions,
-            int frames, double dt, int mode, void* stream, int ablate = 0, const uint8_t* mask = nullptr) {
+            int frames, double dt, int mode, void* stream, int ablate = 0, const uint8_t* mask = nullptr,
+            const SimObs* ob = nullptr) {
   int rc = check_state(s, R);
   if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!P || frames < 0 || P->n_target_speeds < 1 || P->n_target_speeds > 8) return TTRL_E_ARG;
   hipStream_t st = (hipStream_t)stream;
-  return s->dtype == TTRL_F64 ? dispatch_sim<double>(*s, *R, *P, actions, mask, frames, dt, mode, ablate, st)
-                              : dispatch_sim<float>(*s, *R, *P, actions, mask, frames, dt, mode, ablate, st);
+  SimObs none{};
+  const SimObs& o = ob ? *ob : none;
+  return s->dtype == TTRL_F64 ? dispatch_sim<double>(*s, *R, *P, actions, mask, frames, dt, mode, ablate, st, o)
+                              : dispatch_sim<float>(*s, *R, *P, actions, mask, frames, dt, mode, ablate, st, o);
+}
+
+int check_kin_cfg(const ttrl_state_t* s, const ttrl_kin_cfg_t* cfg) {
+  if (!cfg || cfg->vehicles_count < 1 || cfg->n_features < 1 || cfg->n_features > TTRL_N_FEATURES) return TTRL_E_ARG;
+  if (cfg->order_shuffled < 0 || cfg->order_shuffled > 2) return TTRL_E_ARG;
+  if (cfg->order_shuffled == 2 && (!s->rng || cfg->vehicles_count - 1 > 64)) return TTRL_E_ARG;
+  for (int c = 0; c < cfg->n_features; ++c)
+    if (cfg->features[c] < 0 || cfg->features[c] >= TTRL_F_ON_ROAD) return TTRL_E_ARG;
+  return TTRL_OK;
 }
 
 template <typename T, int NS, int EPW>
@@ -3529,6 +3598,16 @@ int ttrl_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
   return run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream);
 }
 
+int ttrl_simulate_observe(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                          const int32_t* actions, int32_t frames, double dt, const ttrl_kin_cfg_t* cfg, float* out,
+                          int32_t* ids, void* stream) {
+  int rc = check_state(s, road);
+  if (rc) return rc < 0 ? rc : TTRL_OK;
+  if (!out || check_kin_cfg(s, cfg) || is_graph(*road)) return TTRL_E_ARG;
+  const SimObs ob{*cfg, out, ids};
+  return run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream, 0, nullptr, &ob);
+}
+
 /* Diagnostic only (not in include/): the fused loop with phases ablated, for profiling. */
 int ttrl_diag_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                        const int32_t* actions, int32_t frames, double dt, int32_t ablate, void* stream) {
@@ -3573,12 +3652,7 @@ int ttrl_observe_kinematics_masked(const ttrl_state_t* s, const ttrl_lane_table_
                                    void* stream) {
   int rc = check_state(s, road);
   if (rc) return rc < 0 ? rc : TTRL_OK;
-  if (!p || !cfg || !out || cfg->vehicles_count < 1 || cfg->n_features < 1 || cfg->n_features > TTRL_N_FEATURES)
-    return TTRL_E_ARG;
-  if (cfg->order_shuffled < 0 || cfg->order_shuffled > 2) return TTRL_E_ARG;
-  if (cfg->order_shuffled == 2 && (!s->rng || cfg->vehicles_count - 1 > 64)) return TTRL_E_ARG;
-  for (int c = 0; c < cfg->n_features; ++c)
-    if (cfg->features[c] < 0 || cfg->features[c] >= TTRL_F_ON_ROAD) return TTRL_E_ARG;
+  if (!p || !out || check_kin_cfg(s, cfg)) return TTRL_E_ARG;
   hipStream_t st = (hipStream_t)stream;
   return s->dtype == TTRL_F64 ? dispatch_kin<double>(*s, *road, *p, *cfg, mask, out, ids, st)
                               : dispatch_kin<float>(*s, *road, *p, *cfg, mask, out, ids, st);

@@ -18,7 +18,7 @@ import torch
 
 from . import _abi, _lib
 from .action import action_factory
-from .observation import observation_factory
+from .observation import BatchedKinematicObservation, observation_factory
 from .road import BatchedRoad, RoadNetwork
 from .state import BatchState
 
@@ -231,8 +231,9 @@ class VecHighwayEnv:
         """abstract.py:224-250: (obs, reward[E], terminated[E], truncated[E], info)."""
         if self.road is None:
             raise NotImplementedError("The road and vehicle must be initialized in the environment implementation")
-        self._simulate(action)
-        obs = self.observation_type.observe()
+        obs = self._simulate(action, observe=True)
+        if obs is None:
+            obs = self.observation_type.observe()
         # time += 1 / policy_frequency (abstract.py:239) runs in the rewards launch: nothing in
         # between reads it
         reward, terminated, truncated = self._rewards_and_dones(1 / self.config["policy_frequency"])
@@ -246,14 +247,20 @@ class VecHighwayEnv:
             obs = self.observation_type.observe()
         return obs, reward, terminated, truncated, info
 
-    def _simulate(self, action=None) -> None:
-        """abstract.py:252-282 as one fused launch: meta-action at frame 0, then frames x (act, step)."""
+    def _simulate(self, action=None, observe: bool = False):
+        """abstract.py:252-282 as one fused launch: meta-action at frame 0, then frames x (act, step).
+        With ``observe`` and a Kinematics observation, the same launch also writes the observation of
+        the final state (ttrl_simulate_observe) and returns it; otherwise returns None."""
         frames = int(self.config["simulation_frequency"] // self.config["policy_frequency"])
         codes = None
         if action is not None and not self.config["manual_control"]:
             codes = self.action_type._codes(action)
-        self.road.simulate(codes, frames, 1 / self.config["simulation_frequency"])
+        fused = None
+        if observe and isinstance(self.observation_type, BatchedKinematicObservation):
+            fused = self.observation_type.fused_outputs()
+        self.road.simulate(codes, frames, 1 / self.config["simulation_frequency"], observe=fused)
         self.steps += frames
+        return None if fused is None else fused[1]
 
     REWARD_TERMS = ["collision_reward", "high_speed_reward", "arrived_reward", "on_road_reward"]
 

@@ -134,6 +134,19 @@ class BatchedKinematicObservation(BatchedObservationType):
                                           mask=mask)
         return self._out
 
+    def fused_outputs(self):
+        """(cfg, out, ids) for an observation written by the simulate launch itself
+        (BatchedRoad.simulate(observe=...)); the same per-call bookkeeping as observe()."""
+        if self.order == "shuffled" and self.cfg.order_shuffled == 1:
+            self.cfg.shuffle_seed = int(self.env.shuffle_seed)
+            self.cfg.shuffle_offset = self._calls
+        self._calls += 1
+        st = self.env.road.state
+        V, F = self.cfg.vehicles_count, self.cfg.n_features
+        self._out = torch.empty((st.n_envs, V, F), dtype=torch.float32, device=st.device)
+        self._ids = torch.empty((st.n_envs, max(V - 1, 1)), dtype=torch.int32, device=st.device)
+        return self.cfg, self._out, self._ids
+
     @property
     def observed_ids(self) -> torch.Tensor:
         """Slot ids of rows 1.. of the last observation (sorted order), -1 for padding."""

@@ -101,12 +101,19 @@ class BatchedRoad:
         s, r, p = self._args()
         _lib.call("ttrl_meta_action", s, r, p, a.data_ptr(), _stream(self.state.device))
 
-    def simulate(self, actions: torch.Tensor | None, frames: int = 15, dt: float = 1 / 15) -> None:
-        """Fused AbstractEnv._simulate (abstract.py:252-282) for `frames` frames."""
+    def simulate(self, actions: torch.Tensor | None, frames: int = 15, dt: float = 1 / 15, observe=None) -> None:
+        """Fused AbstractEnv._simulate (abstract.py:252-282) for `frames` frames.  ``observe`` =
+        (KinCfg, out [E, V, F] float32, ids [E, V-1] int32): the Kinematics observation of the final
+        state is written in the same launch (ttrl_simulate_observe)."""
         a = None if actions is None else self._actions(actions)
         s, r, p = self._args()
-        _lib.call("ttrl_simulate", s, r, p, None if a is None else a.data_ptr(), int(frames), float(dt),
-                  _stream(self.state.device))
+        ap = None if a is None else a.data_ptr()
+        if observe is None:
+            _lib.call("ttrl_simulate", s, r, p, ap, int(frames), float(dt), _stream(self.state.device))
+        else:
+            cfg, out, ids = observe
+            _lib.call("ttrl_simulate_observe", s, r, p, ap, int(frames), float(dt), C.byref(cfg), out.data_ptr(),
+                      ids.data_ptr(), _stream(self.state.device))
 
     def neighbour_vehicles(self, query_lane: torch.Tensor | None = None):
         """Road.neighbour_vehicles (road.py:480-513) for every vehicle: (front, rear) slot ids, -1 = None."""
