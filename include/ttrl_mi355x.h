@@ -278,14 +278,17 @@ int ttrl_road_step(const ttrl_state_t* s, const ttrl_lane_table_t* road,
 int ttrl_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road,
                   const ttrl_params_t* p, const int32_t* actions, int32_t frames,
                   double dt, void* stream);
-/* ttrl_simulate followed by ttrl_observe_kinematics of the final state, in the same launch (the
- * observation is computed from the on-chip state after the last frame; AbstractEnv.step's
- * _simulate + observation_type.observe, abstract.py:234-242).  Same outputs as the two calls;
- * not for road networks with routes (TTRL_E_ARG). */
-int ttrl_simulate_observe(const ttrl_state_t* s, const ttrl_lane_table_t* road,
-                          const ttrl_params_t* p, const int32_t* actions, int32_t frames,
-                          double dt, const ttrl_kin_cfg_t* cfg, float* out, int32_t* ids,
-                          void* stream);
+/* AbstractEnv.step (abstract.py:224-250) in one launch: ttrl_simulate, then from the on-chip final
+ * state the Kinematics observation (ttrl_observe_kinematics; skipped when obs_cfg is NULL) and the
+ * step tail of ttrl_rewards_step (time += time_inc, reward, terminated, truncated, components, the
+ * info's ego speed / crashed; skipped when reward_cfg is NULL).  Same outputs as the separate
+ * calls; not for road networks with routes (TTRL_E_ARG). */
+int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                  const int32_t* actions, int32_t frames, double dt,
+                  const ttrl_kin_cfg_t* obs_cfg, float* obs, int32_t* obs_ids,
+                  const ttrl_reward_cfg_t* reward_cfg, double* time, double time_inc,
+                  float* reward, uint8_t* terminated, uint8_t* truncated, float* components,
+                  void* ego_speed, uint8_t* ego_crashed, void* stream);
 /* Road.neighbour_vehicles(v, lane) for every vehicle; query_lane [E*N] int32
  * (-1 = the vehicle's own lane).  front/rear [E*N] int32 vehicle index or -1. */
 int ttrl_neighbours(const ttrl_state_t* s, const ttrl_lane_table_t* road,

@@ -273,8 +273,9 @@ def test_fused_ego_attention_shapes_and_biases(heads, F_, NE, A, B, hip_device):
 @pytest.mark.parametrize("road,N,dtype,order", [("straight", 64, "f64", "sorted"), ("straight", 24, "f32", "sorted"),
                                                 ("straight", 100, "f64", "shuffled"), ("sine", 40, "f64", "sorted")])
 def test_fused_step_observation_equals_separate_observe(road, N, dtype, order, hip_device):
-    """env.step's observation written by the simulate launch itself (ttrl_simulate_observe) ==
-    ttrl_simulate followed by ttrl_observe_kinematics, bit for bit (rows and observed slot ids)."""
+    """env.step in one launch (ttrl_env_step: simulate, then the observation and the step tail from
+    the on-chip state) == ttrl_simulate, ttrl_observe_kinematics and ttrl_rewards_step, bit for bit
+    (rows, observed slot ids, rewards, dones, info, time)."""
     obs_cfg = dict(KIN15, order=order)
     kw = dict(road=road, lanes_count=4 if road == "straight" else 3)
     a, b = make(16, N, obs=obs_cfg, dtype=dtype, **kw), make(16, N, obs=obs_cfg, dtype=dtype, **kw)
@@ -283,10 +284,14 @@ def test_fused_step_observation_equals_separate_observe(road, N, dtype, order, h
     rng = np.random.default_rng(4)
     for _ in range(4):
         act = torch.from_numpy(rng.integers(0, 5, size=16))
-        oa, *_ = a.step(act)
+        oa, ra, ta, ua, ia = a.step(act)
         b._simulate(act)
         ob = b.observation_type.observe()
+        rb, tb, ub = b._rewards_and_dones(1.0)
+        ib = b._info(ob, act)
         assert torch.equal(oa, ob)
         assert torch.equal(a.observation_type.observed_ids, b.observation_type.observed_ids)
         assert torch.equal(a.state["x"], b.state["x"])
-        b._rewards_and_dones(1.0)
+        assert torch.equal(ra, rb) and torch.equal(ta, tb) and torch.equal(ua, ub)
+        assert torch.equal(ia["speed"], ib["speed"]) and torch.equal(ia["crashed"], ib["crashed"])
+        assert torch.equal(a._components, b._components) and torch.equal(a.time, b.time)

@@ -1416,6 +1416,23 @@ __device__ __forceinline__ void kin_observe(const ttrl_state_t& st, const LaneT<
                                             int* s_cnt, int* s_ego, int (*s_perm)[64], float* __restrict__ out,
                                             int32_t* __restrict__ ids);
 
+// What ttrl_env_step adds after the last frame (null pointers: nothing): the Kinematics observation
+// of the final state and the step tail of ttrl_rewards_step (time, reward, terminated, truncated,
+// reward components, the info's ego speed / crashed), both from the on-chip view.
+struct StepOut {
+  ttrl_kin_cfg_t kcfg;
+  float* obs;
+  int32_t* ids;
+  ttrl_reward_cfg_t rcfg;
+  double* time;
+  double time_inc;
+  float* reward;
+  uint8_t *term, *trunc;
+  float* comp;
+  void* ego_speed;
+  uint8_t* ego_crashed;
+};
+
 // Fused frame loop.  EPW envs per workgroup, NS slots per env, blockDim = EPW*NS.  The whole
 // vehicle state of the workgroup's envs is resident in LDS for the launch (HBM is read once
 // and written once); each phase loads the few fields it needs into registers, so no state is
@@ -1430,8 +1447,7 @@ __global__ void __launch_bounds__(NS* EPW, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES
                                                                : (NET == NET_STRAIGHT ? 4
                                                                   : (sizeof(T) == 8 || NET == NET_GRAPH ? 2 : 4)))
 simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int32_t* __restrict__ actions,
-                const uint8_t* __restrict__ env_mask, int frames, double dt_d, int mode, int ablate, ttrl_kin_cfg_t kcfg,
-                float* __restrict__ obs_out, int32_t* __restrict__ obs_ids) {
+                const uint8_t* __restrict__ env_mask, int frames, double dt_d, int mode, int ablate, StepOut so) {
   constexpr bool CV = NET != NET_STRAIGHT;  // curved lane classes possible
   constexpr bool GR = NET == NET_GRAPH;     // roads, routes, RegulatedRoad
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2244,22 +2260,36 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   }
   PH(16);
   if constexpr (!GR) {
-    if (obs_out) {  // ttrl_simulate_observe: the Kinematics observation of the final state, from LDS
-      // scratch over the act phase's (dead) block
-      constexpr int M = EPW * NS;
-      char* scr = (char*)V.afree;
-      T* s_key = (T*)scr;
-      int(*s_perm)[64] = (int(*)[64])(scr + ((sizeof(T) * M + 15) & ~(size_t)15));
-      int* s_cnt = (int*)(s_perm + EPW);
-      int* s_ego = s_cnt + EPW;
+    // ttrl_env_step's tail, from LDS; scratch over the act phase's (dead) block
+    constexpr int M = EPW * NS;
+    char* scr = (char*)V.afree;
+    T* s_key = (T*)scr;
+    int(*s_perm)[64] = (int(*)[64])(scr + ((sizeof(T) * M + 15) & ~(size_t)15));
+    int* s_cnt = (int*)(s_perm + EPW);
+    int* s_ego = s_cnt + EPW;
+    if (so.obs) {  // the Kinematics observation of the final state
       __syncthreads();
       auto ego_of = [&](int ego, T& ex, T& ey, T& eh, T& ev, T& ec, T& es, int& elane) {
         ex = V.x[eb + ego]; ey = V.y[eb + ego]; eh = V.h[eb + ego]; ev = V.v[eb + ego]; elane = V.lane[eb + ego];
         ec = V.ch[eb + ego]; es = V.sh[eb + ego];
       };
-      kin_observe<T, NS, EPW>(st, V.lanes, P, kcfg, env_on, env, V.x[me], V.y[me], V.h[me], V.v[me], V.ch[me],
+      kin_observe<T, NS, EPW>(st, V.lanes, P, so.kcfg, env_on, env, V.x[me], V.y[me], V.h[me], V.v[me], V.ch[me],
                               V.sh[me], (int)V.lane[me], present, present && kind == TTRL_MDP, ego_of, s_key, s_cnt,
-                              s_ego, s_perm, obs_out, obs_ids);
+                              s_ego, s_perm, so.obs, so.ids);
+    }
+    if (so.reward) {  // rewards_kernel's step tail (time += 1 / policy_frequency, rewards, dones, info)
+      __syncthreads();
+      if (i == 0) s_ego[le] = N;
+      __syncthreads();
+      if (present && kind == TTRL_MDP) atomicMin(&s_ego[le], i);
+      __syncthreads();
+      if (i == 0 && env_on) {
+        const int ego = s_ego[le];
+        step_tail<T>(R, V.lanes + (ego < N ? (int)V.lane[eb + ego] : 0), so.rcfg, env, ego < N, V.x[eb + ego % N], V.y[eb + ego % N], V.v[eb + ego % N],
+                     (int)V.lane[eb + ego % N], (V.flags[eb + ego % N] & FL_CRASHED) != 0, V.v[eb],
+                     (V.flags[eb] & FL_CRASHED) != 0, so.time, so.time_inc, so.reward, so.term, so.trunc, so.comp,
+                     (T*)so.ego_speed, so.ego_crashed);
+      }
     }
   }
   PH_FLUSH
@@ -2451,7 +2481,7 @@ __device__ __forceinline__ uint4 philox(uint4 c, uint2 key) {
 // workgroup) -- hc, hs: cos / sin of its heading, k_sincos as the simulate kernel keeps them --
 // and ego_of(ego, ex, ey, eh, ev, ec, es, elane) fetches the ego's.  The scratch arrays are
 // s_key[EPW * NS], s_cnt[EPW], s_ego[EPW], s_perm[EPW][64].  Used by kinematics_obs_kernel and,
-// fused after the last frame, by simulate_kernel (ttrl_simulate_observe).
+// fused after the last frame, by simulate_kernel (ttrl_env_step).
 template <typename T, int NS, int EPW, typename EgoFn>
 __device__ __forceinline__ void kin_observe(const ttrl_state_t& st, const LaneT<T>* lanes, const ttrl_params_t& P,
                                             const ttrl_kin_cfg_t& cfg, bool env_ok, int env, T x, T y, T h, T v,
@@ -3057,41 +3087,37 @@ __global__ void reset_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t
 
 // IntersectionEnv._agent_reward / _is_terminated / _is_truncated (intersection_env.py:78-119) and
 // has_arrived (:364-369) for the env's controlled vehicle (its first MDP slot).
+// IntersectionEnv._agent_reward / _is_terminated / _is_truncated (intersection_env.py:78-119) for one
+// env's ego (has_ego false: no controlled vehicle) and AbstractEnv.step's time += 1 / policy
+// frequency (abstract.py:239); ego_speed / ego_crashed: the info's speed / crashed (abstract.py:169-186),
+// of slot 0 when there is no ego.  rewards_kernel and simulate_kernel (ttrl_env_step) both call it.
 template <typename T>
-__global__ void rewards_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_reward_cfg_t cfg, double* __restrict__ time,
-                               double time_inc, float* __restrict__ reward, uint8_t* __restrict__ term,
-                               uint8_t* __restrict__ trunc, float* __restrict__ comp, T* __restrict__ ego_speed,
-                               uint8_t* __restrict__ ego_crashed) {
-  const int env = blockIdx.x * blockDim.x + threadIdx.x;
-  if (env >= st.n_envs) return;
-  const size_t b = (size_t)env * st.n_veh;
-  int ego = 0;
-  while (ego < st.n_veh && st.kind[b + ego] != TTRL_MDP) ++ego;
+__device__ __forceinline__ void step_tail(const ttrl_lane_table_t& R, const LaneT<T>* L, const ttrl_reward_cfg_t& cfg,
+                                          int env, bool has_ego, T x, T y, T v, int l, bool crashed, T v0,
+                                          bool crashed0, double* __restrict__ time, double time_inc,
+                                          float* __restrict__ reward, uint8_t* __restrict__ term,
+                                          uint8_t* __restrict__ trunc, float* __restrict__ comp,
+                                          T* __restrict__ ego_speed, uint8_t* __restrict__ ego_crashed) {
   double t = time[env];
-  if (time_inc != 0.0) {  // AbstractEnv.step's `self.time += 1 / policy_frequency` (abstract.py:239)
+  if (time_inc != 0.0) {
     t += time_inc;
     time[env] = t;
   }
-  if (ego_speed) {  // info speed / crashed (abstract.py:169-186) of the controlled vehicle, slot 0 if none
-    const size_t k0 = b + (ego == st.n_veh ? 0 : ego);
-    ego_speed[env] = ((const T*)st.speed)[k0];
-    ego_crashed[env] = st.crashed[k0] != 0;
+  if (ego_speed) {
+    ego_speed[env] = has_ego ? v : v0;
+    ego_crashed[env] = has_ego ? crashed : crashed0;
   }
   trunc[env] = (uint8_t)(t >= cfg.duration);
-  if (ego == st.n_veh) {
+  if (!has_ego) {
     reward[env] = 0.f; term[env] = 0;
     if (comp) for (int q = 0; q < 4; ++q) comp[(size_t)env * 4 + q] = 0.f;
     return;
   }
-  const size_t k = b + ego;
-  const T v = ((const T*)st.speed)[k], x = ((const T*)st.x)[k], y = ((const T*)st.y)[k];
-  const int l = st.lane[k];
   const T hs = clip(lmap(v, T(cfg.speed_lo), T(cfg.speed_hi), T(0), T(1)), T(0), T(1));
   T s, r;
-  lane_local(make_lane<T>(R, l), x, y, s, r);
+  lane_local(*L, x, y, s, r);  // L: the ego's lane l
   const bool onroad = fabs(r) <= T(R.width[l]) / T(2) + T(0) && -T(5) <= s && s < T(R.length[l]) + T(5);
   const bool arrived = R.exit_lane[l] && s >= T(cfg.exit_distance);
-  const bool crashed = st.crashed[k] != 0;
   T rw = T(cfg.collision_reward) * T(crashed ? 1 : 0) + T(cfg.high_speed_reward) * hs +
          T(cfg.arrived_reward) * T(arrived ? 1 : 0);
   if (arrived) rw = T(cfg.arrived_reward);
@@ -3103,6 +3129,26 @@ __global__ void rewards_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_reward
     float* c = comp + (size_t)env * 4;
     c[0] = crashed ? 1.f : 0.f; c[1] = (float)hs; c[2] = arrived ? 1.f : 0.f; c[3] = onroad ? 1.f : 0.f;
   }
+}
+
+template <typename T>
+__global__ void rewards_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_reward_cfg_t cfg, double* __restrict__ time,
+                               double time_inc, float* __restrict__ reward, uint8_t* __restrict__ term,
+                               uint8_t* __restrict__ trunc, float* __restrict__ comp, T* __restrict__ ego_speed,
+                               uint8_t* __restrict__ ego_crashed) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= st.n_envs) return;
+  const size_t b = (size_t)env * st.n_veh;
+  int ego = 0;
+  while (ego < st.n_veh && st.kind[b + ego] != TTRL_MDP) ++ego;
+  const bool has_ego = ego < st.n_veh;
+  const size_t k = b + (has_ego ? ego : 0);
+  const int l = st.lane[k];
+  LaneT<T> L{};
+  if (has_ego) L = make_lane<T>(R, l);
+  step_tail<T>(R, &L, cfg, env, has_ego, ((const T*)st.x)[k], ((const T*)st.y)[k],
+               ((const T*)st.speed)[k], l, st.crashed[k] != 0, ((const T*)st.speed)[b], st.crashed[b] != 0, time,
+               time_inc, reward, term, trunc, comp, ego_speed, ego_crashed);
 }
 
 // ------------------------------------------------------------ the intersection scenario
@@ -3454,17 +3500,10 @@ int slots_for(int n) { return n <= 32 ? 32 : n <= 64 ? 64 : n <= 128 ? 128 : 256
 
 int launch_status() { return hipGetLastError() == hipSuccess ? TTRL_OK : TTRL_E_LAUNCH; }
 
-// The Kinematics observation fused after the last frame (ttrl_simulate_observe); out == nullptr: none.
-struct SimObs {
-  ttrl_kin_cfg_t cfg;
-  float* out;
-  int32_t* ids;
-};
-
 template <typename T, int NS, int EPW>
 int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const int32_t* actions,
                const uint8_t* mask, int frames, double dt, int mode, int ablate, hipStream_t stream,
-               const SimObs& ob) {
+               const StepOut& ob) {
   const int blocks = (s.n_envs + EPW - 1) / EPW;
   if (blocks == 0) return TTRL_OK;
   const bool graph = is_graph(R);
@@ -3478,20 +3517,20 @@ int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_par
                                      !graph && !curved && sorted_view(NS, EPW, NET_STRAIGHT));
   if (graph)
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_GRAPH>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, P,
-                       actions, mask, frames, dt, mode, ablate, ob.cfg, (float*)nullptr, (int32_t*)nullptr);
+                       actions, mask, frames, dt, mode, ablate, StepOut{});
   else if (curved)
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_CURVED>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R,
-                       P, actions, mask, frames, dt, mode, ablate, ob.cfg, ob.out, ob.ids);
+                       P, actions, mask, frames, dt, mode, ablate, ob);
   else
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_STRAIGHT>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R,
-                       P, actions, mask, frames, dt, mode, ablate, ob.cfg, ob.out, ob.ids);
+                       P, actions, mask, frames, dt, mode, ablate, ob);
   return launch_status();
 }
 
 template <typename T>
 int dispatch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const int32_t* actions,
                  const uint8_t* mask, int frames, double dt, int mode, int ablate, hipStream_t stream,
-                 const SimObs& ob) {
+                 const StepOut& ob) {
   switch (slots_for(s.n_veh)) {
     case 32: return launch_sim<T, 32, 2>(s, R, P, actions, mask, frames, dt, mode, ablate, stream, ob);
     case 64: return launch_sim<T, 64, 1>(s, R, P, actions, mask, frames, dt, mode, ablate, stream, ob);
@@ -3502,13 +3541,13 @@ int dispatch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_p
 
 int run_sim(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P, const int32_t* actions,
             int frames, double dt, int mode, void* stream, int ablate = 0, const uint8_t* mask = nullptr,
-            const SimObs* ob = nullptr) {
+            const StepOut* ob = nullptr) {
   int rc = check_state(s, R);
   if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!P || frames < 0 || P->n_target_speeds < 1 || P->n_target_speeds > 8) return TTRL_E_ARG;
   hipStream_t st = (hipStream_t)stream;
-  SimObs none{};
-  const SimObs& o = ob ? *ob : none;
+  const StepOut none{};
+  const StepOut& o = ob ? *ob : none;
   return s->dtype == TTRL_F64 ? dispatch_sim<double>(*s, *R, *P, actions, mask, frames, dt, mode, ablate, st, o)
                               : dispatch_sim<float>(*s, *R, *P, actions, mask, frames, dt, mode, ablate, st, o);
 }
@@ -3598,14 +3637,23 @@ int ttrl_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
   return run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream);
 }
 
-int ttrl_simulate_observe(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
-                          const int32_t* actions, int32_t frames, double dt, const ttrl_kin_cfg_t* cfg, float* out,
-                          int32_t* ids, void* stream) {
+int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p, const int32_t* actions,
+                  int32_t frames, double dt, const ttrl_kin_cfg_t* obs_cfg, float* obs, int32_t* obs_ids,
+                  const ttrl_reward_cfg_t* reward_cfg, double* time, double time_inc, float* reward,
+                  uint8_t* terminated, uint8_t* truncated, float* components, void* ego_speed, uint8_t* ego_crashed,
+                  void* stream) {
   int rc = check_state(s, road);
   if (rc) return rc < 0 ? rc : TTRL_OK;
-  if (!out || check_kin_cfg(s, cfg) || is_graph(*road)) return TTRL_E_ARG;
-  const SimObs ob{*cfg, out, ids};
-  return run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream, 0, nullptr, &ob);
+  if (is_graph(*road) || (!obs_cfg) != (!obs) || (obs_cfg && check_kin_cfg(s, obs_cfg))) return TTRL_E_ARG;
+  if (reward_cfg && (!time || !reward || !terminated || !truncated || (!ego_speed) != (!ego_crashed)))
+    return TTRL_E_ARG;
+  StepOut so{};
+  if (obs_cfg) { so.kcfg = *obs_cfg; so.obs = obs; so.ids = obs_ids; }
+  if (reward_cfg) {
+    so.rcfg = *reward_cfg; so.time = time; so.time_inc = time_inc; so.reward = reward; so.term = terminated;
+    so.trunc = truncated; so.comp = components; so.ego_speed = ego_speed; so.ego_crashed = ego_crashed;
+  }
+  return run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream, 0, nullptr, &so);
 }
 
 /* Diagnostic only (not in include/): the fused loop with phases ablated, for profiling. */

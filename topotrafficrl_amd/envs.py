@@ -52,24 +52,30 @@ def reset_highway_seeded(state: BatchState, network: RoadNetwork, params: _abi.P
               torch.cuda.current_stream(state.device).cuda_stream)
 
 
-def rewards_and_dones(env, stream: int, time_inc: float = 0.0):
-    """The step tail in one launch (ttrl_rewards_step): env.time += time_inc, then reward [E] f32,
-    terminated / truncated [E] bool, the per-objective block env._components [E, 4] and the info's
-    ego speed / crashed (env._ego_speed, env._ego_crashed), all into fresh tensors.  The kernel
-    writes every element (bool storage is one byte), so nothing needs a clone / cast launch."""
+def _tail_outputs(env):
+    """Fresh step-tail outputs: reward [E] f32, terminated / truncated [E] bool, the per-objective
+    block [E, 4], the info's ego speed / crashed.  The kernels write every element (bool storage is
+    one byte), so nothing needs a clone / cast launch."""
     E, dev = env.num_envs, env.device
-    reward = torch.empty(E, dtype=torch.float32, device=dev)
-    term = torch.empty(E, dtype=torch.bool, device=dev)
-    trunc = torch.empty(E, dtype=torch.bool, device=dev)
-    comp = torch.empty((E, 4), dtype=torch.float32, device=dev)
-    speed = torch.empty(E, dtype=env.state["speed"].dtype, device=dev)
-    crashed = torch.empty(E, dtype=torch.bool, device=dev)
+    return (torch.empty(E, dtype=torch.float32, device=dev), torch.empty(E, dtype=torch.bool, device=dev),
+            torch.empty(E, dtype=torch.bool, device=dev), torch.empty((E, 4), dtype=torch.float32, device=dev),
+            torch.empty(E, dtype=env.state["speed"].dtype, device=dev), torch.empty(E, dtype=torch.bool, device=dev))
+
+
+def _keep_tail(env, outs):
+    env._reward, env._term, env._trunc, env._components, env._ego_speed, env._ego_crashed = outs
+    return outs[:3]
+
+
+def rewards_and_dones(env, stream: int, time_inc: float = 0.0):
+    """The step tail in one launch (ttrl_rewards_step): env.time += time_inc, then reward,
+    terminated, truncated, env._components and the info's ego speed / crashed (_tail_outputs)."""
+    outs = _tail_outputs(env)
+    reward, term, trunc, comp, speed, crashed = outs
     _lib.call("ttrl_rewards_step", C.byref(env.state.struct()), C.byref(env.network.table), C.byref(env.reward_cfg),
               env.time.data_ptr(), float(time_inc), reward.data_ptr(), term.data_ptr(), trunc.data_ptr(),
               comp.data_ptr(), speed.data_ptr(), crashed.data_ptr(), stream)
-    env._reward, env._term, env._trunc, env._components = reward, term, trunc, comp
-    env._ego_speed, env._ego_crashed = speed, crashed
-    return reward, term, trunc
+    return _keep_tail(env, outs)
 
 def _reward_terms(names, components: torch.Tensor) -> dict:
     """[E, 4] component block -> {name: [E] view} (float32; 0/1 for the boolean terms)."""
@@ -231,12 +237,11 @@ class VecHighwayEnv:
         """abstract.py:224-250: (obs, reward[E], terminated[E], truncated[E], info)."""
         if self.road is None:
             raise NotImplementedError("The road and vehicle must be initialized in the environment implementation")
-        obs = self._simulate(action, observe=True)
+        # one launch: _simulate, the Kinematics observation of the final state and the step tail
+        # (time += 1 / policy_frequency, abstract.py:239; rewards, dones, info), ttrl_env_step
+        obs, (reward, terminated, truncated) = self._simulate(action, tail=True)
         if obs is None:
             obs = self.observation_type.observe()
-        # time += 1 / policy_frequency (abstract.py:239) runs in the rewards launch: nothing in
-        # between reads it
-        reward, terminated, truncated = self._rewards_and_dones(1 / self.config["policy_frequency"])
         info = self._info(obs, action)
         if self.config["auto_reset"]:
             # finished envs restart on the device; obs is the new episode's first observation and
@@ -247,20 +252,26 @@ class VecHighwayEnv:
             obs = self.observation_type.observe()
         return obs, reward, terminated, truncated, info
 
-    def _simulate(self, action=None, observe: bool = False):
+    def _simulate(self, action=None, tail: bool = False):
         """abstract.py:252-282 as one fused launch: meta-action at frame 0, then frames x (act, step).
-        With ``observe`` and a Kinematics observation, the same launch also writes the observation of
-        the final state (ttrl_simulate_observe) and returns it; otherwise returns None."""
+        With ``tail`` the same launch also writes the step tail and, for a Kinematics observation, the
+        observation of the final state (ttrl_env_step); returns (obs or None, (reward, terminated,
+        truncated))."""
         frames = int(self.config["simulation_frequency"] // self.config["policy_frequency"])
         codes = None
         if action is not None and not self.config["manual_control"]:
             codes = self.action_type._codes(action)
-        fused = None
-        if observe and isinstance(self.observation_type, BatchedKinematicObservation):
-            fused = self.observation_type.fused_outputs()
-        self.road.simulate(codes, frames, 1 / self.config["simulation_frequency"], observe=fused)
+        fused = outs = None
+        if tail:
+            if isinstance(self.observation_type, BatchedKinematicObservation):
+                fused = self.observation_type.fused_outputs()
+            outs = _tail_outputs(self)
+            tail_args = (self.reward_cfg, self.time, 1 / self.config["policy_frequency"]) + outs
+        self.road.simulate(codes, frames, 1 / self.config["simulation_frequency"], observe=fused,
+                           tail=tail_args if tail else None)
         self.steps += frames
-        return None if fused is None else fused[1]
+        if tail:
+            return None if fused is None else fused[1], _keep_tail(self, outs)
 
     REWARD_TERMS = ["collision_reward", "high_speed_reward", "arrived_reward", "on_road_reward"]
 

@@ -101,19 +101,27 @@ class BatchedRoad:
         s, r, p = self._args()
         _lib.call("ttrl_meta_action", s, r, p, a.data_ptr(), _stream(self.state.device))
 
-    def simulate(self, actions: torch.Tensor | None, frames: int = 15, dt: float = 1 / 15, observe=None) -> None:
-        """Fused AbstractEnv._simulate (abstract.py:252-282) for `frames` frames.  ``observe`` =
-        (KinCfg, out [E, V, F] float32, ids [E, V-1] int32): the Kinematics observation of the final
-        state is written in the same launch (ttrl_simulate_observe)."""
+    def simulate(self, actions: torch.Tensor | None, frames: int = 15, dt: float = 1 / 15, observe=None,
+                 tail=None) -> None:
+        """Fused AbstractEnv._simulate (abstract.py:252-282) for `frames` frames.  With ``observe`` =
+        (KinCfg, out [E, V, F] float32, ids [E, V-1] int32) and / or ``tail`` = (RewardCfg, time [E] f64,
+        time_inc, reward, terminated, truncated, components, ego_speed, ego_crashed) the same launch
+        also writes the Kinematics observation and the step tail of the final state (ttrl_env_step)."""
         a = None if actions is None else self._actions(actions)
         s, r, p = self._args()
         ap = None if a is None else a.data_ptr()
-        if observe is None:
+        if observe is None and tail is None:
             _lib.call("ttrl_simulate", s, r, p, ap, int(frames), float(dt), _stream(self.state.device))
+            return
+        oc, oo, oi = (None, None, None) if observe is None else (C.byref(observe[0]), observe[1].data_ptr(),
+                                                                   observe[2].data_ptr())
+        if tail is None:
+            rc, tail_ptrs = None, [None, 0.0] + [None] * 7
         else:
-            cfg, out, ids = observe
-            _lib.call("ttrl_simulate_observe", s, r, p, ap, int(frames), float(dt), C.byref(cfg), out.data_ptr(),
-                      ids.data_ptr(), _stream(self.state.device))
+            rc = C.byref(tail[0])
+            tail_ptrs = [tail[1].data_ptr(), float(tail[2])] + [t.data_ptr() for t in tail[3:]]
+        _lib.call("ttrl_env_step", s, r, p, ap, int(frames), float(dt), oc, oo, oi, rc, *tail_ptrs,
+                  _stream(self.state.device))
 
     def neighbour_vehicles(self, query_lane: torch.Tensor | None = None):
         """Road.neighbour_vehicles (road.py:480-513) for every vehicle: (front, rear) slot ids, -1 = None."""
