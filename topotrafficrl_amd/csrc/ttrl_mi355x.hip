@@ -1413,8 +1413,8 @@ template <typename T, int NS, int EPW, typename EgoFn>
 __device__ __forceinline__ void kin_observe(const ttrl_state_t& st, const LaneT<T>* lanes, const ttrl_params_t& P,
                                             const ttrl_kin_cfg_t& cfg, bool env_ok, int env, T x, T y, T h, T v,
                                             T hc, T hs, int lane, bool present, bool mdp, EgoFn ego_of, T* s_key,
-                                            int* s_cnt, int* s_ego, int (*s_perm)[64], float* __restrict__ out,
-                                            int32_t* __restrict__ ids);
+                                            int* s_cnt, int* s_ego, int (*s_perm)[64], int (*s_p)[64],
+                                            float* __restrict__ out, int32_t* __restrict__ ids);
 
 // What ttrl_env_step adds after the last frame (null pointers: nothing): the Kinematics observation
 // of the final state and the step tail of ttrl_rewards_step (time, reward, terminated, truncated,
@@ -2265,7 +2265,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
     char* scr = (char*)V.afree;
     T* s_key = (T*)scr;
     int(*s_perm)[64] = (int(*)[64])(scr + ((sizeof(T) * M + 15) & ~(size_t)15));
-    int* s_cnt = (int*)(s_perm + EPW);
+    int(*s_p)[64] = s_perm + EPW;
+    int* s_cnt = (int*)(s_p + EPW);
     int* s_ego = s_cnt + EPW;
     if (so.obs) {  // the Kinematics observation of the final state
       __syncthreads();
@@ -2275,7 +2276,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       };
       kin_observe<T, NS, EPW>(st, V.lanes, P, so.kcfg, env_on, env, V.x[me], V.y[me], V.h[me], V.v[me], V.ch[me],
                               V.sh[me], (int)V.lane[me], present, present && kind == TTRL_MDP, ego_of, s_key, s_cnt,
-                              s_ego, s_perm, so.obs, so.ids);
+                              s_ego, s_perm, s_p, so.obs, so.ids);
     }
     if (so.reward) {  // rewards_kernel's step tail (time += 1 / policy_frequency, rewards, dones, info)
       __syncthreads();
@@ -2480,14 +2481,14 @@ __device__ __forceinline__ uint4 philox(uint4 c, uint2 key) {
 // Every thread of the workgroup calls it with its own vehicle's values (it synchronises the
 // workgroup) -- hc, hs: cos / sin of its heading, k_sincos as the simulate kernel keeps them --
 // and ego_of(ego, ex, ey, eh, ev, ec, es, elane) fetches the ego's.  The scratch arrays are
-// s_key[EPW * NS], s_cnt[EPW], s_ego[EPW], s_perm[EPW][64].  Used by kinematics_obs_kernel and,
+// s_key[EPW * NS], s_cnt[EPW], s_ego[EPW], s_perm[EPW][64], s_p[EPW][64].  Used by kinematics_obs_kernel and,
 // fused after the last frame, by simulate_kernel (ttrl_env_step).
 template <typename T, int NS, int EPW, typename EgoFn>
 __device__ __forceinline__ void kin_observe(const ttrl_state_t& st, const LaneT<T>* lanes, const ttrl_params_t& P,
                                             const ttrl_kin_cfg_t& cfg, bool env_ok, int env, T x, T y, T h, T v,
                                             T hc, T hs, int lane, bool present, bool mdp, EgoFn ego_of, T* s_key,
-                                            int* s_cnt, int* s_ego, int (*s_perm)[64], float* __restrict__ out,
-                                            int32_t* __restrict__ ids) {
+                                            int* s_cnt, int* s_ego, int (*s_perm)[64], int (*s_p)[64],
+                                            float* __restrict__ out, int32_t* __restrict__ ids) {
   const int tid = threadIdx.x, le = tid / NS, i = tid % NS;
   const int N = st.n_veh;
   const bool slot = env_ok && i < N;
@@ -2533,7 +2534,7 @@ __device__ __forceinline__ void kin_observe(const ttrl_state_t& st, const LaneT<
   const bool shuf = cfg.order_shuffled && V - 1 <= 64;
   if (shuf) {
     if (i == 0 && env_ok) {
-      int p[64];
+      int* p = s_p[le];  // in LDS: a private array would sit in scratch memory for every lane
       for (int t = 0; t < V - 1; ++t) p[t] = t;
       if (cfg.order_shuffled == 2) {  // Generator.shuffle: random_interval swaps, i = n-1 .. 1
         uint64_t* w = st.rng + (size_t)env * TTRL_RNG_WORDS;
@@ -2594,7 +2595,7 @@ kinematics_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttr
                       const uint8_t* __restrict__ env_mask, float* __restrict__ out, int32_t* __restrict__ ids) {
   __shared__ T s_key[EPW * NS];
   __shared__ int s_cnt[EPW], s_ego[EPW];
-  __shared__ int s_perm[EPW][64];
+  __shared__ int s_perm[EPW][64], s_p[EPW][64];
   __shared__ LaneT<T> s_lanes[LMAX];
   const int tid = threadIdx.x, le = tid / NS, i = tid % NS;
   const int N = st.n_veh;
@@ -2621,7 +2622,7 @@ kinematics_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttr
   };
   const SinCos<T> sc = k_sincos(h);
   kin_observe<T, NS, EPW>(st, s_lanes, P, cfg, env_ok, env, x, y, h, v, sc.c, sc.s, lane, present, mdp, ego_of, s_key,
-                          s_cnt, s_ego, s_perm, out, ids);
+                          s_cnt, s_ego, s_perm, s_p, out, ids);
 }
 
 // OccupancyGridObservation.observe (observation.py:353-434) + fill_road_layer_by_lanes
@@ -3515,6 +3516,13 @@ int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_par
   const size_t lds = host_view_bytes(sizeof(T) == 8 ? TTRL_F64 : TTRL_F32, EPW, NS,
                                      graph || curved ? R.n_lanes : STRAIGHT_LANE_CAP, graph,
                                      !graph && !curved && sorted_view(NS, EPW, NET_STRAIGHT));
+  if (ob.obs) {  // the observation's scratch must fit the act phase's block it overlays (it does for every NS)
+    const ViewLayout o = view_layout<T>(EPW, NS, graph || curved ? R.n_lanes : STRAIGHT_LANE_CAP, graph,
+                                        !graph && !curved && sorted_view(NS, EPW, NET_STRAIGHT));
+    const size_t M = (size_t)EPW * NS;
+    const size_t need = ((sizeof(T) * M + 15) & ~(size_t)15) + 2 * sizeof(int) * 64 * EPW + 2 * sizeof(int) * EPW;
+    if (o.afree + need > o.item + sizeof(short) * 2 * M) return TTRL_E_UNSUPPORTED;
+  }
   if (graph)
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_GRAPH>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, P,
                        actions, mask, frames, dt, mode, ablate, StepOut{});
