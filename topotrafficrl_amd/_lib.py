@@ -55,7 +55,8 @@ def load(path: str | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    # TTRL_LIB_PATH: an alternative build of the same library (A/B timing of kernel variants)
+    p = path or os.environ.get("TTRL_LIB_PATH") or LIB_PATH
     if not os.path.exists(p):
         raise ImportError(f"HIP library not built: {p} (run __graft_entry__.build())")
     lib = C.CDLL(p)

@@ -529,6 +529,7 @@ template <typename T> struct View {
   float* sxf;                    // [EPW*NS] xf at each sorted position (collision window walk)
   unsigned long long* lmask;     // [EPW][lanes] per lane: sorted positions of the vehicles on it
   int* stie;                     // [EPW] the order has ties in some lane's s (use the slot scans)
+  T *steer, *acc, *ix, *iy;      // [EPW*NS] the action and the pending impact (only the vehicle reads them)
 };
 constexpr int PRED_T = 11;       // np.arange(0.25, 3, 0.25) (regulation.py:86)
 
@@ -537,7 +538,7 @@ constexpr int N_REALS = 8;  // x, y, v, ch, sh, ts, h, delta
 struct ViewLayout {
   size_t lanes, reals[N_REALS], xf, key, afree, powb, pq_tx, pq_ty, pq_ij, bal, cnt, wcnt, nitem, pq_n, mypos, f0, r0, ft,
       mob, item, idx, kind, flags, lane, tgt, pred, rroad, rlane, rn, ynew, rt, onm, live, lperm, pd, pl, onb, sord,
-      spos, sxf, lmask, stie, total;
+      spos, sxf, lmask, stie, own, total;
 };
 
 template <typename T>
@@ -564,6 +565,10 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, 
   o.flags = take(M, 4);
   o.lane = take(M, 4);
   o.tgt = take(M, 4);
+  // The straight one-wave instance (4 waves per SIMD, 128 VGPRs) keeps each vehicle's action and
+  // pending impact here rather than in registers: its view leaves 2.4 KB per float64 env under
+  // the 10 KB budget, and as registers they were spilled to scratch (written back to HBM).
+  o.own = take(sorted ? sizeof(T) * 4 * M : 0, 16);
   // Frame-transient block: the per-lane candidate lists (written by the projection at the end of
   // a frame's step, read by the next frame's act), the act phase's neighbour / MOBIL scratch (read
   // from the start of a frame's act until its last barrier) and, over that scratch, the collision
@@ -671,6 +676,11 @@ __device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lane
     V.sxf = (float*)(smem + o.sxf);
     V.lmask = (unsigned long long*)(smem + o.lmask);
     V.stie = (int*)(smem + o.stie);
+    const size_t M = (size_t)EPW * NS;
+    V.steer = (T*)(smem + o.own);
+    V.acc = V.steer + M;
+    V.ix = V.acc + M;
+    V.iy = V.ix + M;
   }
   return V;
 }
@@ -1415,6 +1425,13 @@ __device__ __forceinline__ void kin_observe(const ttrl_state_t& st, const LaneT<
                                             T hc, T hs, int lane, bool present, bool mdp, EgoFn ego_of, T* s_key,
                                             int* s_cnt, int* s_ego, int (*s_perm)[64], int (*s_p)[64],
                                             float* __restrict__ out, int32_t* __restrict__ ids);
+template <typename T>
+__device__ __forceinline__ void step_tail(const ttrl_lane_table_t& R, const LaneT<T>* L, const ttrl_reward_cfg_t& cfg,
+                                          int env, bool has_ego, T x, T y, T v, int l, bool crashed, T v0,
+                                          bool crashed0, double* __restrict__ time, double time_inc,
+                                          float* __restrict__ reward, uint8_t* __restrict__ term,
+                                          uint8_t* __restrict__ trunc, float* __restrict__ comp,
+                                          T* __restrict__ ego_speed, uint8_t* __restrict__ ego_crashed);
 
 // What ttrl_env_step adds after the last frame (null pointers: nothing): the Kinematics observation
 // of the final state and the step tail of ttrl_rewards_step (time, reward, terminated, truncated,
@@ -1431,6 +1448,21 @@ struct StepOut {
   float* comp;
   void* ego_speed;
   uint8_t* ego_crashed;
+};
+
+// A per-vehicle value only its own thread reads: a register, or (L) its slot in an LDS view array.
+template <bool L, typename T> struct Own {
+  T r;
+  T* p;
+  __device__ __forceinline__ operator T() const {
+    if constexpr (L) return *p;
+    else return r;
+  }
+  __device__ __forceinline__ Own& operator=(T v) {
+    if constexpr (L) *p = v;
+    else r = v;
+    return *this;
+  }
 };
 
 // Fused frame loop.  EPW envs per workgroup, NS slots per env, blockDim = EPW*NS.  The whole
@@ -1493,7 +1525,10 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   bool present;
   // Vehicle state only this thread reads (IDM timer, the action, the pending impact) stays in
   // registers for the launch; what other vehicles read is staged in the LDS view.
-  T my_timer, my_steer, my_acc, my_ix, my_iy;
+  T my_timer;
+  // the action and the pending impact: LDS on the sorted (4 waves per SIMD) instance, see view_layout
+  Own<SO, T> my_steer{T(0), SO ? V.steer + me : nullptr}, my_acc{T(0), SO ? V.acc + me : nullptr},
+      my_ix{T(0), SO ? V.ix + me : nullptr}, my_iy{T(0), SO ? V.iy + me : nullptr};
   int my_sidx;
   int my_sorted = 0;  // SO: the slot at this lane's sorted position
   {  // HBM -> LDS, once per launch (coalesced SoA rows)
