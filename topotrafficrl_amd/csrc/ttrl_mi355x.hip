@@ -2677,19 +2677,20 @@ grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid
   float* s_val = (float*)(s_road + ((C + 31) / 32));  // [F][N] clipped feature values
   const size_t k0 = (size_t)env * N;
   __shared__ int s_ego;  // the observer: the env's first MDP slot (AbstractEnv.vehicle)
-  if (tid == 0) {
-    int e = 0;
-    while (e < N && st.kind[k0 + e] != TTRL_MDP) ++e;
-    s_ego = e;
-  }
+  if (tid == 0) s_ego = N;
   for (int c = tid; c < C; c += blockDim.x) s_win[c] = 0x7fffffff;
   for (int c = tid; c < (C + 31) / 32; c += blockDim.x) s_road[c] = 0u;
   __syncthreads();
-  if (s_ego >= N) {  // no controlled vehicle: an all-zero grid
-    for (int q = tid; q < F * C; q += blockDim.x) out[(size_t)env * F * C + q] = 0.f;
+  for (int j = tid; j < N; j += blockDim.x)
+    if (st.kind[k0 + j] == TTRL_MDP) atomicMin(&s_ego, j);
+  __syncthreads();
+  float* ob = out + (size_t)env * F * C;
+  const int ego = s_ego;
+  if (ego >= N) {  // no controlled vehicle: an all-zero grid
+    for (int q = tid; q < F * C; q += blockDim.x) __builtin_nontemporal_store(0.f, ob + q);
     return;
   }
-  const size_t ke = k0 + s_ego;
+  const size_t ke = k0 + ego;
   const T ex = ((const T*)st.x)[ke], ey = ((const T*)st.y)[ke], eh = ((const T*)st.heading)[ke];
   const T ev = ((const T*)st.speed)[ke];
   const int elane = st.lane[ke];
@@ -2697,33 +2698,40 @@ grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid
   for (int c = 0; c < F; ++c) has_road |= cfg.features[c] == TTRL_F_ON_ROAD;
   const T rx0 = T(cfg.range_lo[TTRL_F_X]), rx1 = T(cfg.range_hi[TTRL_F_X]);
   const T ry0 = T(cfg.range_lo[TTRL_F_Y]), ry1 = T(cfg.range_hi[TTRL_F_Y]);
-  for (int j = tid; j < N; j += blockDim.x) {
-    const size_t k = k0 + j;
-    if (st.kind[k] == TTRL_ABSENT) continue;
-    const T x = ((const T*)st.x)[k], y = ((const T*)st.y)[k], h = ((const T*)st.heading)[k];
-    const T v = ((const T*)st.speed)[k];
-    const int ln = st.lane[k];
-    const LaneT<T> L = make_lane<T>(R, ln), EL = make_lane<T>(R, elane);
-    const T c = t_cos(h), s = t_sin(h), ec = t_cos(eh), es = t_sin(eh);
-    T rx = x - ex, ry = y - ey;
-    for (int ci = 0; ci < F; ++ci) {
-      const int f = cfg.features[ci];
-      T val = feature(L, f, x, y, h, v, c, s);
-      if (f == TTRL_F_X || f == TTRL_F_Y || f == TTRL_F_VX || f == TTRL_F_VY)
-        val -= feature(EL, f, ex, ey, eh, ev, ec, es);
-      if (cfg.has_range[f]) val = lmap(val, T(cfg.range_lo[f]), T(cfg.range_hi[f]), T(-1), T(1));
-      if (cfg.clip) val = clip(val, T(-1), T(1));
-      s_val[ci * N + j] = (float)val;
+  if (tid < N) {  // one thread per vehicle (the ego's cos / sin once per thread, one sincos each)
+    const SinCos<T> esc = t_sincos(eh);
+    for (int j = tid; j < N; j += blockDim.x) {
+      const size_t k = k0 + j;
+      if (st.kind[k] == TTRL_ABSENT) continue;
+      const T x = ((const T*)st.x)[k], y = ((const T*)st.y)[k], h = ((const T*)st.heading)[k];
+      const T v = ((const T*)st.speed)[k];
+      const int ln = st.lane[k];
+      const LaneT<T> L = make_lane<T>(R, ln), EL = make_lane<T>(R, elane);
+      const SinCos<T> sc = t_sincos(h);
+      T rx = x - ex, ry = y - ey;
+      for (int ci = 0; ci < F; ++ci) {
+        const int f = cfg.features[ci];
+        T val = feature(L, f, x, y, h, v, sc.c, sc.s);
+        if (f == TTRL_F_X || f == TTRL_F_Y || f == TTRL_F_VX || f == TTRL_F_VY)
+          val -= feature(EL, f, ex, ey, eh, ev, esc.c, esc.s);
+        if (cfg.has_range[f]) val = lmap(val, T(cfg.range_lo[f]), T(cfg.range_hi[f]), T(-1), T(1));
+        if (cfg.clip) val = clip(val, T(-1), T(1));
+        s_val[ci * N + j] = (float)val;
+      }
+      if (cfg.has_range[TTRL_F_X]) rx = lmap(lmap(rx, rx0, rx1, T(-1), T(1)), T(-1), T(1), rx0, rx1);
+      if (cfg.has_range[TTRL_F_Y]) ry = lmap(lmap(ry, ry0, ry1, T(-1), T(1)), T(-1), T(1), ry0, ry1);
+      const T fx = floor((rx - T(cfg.grid_min_x)) / T(cfg.step_x));
+      const T fy = floor((ry - T(cfg.grid_min_y)) / T(cfg.step_y));
+      if (T(0) <= fx && fx < T(W) && T(0) <= fy && fy < T(H)) atomicMin(&s_win[(int)fx * H + (int)fy], j);
     }
-    if (cfg.has_range[TTRL_F_X]) rx = lmap(lmap(rx, rx0, rx1, T(-1), T(1)), T(-1), T(1), rx0, rx1);
-    if (cfg.has_range[TTRL_F_Y]) ry = lmap(lmap(ry, ry0, ry1, T(-1), T(1)), T(-1), T(1), ry0, ry1);
-    const T fx = floor((rx - T(cfg.grid_min_x)) / T(cfg.step_x));
-    const T fy = floor((ry - T(cfg.grid_min_y)) / T(cfg.step_y));
-    if (T(0) <= fx && fx < T(W) && T(0) <= fy && fy < T(H)) atomicMin(&s_win[(int)fx * H + (int)fy], j);
   }
-  if (has_road) {  // fill_road_layer_by_lanes observation.py:453-483
+  if (has_road) {  // fill_road_layer_by_lanes observation.py:453-483, (lane, waypoint) items over the block
     const T spacing = T(cfg.step_x) < T(cfg.step_y) ? T(cfg.step_x) : T(cfg.step_y);
     const T lpd = T(cfg.lane_perception_distance);
+    // items are handed out from the top of the block down, so the vehicle threads (the low ones)
+    // take the fewest of them
+    const int nt = (int)blockDim.x, rt = nt - 1 - tid;
+    long base = 0;
     for (int l = 0; l < R.n_lanes; ++l) {
       const LaneT<T> L = make_lane<T>(R, l);
       T origin, olat;
@@ -2731,7 +2739,8 @@ grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid
       const T start = origin - lpd, stop = origin + lpd;
       const long n = (long)ceil((stop - start) / spacing);
       const T d1 = (start + spacing) - start;
-      for (long q = tid; q < n; q += blockDim.x) {
+      long q = ((rt - base) % nt + nt) % nt;  // this thread's first waypoint of the lane
+      for (; q < n; q += nt) {
         T wp = q == 0 ? start : (q == 1 ? start + spacing : start + T(q) * d1);
         wp = clip(wp, T(0), T(R.length[l]));
         T px, py;
@@ -2744,10 +2753,11 @@ grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid
           atomicOr(&s_road[c >> 5], 1u << (c & 31));
         }
       }
+      base += n;
     }
   }
   __syncthreads();
-  float* ob = out + (size_t)env * F * C;
+  // the grid streams out once: 16-byte nontemporal stores (no reuse in L2)
   const bool vec4 = (C & 3) == 0;
   for (int ci = 0; ci < F; ++ci) {
     const bool road = cfg.features[ci] == TTRL_F_ON_ROAD;
@@ -2760,14 +2770,15 @@ grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid
           if (road) r[u] = ((s_road[c >> 5] >> (c & 31)) & 1u) ? 1.f : 0.f;
           else { const int w = s_win[c]; r[u] = w == 0x7fffffff ? 0.f : s_val[ci * N + w]; }
         }
-        *reinterpret_cast<float4*>(ob + (size_t)ci * C + c4 * 4) = make_float4(r[0], r[1], r[2], r[3]);
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store((f4){r[0], r[1], r[2], r[3]}, reinterpret_cast<f4*>(ob + (size_t)ci * C + c4 * 4));
       }
     } else {
       for (int c = tid; c < C; c += blockDim.x) {
         float r;
         if (road) r = ((s_road[c >> 5] >> (c & 31)) & 1u) ? 1.f : 0.f;
         else { const int w = s_win[c]; r = w == 0x7fffffff ? 0.f : s_val[ci * N + w]; }
-        ob[(size_t)ci * C + c] = r;
+        __builtin_nontemporal_store(r, ob + (size_t)ci * C + c);
       }
     }
   }
