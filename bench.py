@@ -260,6 +260,21 @@ def main():
         launches[-1].append((s, e))
 
     BatchedRoad.simulate = timed_sim
+    # config 3: the OccupancyGrid launch (the path's HBM-bound kernel) timed the same way
+    from topotrafficrl_amd.observation import BatchedOccupancyGridObservation
+    orig_grid = BatchedOccupancyGridObservation.observe
+    grid_launches = []
+
+    def timed_grid(self_obs):
+        st_ = torch.cuda.current_stream(dev)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(st_)
+        r = orig_grid(self_obs)
+        e.record(st_)
+        grid_launches.append((s, e))
+        return r
+
+    BatchedOccupancyGridObservation.observe = timed_grid
     t0 = time.perf_counter()
     for t in range(args.warmup, args.warmup + args.steps):
         launches.append([])
@@ -270,6 +285,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     BatchedRoad.simulate = orig_sim
+    BatchedOccupancyGridObservation.observe = orig_grid
 
     def span(recs):
         s0 = recs[0][0]
@@ -330,6 +346,18 @@ def main():
             active = pmc["valu_active_cycles_per_wave"] * waves
             out["valu"].update({"active_cycles_per_launch": active, "busy_frac": active / simd_cycles})
             out["roofline"]["limiter"] = "valu" if active / simd_cycles > out["roofline"]["frac"] else "hbm"
+    if grid_launches and C["obs"]["type"] == "OccupancyGrid":
+        # the grid kernel: algorithmic bytes = each vehicle's x, y, heading, speed, lane, kind read
+        # once + the [E, F, W, H] float32 grid written once
+        g_ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in grid_launches]))
+        r_ = 8 if args.dtype == "f64" else 4
+        cells = len(C["obs"]["features"]) * 32 * 32
+        g_bytes = E * (N * (4 * r_ + 4 + 1) + cells * 4)
+        g_ach = g_bytes / (g_ms * 1e-3) / 1e9
+        out["roofline_obs"] = {"bound": "hbm", "achieved": g_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": g_ach / HBM_PEAK_GBS, "traffic": (pmc or {}).get("grid_hbm_bytes_per_launch"),
+                               "kernel": "grid_obs_kernel (OccupancyGridObservation.observe)", "kernel_ms": g_ms,
+                               "alg_bytes_per_launch": g_bytes}
     if ix:
         out["config"]["live_vehicles_per_env"] = veh_steps / (world * E * 15 * args.steps)
         out["config"]["auto_reset"] = True

@@ -309,6 +309,26 @@ def test_ttc_and_lidar_vs_golden(path, dtype, hip_device):
             assert np.mean(np.abs(lid - d["lidar"][p]) > 1e-3) <= 0.05
 
 
+@pytest.mark.parametrize("n,pad", [(40, 48), (100, 128), (128, 128), (200, 256)])
+def test_grid_random_batch_vs_oracle(n, pad, hip_device):
+    """OccupancyGrid over a batch (slots padded, the block sized by the slot count,
+    one env without an ego): f64 bit-identical to the oracle."""
+    E = 37
+    lanes = _abi.straight_lane_table(4)
+    o = Oracle(lanes, P)
+    h = HostState(E, n)
+    o.reset_highway(h, _abi.reset_cfg(n, lanes), list(range(500, 500 + E)))
+    o.simulate(h, np.random.default_rng(n).integers(0, 5, E).astype(np.int32), 15, 1 / 15)
+    h["kind"][5, 0] = _abi.IDM  # env 5 has no controlled vehicle: an all-zero grid
+    dev = to_dev(h, hip_device, pad_to=pad)
+    net = RoadNetwork(lanes)
+    for cfg in (G7, GR):
+        got = occupancy_grid(dev, net, P, cfg).cpu().numpy()
+        want = o.observe_grid(h, cfg)
+        assert np.array_equal(got, want)
+        assert not got[5].any()
+
+
 def test_ttc_and_lidar_random_batch_vs_oracle(hip_device):
     """Many envs, padded slots, crashes: GPU == oracle (f64)."""
     E, n = 64, 48

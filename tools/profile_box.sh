@@ -19,3 +19,13 @@ for DT in f64 f32; do
     python3 bench.py --steps 5 --warmup 1 --dtype $DT --no-cpu-baseline > /dev/null 2> $OUT/grbm_$DT.err
 done
 echo profile done
+# config 3 (4096 x 128, OccupancyGrid 7x32x32): kernel stats + HBM traffic of the simulate and grid launches
+if [ "${CONFIG3:-1}" = "1" ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o trace_c3 -- \
+    python3 bench.py --config 3 --steps 20 --warmup 3 --no-cpu-baseline > $OUT/bench_trace_c3.json 2> $OUT/trace_c3.err
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT -o fetch_c3 -- \
+    python3 bench.py --config 3 --steps 5 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/fetch_c3.err
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT -o write_c3 -- \
+    python3 bench.py --config 3 --steps 5 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/write_c3.err
+fi
+echo profile c3 done

@@ -93,6 +93,32 @@ for dt in ("f64", "f32"):
            f"WAIT_INST_ANY/WAVE_CYCLES {wait_inst / max(wave_cyc, 1):.2f}, ACTIVE_INST_VALU/WAVE_CYCLES "
            f"{act_valu / max(wave_cyc, 1):.2f}",
            f"* effective clock (GRBM_GUI_ACTIVE/8/wall): {clk:.2f} GHz", ""]
+# config 3: the OccupancyGrid kernel (the path's HBM-bound launch) and the NS = 128 simulate launch
+c3 = os.path.join(SRC, "trace_c3_kernel_stats.csv")
+if os.path.exists(c3):
+    shutil.copy(c3, os.path.join(DST, f"{TAG}_kernel_stats_c3.csv"))
+    shutil.copy(os.path.join(SRC, "bench_trace_c3.json"), os.path.join(DST, f"{TAG}_bench_under_rocprof_c3.json"))
+    fetch, _ = counters(os.path.join(SRC, "fetch_c3_counter_collection.csv"))
+    write, _ = counters(os.path.join(SRC, "write_c3_counter_collection.csv"))
+    e = json.loads(open(os.path.join(SRC, "bench_trace_c3.json")).read().strip().splitlines()[-1])
+    stats = {short(r["Name"]): float(r["AverageNs"]) for r in csv.DictReader(open(c3))}
+    entry = {"note": "hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024; FETCH_SIZE doubled per the gfx950 calibration"}
+    md += ["## config 3 (4096 x 128, OccupancyGrid 7x32x32), f64", "", "| kernel | avg us | HBM MB per launch | algorithmic MB |",
+           "|---|---|---|---|"]
+    for tag, pat, alg in (("", SIM, e["roofline"]["alg_bytes_per_launch"]),
+                          ("grid_", "grid_obs_kernel", (e.get("roofline_obs") or {}).get("alg_bytes_per_launch"))):
+        ks = [k for (k, c) in fetch if pat in k]
+        if not ks:
+            continue
+        k = ks[0]
+        hbm = (2 * mean(fetch[(k, "FETCH_SIZE")]) + mean(write[(k, "WRITE_SIZE")])) * 1024
+        avg = [v for n, v in stats.items() if pat in n]
+        entry.update({tag + "kernel": k, tag + "hbm_bytes_per_launch": hbm, tag + "alg_bytes_per_launch": alg,
+                      tag + "kernel_ns_trace_avg": avg[0] if avg else None})
+        md.append(f"| `{k}` | {avg[0] / 1e3 if avg else float('nan'):.1f} | {hbm / 1e6:.1f} | "
+                  f"{(alg or float('nan')) / 1e6:.1f} |")
+    out_json["config3_f64"] = entry
+    md.append("")
 json.dump(out_json, open(os.path.join(DST, "pmc_traffic.json"), "w"), indent=1)
 open(os.path.join(DST, f"{TAG}_summary.md"), "w").write("\n".join(md) + "\n")
 print("\n".join(md))

@@ -2661,9 +2661,9 @@ kinematics_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttr
 }
 
 // OccupancyGridObservation.observe (observation.py:353-434) + fill_road_layer_by_lanes
-// (:453-483).  One workgroup per env; the grid is assembled in LDS as per-cell winner
-// vehicle indices (lowest list index wins = the reference's reverse-order overwrite) and
-// streamed to HBM with 16-byte stores.
+// (:453-483).  One workgroup per env, one thread per slot; the grid is assembled in LDS as
+// per-cell winner vehicle indices (lowest list index wins = the reference's reverse-order
+// overwrite) and streamed to HBM with 16-byte nontemporal stores.
 template <typename T>
 __global__ void __launch_bounds__(256)
 grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid_cfg_t cfg, float* __restrict__ out) {
@@ -2676,61 +2676,88 @@ grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid
   unsigned* s_road = (unsigned*)(s_win + C);       // [ceil(C/32)] on_road bitmap
   float* s_val = (float*)(s_road + ((C + 31) / 32));  // [F][N] clipped feature values
   const size_t k0 = (size_t)env * N;
-  __shared__ int s_ego;  // the observer: the env's first MDP slot (AbstractEnv.vehicle)
+  const int nt = (int)blockDim.x;
+  // the observer (AbstractEnv.vehicle: the env's first MDP slot) and its state, passed through LDS
+  __shared__ int s_ego;
+  __shared__ T s_e[6];  // x, y, heading, speed, cos, sin
+  __shared__ int s_elane;
   if (tid == 0) s_ego = N;
-  for (int c = tid; c < C; c += blockDim.x) s_win[c] = 0x7fffffff;
-  for (int c = tid; c < (C + 31) / 32; c += blockDim.x) s_road[c] = 0u;
+  for (int c = tid; c < C; c += nt) s_win[c] = 0x7fffffff;
+  for (int c = tid; c < (C + 31) / 32; c += nt) s_road[c] = 0u;
+  // this thread's vehicle (slot tid; the block is sized so that normally every slot has one)
+  // is loaded once, before the observer is known, so the block makes one HBM round trip
+  const bool mine = tid < N;
+  const size_t km = k0 + (mine ? tid : 0);
+  const int kd = mine ? (int)st.kind[km] : TTRL_ABSENT;
+  const T x = ((const T*)st.x)[km], y = ((const T*)st.y)[km], h = ((const T*)st.heading)[km];
+  const T v = ((const T*)st.speed)[km];
+  const int ln = st.lane[km];
+  const SinCos<T> sc = t_sincos(h);
   __syncthreads();
-  for (int j = tid; j < N; j += blockDim.x)
-    if (st.kind[k0 + j] == TTRL_MDP) atomicMin(&s_ego, j);
+  for (int j = tid; j < N; j += nt)
+    if ((j == tid ? kd : (int)st.kind[k0 + j]) == TTRL_MDP) atomicMin(&s_ego, j);
   __syncthreads();
   float* ob = out + (size_t)env * F * C;
   const int ego = s_ego;
   if (ego >= N) {  // no controlled vehicle: an all-zero grid
-    for (int q = tid; q < F * C; q += blockDim.x) __builtin_nontemporal_store(0.f, ob + q);
+    for (int q = tid; q < F * C; q += nt) __builtin_nontemporal_store(0.f, ob + q);
     return;
   }
-  const size_t ke = k0 + ego;
-  const T ex = ((const T*)st.x)[ke], ey = ((const T*)st.y)[ke], eh = ((const T*)st.heading)[ke];
-  const T ev = ((const T*)st.speed)[ke];
-  const int elane = st.lane[ke];
+  if (tid == ego % nt) {
+    if (ego == tid) {
+      s_e[0] = x; s_e[1] = y; s_e[2] = h; s_e[3] = v; s_e[4] = sc.c; s_e[5] = sc.s; s_elane = ln;
+    } else {
+      const size_t ke = k0 + ego;
+      const T eh = ((const T*)st.heading)[ke];
+      const SinCos<T> esc = t_sincos(eh);
+      s_e[0] = ((const T*)st.x)[ke]; s_e[1] = ((const T*)st.y)[ke]; s_e[2] = eh; s_e[3] = ((const T*)st.speed)[ke];
+      s_e[4] = esc.c; s_e[5] = esc.s; s_elane = st.lane[ke];
+    }
+  }
+  __syncthreads();
+  const T ex = s_e[0], ey = s_e[1], eh = s_e[2], ev = s_e[3], ec = s_e[4], es = s_e[5];
+  const int elane = s_elane;
   bool has_road = false;
   for (int c = 0; c < F; ++c) has_road |= cfg.features[c] == TTRL_F_ON_ROAD;
   const T rx0 = T(cfg.range_lo[TTRL_F_X]), rx1 = T(cfg.range_hi[TTRL_F_X]);
   const T ry0 = T(cfg.range_lo[TTRL_F_Y]), ry1 = T(cfg.range_hi[TTRL_F_Y]);
-  if (tid < N) {  // one thread per vehicle (the ego's cos / sin once per thread, one sincos each)
-    const SinCos<T> esc = t_sincos(eh);
-    for (int j = tid; j < N; j += blockDim.x) {
+  const LaneT<T> EL = make_lane<T>(R, elane);
+  for (int j = tid; j < N; j += nt) {
+    T vx = x, vy = y, vh = h, vv = v, vc = sc.c, vs = sc.s;
+    int vl = ln;
+    if (j != tid) {  // slots beyond the block (N > blockDim)
       const size_t k = k0 + j;
       if (st.kind[k] == TTRL_ABSENT) continue;
-      const T x = ((const T*)st.x)[k], y = ((const T*)st.y)[k], h = ((const T*)st.heading)[k];
-      const T v = ((const T*)st.speed)[k];
-      const int ln = st.lane[k];
-      const LaneT<T> L = make_lane<T>(R, ln), EL = make_lane<T>(R, elane);
-      const SinCos<T> sc = t_sincos(h);
-      T rx = x - ex, ry = y - ey;
-      for (int ci = 0; ci < F; ++ci) {
-        const int f = cfg.features[ci];
-        T val = feature(L, f, x, y, h, v, sc.c, sc.s);
-        if (f == TTRL_F_X || f == TTRL_F_Y || f == TTRL_F_VX || f == TTRL_F_VY)
-          val -= feature(EL, f, ex, ey, eh, ev, esc.c, esc.s);
-        if (cfg.has_range[f]) val = lmap(val, T(cfg.range_lo[f]), T(cfg.range_hi[f]), T(-1), T(1));
-        if (cfg.clip) val = clip(val, T(-1), T(1));
-        s_val[ci * N + j] = (float)val;
-      }
-      if (cfg.has_range[TTRL_F_X]) rx = lmap(lmap(rx, rx0, rx1, T(-1), T(1)), T(-1), T(1), rx0, rx1);
-      if (cfg.has_range[TTRL_F_Y]) ry = lmap(lmap(ry, ry0, ry1, T(-1), T(1)), T(-1), T(1), ry0, ry1);
-      const T fx = floor((rx - T(cfg.grid_min_x)) / T(cfg.step_x));
-      const T fy = floor((ry - T(cfg.grid_min_y)) / T(cfg.step_y));
-      if (T(0) <= fx && fx < T(W) && T(0) <= fy && fy < T(H)) atomicMin(&s_win[(int)fx * H + (int)fy], j);
+      vx = ((const T*)st.x)[k]; vy = ((const T*)st.y)[k]; vh = ((const T*)st.heading)[k]; vv = ((const T*)st.speed)[k];
+      vl = st.lane[k];
+      const SinCos<T> q = t_sincos(vh);
+      vc = q.c; vs = q.s;
+    } else if (kd == TTRL_ABSENT) {
+      continue;
     }
+    const LaneT<T> L = make_lane<T>(R, vl);
+    T rx = vx - ex, ry = vy - ey;
+    for (int ci = 0; ci < F; ++ci) {
+      const int f = cfg.features[ci];
+      T val = feature(L, f, vx, vy, vh, vv, vc, vs);
+      if (f == TTRL_F_X || f == TTRL_F_Y || f == TTRL_F_VX || f == TTRL_F_VY)
+        val -= feature(EL, f, ex, ey, eh, ev, ec, es);
+      if (cfg.has_range[f]) val = lmap(val, T(cfg.range_lo[f]), T(cfg.range_hi[f]), T(-1), T(1));
+      if (cfg.clip) val = clip(val, T(-1), T(1));
+      s_val[ci * N + j] = (float)val;
+    }
+    if (cfg.has_range[TTRL_F_X]) rx = lmap(lmap(rx, rx0, rx1, T(-1), T(1)), T(-1), T(1), rx0, rx1);
+    if (cfg.has_range[TTRL_F_Y]) ry = lmap(lmap(ry, ry0, ry1, T(-1), T(1)), T(-1), T(1), ry0, ry1);
+    const T fx = floor((rx - T(cfg.grid_min_x)) / T(cfg.step_x));
+    const T fy = floor((ry - T(cfg.grid_min_y)) / T(cfg.step_y));
+    if (T(0) <= fx && fx < T(W) && T(0) <= fy && fy < T(H)) atomicMin(&s_win[(int)fx * H + (int)fy], j);
   }
   if (has_road) {  // fill_road_layer_by_lanes observation.py:453-483, (lane, waypoint) items over the block
     const T spacing = T(cfg.step_x) < T(cfg.step_y) ? T(cfg.step_x) : T(cfg.step_y);
     const T lpd = T(cfg.lane_perception_distance);
     // items are handed out from the top of the block down, so the vehicle threads (the low ones)
     // take the fewest of them
-    const int nt = (int)blockDim.x, rt = nt - 1 - tid;
+    const int rt = nt - 1 - tid;
     long base = 0;
     for (int l = 0; l < R.n_lanes; ++l) {
       const LaneT<T> L = make_lane<T>(R, l);
@@ -3779,10 +3806,13 @@ int ttrl_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
   if (lds > 160 * 1024) return TTRL_E_UNSUPPORTED;
   if (s->n_envs == 0) return TTRL_OK;
   hipStream_t st = (hipStream_t)stream;
+  // one thread per slot (64 .. 256): smaller blocks for fewer vehicles keep more envs in flight
+  // (4096 x 128: 2 waves per env, all 4096 envs resident at once)
+  const int nt = s->n_veh <= 64 ? 64 : (s->n_veh <= 128 ? 128 : (s->n_veh <= 192 ? 192 : 256));
   if (s->dtype == TTRL_F64)
-    hipLaunchKernelGGL(grid_obs_kernel<double>, dim3(s->n_envs), dim3(256), lds, st, *s, *road, *p, *cfg, out);
+    hipLaunchKernelGGL(grid_obs_kernel<double>, dim3(s->n_envs), dim3(nt), lds, st, *s, *road, *p, *cfg, out);
   else
-    hipLaunchKernelGGL(grid_obs_kernel<float>, dim3(s->n_envs), dim3(256), lds, st, *s, *road, *p, *cfg, out);
+    hipLaunchKernelGGL(grid_obs_kernel<float>, dim3(s->n_envs), dim3(nt), lds, st, *s, *road, *p, *cfg, out);
   return launch_status();
 }
 
