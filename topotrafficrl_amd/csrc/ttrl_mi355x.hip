@@ -2784,24 +2784,31 @@ grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid
     }
   }
   __syncthreads();
-  // the grid streams out once: 16-byte nontemporal stores (no reuse in L2)
-  const bool vec4 = (C & 3) == 0;
-  for (int ci = 0; ci < F; ++ci) {
-    const bool road = cfg.features[ci] == TTRL_F_ON_ROAD;
-    if (vec4) {
-      for (int c4 = tid; c4 < C / 4; c4 += blockDim.x) {
-        float r[4];
+  // the grid streams out once: 16-byte nontemporal stores (no reuse in L2); each thread owns
+  // 4-cell groups and looks their winners up once for all feature layers
+  if ((C & 3) == 0) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    for (int c4 = tid; c4 < C / 4; c4 += nt) {
+      int w[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int c = c4 * 4 + u;
-          if (road) r[u] = ((s_road[c >> 5] >> (c & 31)) & 1u) ? 1.f : 0.f;
-          else { const int w = s_win[c]; r[u] = w == 0x7fffffff ? 0.f : s_val[ci * N + w]; }
+      for (int u = 0; u < 4; ++u) w[u] = s_win[c4 * 4 + u];
+      const unsigned rb = (s_road[c4 >> 3] >> ((c4 & 7) * 4)) & 0xfu;  // the 4 cells' on_road bits
+      for (int ci = 0; ci < F; ++ci) {
+        float r[4];
+        if (cfg.features[ci] == TTRL_F_ON_ROAD) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) r[u] = ((rb >> u) & 1u) ? 1.f : 0.f;
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) r[u] = w[u] == 0x7fffffff ? 0.f : s_val[ci * N + w[u]];
         }
-        typedef float f4 __attribute__((ext_vector_type(4)));
         __builtin_nontemporal_store((f4){r[0], r[1], r[2], r[3]}, reinterpret_cast<f4*>(ob + (size_t)ci * C + c4 * 4));
       }
-    } else {
-      for (int c = tid; c < C; c += blockDim.x) {
+    }
+  } else {
+    for (int ci = 0; ci < F; ++ci) {
+      const bool road = cfg.features[ci] == TTRL_F_ON_ROAD;
+      for (int c = tid; c < C; c += nt) {
         float r;
         if (road) r = ((s_road[c >> 5] >> (c & 31)) & 1u) ? 1.f : 0.f;
         else { const int w = s_win[c]; r = w == 0x7fffffff ? 0.f : s_val[ci * N + w]; }
