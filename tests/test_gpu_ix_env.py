@@ -213,10 +213,12 @@ def test_dqn_training_on_the_intersection(hip_device):
     assert len(L.memory) == 512 and L.steps == 8 and torch.isfinite(L.last_loss)
 
 
-def test_overlapped_resets_equal_in_place_resets(hip_device):
-    """overlap_resets (next-episode scenes prepared on a side stream, swapped in when an env
-    finishes) gives the same trajectories, bit for bit, as resetting in place."""
-    cfg = {**ENV_JSON, "num_envs": 48, "device": hip_device, "auto_reset": True, "duration": 3}
+@pytest.mark.parametrize("duration", [1, 3])
+def test_overlapped_resets_equal_in_place_resets(duration, hip_device):
+    """overlap_resets (each env's next two episodes prepared on a side stream, swapped in from
+    alternating spare slots when an env finishes) gives the same trajectories, bit for bit, as
+    resetting in place; duration 1 finishes every env at every step (both slots in turn)."""
+    cfg = {**ENV_JSON, "num_envs": 48, "device": hip_device, "auto_reset": True, "duration": duration}
     a = VecIntersectionEnv({**cfg, "overlap_resets": True})
     b = VecIntersectionEnv({**cfg, "overlap_resets": False})
     oa, _ = a.reset(seed=21)

@@ -313,13 +313,20 @@ class VecIntersectionEnv:
         self._trunc = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
         self._components = torch.zeros((self.num_envs, 4), dtype=torch.float32, device=self.device)
         self._entropy = None  # [E, words + 1]: seed words, then the auto-reset episode counter
-        self._spare = None    # next-episode scenes (overlap_resets), prepared on self._side
+        # overlap_resets: every env's next two episodes are prepared ahead of time on self._side, in
+        # two spare scenes per env (rows [0, E) and [E, 2E) of self._spare).  An env finishing
+        # takes its scene from slot _spare_par[e], which was prepared at least two steps earlier
+        # (the slots alternate), so the step waits only for the side-stream work launched two steps
+        # back (_spare_prev), while the last step's resets still run beside this step's launches.
+        self._spare = None
         if c["auto_reset"] and c["overlap_resets"]:
-            self._spare = BatchState(self.num_envs, int(c["vehicle_slots"]), device=self.device, dtype=c["dtype"])
+            E = self.num_envs
+            self._spare = BatchState(2 * E, int(c["vehicle_slots"]), device=self.device, dtype=c["dtype"])
+            self._spare_slot = (self._spare.rows(0, E), self._spare.rows(E, E))
+            self._spare_par = torch.zeros(E, dtype=torch.int32, device=self.device)
             self._side = torch.cuda.Stream(self.device)
-            self._spare_ready = torch.cuda.Event()
-            self._spare_mask = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
-            self._spare_entropy = None
+            self._spare_ready = self._spare_prev = torch.cuda.Event()
+            self._spare_entropy = None  # [2E, words + 1]: each spare scene's seed words and episode
         self.define_spaces()
 
     @property
@@ -363,23 +370,33 @@ class VecIntersectionEnv:
         self.steps = 0
         self.done = False
         ix_reset(self.state, self.network, self.params, self.ix, self._entropy[:, :-1])
-        if self._spare is not None:  # every env's second episode, in the background
-            self._spare_entropy = self._entropy.clone()
-            self._spare_entropy[:, -1] += 1
+        if self._spare is not None:  # every env's second and third episodes, in the background
+            self._spare_entropy = torch.cat([self._entropy, self._entropy])
+            self._spare_entropy[:self.num_envs, -1] += 1
+            self._spare_entropy[self.num_envs:, -1] += 2
+            self._spare_par.zero_()
             self._prepare_spares(None)
+            self._spare_prev = self._spare_ready
         obs = self.observation_type.observe()
         self._rewards_and_dones()  # abstract.py:211 reset's _info evaluates _rewards too
         return obs, self._info(obs, None)
 
     def _prepare_spares(self, mask: torch.Tensor | None) -> None:
-        """Reset the spare scenes of ``mask`` (all envs: None) to their next episode on the side
-        stream, after the main stream's work so far (the swap that consumed them)."""
+        """Reset the spare scenes of ``mask`` ([2E]; all: None) on the side stream, after the main
+        stream's work so far (the swap that consumed them).  The side stream reads snapshots of the
+        mask and the seed words, so the main stream may update both while it runs."""
         main = torch.cuda.current_stream(self.device)
+        ent = self._spare_entropy.clone()
+        m = None if mask is None else mask.clone()
         self._side.wait_stream(main)
         with torch.cuda.stream(self._side):
-            ix_reset(self._spare, self.network, self.params, self.ix, self._spare_entropy,
-                     None if mask is None else self._spare_mask)
-            self._spare_ready.record(self._side)
+            ix_reset(self._spare, self.network, self.params, self.ix, ent, m)
+            ev = torch.cuda.Event()
+            ev.record(self._side)
+        ent.record_stream(self._side)
+        if m is not None:
+            m.record_stream(self._side)
+        self._spare_prev, self._spare_ready = self._spare_ready, ev
 
     def step(self, action):
         """IntersectionEnv.step (intersection_env.py:135-139) over AbstractEnv.step (abstract.py:224-250)."""
@@ -433,11 +450,15 @@ class VecIntersectionEnv:
         if self._spare is None:
             ix_reset(self.state, self.network, self.params, self.ix, self._entropy, d)
         else:
-            torch.cuda.current_stream(self.device).wait_event(self._spare_ready)
-            copy_envs(self.state, self._spare, d)
-            self._spare_mask.copy_(d)
-            self._spare_entropy[:, -1] += d
-            self._prepare_spares(self._spare_mask)
+            torch.cuda.current_stream(self.device).wait_event(self._spare_prev)
+            m1 = d * self._spare_par
+            m0 = d - m1
+            copy_envs(self.state, self._spare_slot[0], m0)
+            copy_envs(self.state, self._spare_slot[1], m1)
+            mask = torch.cat([m0, m1])
+            self._spare_entropy[:, -1] += 2 * mask  # the taken slot's next scene: two episodes on
+            self._spare_par.bitwise_xor_(d)
+            self._prepare_spares(mask)
         self.time.masked_fill_(done, 0.0)
         self.observation_type.observe(mask=d, out=obs)
 
@@ -462,13 +483,15 @@ class VecIntersectionEnv:
         new.time = self.time.clone()
         if self._entropy is not None:
             new._entropy = self._entropy.clone()
-        if self._spare is not None:  # its own spare scenes, side stream and event
+        if self._spare is not None:  # its own spare scenes, side stream and events
             torch.cuda.current_stream(self.device).wait_event(self._spare_ready)
             new._spare = self._spare.clone()
+            new._spare_slot = (new._spare.rows(0, self.num_envs), new._spare.rows(self.num_envs, self.num_envs))
             new._spare_entropy = self._spare_entropy.clone()
-            new._spare_mask = self._spare_mask.clone()
+            new._spare_par = self._spare_par.clone()
             new._side = torch.cuda.Stream(self.device)
             new._spare_ready = torch.cuda.Event()
             new._spare_ready.record(torch.cuda.current_stream(self.device))
+            new._spare_prev = new._spare_ready
         new.define_spaces()
         return new

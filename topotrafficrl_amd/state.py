@@ -102,6 +102,14 @@ class BatchState:
         b._struct = None
         return b
 
+    def rows(self, start: int, n: int) -> "BatchState":
+        """A view of envs [start, start + n) sharing this state's storage."""
+        b = BatchState.__new__(BatchState)
+        b.n_envs, b.n_veh, b.device, b.dtype = int(n), self.n_veh, self.device, self.dtype
+        b.t = {k: v[start:start + n] for k, v in self.t.items()}
+        b._struct = None
+        return b
+
     def copy_(self, other: "BatchState") -> "BatchState":
         for k, v in self.t.items():
             v.copy_(other.t[k])
