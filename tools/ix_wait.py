@@ -28,8 +28,8 @@ def run(mode: str, steps: int = 60, warm: int = 10) -> float:
     if mode == "no_wait":
         def prepare(mask):
             main = torch.cuda.current_stream(dev)
-            ent = env._spare_entropy.clone()
-            m = None if mask is None else mask.clone()
+            ent = torch.cat([env._spare_words, env._spare_ep.unsqueeze(1)], 1)
+            m = mask
             env._side.wait_stream(main)
             ev = torch.cuda.Event()
             ev.record(env._side)  # before the work: the main stream does not wait for it

@@ -323,10 +323,11 @@ class VecIntersectionEnv:
             E = self.num_envs
             self._spare = BatchState(2 * E, int(c["vehicle_slots"]), device=self.device, dtype=c["dtype"])
             self._spare_slot = (self._spare.rows(0, E), self._spare.rows(E, E))
-            self._spare_par = torch.zeros(E, dtype=torch.int32, device=self.device)
+            self._spare_par = torch.zeros(E, dtype=torch.uint8, device=self.device)
             self._side = torch.cuda.Stream(self.device)
             self._spare_ready = self._spare_prev = torch.cuda.Event()
-            self._spare_entropy = None  # [2E, words + 1]: each spare scene's seed words and episode
+            self._spare_words = None  # [2E, words]: each spare scene's seed words ...
+            self._spare_ep = None     # [2E]: ... and episode counter
         self.define_spaces()
 
     @property
@@ -358,7 +359,7 @@ class VecIntersectionEnv:
         ``IntersectionEnv.reset(seed=seed + env_id_offset + e)``."""
         if self._spare is not None:
             # the side stream may still be resetting the spares (it writes _spare and reads
-            # _spare_entropy): join it before either buffer is replaced or freed below
+            # the spare counters): join it before either buffer is replaced or freed below
             torch.cuda.current_stream(self.device).wait_event(self._spare_ready)
         if options and "config" in options:
             self.configure(options["config"])
@@ -371,9 +372,8 @@ class VecIntersectionEnv:
         self.done = False
         ix_reset(self.state, self.network, self.params, self.ix, self._entropy[:, :-1])
         if self._spare is not None:  # every env's second and third episodes, in the background
-            self._spare_entropy = torch.cat([self._entropy, self._entropy])
-            self._spare_entropy[:self.num_envs, -1] += 1
-            self._spare_entropy[self.num_envs:, -1] += 2
+            self._spare_words = torch.cat([self._entropy[:, :-1], self._entropy[:, :-1]])
+            self._spare_ep = torch.cat([self._entropy[:, -1] + 1, self._entropy[:, -1] + 2])
             self._spare_par.zero_()
             self._prepare_spares(None)
             self._spare_prev = self._spare_ready
@@ -383,11 +383,12 @@ class VecIntersectionEnv:
 
     def _prepare_spares(self, mask: torch.Tensor | None) -> None:
         """Reset the spare scenes of ``mask`` ([2E]; all: None) on the side stream, after the main
-        stream's work so far (the swap that consumed them).  The side stream reads snapshots of the
-        mask and the seed words, so the main stream may update both while it runs."""
+        stream's work so far (the swap that consumed them).  The side stream reads its own copy of
+        the seed words and episode counters and a mask the main stream never writes again, so the
+        main stream may go on updating the counters while it runs."""
         main = torch.cuda.current_stream(self.device)
-        ent = self._spare_entropy.clone()
-        m = None if mask is None else mask.clone()
+        ent = torch.cat([self._spare_words, self._spare_ep.unsqueeze(1)], 1)
+        m = mask
         self._side.wait_stream(main)
         with torch.cuda.stream(self._side):
             ix_reset(self._spare, self.network, self.params, self.ix, ent, m)
@@ -445,18 +446,18 @@ class VecIntersectionEnv:
         their first observation is written into ``obs``; the others are untouched.  With
         overlap_resets the new scene is swapped in from the spare buffer (reset ahead of time,
         bit-identical) and the episode after it is prepared in the background."""
-        d = done.to(torch.int32)
+        d = done.view(torch.uint8)  # bool storage is one byte per env: the uint8 mask, no launch
         self._entropy[:, -1] += d
         if self._spare is None:
             ix_reset(self.state, self.network, self.params, self.ix, self._entropy, d)
         else:
             torch.cuda.current_stream(self.device).wait_event(self._spare_prev)
-            m1 = d * self._spare_par
-            m0 = d - m1
+            m1 = d & self._spare_par
+            m0 = d ^ m1
             copy_envs(self.state, self._spare_slot[0], m0)
             copy_envs(self.state, self._spare_slot[1], m1)
             mask = torch.cat([m0, m1])
-            self._spare_entropy[:, -1] += 2 * mask  # the taken slot's next scene: two episodes on
+            self._spare_ep.add_(mask, alpha=2)  # the taken slot's next scene: two episodes on
             self._spare_par.bitwise_xor_(d)
             self._prepare_spares(mask)
         self.time.masked_fill_(done, 0.0)
@@ -487,7 +488,8 @@ class VecIntersectionEnv:
             torch.cuda.current_stream(self.device).wait_event(self._spare_ready)
             new._spare = self._spare.clone()
             new._spare_slot = (new._spare.rows(0, self.num_envs), new._spare.rows(self.num_envs, self.num_envs))
-            new._spare_entropy = self._spare_entropy.clone()
+            new._spare_words = self._spare_words.clone()
+            new._spare_ep = self._spare_ep.clone()
             new._spare_par = self._spare_par.clone()
             new._side = torch.cuda.Stream(self.device)
             new._spare_ready = torch.cuda.Event()
