@@ -1,0 +1,124 @@
+"""Parity at the BASELINE.json sizes: every GPU configuration of SURVEY.md §8(d) stepped on the
+MI355X and through the float64 oracle (OpenMP over envs) from the same seeds and actions.
+
+* config 2: 4096 envs x 32 vehicles, Kinematics 15x7
+* config 3: 4096 envs x 128 vehicles, OccupancyGrid 7x32x32 (NS = 128: two waves per env)
+* config 4: 4096 envs x 64 vehicles, Kinematics 15x7 (the headline; 4 waves/SIMD, all resident)
+* config 5: 8192 envs x 64 vehicles, the fused EgoAttention-2h forward's greedy actions fed back
+
+float64 product path: discrete fields (lane, target_lane, crashed, has_impact, speed_index,
+observed slot ids, terminated / truncated) exact; continuous state within 1e-6·(1+|x|) after
+every policy step (the reference's own tolerance for fused multi-frame rollouts);
+Kinematics rows within 1e-6; the OccupancyGrid bit-identical.  The occupancy, packing and
+residency paths these configurations take (16 one-wave workgroups per CU at 64 vehicles, the
+two-wave NS = 128 instance, the two-env-per-wave NS = 32 instance) are only exercised here.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle.oracle import HostState, Oracle
+from topotrafficrl_amd import _abi
+from topotrafficrl_amd.envs import VecHighwayEnv
+
+pytestmark = pytest.mark.gpu
+
+KIN15 = {"type": "Kinematics", "vehicles_count": 15, "features": ["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"],
+         "features_range": {"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]},
+         "absolute": False, "order": "sorted"}
+GRID7 = {"type": "OccupancyGrid", "features": ["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"],
+         "features_range": {"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]},
+         "grid_size": [[-32, 32], [-32, 32]], "grid_step": [2, 2], "absolute": False}
+DISCRETE = ["lane", "target_lane", "speed_index", "kind", "crashed", "has_impact", "lane_change"]
+CONTINUOUS = ["x", "y", "heading", "speed", "target_speed", "timer", "delta", "steer", "acc"]
+
+
+def _compare_state(env, h, where):
+    got = env.state.to_numpy()
+    for f in DISCRETE:
+        bad = np.argwhere(got[f] != h[f])
+        assert len(bad) == 0, f"{where}: {f} differs at (env, slot) {bad[:5].tolist()} of {len(bad)}"
+    for f in CONTINUOUS:
+        d = np.abs(got[f] - h[f]) / (1 + np.abs(h[f]))
+        assert float(d.max()) <= 1e-6, f"{where}: {f} max rel diff {float(d.max()):.3g} at {np.unravel_index(d.argmax(), d.shape)}"
+    for f in ("impact_x", "impact_y"):  # meaningful only while has_impact is set
+        m = h["has_impact"] != 0
+        if m.any():
+            d = np.abs(got[f][m] - h[f][m]) / (1 + np.abs(h[f][m]))
+            assert float(d.max()) <= 1e-6, f"{where}: {f}"
+
+
+def _make(E, N, obs, seed):
+    env = VecHighwayEnv({"num_envs": E, "vehicles_count": N, "observation": obs, "device": "cuda:0", "dtype": "f64"})
+    obs0, _ = env.reset(seed=seed)
+    o = Oracle(env.network.table, env.params)
+    h = HostState(E, N)
+    o.reset_highway(h, env.reset_cfg, [seed + e for e in range(E)])
+    return env, obs0, o, h
+
+
+def _rollout(E, N, obs_cfg, seed, steps, actions_fn=None):
+    env, obs, o, h = _make(E, N, obs_cfg, seed)
+    _compare_state(env, h, "reset")
+    kin = _abi.kin_cfg(**{k: v for k, v in obs_cfg.items() if k != "type"}) if obs_cfg["type"] == "Kinematics" else None
+    grid = None if kin is not None else _abi.grid_cfg(**{k: v for k, v in obs_cfg.items() if k != "type"})
+    rng = np.random.default_rng(seed)
+    crashed = 0
+    for t in range(1, steps + 1):
+        a = rng.integers(0, 5, size=E) if actions_fn is None else actions_fn(obs, h, kin)
+        obs, rew, term, trunc, info = env.step(torch.from_numpy(np.asarray(a)).to(env.device))
+        o.simulate(h, np.asarray(a, dtype=np.int32), 15, 1 / 15)
+        _compare_state(env, h, f"step {t}")
+        if kin is not None:
+            ref, ids = o.observe_kinematics(h, kin)
+            assert np.max(np.abs(obs.cpu().numpy() - ref)) <= 1e-6, f"step {t}: Kinematics rows"
+            assert np.array_equal(env.observation_type.observed_ids.cpu().numpy(), ids), f"step {t}: observed ids"
+        else:
+            ref = o.observe_grid(h, grid)
+            got = obs.cpu().numpy()
+            bad = np.argwhere(got != ref)
+            assert len(bad) == 0, f"step {t}: grid differs in {len(bad)} cells, first {bad[:3].tolist()}"
+        r_ref, te_ref, tr_ref = o.rewards(h, env.reward_cfg, float(t))
+        assert np.allclose(rew.cpu().numpy(), r_ref, atol=1e-6)
+        assert np.array_equal(term.cpu().numpy(), te_ref) and np.array_equal(trunc.cpu().numpy(), tr_ref)
+        crashed = int((h["crashed"] != 0).sum())
+    return env, h, crashed
+
+
+@pytest.mark.parametrize("E,N,seed", [(4096, 32, 101), (4096, 64, 202)], ids=["config2_4096x32", "config4_4096x64"])
+def test_full_size_kinematics_vs_oracle(E, N, seed, hip_device):
+    env, h, crashed = _rollout(E, N, KIN15, seed, steps=3)
+    assert crashed > 0  # the batch is big enough to hold crashes, impacts and their SAT pairs
+    assert (h["lane"] != h["target_lane"]).any() or (h["lane"][:, 1:] != 0).any()
+
+
+def test_full_size_occupancy_grid_vs_oracle(hip_device):
+    """config 3: 4096 x 128, OccupancyGrid 7x32x32 of the two-wave NS = 128 instance."""
+    _rollout(4096, 128, GRID7, 303, steps=2)
+
+
+def test_full_size_policy_in_the_loop_vs_oracle(hip_device):
+    """config 5: 8192 x 64; the fused EgoAttention-2h forward picks each env's action from the GPU
+    observation (greedy); the oracle steps with the same actions, and the float32 torch forward
+    of the oracle's own observation picks the same action wherever its top-two Q margin is clear."""
+    from topotrafficrl_amd.agent import EgoAttentionPolicy
+    pol = EgoAttentionPolicy(hip_device, seed=0)
+    cpu_net = EgoAttentionPolicy("cpu", seed=0, fused=False).value_net
+    env, obs, o, h = _make(8192, 64, KIN15, 404)
+    kin = _abi.kin_cfg(**{k: v for k, v in KIN15.items() if k != "type"})
+    for t in range(1, 4):
+        q = pol.value_net.fused_q(obs)
+        a = q.argmax(1).cpu().numpy()
+        ref_obs, _ = o.observe_kinematics(h, kin)
+        with torch.no_grad():
+            q_ref = cpu_net(torch.from_numpy(ref_obs)).numpy()
+        srt = np.sort(q_ref, axis=1)
+        clear = (srt[:, -1] - srt[:, -2]) > 1e-4
+        assert (a[clear] == q_ref.argmax(1)[clear]).all(), f"step {t}: greedy actions"
+        assert np.allclose(q.cpu().numpy(), q_ref, rtol=1e-4, atol=1e-5)
+        obs, rew, term, trunc, info = env.step(torch.from_numpy(a).to(env.device))
+        o.simulate(h, a.astype(np.int32), 15, 1 / 15)
+        _compare_state(env, h, f"step {t}")
+        ref_obs, ids = o.observe_kinematics(h, kin)
+        assert np.max(np.abs(obs.cpu().numpy() - ref_obs)) <= 1e-6
+        assert np.array_equal(env.observation_type.observed_ids.cpu().numpy(), ids)

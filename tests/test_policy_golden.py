@@ -1,0 +1,148 @@
+"""Config 5 (policy in the loop) and the DQN update, pinned to fixtures from the reference's own
+code (oracle/gen_golden_policy.py runs ttrl_agent's EgoAttentionNetwork, DQNAgent,
+ReplayMemory and EpsilonGreedy):
+
+* EgoAttentionNetwork.forward      models.py:237-312, EgoAttention :157-194, attention :370-388
+* compute_bellman_residual / step_optimizer / update_target_network
+                                   deep_q_network/pytorch.py:32-73, abstract.py:95-100
+* ReplayMemory.collapse_n_steps    common/memory.py:63-82
+* EpsilonGreedy.update             exploration/epsilon_greedy.py:37-48
+
+Tolerances: the torch restatement on the CPU against the reference forward: rtol 1e-5,
+atol 1e-6 (same float32 operations, different summation order in the attention).  The fused
+HIP forward (ttrl_ego_attention_q): rtol 1e-4, atol 1e-5 on Q-values (float32, MFMA and
+online softmax).  DQN updates: loss / targets to 1e-5 relative; weights after each Adam step
+to 1e-6 absolute (one Adam step moves a weight by at most lr = 5e-4).
+"""
+import copy
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, load_golden
+from topotrafficrl_amd.agent import EGO_ATTENTION_2H, EgoAttentionNetwork, EgoAttentionPolicy
+from topotrafficrl_amd.dqn import DQNLearner, ReplayMemory
+
+POLICY = ["policy_2h_a5", "policy_2h_a3", "policy_1h_a3"]
+
+
+def _network(z, device="cpu"):
+    cfg = copy.deepcopy(EGO_ATTENTION_2H)
+    cfg["attention_layer"]["heads"] = int(z["heads"])
+    net = EgoAttentionNetwork(int(z["n_actions"]), cfg)
+    sd = {k[2:]: torch.from_numpy(v) for k, v in z.items() if k.startswith("w/")}
+    net.load_state_dict(sd, strict=True)
+    return net.to(device).eval()
+
+
+def _state_dict(z, prefix):
+    return {k[len(prefix):]: torch.from_numpy(v) for k, v in z.items() if k.startswith(prefix)}
+
+
+@pytest.mark.parametrize("name", POLICY)
+def test_torch_forward_matches_reference_network(name):
+    z = load_golden(os.path.join(GOLDEN, name + ".npz"))
+    net = _network(z)
+    assert sum(p.numel() for p in net.parameters()) == sum(v.size for k, v in z.items() if k.startswith("w/"))
+    with torch.no_grad():
+        for b in (1, 37, 1000):
+            x = torch.from_numpy(z["x"][:b])
+            q = net(x).numpy()
+            np.testing.assert_allclose(q, z[f"q_b{b}"], rtol=1e-5, atol=1e-6)
+            ego, others = x[:, 0:1], x[:, 1:]
+            mask = x[:, :, 0:1] < 0.5
+            _, att = net.attention_layer(net.ego_embedding(ego), net.others_embedding(others), mask)
+            np.testing.assert_allclose(att.numpy(), z[f"att_b{b}"], rtol=1e-5, atol=1e-6)
+
+
+def test_policy_fixtures_cover_masks():
+    z = load_golden(os.path.join(GOLDEN, "policy_2h_a5.npz"))
+    pres = z["x"][..., 0]
+    assert (pres.sum(1) == 0).sum() >= 10  # fully masked envs (uniform softmax over -1e9 scores)
+    assert ((pres[:, 0] == 1) & (pres[:, 1:].sum(1) < 14) & (pres[:, 1:].sum(1) > 0)).sum() >= 100
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", POLICY)
+def test_fused_hip_forward_matches_reference_network(name, hip_device):
+    z = load_golden(os.path.join(GOLDEN, name + ".npz"))
+    net = _network(z, hip_device)
+    for b in (1, 37, 1000):
+        x = torch.from_numpy(z["x"][:b]).to(hip_device)
+        q = net.fused_q(x).cpu().numpy()
+        np.testing.assert_allclose(q, z[f"q_b{b}"], rtol=1e-4, atol=1e-5)
+        with torch.no_grad():
+            qt = net(x).cpu().numpy()
+        np.testing.assert_allclose(qt, z[f"q_b{b}"], rtol=1e-4, atol=1e-5)
+        # greedy actions agree wherever the reference's top two Q-values are apart
+        ref = z[f"q_b{b}"]
+        srt = np.sort(ref, axis=1)
+        clear = (srt[:, -1] - srt[:, -2]) > 1e-4
+        assert (q.argmax(1)[clear] == ref.argmax(1)[clear]).all()
+
+
+def _learner(z, device):
+    net = EgoAttentionNetwork(5).to(device)
+    net.load_state_dict({k: v.to(device) for k, v in _state_dict(z, "w0/").items()}, strict=True)
+    cfg = {"double": bool(z["double"]), "gamma": float(z["gamma"]), "target_update": int(z["target_update"]),
+           "optimizer": {"type": "ADAM", "lr": float(z["lr"]), "weight_decay": 0, "k": 5}}
+    return DQNLearner(net, (15, 7), device, cfg)
+
+
+def _check_dqn(name, device):
+    z = load_golden(os.path.join(GOLDEN, name + ".npz"))
+    lrn = _learner(z, device)
+    for step in range(4):
+        p = f"s{step}/"
+        dev = lambda k, dt=None: torch.from_numpy(z[p + k]).to(device, dt)  # noqa: E731
+        batch = (dev("state"), dev("action"), dev("reward"), dev("next_state"), dev("terminal"))
+        loss, target = lrn.compute_bellman_residual(batch)
+        np.testing.assert_allclose(target.detach().cpu().numpy(), z[p + "target"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(float(loss.detach()), float(z[p + "loss"]), rtol=1e-5)
+        lrn.step_optimizer(loss)
+        lrn.update_target_network()
+        for k, v in lrn.value_net.state_dict().items():
+            np.testing.assert_allclose(v.cpu().numpy(), z[p + "w/" + k], rtol=0, atol=1e-6, err_msg=k)
+        for k, v in lrn.target_net.state_dict().items():
+            np.testing.assert_allclose(v.cpu().numpy(), z[p + "tw/" + k], rtol=0, atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("name", ["dqn_double", "dqn_plain"])
+def test_dqn_update_matches_reference_agent(name):
+    _check_dqn(name, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["dqn_double", "dqn_plain"])
+def test_dqn_update_matches_reference_agent_on_gpu(name, hip_device):
+    _check_dqn(name, hip_device)
+
+
+@pytest.mark.parametrize("n_steps", [1, 2, 3, 5])
+def test_n_step_collapse_matches_reference_memory(n_steps):
+    z = load_golden(os.path.join(GOLDEN, "dqn_memory.npz"))
+    p = f"n{n_steps}/"
+    T = len(z[p + "action"])
+    mem = ReplayMemory(64, (1,), "cpu", n_steps=n_steps, gamma=0.95)
+    st = torch.from_numpy(z[p + "state"].astype(np.float32))
+    for i in range(T):  # one env: one transition per push, like the reference's push loop
+        mem.push(st[i:i + 1, None], torch.tensor([int(z[p + "action"][i])]),
+                 torch.tensor([float(z[p + "reward"][i])], dtype=torch.float64), st[i + 1:i + 2, None],
+                 torch.tensor([bool(z[p + "done"][i])]))
+    s, a, r, s2, t = mem.gather(torch.arange(T))
+    np.testing.assert_array_equal(s[:, 0].numpy(), z[p + "c_state"])
+    np.testing.assert_array_equal(a.numpy(), z[p + "c_action"])
+    np.testing.assert_allclose(r.numpy(), z[p + "c_reward"], rtol=1e-6)
+    np.testing.assert_array_equal(s2[:, 0].numpy(), z[p + "c_next_state"])
+    np.testing.assert_array_equal(t.numpy(), z[p + "c_done"])
+
+
+def test_epsilon_greedy_schedule_matches_reference():
+    z = load_golden(os.path.join(GOLDEN, "dqn_memory.npz"))
+    pol = EgoAttentionPolicy("cpu", tau=float(z["eps/tau"]), temperature=float(z["eps/temperature"]),
+                             final_temperature=float(z["eps/final_temperature"]), fused=False)
+    for t, e, v, g in zip(z["eps/time"], z["eps/epsilon"], z["eps/values"], z["eps/greedy"]):
+        assert abs(pol.epsilon(int(t)) - e) <= 1e-15
+        assert int(torch.from_numpy(v).argmax()) == g

@@ -103,6 +103,11 @@ class ReplayMemory:
         if batch_size > self.size:
             raise ValueError("not enough transitions")
         pick = torch.randperm(self.size, device=self.device, generator=generator)[:batch_size]
+        return self.gather(pick)
+
+    def gather(self, pick: torch.Tensor):
+        """The n-step collapsed transitions starting at ages ``pick`` (0 = the oldest stored
+        transition): ``collapse_n_steps`` (memory.py:63-82) of ``memory[i:i + n_steps]``."""
         oldest = (self.position - self.size) % self.capacity
         idx = (oldest + pick) % self.capacity
         s, a = self.state[idx], self.action[idx]
