@@ -120,6 +120,7 @@ _SIGS = {
     "oracle_ix_reset": [C.c_void_p] * 5,
     "oracle_ix_clear_spawn": [C.c_void_p] * 5,
     "oracle_rng_ops": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p],
+    "oracle_frame_margins": [C.c_void_p] * 4 + [C.c_double, C.c_int32, C.c_void_p, C.c_void_p],
 }
 
 
@@ -158,6 +159,20 @@ class Oracle:
         a = None if actions is None else np.ascontiguousarray(actions, dtype=np.int32)
         self._ok(self.lib.oracle_simulate(C.byref(s), C.byref(self.lanes), C.byref(self.params),
                                           None if a is None else a.ctypes.data, frames, dt, None))
+
+    def frame_margins(self, h: HostState, actions=None, dt: float = 1 / 15, sites: bool = False,
+                      act: bool = True, step: bool = True):
+        """One frame (meta-action when ``actions`` is given, then Road.act and / or Road.step) applied
+        to ``h`` in place; returns [E, N] float64: each vehicle's smallest relative decision margin
+        (and, with ``sites``, the oracle source line of that decision, [E, N] int32)."""
+        s = h.struct()
+        a = None if actions is None else np.ascontiguousarray(actions, dtype=np.int32)
+        m = np.empty((h.E, h.N), dtype=np.float64)
+        line = np.zeros((h.E, h.N), dtype=np.int32)
+        self._ok(self.lib.oracle_frame_margins(C.byref(s), C.byref(self.lanes), C.byref(self.params),
+                                               None if a is None else a.ctypes.data, dt,
+                                               int(act) | 2 * int(step), m.ctypes.data, line.ctypes.data))
+        return (m, line) if sites else m
 
     def neighbours(self, h: HostState, query_lane=None):
         s = h.struct()

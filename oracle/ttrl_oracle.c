@@ -30,6 +30,8 @@ typedef struct {
   uint8_t* yield;
   int32_t* reg;
   uint64_t* rng;                /* [E][TTRL_RNG_WORDS] np_random */
+  double* mg;                   /* [E*N] decision margins (oracle_frame_margins), NULL otherwise */
+  int32_t* mgsite;              /* [E*N] source line of each vehicle's smallest margin */
 } S;
 
 static S view(const ttrl_state_t* s) {
@@ -42,8 +44,20 @@ static S view(const ttrl_state_t* s) {
   o.kind = s->kind; o.crashed = s->crashed; o.hasimp = s->has_impact; o.lc = s->lane_change;
   o.rroad = s->route_road; o.rlane = s->route_lane; o.rn = s->route_n; o.yield = s->yielding; o.reg = s->reg_steps;
   o.rng = s->rng;
+  o.mg = NULL; o.mgsite = NULL;
   return o;
 }
+
+/* Decision margins (oracle_frame_margins only): every comparison whose outcome is discrete
+ * (a threshold, an argmin, a tie-break) records |distance to the switch point| / (1 + |scale|)
+ * for the vehicle it decides for, keeping the minimum.  A float32 result may legitimately flip
+ * such a decision only where this float64 margin is below the float32 working precision. */
+static void mg_at(const S* o, int k, double m, double scale, int line) {
+  if (!o->mg) return;
+  double r = fabs(m) / (1.0 + fabs(scale));
+  if (r < o->mg[k]) { o->mg[k] = r; if (o->mgsite) o->mgsite[k] = line; }
+}
+#define mg(o, k, m, scale) mg_at(o, k, m, scale, __LINE__)
 
 static const double PI = 3.141592653589793;
 
@@ -305,9 +319,24 @@ static void neighbour(const S* o, const ttrl_lane_table_t* R, const ttrl_params_
   for (int j = 0; j < o->N; ++j) {
     if (j == self || o->kind[base + j] == TTRL_ABSENT) continue;
     double sv, lv; local(R, l, o->x[base + j], o->y[base + j], &sv, &lv);
+    if (o->mg) {                                                /* on_lane membership, s <= sv */
+      mg(o, base + self, fabs(lv) - (R->width[l] / 2 + 1.0), lv);
+      mg(o, base + self, sv + P->lane_vehicle_length, sv);
+      mg(o, base + self, R->length[l] + P->lane_vehicle_length - sv, sv);
+    }
     if (!on_lane(R, P, l, sv, lv, 1.0)) continue;
+    if (o->mg) mg(o, base + self, sv - s, s);
     if (s <= sv && (!hf || sv <= sf)) { sf = sv; hf = 1; *front = j; }
     if (sv < s && (!hr || sv > sr)) { sr = sv; hr = 1; *rear = j; }
+  }
+  if (o->mg && (hf || hr)) {                                    /* runner-up gaps of the two argmins */
+    for (int j = 0; j < o->N; ++j) {
+      if (j == self || j == *front || j == *rear || o->kind[base + j] == TTRL_ABSENT) continue;
+      double sv, lv; local(R, l, o->x[base + j], o->y[base + j], &sv, &lv);
+      if (!on_lane(R, P, l, sv, lv, 1.0)) continue;
+      if (hf && s <= sv) mg(o, base + self, sv - sf, sf);
+      if (hr && sv < s) mg(o, base + self, sr - sv, sr);
+    }
   }
 }
 
@@ -343,6 +372,7 @@ static int mobil(const S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P,
   int np_, nf; neighbour(o, R, P, base, self, l, &np_, &nf);
   double nfa = idm_acc(o, R, P, base, d, nf, np_);
   double nfpa = idm_acc(o, R, P, base, d, nf, self);
+  mg(o, base + self, nfpa + P->lane_change_max_braking, nfpa);
   if (nfpa < -P->lane_change_max_braking) return 0;
   int op, of; neighbour(o, R, P, base, self, o->lane[base + self], &op, &of);
   double spa = idm_acc(o, R, P, base, d, self, np_);
@@ -357,6 +387,7 @@ static int mobil(const S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P,
   double ofa = idm_acc(o, R, P, base, d, of, self);
   double ofpa = idm_acc(o, R, P, base, d, of, op);
   double jerk = spa - sa + P->politeness * (nfpa - nfa + ofpa - ofa);
+  mg(o, base + self, jerk - P->lane_change_min_acc_gain, fabs(spa) + fabs(sa));
   if (jerk < P->lane_change_min_acc_gain) return 0;
   return 1;
 }
@@ -371,17 +402,27 @@ static void change_lane_policy(S* o, const ttrl_lane_table_t* R, const ttrl_para
       if (o->lane[base + j] != tgt && o->tgt[base + j] == tgt) {
         double d = lane_distance(o, R, base, self, j);
         double ds = desired_gap(o, P, base, self, j);
+        mg(o, base + self, d, d);
+        mg(o, base + self, d - ds, d);
         if (0 < d && d < ds) { o->tgt[base + self] = lane; break; }
       }
     }
     return;
   }
+  mg(o, base + self, o->timer[base + self] - P->lane_change_delay, 0);
   if (!(P->lane_change_delay < o->timer[base + self])) return;   /* utils.do_every */
   o->timer[base + self] = 0;
   int cand[2], nc = 0;                                             /* RoadNetwork.side_lanes road.py:200-211 */
   if (R->lane_id[lane] > 0) cand[nc++] = lane - 1;
   if (R->lane_id[lane] < R->road_n[R->road[lane]] - 1) cand[nc++] = lane + 1;
   for (int k = 0; k < nc; ++k) {
+    if (o->mg) {
+      double s, r; local(R, cand[k], o->x[base + self], o->y[base + self], &s, &r);
+      mg(o, base + self, 2 * R->width[cand[k]] - fabs(r), r);
+      mg(o, base + self, s, s);
+      mg(o, base + self, R->length[cand[k]] + P->lane_vehicle_length - s, s);
+      mg(o, base + self, fabs(o->v[base + self]) - 1, 0);
+    }
     if (!reachable(R, P, cand[k], o->x[base + self], o->y[base + self])) continue;
     if (fabs(o->v[base + self]) < 1) continue;
     if (mobil(o, R, P, base, self, cand[k])) o->tgt[base + self] = cand[k];
@@ -448,6 +489,11 @@ static int speed_to_index(const ttrl_params_t* P, double v) {
 /* MDPVehicle.act controller.py:295-315 */
 static void mdp_act(S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base, int i, int action) {
   if (action == TTRL_FASTER || action == TTRL_SLOWER) {
+    if (o->mg) {                                               /* np.round half-way point */
+      const int n = P->n_target_speeds;
+      const double x = (o->v[base + i] - P->target_speeds[0]) / (P->target_speeds[n - 1] - P->target_speeds[0]) * (n - 1);
+      mg(o, base + i, x - floor(x) - 0.5, x);
+    }
     int si = speed_to_index(P, o->v[base + i]) + (action == TTRL_FASTER ? 1 : -1);
     if (si < 0) si = 0;
     if (si > P->n_target_speeds - 1) si = P->n_target_speeds - 1;
@@ -473,6 +519,18 @@ static void vehicle_step(S* o, const ttrl_lane_table_t* R, const ttrl_params_t* 
   o->h[k] += o->v[k] * sin(beta) / (P->length / 2) * dt;
   o->v[k] += o->acc[k] * dt;
   o->lane[k] = closest_lane(R, o->x[k], o->y[k], o->h[k]);
+  if (o->mg && R->n_lanes > 1) {                              /* argmin runner-up gap */
+    double d1 = INFINITY, d2 = INFINITY;
+    for (int l = 0; l < R->n_lanes; ++l) {
+      double s, r; local(R, l, o->x[k], o->y[k], &s, &r);
+      double ang = fabs(wrap_to_pi(o->h[k] - heading_at(R, l, s)));
+      double a = s - R->length[l]; if (!(a > 0)) a = 0;
+      double b = 0 - s; if (!(b > 0)) b = 0;
+      double d = fabs(r) + a + b + 1.0 * ang;
+      if (d < d1) { d2 = d1; d1 = d; } else if (d < d2) d2 = d;
+    }
+    mg(o, k, d2 - d1, d1);
+  }
 }
 
 /* RoadObject.polygon objects.py:168-180 (closed: 5 points) */
@@ -498,9 +556,10 @@ static double interval_distance(double mina, double maxa, double minb, double ma
 }
 /* utils.are_polygons_intersecting utils.py:194-239 */
 static void sat(double a[5][2], double b[5][2], double dax, double day, double dbx, double dby,
-                int* inter, int* will, double* tx, double* ty) {
+                int* inter, int* will, double* tx, double* ty, double* smg, int* smg_line) {
   int it = 1, wi = 1; double mind = INFINITY, axx = 0, axy = 0;
   double (*polys[2])[2] = {a, b};
+  double cand_d[8], cand_x[8], cand_y[8]; int nc = 0;            /* margins: every axis's |dist|, axis */
   for (int pi = 0; pi < 2; ++pi) {
     double (*pg)[2] = polys[pi];
     for (int e = 0; e < 4; ++e) {
@@ -510,37 +569,75 @@ static void sat(double a[5][2], double b[5][2], double dax, double day, double d
       double mina = 0, maxa = 0, minb = 0, maxb = 0;
       project(a, nx, ny, &mina, &maxa);
       project(b, nx, ny, &minb, &maxb);
+      const double scale = fabs(mina) + fabs(maxb);
+      if (smg) {  /* the separation test, and the branch of interval_distance where its two values differ */
+        double m0 = fabs(interval_distance(mina, maxa, minb, maxb)) / (1 + scale);
+        if (m0 < *smg) { *smg = m0; *smg_line = __LINE__; }
+        if (fabs((minb - maxa) - (mina - maxb)) > 1e-9 * (1 + scale)) {
+          double m1 = fabs(mina - minb) / (1 + scale);
+          if (m1 < *smg) { *smg = m1; *smg_line = __LINE__; }
+        }
+      }
       if (interval_distance(mina, maxa, minb, maxb) > 0) it = 0;
       double vp = nx * (dax - dbx) + ny * (day - dby);
       if (vp < 0) mina += vp; else maxa += vp;
       double dist = interval_distance(mina, maxa, minb, maxb);
+      if (smg) {
+        double m2 = fabs(dist) / (1 + scale);
+        if (m2 < *smg) { *smg = m2; *smg_line = __LINE__; }
+        if (fabs((minb - maxa) - (mina - maxb)) > 1e-9 * (1 + scale)) {
+          double m3 = fabs(mina - minb) / (1 + scale);
+          if (m3 < *smg) { *smg = m3; *smg_line = __LINE__; }
+        }
+      }
       if (dist > 0) wi = 0;
       if (!it && !wi) break;
+      double cax = (((a[0][0] + a[1][0]) + a[2][0]) + a[3][0]) / 4, cay = (((a[0][1] + a[1][1]) + a[2][1]) + a[3][1]) / 4;
+      double cbx = (((b[0][0] + b[1][0]) + b[2][0]) + b[3][0]) / 4, cby = (((b[0][1] + b[1][1]) + b[2][1]) + b[3][1]) / 4;
+      double dx = cax - cbx, dy = cay - cby;
+      const double sgnd = dx * nx + dy * ny;
+      if (smg) {
+        cand_d[nc] = fabs(dist); cand_x[nc] = sgnd > 0 ? nx : -nx; cand_y[nc] = sgnd > 0 ? ny : -ny; ++nc;
+        const double m4 = fabs(sgnd) / (1 + fabs(dx) + fabs(dy));  /* the translation's sign choice */
+        if (fabs(dist) > 1e-9 && m4 < *smg) { *smg = m4; *smg_line = __LINE__; }
+      }
       if (fabs(dist) < mind) {
         mind = fabs(dist);
-        double cax = (((a[0][0] + a[1][0]) + a[2][0]) + a[3][0]) / 4, cay = (((a[0][1] + a[1][1]) + a[2][1]) + a[3][1]) / 4;
-        double cbx = (((b[0][0] + b[1][0]) + b[2][0]) + b[3][0]) / 4, cby = (((b[0][1] + b[1][1]) + b[2][1]) + b[3][1]) / 4;
-        double dx = cax - cbx, dy = cay - cby;
-        if (dx * nx + dy * ny > 0) { axx = nx; axy = ny; } else { axx = -nx; axy = -ny; }
+        if (sgnd > 0) { axx = nx; axy = ny; } else { axx = -nx; axy = -ny; }
       }
     }
   }
   *inter = it; *will = wi;
   *tx = wi ? mind * axx : 0; *ty = wi ? mind * axy : 0;
+  if (smg && wi) {  /* the translation: argmin of |dist| over the axes whose translation differs */
+    for (int q = 0; q < nc; ++q) {
+      const double jump = fabs(cand_d[q] * cand_x[q] - mind * axx) + fabs(cand_d[q] * cand_y[q] - mind * axy);
+      if (jump <= 1e-9) continue;                                  /* the winner, or the same push */
+      const double m = (cand_d[q] - mind) / (1 + mind);
+      if (m < *smg) { *smg = m; *smg_line = __LINE__; }
+    }
+  }
 }
 
 /* RoadObject.handle_collisions objects.py:91-137 for a vehicle pair i<j */
 static void handle_collisions(S* o, const ttrl_params_t* P, int base, int i, int j, double dt) {
   int a = base + i, b = base + j;
   double dx = o->x[b] - o->x[a], dy = o->y[b] - o->y[a];
-  if (sqrt(dx * dx + dy * dy) > (P->diagonal + P->diagonal) / 2 + o->v[a] * dt) return;
+  const double thr = (P->diagonal + P->diagonal) / 2 + o->v[a] * dt;
+  if (o->mg) {
+    mg(o, a, sqrt(dx * dx + dy * dy) - thr, o->x[a]);
+    mg(o, b, sqrt(dx * dx + dy * dy) - thr, o->x[a]);
+  }
+  if (sqrt(dx * dx + dy * dy) > thr) return;
   double pa[5][2], pb[5][2];
   polygon(P, o->x[a], o->y[a], o->h[a], pa);
   polygon(P, o->x[b], o->y[b], o->h[b], pb);
   double ca = cos(o->h[a]), sa = sin(o->h[a]), cb = cos(o->h[b]), sb = sin(o->h[b]);
   double dax = o->v[a] * ca * dt, day = o->v[a] * sa * dt, dbx = o->v[b] * cb * dt, dby = o->v[b] * sb * dt;
   int inter, will; double tx, ty;
-  sat(pa, pb, dax, day, dbx, dby, &inter, &will, &tx, &ty);
+  double smg = INFINITY; int smg_line = 0;
+  sat(pa, pb, dax, day, dbx, dby, &inter, &will, &tx, &ty, o->mg ? &smg : NULL, &smg_line);
+  if (o->mg && smg < INFINITY) { mg_at(o, a, smg, 0, smg_line); mg_at(o, b, smg, 0, smg_line); }
   if (will) {
     o->ix[a] = tx / 2; o->iy[a] = ty / 2; o->hasimp[a] = 1;
     o->ix[b] = -tx / 2; o->iy[b] = -ty / 2; o->hasimp[b] = 1;
@@ -711,6 +808,30 @@ int oracle_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttr
     if (f == 0 && actions && (rc = oracle_meta_action(s, R, P, actions, stream))) return rc;
     if ((rc = oracle_road_act(s, R, P, stream))) return rc;
     if ((rc = oracle_road_step(s, R, P, dt, stream))) return rc;
+  }
+  return 0;
+}
+
+/* One frame (the meta-action first when `actions` is given, then Road.act if phases & 1 and
+ * Road.step(dt) if phases & 2) with every discrete decision's float64 margin recorded per vehicle
+ * into margin[E*N] (see mg()) and its source line into site[E*N]: the classifier of float32
+ * decision flips (SURVEY.md §8(d) parity tolerance). */
+int oracle_frame_margins(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                         const int32_t* actions, double dt, int32_t phases, double* margin, int32_t* site) {
+  if (check(s) || !margin) return TTRL_E_ARG;
+  S o = view(s);
+  for (int k = 0; k < o.E * o.N; ++k) { margin[k] = INFINITY; if (site) site[k] = 0; }
+  o.mg = margin; o.mgsite = site;
+  for (int e = 0; e < o.E; ++e)
+    if (actions && (actions[e] < 0 || actions[e] > 4)) return TTRL_E_ARG;
+#pragma omp parallel for schedule(static)
+  for (int e = 0; e < o.E; ++e) {
+    const int base = e * o.N;
+    if (actions)
+      for (int i = 0; i < o.N; ++i)
+        if (o.kind[base + i] == TTRL_MDP) { mdp_act(&o, R, P, base, i, actions[e]); break; }
+    if (phases & 1) act_env(&o, R, P, e);
+    if (phases & 2) step_env(&o, R, P, e, dt);
   }
   return 0;
 }

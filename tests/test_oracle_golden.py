@@ -58,6 +58,23 @@ def test_every_frame(name, cases):
 
 
 @pytest.mark.parametrize("name", [IDS(p) for p in golden_files()])
+def test_frame_margins_leave_the_frame_unchanged(name, cases):
+    """oracle_frame_margins (the float32 flip classifier) steps the frame exactly as Road.act +
+    Road.step do, and reports a finite margin for every vehicle that decides anything."""
+    d = cases[name]
+    o = Oracle(_abi.lane_table_from_arrays(d["lane_table"]), P)
+    tiny = 0
+    for f in range(d["x"].shape[0] - 1):
+        h = HostState.from_golden(d, f)
+        act = [int(d["actions"][f // 15])] if f % 15 == 0 else None
+        m = o.frame_margins(h, act)
+        check(h, HostState.from_golden(d, f + 1), 1e-12)
+        assert np.all(m >= 0) and np.all(np.isfinite(m))
+        tiny += int((m < 1e-5).sum())
+    assert tiny < 0.5 * m.size * (d["x"].shape[0] - 1)  # small margins are the exception (pile-ups: contacts)
+
+
+@pytest.mark.parametrize("name", [IDS(p) for p in golden_files()])
 def test_policy_step_rollout(name, cases):
     d = cases[name]
     o = Oracle(_abi.lane_table_from_arrays(d["lane_table"]), P)
