@@ -245,21 +245,25 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
-    # HIP events bracket every fused simulate launch on the stream it is enqueued on; a step's
-    # simulate time is the span from its first launch's start to its last one's end
+    # HIP events bracket every fused simulate launch (BatchedRoad.simulate, or the one-launch
+    # env.step BatchedRoad.env_step) on the stream it is enqueued on; a step's simulate time is the
+    # span from its first launch's start to its last one's end
     from topotrafficrl_amd.road import BatchedRoad
-    orig_sim = BatchedRoad.simulate
+    orig_sim, orig_env_step = BatchedRoad.simulate, BatchedRoad.env_step
     launches = []
 
-    def timed_sim(self_road, *a, **kw):
-        st_ = torch.cuda.current_stream(dev)
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record(st_)
-        orig_sim(self_road, *a, **kw)
-        e.record(st_)
-        launches[-1].append((s, e))
+    def timed(fn):
+        def wrapper(self_road, *a, **kw):
+            st_ = torch.cuda.current_stream(dev)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record(st_)
+            r = fn(self_road, *a, **kw)
+            e.record(st_)
+            launches[-1].append((s, e))
+            return r
+        return wrapper
 
-    BatchedRoad.simulate = timed_sim
+    BatchedRoad.simulate, BatchedRoad.env_step = timed(orig_sim), timed(orig_env_step)
     # config 3: the OccupancyGrid launch (the path's HBM-bound kernel) timed the same way
     from topotrafficrl_amd.observation import BatchedOccupancyGridObservation
     orig_grid = BatchedOccupancyGridObservation.observe
@@ -284,7 +288,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    BatchedRoad.simulate = orig_sim
+    BatchedRoad.simulate, BatchedRoad.env_step = orig_sim, orig_env_step
     BatchedOccupancyGridObservation.observe = orig_grid
 
     def span(recs):

@@ -1,7 +1,9 @@
-"""Loader of the in-tree HIP library (topotrafficrl_amd/lib/libttrl_mi355x.so).
+"""ctypes loader of the in-tree C ABI library (topotrafficrl_amd/lib/libttrl_mi355x.so).
 
-There is no fallback: if the library is missing or fails to load, every product
-entry point raises.  Build it with ``python -c "import __graft_entry__ as g; g.build()"``
+The product calls the library through the PyTorch operators of ops.py (lib/libttrl_torch.so,
+linked against it); this loader checks the ABI version and the exported symbols, and serves the
+ABI tests and the kernel-timing tools.  There is no fallback: if the library is missing or fails
+to load, every product entry point raises.  Build it with ``python -c "import __graft_entry__ as g; g.build()"``
 or ``python -m topotrafficrl_amd.build``.
 """
 from __future__ import annotations
@@ -55,8 +57,9 @@ def load(path: str | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    # TTRL_LIB_PATH: an alternative build of the same library (A/B timing of kernel variants)
-    p = path or os.environ.get("TTRL_LIB_PATH") or LIB_PATH
+    # `path`: an alternative build of the same library, for the A/B timing tools only (tools/);
+    # the product always runs lib/libttrl_mi355x.so, which the operator library links by rpath
+    p = path or LIB_PATH
     if not os.path.exists(p):
         raise ImportError(f"HIP library not built: {p} (run __graft_entry__.build())")
     lib = C.CDLL(p)

@@ -12,7 +12,6 @@ no host round trip between env.step and the next action.
 """
 from __future__ import annotations
 
-import ctypes as C
 import math
 
 import torch
@@ -127,20 +126,10 @@ class EgoAttentionNetwork(nn.Module):
 
     @torch.no_grad()
     def fused_q(self, x: torch.Tensor) -> torch.Tensor:
-        """Q-values through the fused HIP forward (ttrl_ego_attention_q): inference only."""
-        from . import _lib
-        x = x.contiguous().float()
-        B, NE, F_ = x.shape
-        A = self.output_layer.predict.out_features
-        w = self.packed_weights()
-        lib = _lib.load()
-        n_scratch = C.c_int64()
-        lib.ttrl_ego_attention_sizes(F_, A, B, NE, C.byref(n_scratch))
-        scratch = torch.empty(int(n_scratch.value), dtype=torch.float32, device=x.device)
-        q = torch.empty((B, A), dtype=torch.float32, device=x.device)
-        _lib.call("ttrl_ego_attention_q", x.data_ptr(), B, NE, F_, self.attention_layer.h, w.data_ptr(), A,
-                  scratch.data_ptr(), q.data_ptr(), torch.cuda.current_stream(x.device).cuda_stream)
-        return q
+        """Q-values through the fused HIP forward (torch.ops.ttrl.ego_attention_q): inference only."""
+        from . import ops
+        return ops.T.ego_attention_q(x.float(), self.packed_weights(), self.attention_layer.h,
+                                     self.output_layer.predict.out_features)
 
     def forward(self, x):
         # contiguous copies: hipBLASLt takes a 6x slower path on the strided [:, 1:, :] view

@@ -3076,47 +3076,33 @@ struct SeedSeq {
   }
 };
 
+// RoadNetwork.get_closest_lane_index (road.py:55-71) in float64 over every lane, first minimum.
+__device__ inline int closest_lane_index(const ttrl_lane_table_t& R, double x, double y, double h) {
+  int best = 0; double bd = 0;
+  for (int l = 0; l < R.n_lanes; ++l) {
+    const LaneT<double> L = make_lane<double>(R, l);
+    double s, r;
+    lane_local(L, x, y, s, r);
+    const double ang = fabs(wrap_to_pi(h - heading_at(L, s)));
+    double a = s - R.length[l]; if (!(a > 0)) a = 0;
+    double c = 0 - s; if (!(c > 0)) c = 0;
+    const double d = fabs(r) + a + c + 1.0 * ang;
+    if (l == 0 || d < bd) { bd = d; best = l; }
+  }
+  return best;
+}
+
 // Scene generation: ego MDPVehicle, then n-1 x IDMVehicle.create_random
 // (kinematics.py:50-104) + randomize_behavior (behavior.py:66-69), the numpy RNG stream
-// reproduced bit for bit.  One thread per env (the spawn order is sequential by nature).
-// Either `pcg` holds each env's initial PCG64 state ({state_hi, state_lo, inc_hi, inc_lo}) or
-// `words` holds each env's SeedSequence entropy ([E][n_words] uint32); `mask` (optional)
-// restricts the reset to the envs with mask[e] != 0, leaving the others untouched.
+// reproduced bit for bit, one env in draw order.
 template <typename T>
-__global__ void reset_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_reset_cfg_t cfg,
-                             const unsigned long long* __restrict__ pcg, const unsigned* __restrict__ words,
-                             int n_words, const uint8_t* __restrict__ mask) {
-  const int env = blockIdx.x * blockDim.x + threadIdx.x;
-  if (env >= st.n_envs || (mask && !mask[env])) return;
+__device__ void reset_env_serial(const ttrl_state_t& st, const ttrl_lane_table_t& R, const ttrl_params_t& P,
+                                 const ttrl_reset_cfg_t& cfg, Pcg g, int env) {
   const int N = st.n_veh, nl = R.n_lanes;
   const size_t b = (size_t)env * N;
   T* X = (T*)st.x; T* Y = (T*)st.y; T* Hh = (T*)st.heading; T* Vv = (T*)st.speed; T* TS = (T*)st.target_speed;
   T* TM = (T*)st.timer; T* DL = (T*)st.delta;
-  Pcg g;
-  unsigned long long s4[4];
-  if (pcg) {
-    for (int k = 0; k < 4; ++k) s4[k] = pcg[4 * env + k];
-  } else {
-    SeedSeq::pcg64_seed(words + (size_t)env * n_words, n_words, s4);
-  }
-  g.st = U128{s4[0], s4[1]};
-  g.inc = U128{s4[2], s4[3]};
-  g.has32 = false; g.u32 = 0;
   double smax[LMAX];
-  auto closest = [&](double x, double y, double h) {
-    int best = 0; double bd = 0;
-    for (int l = 0; l < nl; ++l) {
-      const LaneT<double> L = make_lane<double>(R, l);
-      double s, r;
-      lane_local(L, x, y, s, r);
-      const double ang = fabs(wrap_to_pi(h - heading_at(L, s)));
-      double a = s - R.length[l]; if (!(a > 0)) a = 0;
-      double c = 0 - s; if (!(c > 0)) c = 0;
-      const double d = fabs(r) + a + c + 1.0 * ang;
-      if (l == 0 || d < bd) { bd = d; best = l; }
-    }
-    return best;
-  };
   auto track = [&](double x, double y, bool first) {
     for (int l = 0; l < nl; ++l) {
       double s, r;
@@ -3138,7 +3124,7 @@ __global__ void reset_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t
     lane_position(L, cfg.ego_x, 0.0, ex, ey);
     const double eh = heading_at(L, cfg.ego_x);
     st.kind[b] = TTRL_MDP; X[b] = T(ex); Y[b] = T(ey); Hh[b] = T(eh); Vv[b] = T(cfg.ego_speed);
-    const int ln = closest(ex, ey, eh);
+    const int ln = closest_lane_index(R, ex, ey, eh);
     st.lane[b] = st.target_lane[b] = ln;
     const int si = speed_to_index(P, cfg.ego_speed);
     st.speed_index[b] = si;
@@ -3158,11 +3144,187 @@ __global__ void reset_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t
     const double ph = heading_at(L, x0);
     st.kind[k] = TTRL_IDM; st.lane_change[k] = (uint8_t)cfg.lane_change;
     X[k] = T(px); Y[k] = T(py); Hh[k] = T(ph); Vv[k] = T(sp); TS[k] = T(sp);
-    const int ln = closest(px, py, ph);
+    const int ln = closest_lane_index(R, px, py, ph);
     st.lane[k] = st.target_lane[k] = ln;
     TM[k] = T(pymod((px + py) * 3.141592653589793, P.lane_change_delay));
     DL[k] = T(cfg.delta_lo + (cfg.delta_hi - cfg.delta_lo) * pcg_double(g));
     track(px, py, false);
+  }
+}
+
+// numpy pcg64_advance (pcg_advance_lcg_128): the LCG state `delta` steps ahead, by
+// square-and-multiply of the affine map s -> M s + inc.
+__device__ __forceinline__ U128 pcg_advance(U128 st, U128 inc, unsigned long long delta) {
+  U128 acc_mult = {0ull, 1ull}, acc_plus = {0ull, 0ull};
+  U128 cur_mult = {0x2360ED051FC65DA4ull, 0x4385DF649FCCF645ull}, cur_plus = inc;
+  while (delta) {
+    if (delta & 1ull) {
+      acc_mult = mul128(acc_mult, cur_mult);
+      acc_plus = add128(mul128(acc_plus, cur_mult), cur_plus);
+    }
+    cur_plus = mul128(add128(cur_mult, U128{0ull, 1ull}), cur_plus);
+    cur_mult = mul128(cur_mult, cur_mult);
+    delta >>= 1;
+  }
+  return add128(mul128(acc_mult, st), acc_plus);
+}
+__device__ __forceinline__ unsigned long long pcg_output(U128 st) {  // pcg_next64's output of a state
+  const unsigned long long x = st.hi ^ st.lo;
+  const unsigned rot = (unsigned)(st.hi >> 58);
+  return (x >> rot) | (x << ((64 - rot) & 63));
+}
+__device__ __forceinline__ double pcg_unit(unsigned long long o) {
+  return (double)(o >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// The same scene as reset_env_serial, one wavefront per env (lane = vehicle slot), for the masked
+// auto-reset on the critical path of env.step.  numpy's draw order is sequential, but its stream
+// is not: vehicle i (1-based) consumes the 64-bit outputs from index c(i) = 3 (i - 1) + i / 2 on
+// (odd i: one output for integers(0, lanes) -- its high half buffered -- and three for the
+// uniforms; even i: the buffered half, then three), so every lane jumps its own generator copy
+// to c(i) (pcg_advance) and draws its vehicle's lane, speed, gap and DELTA in parallel.  Only the
+// placement is a recurrence (x0 = the max s on the drawn lane so far + the gap): one lane walks
+// it over the drawn gaps in LDS with reset_env_serial's exact arithmetic; then every lane assigns its
+// vehicle's lane and timer and the rows are written coalesced.  A Lemire rejection in
+// integers() (probability < 2^-31 per draw, never for a power-of-two lane count) would shift the
+// stream: such an env is regenerated by the sequential replay (reset_env_serial).
+template <typename T>
+__global__ void __launch_bounds__(64) reset_wave_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P,
+                                                        ttrl_reset_cfg_t cfg, const unsigned long long* __restrict__ pcg,
+                                                        const unsigned* __restrict__ words, int n_words,
+                                                        const uint8_t* __restrict__ mask) {
+  const int env = blockIdx.x, lane = threadIdx.x;
+  if (env >= st.n_envs || (mask && !mask[env])) return;
+  const int N = st.n_veh, nl = R.n_lanes, nv = min(cfg.n_vehicles, N);
+  const size_t b = (size_t)env * N;
+  T* X = (T*)st.x; T* Y = (T*)st.y; T* Hh = (T*)st.heading; T* Vv = (T*)st.speed; T* TS = (T*)st.target_speed;
+  T* TM = (T*)st.timer; T* DL = (T*)st.delta;
+  unsigned long long s4[4];
+  if (pcg) {
+    for (int k = 0; k < 4; ++k) s4[k] = pcg[4 * env + k];
+  } else {
+    SeedSeq::pcg64_seed(words + (size_t)env * n_words, n_words, s4);
+  }
+  const U128 s0 = {s4[0], s4[1]}, inc = {s4[2], s4[3]};
+  __shared__ double s_d[64], s_px[64], s_py[64], s_ph[64];
+  __shared__ int s_lid[64];
+  __shared__ double smax[LMAX];  // the max s per lane of the vehicles placed so far (lane 0)
+  // the ego MDPVehicle (lane 0 of the first chunk)
+  double ex = 0, ey = 0, eh = 0;
+  {
+    const LaneT<double> L = make_lane<double>(R, cfg.ego_lane);
+    lane_position(L, cfg.ego_x, 0.0, ex, ey);
+    eh = heading_at(L, cfg.ego_x);
+    if (lane == 0)
+      for (int l = 0; l < nl; ++l) {
+        double s, r;
+        lane_local(make_lane<double>(R, l), ex, ey, s, r);
+        smax[l] = s;
+      }
+  }
+  const unsigned rng_ = (unsigned)nl - 1;
+  const unsigned long long rexcl = (unsigned long long)rng_ + 1;
+  const unsigned thr = nl > 1 ? (unsigned)((0xFFFFFFFFull - rng_) % rexcl) : 0u;
+  unsigned carry_hi = 0;  // the buffered half of the previous chunk's last (odd) vehicle
+  bool reject = false;
+  for (int c0 = 0; c0 < N; c0 += 64) {
+    const int i = c0 + lane;
+    const bool drawn = i >= 1 && i < nv;
+    // ---- parallel draws (lane = vehicle i)
+    double sp = 0, d = 0, delta = 0;
+    int lid = 0;
+    unsigned u32 = 0, hi32 = 0;
+    unsigned long long o1 = 0, o2 = 0, o3 = 0;
+    if (drawn) {
+      const U128 M = {0x2360ED051FC65DA4ull, 0x4385DF649FCCF645ull};
+      const unsigned long long ci = 3ull * (unsigned long long)(i - 1) + (unsigned long long)(i / 2);
+      U128 g = pcg_advance(s0, inc, ci);
+      if (i & 1) {  // integers(0, lanes) draws a fresh output: low half now, high half buffered
+        g = add128(mul128(g, M), inc);
+        const unsigned long long o = pcg_output(g);
+        u32 = (unsigned)o;
+        hi32 = (unsigned)(o >> 32);
+      }
+      g = add128(mul128(g, M), inc); o1 = pcg_output(g);
+      g = add128(mul128(g, M), inc); o2 = pcg_output(g);
+      g = add128(mul128(g, M), inc); o3 = pcg_output(g);
+    }
+    // even vehicles take the previous (odd) vehicle's buffered half: lane - 1, or the carry
+    const unsigned prev_hi = (unsigned)__shfl((int)hi32, (lane + 63) & 63, 64);
+    if (drawn) {
+      if (!(i & 1)) u32 = lane == 0 ? carry_hi : prev_hi;
+      if (nl > 1) {
+        const unsigned long long m = (unsigned long long)u32 * rexcl;
+        if ((unsigned)m < thr) reject = true;
+        lid = (int)(m >> 32);
+      }
+      sp = cfg.speed_lo + (cfg.speed_hi - cfg.speed_lo) * pcg_unit(o1);
+      const double offset = cfg.spacing * (12 + 1.0 * sp) * cfg.density_factor;
+      d = offset * (0.9 + (1.1 - 0.9) * pcg_unit(o2));
+      delta = cfg.delta_lo + (cfg.delta_hi - cfg.delta_lo) * pcg_unit(o3);
+    }
+    carry_hi = (unsigned)__shfl((int)hi32, 63, 64);
+    s_d[lane] = d;
+    s_lid[lane] = lid;
+    __syncthreads();
+    // ---- the placement recurrence (one lane; reset_env_serial's arithmetic)
+    if (lane == 0) {
+      const int n = min(64, nv - c0);
+      for (int q = c0 == 0 ? 1 : 0; q < n; ++q) {
+        const int l = s_lid[q];
+        double x0 = smax[l];
+        x0 += s_d[q];
+        const LaneT<double> L = make_lane<double>(R, l);
+        double px, py;
+        lane_position(L, x0, 0.0, px, py);
+        s_px[q] = px; s_py[q] = py; s_ph[q] = heading_at(L, x0);
+        for (int k = 0; k < nl; ++k) {
+          double s, r;
+          lane_local(make_lane<double>(R, k), px, py, s, r);
+          if (s > smax[k]) smax[k] = s;
+        }
+      }
+    }
+    __syncthreads();
+    // ---- every slot of the chunk, coalesced
+    if (i < N) {
+      const size_t k = b + i;
+      const T z = T(0);
+      ((T*)st.steer)[k] = z; ((T*)st.acc)[k] = z; ((T*)st.impact_x)[k] = z; ((T*)st.impact_y)[k] = z;
+      st.crashed[k] = 0; st.has_impact[k] = 0;
+      if (i == 0) {
+        st.kind[k] = TTRL_MDP; st.lane_change[k] = 0;
+        X[k] = T(ex); Y[k] = T(ey); Hh[k] = T(eh); Vv[k] = T(cfg.ego_speed);
+        const int ln = closest_lane_index(R, ex, ey, eh);
+        st.lane[k] = st.target_lane[k] = ln;
+        const int si = speed_to_index(P, cfg.ego_speed);
+        st.speed_index[k] = si;
+        TS[k] = T(P.target_speeds[si]);
+        TM[k] = z; DL[k] = T(4);
+      } else if (i < nv) {
+        const double px = s_px[lane], py = s_py[lane], ph = s_ph[lane];
+        st.kind[k] = TTRL_IDM; st.lane_change[k] = (uint8_t)cfg.lane_change;
+        X[k] = T(px); Y[k] = T(py); Hh[k] = T(ph); Vv[k] = T(sp); TS[k] = T(sp);
+        const int ln = closest_lane_index(R, px, py, ph);
+        st.lane[k] = st.target_lane[k] = ln;
+        st.speed_index[k] = -1;
+        TM[k] = T(pymod((px + py) * 3.141592653589793, P.lane_change_delay));
+        DL[k] = T(delta);
+      } else {
+        st.kind[k] = TTRL_ABSENT; st.lane_change[k] = 0;
+        X[k] = Y[k] = Hh[k] = Vv[k] = TS[k] = TM[k] = z;
+        DL[k] = T(4); st.lane[k] = st.target_lane[k] = 0; st.speed_index[k] = -1;
+      }
+    }
+    __syncthreads();
+  }
+  if (__any(reject)) {  // a rejected integers() draw shifts the stream: replay this env in order
+    __syncthreads();
+    if (lane == 0) {
+      Pcg g;
+      g.st = s0; g.inc = inc; g.has32 = false; g.u32 = 0;
+      reset_env_serial<T>(st, R, P, cfg, g, env);
+    }
   }
 }
 
@@ -3865,12 +4027,11 @@ int ttrl_reset_highway(const ttrl_state_t* s, const ttrl_lane_table_t* road, con
     return TTRL_E_ARG;
   if (s->n_envs == 0) return TTRL_OK;
   hipStream_t st = (hipStream_t)stream;
-  const int blocks = (s->n_envs + 63) / 64;
   if (s->dtype == TTRL_F64)
-    hipLaunchKernelGGL(reset_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg,
+    hipLaunchKernelGGL(reset_wave_kernel<double>, dim3(s->n_envs), dim3(64), 0, st, *s, *road, *p, *cfg,
                        (const unsigned long long*)pcg, (const unsigned*)nullptr, 0, (const uint8_t*)nullptr);
   else
-    hipLaunchKernelGGL(reset_kernel<float>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg,
+    hipLaunchKernelGGL(reset_wave_kernel<float>, dim3(s->n_envs), dim3(64), 0, st, *s, *road, *p, *cfg,
                        (const unsigned long long*)pcg, (const unsigned*)nullptr, 0, (const uint8_t*)nullptr);
   return launch_status();
 }
@@ -3885,12 +4046,11 @@ int ttrl_reset_highway_seeded(const ttrl_state_t* s, const ttrl_lane_table_t* ro
     return TTRL_E_ARG;
   if (s->n_envs == 0) return TTRL_OK;
   hipStream_t st = (hipStream_t)stream;
-  const int blocks = (s->n_envs + 63) / 64;
   if (s->dtype == TTRL_F64)
-    hipLaunchKernelGGL(reset_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg,
+    hipLaunchKernelGGL(reset_wave_kernel<double>, dim3(s->n_envs), dim3(64), 0, st, *s, *road, *p, *cfg,
                        (const unsigned long long*)nullptr, (const unsigned*)entropy, (int)n_words, mask);
   else
-    hipLaunchKernelGGL(reset_kernel<float>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg,
+    hipLaunchKernelGGL(reset_wave_kernel<float>, dim3(s->n_envs), dim3(64), 0, st, *s, *road, *p, *cfg,
                        (const unsigned long long*)nullptr, (const unsigned*)entropy, (int)n_words, mask);
   return launch_status();
 }

@@ -11,12 +11,11 @@ Reward / termination follow IntersectionEnv._agent_reward (intersection_env.py:7
 from __future__ import annotations
 
 import copy
-import ctypes as C
 
 import numpy as np
 import torch
 
-from . import _abi, _lib
+from . import _abi, ops
 from .action import action_factory
 from .observation import BatchedKinematicObservation, observation_factory
 from .road import BatchedRoad, RoadNetwork
@@ -32,9 +31,9 @@ def reset_highway(state: BatchState, network: RoadNetwork, params: _abi.Params, 
         words = torch.tensor(np.asarray(seeds, dtype=np.uint32).view(np.int32), device=state.device).view(-1, 1)
         reset_highway_seeded(state, network, params, cfg, words)
         return
+    _device_only(state)
     pcg = torch.from_numpy(_abi.pcg64_states(seeds).view(np.int64)).to(state.device)
-    _lib.call("ttrl_reset_highway", C.byref(state.struct()), C.byref(network.table), C.byref(params),
-              C.byref(cfg), pcg.data_ptr(), torch.cuda.current_stream(state.device).cuda_stream)
+    ops.T.reset_highway_(state.tensors(), ops.st(network.table), ops.st(params), ops.st(cfg), pcg)
 
 
 def reset_highway_seeded(state: BatchState, network: RoadNetwork, params: _abi.Params, cfg: _abi.ResetCfg,
@@ -45,37 +44,30 @@ def reset_highway_seeded(state: BatchState, network: RoadNetwork, params: _abi.P
         raise ValueError("entropy must be an int32 [n_envs, n_words] tensor of uint32 words")
     if entropy.device != state.device or (mask is not None and mask.device != state.device):
         raise ValueError("entropy / mask must live on the state's device")
-    entropy = entropy.contiguous()
-    m = None if mask is None else mask.to(torch.uint8).contiguous()
-    _lib.call("ttrl_reset_highway_seeded", C.byref(state.struct()), C.byref(network.table), C.byref(params),
-              C.byref(cfg), entropy.data_ptr(), int(entropy.shape[1]), None if m is None else m.data_ptr(),
-              torch.cuda.current_stream(state.device).cuda_stream)
+    _device_only(state)
+    ops.T.reset_highway_seeded_(state.tensors(), ops.st(network.table), ops.st(params), ops.st(cfg), entropy, mask)
 
 
-def _tail_outputs(env):
-    """Fresh step-tail outputs: reward [E] f32, terminated / truncated [E] bool, the per-objective
-    block [E, 4], the info's ego speed / crashed.  The kernels write every element (bool storage is
-    one byte), so nothing needs a clone / cast launch."""
-    E, dev = env.num_envs, env.device
-    return (torch.empty(E, dtype=torch.float32, device=dev), torch.empty(E, dtype=torch.bool, device=dev),
-            torch.empty(E, dtype=torch.bool, device=dev), torch.empty((E, 4), dtype=torch.float32, device=dev),
-            torch.empty(E, dtype=env.state["speed"].dtype, device=dev), torch.empty(E, dtype=torch.bool, device=dev))
+def _device_only(state: BatchState) -> None:
+    if state.device.type != "cuda":
+        raise RuntimeError("the simulator runs on a HIP device only (no CPU fallback)")
 
 
 def _keep_tail(env, outs):
+    """outs = (reward, terminated, truncated, components, ego speed, ego crashed): kept for
+    ``_info`` and returned as (reward, terminated, truncated)."""
     env._reward, env._term, env._trunc, env._components, env._ego_speed, env._ego_crashed = outs
     return outs[:3]
 
 
-def rewards_and_dones(env, stream: int, time_inc: float = 0.0):
-    """The step tail in one launch (ttrl_rewards_step): env.time += time_inc, then reward,
-    terminated, truncated, env._components and the info's ego speed / crashed (_tail_outputs)."""
-    outs = _tail_outputs(env)
-    reward, term, trunc, comp, speed, crashed = outs
-    _lib.call("ttrl_rewards_step", C.byref(env.state.struct()), C.byref(env.network.table), C.byref(env.reward_cfg),
-              env.time.data_ptr(), float(time_inc), reward.data_ptr(), term.data_ptr(), trunc.data_ptr(),
-              comp.data_ptr(), speed.data_ptr(), crashed.data_ptr(), stream)
+def rewards_and_dones(env, time_inc: float = 0.0):
+    """The step tail in one launch (ttrl::rewards_step_): env.time += time_inc, then reward,
+    terminated, truncated, env._components and the info's ego speed / crashed."""
+    _device_only(env.state)
+    outs = ops.T.rewards_step_(env.state.tensors(), ops.st(env.network.table), ops.st(env.reward_cfg), env.time,
+                               float(time_inc))
     return _keep_tail(env, outs)
+
 
 def _reward_terms(names, components: torch.Tensor) -> dict:
     """[E, 4] component block -> {name: [E] view} (float32; 0/1 for the boolean terms)."""
@@ -245,40 +237,45 @@ class VecHighwayEnv:
         info = self._info(obs, action)
         if self.config["auto_reset"]:
             # finished envs restart on the device; obs is the new episode's first observation and
-            # info["final_observation"] the finished episode's last (no host round trip)
+            # info["final_observation"] the finished episode's last (no host round trip): only the
+            # finished envs are regenerated and re-observed (masked launches)
             done = terminated | truncated
             info["final_observation"], info["final_mask"] = obs, done
             self._auto_reset(done)
-            obs = self.observation_type.observe()
+            if isinstance(self.observation_type, BatchedKinematicObservation):
+                obs = self.observation_type.observe(mask=done, out=obs.clone())
+            else:
+                obs = self.observation_type.observe()
         return obs, reward, terminated, truncated, info
 
     def _simulate(self, action=None, tail: bool = False):
         """abstract.py:252-282 as one fused launch: meta-action at frame 0, then frames x (act, step).
         With ``tail`` the same launch also writes the step tail and, for a Kinematics observation, the
-        observation of the final state (ttrl_env_step); returns (obs or None, (reward, terminated,
+        observation of the final state (ttrl::env_step_); returns (obs or None, (reward, terminated,
         truncated))."""
         frames = int(self.config["simulation_frequency"] // self.config["policy_frequency"])
+        dt = 1 / self.config["simulation_frequency"]
         codes = None
         if action is not None and not self.config["manual_control"]:
             codes = self.action_type._codes(action)
-        fused = outs = None
-        if tail:
-            if isinstance(self.observation_type, BatchedKinematicObservation):
-                fused = self.observation_type.fused_outputs()
-            outs = _tail_outputs(self)
-            tail_args = (self.reward_cfg, self.time, 1 / self.config["policy_frequency"]) + outs
-        self.road.simulate(codes, frames, 1 / self.config["simulation_frequency"], observe=fused,
-                           tail=tail_args if tail else None)
         self.steps += frames
-        if tail:
-            return None if fused is None else fused[1], _keep_tail(self, outs)
+        if not tail:
+            self.road.simulate(codes, frames, dt)
+            return None
+        kin = isinstance(self.observation_type, BatchedKinematicObservation)
+        kc = self.observation_type.fused_cfg() if kin else None
+        obs, ids, *outs = self.road.env_step(codes, frames, dt, kc, self.reward_cfg, self.time,
+                                             1 / self.config["policy_frequency"])
+        if kin:
+            self.observation_type.fused_result(obs, ids)
+        return (obs if kin else None), _keep_tail(self, outs)
 
     REWARD_TERMS = ["collision_reward", "high_speed_reward", "arrived_reward", "on_road_reward"]
 
     def _rewards_and_dones(self, time_inc: float = 0.0):
         """reward, terminated, truncated [E]; the per-objective terms (_agent_rewards,
         intersection_env.py:95-104) go to self._components [E, 4] for info["rewards"]."""
-        return rewards_and_dones(self, torch.cuda.current_stream(self.device).cuda_stream, time_inc)
+        return rewards_and_dones(self, time_inc)
 
     def _info(self, obs, action) -> dict:
         """abstract.py:169-186 batched: device tensors [E]; info["rewards"] holds the per-objective
@@ -288,7 +285,7 @@ class VecHighwayEnv:
 
     def _auto_reset(self, done: torch.Tensor) -> None:
         """Masked auto-reset of finished envs on the device."""
-        d = done.to(torch.int32)
+        d = done.view(torch.uint8) if done.dtype == torch.bool else done.to(torch.uint8)
         self._entropy[:, 2] += d
         reset_highway_seeded(self.state, self.network, self.params, self.reset_cfg, self._entropy, d)
         self.time.masked_fill_(done, 0.0)

@@ -18,12 +18,11 @@ replays ``IntersectionEnv.reset(seed=s)`` and its steps (tests/test_ix_env.py).
 from __future__ import annotations
 
 import copy
-import ctypes as C
 
 import numpy as np
 import torch
 
-from . import _abi, _lib
+from . import _abi, ops
 from .action import action_factory
 from .envs import _reward_terms, rewards_and_dones
 from .observation import observation_factory
@@ -174,10 +173,9 @@ def ix_cfg(network: RoadNetwork, config: dict, params: _abi.Params) -> _abi.IxCf
     return c
 
 
-def _stream(device):
-    if device.type != "cuda":
+def _device_only(state: BatchState) -> None:
+    if state.device.type != "cuda":
         raise RuntimeError("the intersection env runs on a HIP device only (no CPU fallback)")
-    return torch.cuda.current_stream(device).cuda_stream
 
 
 def ix_reset(state: BatchState, network: RoadNetwork, params: _abi.Params, cfg: _abi.IxCfg,
@@ -185,24 +183,22 @@ def ix_reset(state: BatchState, network: RoadNetwork, params: _abi.Params, cfg: 
     """IntersectionEnv.reset on the device: env e replays ``default_rng(list(entropy[e]))``."""
     if entropy.dim() != 2 or entropy.shape[0] != state.n_envs or entropy.dtype != torch.int32:
         raise ValueError("entropy must be an int32 [n_envs, n_words] tensor of uint32 words")
-    entropy = entropy.to(state.device).contiguous()
-    m = None if mask is None else mask.to(device=state.device, dtype=torch.uint8).contiguous()
-    _lib.call("ttrl_ix_reset", C.byref(state.struct()), C.byref(network.table), C.byref(params), C.byref(cfg),
-              entropy.data_ptr(), int(entropy.shape[1]), None if m is None else m.data_ptr(), _stream(state.device))
+    _device_only(state)
+    ops.T.ix_reset_(state.tensors(), ops.st(network.table), ops.st(params), ops.st(cfg),
+                    entropy.to(state.device), mask)
 
 
 def ix_clear_spawn(state: BatchState, network: RoadNetwork, params: _abi.Params, cfg: _abi.IxCfg,
                    mask: torch.Tensor | None = None) -> None:
     """IntersectionEnv.step tail: _clear_vehicles then _spawn_vehicle, on the device."""
-    m = None if mask is None else mask.to(device=state.device, dtype=torch.uint8).contiguous()
-    _lib.call("ttrl_ix_clear_spawn", C.byref(state.struct()), C.byref(network.table), C.byref(params), C.byref(cfg),
-              None if m is None else m.data_ptr(), _stream(state.device))
+    _device_only(state)
+    ops.T.ix_clear_spawn_(state.tensors(), ops.st(network.table), ops.st(params), ops.st(cfg), mask)
 
 
 def copy_envs(dst: BatchState, src: BatchState, mask: torch.Tensor) -> None:
     """Copy the whole rows of the masked envs from ``src`` into ``dst`` (same shape and dtype)."""
-    m = mask.to(device=dst.device, dtype=torch.uint8).contiguous()
-    _lib.call("ttrl_copy_envs", C.byref(dst.struct()), C.byref(src.struct()), m.data_ptr(), _stream(dst.device))
+    _device_only(dst)
+    ops.T.copy_envs_(dst.tensors(), src.tensors(), mask)
 
 
 def seed_words(seeds) -> np.ndarray:
@@ -429,7 +425,7 @@ class VecIntersectionEnv:
     def _rewards_and_dones(self, time_inc: float = 0.0):
         """reward, terminated, truncated [E]; the per-objective terms (_agent_rewards,
         intersection_env.py:95-104) go to self._components [E, 4] for info["rewards"]."""
-        return rewards_and_dones(self, _stream(self.device), time_inc)
+        return rewards_and_dones(self, time_inc)
 
     def _info(self, obs, action) -> dict:
         """IntersectionEnv._info (intersection_env.py:120-128) over abstract.py:169-186, batched: device

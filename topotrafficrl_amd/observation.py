@@ -11,73 +11,59 @@ tensor [n_envs, ...] computed by the HIP kernels for every env's ego.
 """
 from __future__ import annotations
 
-import ctypes as C
-
 import torch
 
-from . import _abi, _lib
+from . import _abi, ops
 from .spaces import Box
 
 
-def _stream(device):
+def _device_only(device):
     if device.type != "cuda":
         raise RuntimeError("observations run on a HIP device only (no CPU fallback)")
-    return torch.cuda.current_stream(device).cuda_stream
 
 
 def kinematics(state, network, params, cfg: _abi.KinCfg, out=None, ids=None, mask=None):
     """KinematicObservation.observe for every env: ([E, V, F] float32, [E, V-1] int32 slot ids).
     ``mask`` (uint8/bool [E]): only those envs are observed (their np_random advanced); the other
     rows of ``out`` / ``ids`` are left as they were."""
+    _device_only(state.device)
+    if cfg.order_shuffled == 2 and state["rng"] is None:
+        raise ValueError("np_random-shuffled observation needs the state's rng")
+    args = (state.tensors(), ops.st(network.table), ops.st(params), ops.kin_cfg_tensor(cfg))
+    if mask is None and out is None and ids is None:
+        return ops.T.kinematics_obs(*args)
     E, V, F = state.n_envs, cfg.vehicles_count, cfg.n_features
     if out is None:
         out = torch.empty((E, V, F), dtype=torch.float32, device=state.device)
     if ids is None:
         ids = torch.empty((E, max(V - 1, 1)), dtype=torch.int32, device=state.device)
-    m = None
-    if mask is not None:
-        m = mask.to(device=state.device, dtype=torch.uint8).contiguous()
-        if m.numel() != E:
-            raise ValueError("mask must have one entry per env")
-    if cfg.order_shuffled == 2 and state["rng"] is None:
-        raise ValueError("np_random-shuffled observation needs the state's rng")
-    _lib.call("ttrl_observe_kinematics_masked", C.byref(state.struct()), C.byref(network.table), C.byref(params),
-              C.byref(cfg), None if m is None else m.data_ptr(), out.data_ptr(), ids.data_ptr(),
-              _stream(state.device))
+    if mask is None:
+        mask = torch.ones(E, dtype=torch.uint8, device=state.device)
+    elif mask.numel() != E:
+        raise ValueError("mask must have one entry per env")
+    elif mask.dtype == torch.bool:
+        mask = mask.view(torch.uint8)
+    ops.T.kinematics_obs_masked_(*args, mask, out, ids)
     return out, ids
 
 
-def occupancy_grid(state, network, params, cfg: _abi.GridCfg, out=None):
+def occupancy_grid(state, network, params, cfg: _abi.GridCfg):
     """OccupancyGridObservation.observe for every env: [E, F, W, H] float32."""
-    shape = (state.n_envs, cfg.n_features, cfg.shape_x, cfg.shape_y)
-    if out is None:
-        out = torch.empty(shape, dtype=torch.float32, device=state.device)
-    _lib.call("ttrl_observe_grid", C.byref(state.struct()), C.byref(network.table), C.byref(params),
-              C.byref(cfg), out.data_ptr(), _stream(state.device))
-    return out
+    _device_only(state.device)
+    return ops.T.occupancy_grid(state.tensors(), ops.st(network.table), ops.st(params), ops.st(cfg))
 
 
-def time_to_collision(state, network, params, cfg: _abi.TtcCfg, out=None):
+def time_to_collision(state, network, params, cfg: _abi.TtcCfg):
     """TimeToCollisionObservation.observe for every env: [E, 3 speeds, 3 lanes, T] float32; with a
     raw cfg (obs_speeds = obs_lanes = 0) the whole compute_ttc_grid [E, speeds, lanes, T]."""
-    if cfg.obs_speeds == 0 and cfg.obs_lanes == 0:
-        shape = (state.n_envs, params.n_target_speeds, network.table.n_lanes, cfg.horizon_bins)
-    else:
-        shape = (state.n_envs, cfg.obs_speeds, cfg.obs_lanes, cfg.horizon_bins)
-    if out is None:
-        out = torch.empty(shape, dtype=torch.float32, device=state.device)
-    _lib.call("ttrl_observe_ttc", C.byref(state.struct()), C.byref(network.table), C.byref(params),
-              C.byref(cfg), out.data_ptr(), _stream(state.device))
-    return out
+    _device_only(state.device)
+    return ops.T.observe_ttc(state.tensors(), ops.st(network.table), ops.st(params), ops.st(cfg))
 
 
-def lidar(state, network, params, cfg: _abi.LidarCfg, out=None):
+def lidar(state, network, params, cfg: _abi.LidarCfg):
     """LidarObservation.observe for every env: [E, cells, 2] float32 (distance, relative speed)."""
-    if out is None:
-        out = torch.empty((state.n_envs, cfg.cells, 2), dtype=torch.float32, device=state.device)
-    _lib.call("ttrl_observe_lidar", C.byref(state.struct()), C.byref(network.table), C.byref(params),
-              C.byref(cfg), out.data_ptr(), _stream(state.device))
-    return out
+    _device_only(state.device)
+    return ops.T.observe_lidar(state.tensors(), ops.st(network.table), ops.st(params), ops.st(cfg))
 
 
 class BatchedObservationType:
@@ -134,18 +120,17 @@ class BatchedKinematicObservation(BatchedObservationType):
                                           mask=mask)
         return self._out
 
-    def fused_outputs(self):
-        """(cfg, out, ids) for an observation written by the simulate launch itself
-        (BatchedRoad.simulate(observe=...)); the same per-call bookkeeping as observe()."""
+    def fused_cfg(self) -> _abi.KinCfg:
+        """The cfg for an observation written by the env.step launch itself (BatchedRoad.env_step),
+        with the same per-call bookkeeping as observe(); hand the outputs to fused_result()."""
         if self.order == "shuffled" and self.cfg.order_shuffled == 1:
             self.cfg.shuffle_seed = int(self.env.shuffle_seed)
             self.cfg.shuffle_offset = self._calls
         self._calls += 1
-        st = self.env.road.state
-        V, F = self.cfg.vehicles_count, self.cfg.n_features
-        self._out = torch.empty((st.n_envs, V, F), dtype=torch.float32, device=st.device)
-        self._ids = torch.empty((st.n_envs, max(V - 1, 1)), dtype=torch.int32, device=st.device)
-        return self.cfg, self._out, self._ids
+        return self.cfg
+
+    def fused_result(self, out: torch.Tensor, ids: torch.Tensor) -> None:
+        self._out, self._ids = out, ids
 
     @property
     def observed_ids(self) -> torch.Tensor:

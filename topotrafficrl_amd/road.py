@@ -7,12 +7,10 @@ All work is enqueued on the current HIP stream of the state's device.
 """
 from __future__ import annotations
 
-import ctypes as C
-
 import numpy as np
 import torch
 
-from . import _abi, _lib
+from . import _abi, ops
 from .state import BatchState
 
 
@@ -67,78 +65,65 @@ class RoadNetwork:
                          for i in range(t.n_lanes)])
 
 
-def _stream(device: torch.device) -> int:
+def _check_device(device: torch.device) -> None:
     if device.type != "cuda":
         raise RuntimeError("BatchedRoad runs on a HIP device only (no CPU fallback)")
-    return torch.cuda.current_stream(device).cuda_stream
 
 
 class BatchedRoad:
-    """Batched ``Road``: the vehicles of every env as one ``BatchState``."""
+    """Batched ``Road``: the vehicles of every env as one ``BatchState``.  Every method is one
+    ``torch.ops.ttrl`` operator (csrc/ttrl_torch_ops.cpp) on the current HIP stream."""
 
     def __init__(self, network: RoadNetwork, state: BatchState, params: _abi.Params | None = None):
         self.network = network
         self.state = state
         self.params = params if params is not None else _abi.default_params()
-        _lib.load()
 
     def _args(self):
-        return C.byref(self.state.struct()), C.byref(self.network.table), C.byref(self.params)
+        _check_device(self.state.device)
+        return self.state.tensors(), ops.st(self.network.table), ops.st(self.params)
 
     def act(self) -> None:
         """Road.act (road.py:461-464): every vehicle decides, in list order."""
-        s, r, p = self._args()
-        _lib.call("ttrl_road_act", s, r, p, _stream(self.state.device))
+        ops.T.road_act_(*self._args())
 
     def step(self, dt: float) -> None:
         """Road.step (road.py:466-478): kinematics, lane update, collisions."""
-        s, r, p = self._args()
-        _lib.call("ttrl_road_step", s, r, p, float(dt), _stream(self.state.device))
+        ops.T.road_step_(*self._args(), float(dt))
 
     def meta_action(self, actions: torch.Tensor) -> None:
         """DiscreteMetaAction.act for the ego of every env (action.py:259-260)."""
-        a = self._actions(actions)
-        s, r, p = self._args()
-        _lib.call("ttrl_meta_action", s, r, p, a.data_ptr(), _stream(self.state.device))
+        ops.T.meta_action_(*self._args(), self._actions(actions))
 
-    def simulate(self, actions: torch.Tensor | None, frames: int = 15, dt: float = 1 / 15, observe=None,
-                 tail=None) -> None:
-        """Fused AbstractEnv._simulate (abstract.py:252-282) for `frames` frames.  With ``observe`` =
-        (KinCfg, out [E, V, F] float32, ids [E, V-1] int32) and / or ``tail`` = (RewardCfg, time [E] f64,
-        time_inc, reward, terminated, truncated, components, ego_speed, ego_crashed) the same launch
-        also writes the Kinematics observation and the step tail of the final state (ttrl_env_step)."""
+    def simulate(self, actions: torch.Tensor | None, frames: int = 15, dt: float = 1 / 15) -> None:
+        """Fused AbstractEnv._simulate (abstract.py:252-282) for `frames` frames."""
         a = None if actions is None else self._actions(actions)
-        s, r, p = self._args()
-        ap = None if a is None else a.data_ptr()
-        if observe is None and tail is None:
-            _lib.call("ttrl_simulate", s, r, p, ap, int(frames), float(dt), _stream(self.state.device))
-            return
-        oc, oo, oi = (None, None, None) if observe is None else (C.byref(observe[0]), observe[1].data_ptr(),
-                                                                   observe[2].data_ptr())
-        if tail is None:
-            rc, tail_ptrs = None, [None, 0.0] + [None] * 7
-        else:
-            rc = C.byref(tail[0])
-            tail_ptrs = [tail[1].data_ptr(), float(tail[2])] + [t.data_ptr() for t in tail[3:]]
-        _lib.call("ttrl_env_step", s, r, p, ap, int(frames), float(dt), oc, oo, oi, rc, *tail_ptrs,
-                  _stream(self.state.device))
+        ops.T.simulate_(*self._args(), a, int(frames), float(dt))
+
+    def env_step(self, actions: torch.Tensor | None, frames: int, dt: float, kin_cfg: _abi.KinCfg | None,
+                 reward_cfg: _abi.RewardCfg, time: torch.Tensor, time_inc: float):
+        """AbstractEnv.step (abstract.py:224-250) in one launch (ttrl_env_step): the fused frames, the
+        Kinematics observation of the final state (``kin_cfg``; else obs / ids are empty) and the step
+        tail (time += time_inc, reward, terminated, truncated, components, the info's ego speed /
+        crashed).  Returns those 8 tensors."""
+        a = None if actions is None else self._actions(actions)
+        kc = None if kin_cfg is None else ops.kin_cfg_tensor(kin_cfg)
+        return ops.T.env_step_(*self._args(), a, int(frames), float(dt), kc, ops.st(reward_cfg), time,
+                               float(time_inc))
 
     def neighbour_vehicles(self, query_lane: torch.Tensor | None = None):
         """Road.neighbour_vehicles (road.py:480-513) for every vehicle: (front, rear) slot ids, -1 = None."""
         st = self.state
-        front = torch.empty((st.n_envs, st.n_veh), dtype=torch.int32, device=st.device)
-        rear = torch.empty_like(front)
-        q = None
-        if query_lane is not None:
-            q = query_lane.to(device=st.device, dtype=torch.int32).contiguous()
-            if q.shape != front.shape:
-                raise ValueError("query_lane must be [n_envs, n_veh]")
-        _lib.call("ttrl_neighbours", C.byref(st.struct()), C.byref(self.network.table),
-                  None if q is None else q.data_ptr(), front.data_ptr(), rear.data_ptr(), _stream(st.device))
-        return front, rear
+        _check_device(st.device)
+        if query_lane is not None and tuple(query_lane.shape) != (st.n_envs, st.n_veh):
+            raise ValueError("query_lane must be [n_envs, n_veh]")
+        return ops.T.neighbours(st.tensors(), ops.st(self.network.table), query_lane)
 
     def _actions(self, actions) -> torch.Tensor:
-        a = torch.as_tensor(actions).to(device=self.state.device, dtype=torch.int32).reshape(-1).contiguous()
+        a = torch.as_tensor(actions)
+        if a.device != self.state.device or a.dtype != torch.int32:
+            a = a.to(device=self.state.device, dtype=torch.int32)
+        a = a.reshape(-1)
         if a.numel() != self.state.n_envs:
             raise ValueError(f"expected {self.state.n_envs} actions, got {a.numel()}")
-        return a
+        return a.contiguous()

@@ -52,6 +52,7 @@ class BatchState:
         # AbstractEnv.np_random of each env (numpy Generator(PCG64) words, see _abi.RNG_WORDS)
         self.t["rng"] = torch.zeros((self.n_envs, _abi.RNG_WORDS), dtype=torch.int64, device=self.device)
         self._struct = None
+        self._tensors = None
 
     def __getitem__(self, k: str) -> torch.Tensor:
         return self.t[k]
@@ -68,7 +69,9 @@ class BatchState:
 
     def tensors(self) -> list:
         """The state tensors in _abi.ALL_FIELDS order (the ``state`` argument of torch.ops.ttrl)."""
-        return [self.t[f] for f in _abi.ALL_FIELDS]
+        if self._tensors is None:
+            self._tensors = [self.t[f] for f in _abi.ALL_FIELDS]
+        return self._tensors
 
     def ego_index(self) -> torch.Tensor:
         """[E] slot of each env's controlled vehicle: its first MDP slot (AbstractEnv.vehicle)."""
@@ -99,7 +102,7 @@ class BatchState:
         b = BatchState.__new__(BatchState)
         b.n_envs, b.n_veh, b.device, b.dtype = self.n_envs, self.n_veh, self.device, self.dtype
         b.t = {k: v.clone() for k, v in self.t.items()}
-        b._struct = None
+        b._struct = b._tensors = None
         return b
 
     def rows(self, start: int, n: int) -> "BatchState":
@@ -107,7 +110,7 @@ class BatchState:
         b = BatchState.__new__(BatchState)
         b.n_envs, b.n_veh, b.device, b.dtype = int(n), self.n_veh, self.device, self.dtype
         b.t = {k: v[start:start + n] for k, v in self.t.items()}
-        b._struct = None
+        b._struct = b._tensors = None
         return b
 
     def copy_(self, other: "BatchState") -> "BatchState":
