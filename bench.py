@@ -10,7 +10,7 @@ Default workload (config 4, per GPU): 4096 envs x 64 vehicles, Kinematics 15x7
 (env.json ranges, absolute=false, sorted), synthetic straight 4-lane highway,
 random-seeded scenes and uniformly random ego actions (pre-drawn on the device).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype f64|f32] [--config 2|3|4|5]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype f64|f32] [--config 1..6] [--auto-reset]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 """
 from __future__ import annotations
@@ -34,7 +34,11 @@ KIN15 = {"type": "Kinematics", "vehicles_count": 15,
 GRID7 = {"type": "OccupancyGrid", "features": ["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"],
          "features_range": {"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]},
          "grid_size": [[-32, 32], [-32, 32]], "grid_step": [2, 2], "absolute": False}
+KIN5 = {"type": "Kinematics"}  # KinematicObservation defaults: 5 x 5, sorted, relative (observation.py:159-196)
 CONFIGS = {
+    # the reference's plumbing case (scripts/example.py scale): one env, 50 vehicles; the GPU line is
+    # launch-latency bound by construction, the CPU line is the oracle on one core
+    1: dict(num_envs=1, vehicles=50, obs=KIN5, name="1 env x 50 vehicles, Kinematics 5x5 defaults"),
     2: dict(num_envs=4096, vehicles=32, obs=KIN15, name="4096 envs x 32 vehicles, Kinematics 15x7"),
     3: dict(num_envs=4096, vehicles=128, obs=GRID7, name="4096 envs x 128 vehicles, OccupancyGrid 7x32x32"),
     4: dict(num_envs=4096, vehicles=64, obs=KIN15, name="4096 envs x 64 vehicles per GPU, Kinematics 15x7"),
@@ -54,17 +58,25 @@ def state_bytes(dtype: str) -> tuple[int, int]:
     return 11 * r + 3 * 4 + 4, 10 * r + 3 * 4 + 2
 
 
-def cpu_baseline(vehicles: int, obs_cfg: dict, seconds_target: float = 10.0) -> dict:
+def host_threads() -> int:
+    """The host cores the CPU baseline uses: the granted CPU share when the job is given one
+    (OMP_NUM_THREADS: 16 on the GPU box, whose os.cpu_count() reports the whole machine), else
+    every core os.cpu_count() reports."""
+    return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+
+
+def cpu_baseline(vehicles: int, obs_cfg: dict, seconds_target: float = 10.0, envs: int = 4096,
+                 threads: int | None = None) -> dict:
     """The float64 C restatement (oracle/) on host cores, bounded sample of the same workload."""
+    threads = threads or host_threads()
+    os.environ["OMP_NUM_THREADS"] = str(threads)
     from oracle.oracle import HostState, Oracle
     from topotrafficrl_amd import _abi
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    os.environ["OMP_NUM_THREADS"] = str(threads)
     lanes = _abi.straight_lane_table(4)
     o = Oracle(lanes, _abi.default_params())
     kin = _abi.kin_cfg(**{k: v for k, v in obs_cfg.items() if k != "type"}) if obs_cfg["type"] == "Kinematics" else None
     grid = _abi.grid_cfg(**{k: v for k, v in obs_cfg.items() if k != "type"}) if kin is None else None
-    E = 4096  # the same batch as the GPU workload
+    E = envs  # the same batch as the GPU workload
     h = HostState(E, vehicles)
     o.reset_highway(h, _abi.reset_cfg(vehicles, lanes), list(range(E)))
     rng = np.random.default_rng(0)
@@ -77,9 +89,10 @@ def cpu_baseline(vehicles: int, obs_cfg: dict, seconds_target: float = 10.0) -> 
             o.observe_grid(h, grid)
         steps += 1
         el = time.perf_counter() - t0
-        if el >= seconds_target or steps >= 200:
+        if el >= seconds_target or steps >= (200 if E > 1 else 20000):
             break
     return {"value": E * vehicles * 15 * steps / el, "unit": "vehicle-steps/s", "cores": threads, "kind": "port",
+            "host_cpus": os.cpu_count(),
             "sample": f"{E} envs x {vehicles} vehicles x {steps} env.step (15 frames + obs), float64 C restatement "
                       f"of the reference loop order (oracle/ttrl_oracle.c), OpenMP over envs, {el:.1f} s"}
 
@@ -91,7 +104,7 @@ def cpu_baseline_ix(seconds_target: float = 10.0) -> dict:
     from oracle.oracle import HostState, Oracle
     from topotrafficrl_amd import _abi
     from topotrafficrl_amd.intersection import VecIntersectionEnv, intersection_network, ix_cfg
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = host_threads()
     os.environ["OMP_NUM_THREADS"] = str(threads)
     cfg = VecIntersectionEnv.default_config()
     net = intersection_network()
@@ -129,20 +142,34 @@ def cpu_baseline_ix(seconds_target: float = 10.0) -> dict:
         if el >= seconds_target or steps >= 2000:
             break
     return {"value": live * 15 / el, "unit": "vehicle-steps/s (live vehicles)", "cores": threads, "kind": "port",
+            "host_cpus": os.cpu_count(),
             "sample": f"{E} intersection envs x {steps} env.step (15 frames + shuffled Kinematics + rewards + "
                       f"clear/spawn + auto-resets), float64 C restatement (oracle/ttrl_oracle.c), OpenMP over "
                       f"envs, {el:.1f} s"}
 
 
-def read_pmc(dtype: str, cfg_id: int) -> dict | None:
+def lib_sha16() -> str:
+    import hashlib
+    p = os.path.join(ROOT, "topotrafficrl_amd", "lib", "libttrl_mi355x.so")
+    return hashlib.sha256(open(p, "rb").read()).hexdigest()[:16]
+
+
+def read_pmc(dtype: str, cfg_id: int) -> tuple[dict | None, str]:
+    """The committed PMC profile of this configuration's kernels (profiles/pmc_traffic.json), used
+    only if it was measured on this very build of the kernel library (its sha256 prefix)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
-        return None
+        return None, "no profiles/pmc_traffic.json"
     try:
         d = json.load(open(p))
-        return d.get(f"config{cfg_id}_{dtype}")
-    except Exception:
-        return None
+    except ValueError:
+        return None, "unreadable profiles/pmc_traffic.json"
+    e = d.get(f"config{cfg_id}_{dtype}")
+    if e is None:
+        return None, f"no PMC profile for config {cfg_id} {dtype}"
+    if e.get("so_sha16") != lib_sha16():
+        return None, f"PMC profile {e.get('profile', '?')} was measured on another build of libttrl_mi355x.so"
+    return e, f"profiles/pmc_traffic.json ({e.get('profile', '?')}, libttrl_mi355x.so {e['so_sha16']})"
 
 
 def main():
@@ -151,7 +178,9 @@ def main():
     ap.add_argument("--steps", type=int, default=None, help="default 20 (config 6: 100)")
     ap.add_argument("--warmup", type=int, default=None, help="default 3 (config 6: 10)")
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
-    ap.add_argument("--config", type=int, default=4, choices=[2, 3, 4, 5, 6])
+    ap.add_argument("--config", type=int, default=4, choices=[1, 2, 3, 4, 5, 6])
+    ap.add_argument("--auto-reset", action="store_true",
+                    help="highway envs restart on termination inside env.step (the RL rollout mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--graph", action="store_true",
@@ -160,7 +189,7 @@ def main():
     # intersection steps are short (~2 ms) and their background resets settle over a few steps:
     # a longer timed window keeps the number stable from run to run
     if args.steps is None:
-        args.steps = 100 if args.config == 6 else 20
+        args.steps = 100 if args.config in (1, 6) else 20
     if args.warmup is None:
         args.warmup = 10 if args.config == 6 else 3
 
@@ -195,7 +224,7 @@ def main():
                                   "dtype": args.dtype, "env_id_offset": offset, "auto_reset": True})
     else:
         env = VecHighwayEnv({"num_envs": E, "vehicles_count": N, "observation": C["obs"], "device": str(dev),
-                             "dtype": args.dtype, "env_id_offset": offset})
+                             "dtype": args.dtype, "env_id_offset": offset, "auto_reset": bool(args.auto_reset)})
     policy = None
     if args.config == 5:
         from topotrafficrl_amd.agent import EgoAttentionPolicy
@@ -305,12 +334,15 @@ def main():
     rd, wr = state_bytes(args.dtype)
     alg_bytes = E * N * (rd + wr)  # per fused simulate launch
     kernel = "simulate_kernel (fused 15-frame Road.act+Road.step)"
-    if C["obs"]["type"] == "Kinematics" and not ix:  # the launch also writes the observation (ttrl_simulate_observe)
-        V, F = C["obs"]["vehicles_count"], len(C["obs"]["features"])
+    if C["obs"]["type"] == "Kinematics" and not ix:  # the launch also writes the observation (ttrl_env_step)
+        V = C["obs"].get("vehicles_count", 5)
+        F = len(C["obs"].get("features", ["presence", "x", "y", "vx", "vy"]))
         alg_bytes += E * (V * F * 4 + (V - 1) * 4)
         kernel = "simulate_kernel (fused 15-frame Road.act+Road.step + Kinematics observation)"
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    pmc = read_pmc(args.dtype, args.config)
+    pmc, pmc_source = read_pmc(args.dtype, args.config)
+    hbm = {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+           "traffic": (pmc or {}).get("hbm_bytes_per_launch"), "traffic_source": pmc_source}
     out = {
         "metric": "vehicle-steps/sec at 4096 envs×64 vehicles; 1/2/4/8 GPUs; HBM GB/s achieved",
         "value": value,
@@ -326,36 +358,38 @@ def main():
         "data": "synthetic",
         "config": {"workload": C["name"], "envs_per_gpu": E, "vehicles_per_env": N, "frames_per_step": 15,
                    "observation": C["obs"]["type"], "parallelism": f"env-sharded x{world}, no collective on the step",
-                   "hip_graph": bool(args.graph)},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
-                     "kernel": kernel,
-                     "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
-                     "alg_bytes_per_vehicle_step": alg_bytes / (E * N * 15.0)},
+                   "hip_graph": bool(args.graph), "auto_reset": bool(args.auto_reset or ix)},
+        # the HBM roofline of the fused launch: algorithmic bytes (state read + written once, the
+        # observation written once) over the launch time measured here with HIP events
+        "roofline": dict(bound="hbm", **hbm, kernel=kernel, kernel_ms=kern_ms, alg_bytes_per_launch=alg_bytes,
+                         alg_bytes_per_vehicle_step=alg_bytes / (E * N * 15.0)),
         "env_steps_per_s": world * E * args.steps / elapsed,
     }
-    if pmc and pmc.get("valu_insts_per_wave") and pmc.get("sq_waves"):
-        # The bound that applies: the fused kernel is VALU-issue bound, not HBM
-        # bound.  From the committed PMC profile of this kernel (profiles/pmc_traffic.json):
-        # SQ_ACTIVE_INST_VALU (quad-cycles, x4) summed over the launch's waves against every SIMD's
-        # cycles in the live kernel time (1024 SIMDs x the GRBM clock) -- the measured VALU-busy
-        # fraction; the instruction count is SQ_INSTS_VALU.
+    if pmc and pmc.get("valu_active_cycles_per_wave") and pmc.get("sq_waves"):
+        # The roofline that binds: the fused kernel is VALU-issue / latency bound,
+        # not HBM bound.  From the PMC profile of this build of the kernel (hash-checked):
+        # SQ_ACTIVE_INST_VALU (quad-cycles, x4) over the launch's waves against every SIMD's cycles in
+        # the kernel time measured here (1024 SIMDs x the GRBM clock) -- the VALU-busy fraction.
+        # The bound is the larger of the two fractions; the HBM view stays in roofline["hbm"].
         waves = pmc["sq_waves"]
         clk = pmc.get("effective_clock_ghz") or 2.4
-        simd_cycles = 1024 * clk * 1e9 * kern_ms * 1e-3
-        out["valu"] = {"insts_per_launch": pmc["valu_insts_per_wave"] * waves, "simd_cycles": simd_cycles,
-                       "source": "profiles/pmc_traffic.json (SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU, SQ_WAVES, GRBM clock)"}
-        if pmc.get("valu_active_cycles_per_wave"):
-            active = pmc["valu_active_cycles_per_wave"] * waves
-            out["valu"].update({"active_cycles_per_launch": active, "busy_frac": active / simd_cycles})
-            out["roofline"]["limiter"] = "valu" if active / simd_cycles > out["roofline"]["frac"] else "hbm"
+        simd_cycles_per_s = 1024 * clk * 1e9
+        active = pmc["valu_active_cycles_per_wave"] * waves
+        busy = active / (simd_cycles_per_s * kern_ms * 1e-3)
+        if busy > hbm["frac"]:
+            out["roofline"] = dict(bound="valu", achieved=active / (kern_ms * 1e-3), peak=simd_cycles_per_s,
+                                   unit="VALU-busy SIMD cycles/s", frac=busy, traffic=hbm["traffic"],
+                                   kernel=kernel, kernel_ms=kern_ms, alg_bytes_per_launch=alg_bytes,
+                                   alg_bytes_per_vehicle_step=alg_bytes / (E * N * 15.0), hbm=hbm,
+                                   valu_insts_per_launch=pmc["valu_insts_per_wave"] * waves,
+                                   counters=pmc_source + ": SQ_ACTIVE_INST_VALU, SQ_INSTS_VALU, SQ_WAVES, "
+                                                         "GRBM_GUI_ACTIVE")
     if grid_launches and C["obs"]["type"] == "OccupancyGrid":
         # the grid kernel: algorithmic bytes = each vehicle's x, y, heading, speed, lane, kind read
         # once + the [E, F, W, H] float32 grid written once
         g_ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in grid_launches]))
         r_ = 8 if args.dtype == "f64" else 4
-        cells = len(C["obs"]["features"]) * 32 * 32
+        cells = len(C["obs"]["features"]) * int(np.prod(env.observation_space.shape[1:]))
         g_bytes = E * (N * (4 * r_ + 4 + 1) + cells * 4)
         g_ach = g_bytes / (g_ms * 1e-3) / 1e9
         out["roofline_obs"] = {"bound": "hbm", "achieved": g_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -364,11 +398,10 @@ def main():
                                "alg_bytes_per_launch": g_bytes}
     if ix:
         out["config"]["live_vehicles_per_env"] = veh_steps / (world * E * 15 * args.steps)
-        out["config"]["auto_reset"] = True
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = (cpu_baseline_ix(args.cpu_seconds) if ix else
                                cpu_baseline(N, C["obs"] if C["obs"]["type"] == "Kinematics" else GRID7,
-                                            args.cpu_seconds))
+                                            args.cpu_seconds, envs=E, threads=1 if E == 1 else None))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

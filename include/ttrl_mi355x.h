@@ -24,6 +24,7 @@
  *                            IDMVehicle.__init__/randomize_behavior behavior.py:48-69
  *   ttrl_rewards             reward/termination template  ttrl_env/envs/intersection_env.py:78-119
  *   ttrl_rewards_step        + the step's time / info     ttrl_env/envs/common/abstract.py:169-186, :239
+ *   ttrl_auto_reset_highway  AbstractEnv.reset of the finished envs inside env.step (abstract.py:188-214)
  *   ttrl_ix_reset            IntersectionEnv._reset        ttrl_env/envs/intersection_env.py:135-318
  *                            (_make_vehicles :251-318, _spawn_vehicle :320-348, AbstractEnv.reset abstract.py:188-214)
  *   ttrl_ix_clear_spawn      IntersectionEnv.step tail     ttrl_env/envs/intersection_env.py:135-139
@@ -329,6 +330,13 @@ int ttrl_reset_highway_seeded(const ttrl_state_t* s, const ttrl_lane_table_t* ro
                               const ttrl_params_t* p, const ttrl_reset_cfg_t* cfg,
                               const uint32_t* entropy, int32_t n_words, const uint8_t* mask,
                               void* stream);
+/* VecHighwayEnv.step's auto-reset in one launch: done[e] = terminated[e] | truncated[e]; each done
+ * env increments entropy[e][episode_word] (its episode counter), is regenerated as by
+ * ttrl_reset_highway_seeded from the incremented words (n_words <= 8) and gets time[e] = 0. */
+int ttrl_auto_reset_highway(const ttrl_state_t* s, const ttrl_lane_table_t* road,
+                            const ttrl_params_t* p, const ttrl_reset_cfg_t* cfg, uint32_t* entropy,
+                            int32_t n_words, int32_t episode_word, const uint8_t* terminated,
+                            const uint8_t* truncated, double* time, uint8_t* done, void* stream);
 /* Host helper: the initial PCG64 state {state_hi, state_lo, inc_hi, inc_lo} of
  * np.random.PCG64(SeedSequence(entropy words)) (numpy bit_generator.pyx / pcg64.h). */
 int ttrl_seed_pcg64(const uint32_t* entropy, int32_t n_words, uint64_t* state4);

@@ -14,8 +14,8 @@ from topotrafficrl_amd.state import BatchState
 LANES = ops.struct_tensor(_abi.straight_lane_table(4))
 PARAMS = ops.struct_tensor(_abi.default_params())
 MUTATES = {"simulate_", "road_act_", "road_step_", "meta_action_", "env_step_", "kinematics_obs",
-           "kinematics_obs_masked_", "reset_highway_", "reset_highway_seeded_", "ix_reset_", "ix_clear_spawn_",
-           "copy_envs_"}
+           "kinematics_obs_masked_", "reset_highway_", "reset_highway_seeded_", "auto_reset_highway_", "ix_reset_",
+           "ix_clear_spawn_", "copy_envs_"}
 
 
 def test_every_device_entry_point_is_an_operator():
@@ -25,7 +25,8 @@ def test_every_device_entry_point_is_an_operator():
                           "kinematics_obs": "observe_kinematics", "kinematics_obs_masked_": "observe_kinematics_masked",
                           "occupancy_grid": "observe_grid", "observe_ttc": "observe_ttc",
                           "observe_lidar": "observe_lidar", "reset_highway_": "reset_highway",
-                          "reset_highway_seeded_": "reset_highway_seeded", "ix_reset_": "ix_reset",
+                          "reset_highway_seeded_": "reset_highway_seeded",
+                          "auto_reset_highway_": "auto_reset_highway", "ix_reset_": "ix_reset",
                           "ix_clear_spawn_": "ix_clear_spawn", "copy_envs_": "copy_envs", "rewards": "rewards",
                           "rewards_ex": "rewards_ex", "rewards_step_": "rewards_step",
                           "ego_attention_q": "ego_attention_q"}[o] for o in ops.OPS}
@@ -43,7 +44,7 @@ def test_schemas_declare_mutation(name):
 
 
 def test_time_is_mutated_by_the_step_ops():
-    for name in ("env_step_", "rewards_step_"):
+    for name in ("env_step_", "rewards_step_", "auto_reset_highway_"):
         s = getattr(torch.ops.ttrl, name).default._schema
         t = [a for a in s.arguments if a.name == "time"][0]
         assert t.alias_info is not None and t.alias_info.is_write
@@ -239,6 +240,37 @@ def test_reset_ops_equal_the_c_abi(hip_device):
     torch.ops.ttrl.reset_highway_seeded_(other.tensors(), lanes, params, cfg, words, mask)
     torch.cuda.synchronize()
     _equal(st, other)
+
+
+@pytest.mark.gpu
+def test_auto_reset_op_equals_the_c_abi_and_the_seeded_reset(hip_device):
+    """ttrl::auto_reset_highway_ == its C ABI call, and == the bookkeeping done by hand (done mask,
+    episode word + 1, time 0) followed by ttrl_reset_highway_seeded of the done envs."""
+    env, other = _pair(hip_device)
+    third = env.state.clone()
+    lib = _lib.load()
+    lanes, params, cfg = ops.st(env.network.table), ops.st(env.params), ops.st(env.reset_cfg)
+    R, P, RC = C.byref(env.network.table), C.byref(env.params), C.byref(env.reset_cfg)
+    g = torch.Generator(device=hip_device).manual_seed(5)
+    term = torch.rand(64, device=hip_device, generator=g) < 0.2
+    trunc = torch.rand(64, device=hip_device, generator=g) < 0.1
+    ent = torch.randint(0, 2 ** 31, (64, 3), dtype=torch.int32, device=hip_device, generator=g)
+    e1, e2, e3 = ent.clone(), ent.clone(), ent.clone()
+    t1 = torch.full((64,), 7.0, dtype=torch.float64, device=hip_device)
+    t2, t3 = t1.clone(), t1.clone()
+    d1 = torch.empty(64, dtype=torch.uint8, device=hip_device)
+    assert lib.ttrl_auto_reset_highway(_c(env.state), R, P, RC, e1.data_ptr(), 3, 2, term.data_ptr(), trunc.data_ptr(),
+                                       t1.data_ptr(), d1.data_ptr(), _stream()) == 0
+    d2 = torch.ops.ttrl.auto_reset_highway_(other.tensors(), lanes, params, cfg, e2, 2, term, trunc, t2)
+    done = term | trunc
+    e3[:, 2] += done.to(torch.int32)
+    t3.masked_fill_(done, 0.0)
+    torch.ops.ttrl.reset_highway_seeded_(third.tensors(), lanes, params, cfg, e3, done.to(torch.uint8))
+    torch.cuda.synchronize()
+    assert torch.equal(d1.bool(), d2) and torch.equal(d2, done)
+    assert torch.equal(e1, e2) and torch.equal(e2, e3) and torch.equal(t1, t2) and torch.equal(t2, t3)
+    _equal(env.state, other)
+    _equal(other, third)
 
 
 @pytest.mark.gpu

@@ -41,6 +41,9 @@ def mean(v):
     return sum(v) / len(v) if v else float("nan")
 
 
+import hashlib  # noqa: E402
+SO_SHA16 = hashlib.sha256(open(os.path.join(ROOT, "topotrafficrl_amd", "lib", "libttrl_mi355x.so"), "rb").read()
+                          ).hexdigest()[:16]  # the build the counters were measured on (shipped from this tree)
 out_json = {}
 md = [f"# Profile {TAG}: `python bench.py` (config 4: 4096 envs x 64 vehicles, Kinematics 15x7), MI355X", ""]
 for dt in ("f64", "f32"):
@@ -82,7 +85,7 @@ for dt in ("f64", "f32"):
         "salu_insts_per_wave": salu / waves, "effective_clock_ghz": clk,
         # SQ_ACTIVE_INST_VALU counts quad-cycles (4 shader cycles) per wave
         "valu_active_cycles_per_wave": 4 * act_valu / waves,
-        "kernel_ns_trace_avg": sim_avg}
+        "kernel_ns_trace_avg": sim_avg, "profile": TAG, "so_sha16": SO_SHA16}
     md += ["", f"Fused `{simk}`: trace avg {sim_avg / 1e3:.1f} us per 15-frame launch "
                f"(bench line under rocprof: {e['value']:.3e} veh-steps/s).",
            f"* HBM per launch (PMC, separate passes): FETCH_SIZE {f_kib:.0f} KiB (x2 gfx950) + WRITE_SIZE "
@@ -102,7 +105,8 @@ if os.path.exists(c3):
     write, _ = counters(os.path.join(SRC, "write_c3_counter_collection.csv"))
     e = json.loads(open(os.path.join(SRC, "bench_trace_c3.json")).read().strip().splitlines()[-1])
     stats = {short(r["Name"]): float(r["AverageNs"]) for r in csv.DictReader(open(c3))}
-    entry = {"note": "hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024; FETCH_SIZE doubled per the gfx950 calibration"}
+    entry = {"note": "hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024; FETCH_SIZE doubled per the gfx950 calibration",
+             "profile": TAG, "so_sha16": SO_SHA16}
     md += ["## config 3 (4096 x 128, OccupancyGrid 7x32x32), f64", "", "| kernel | avg us | HBM MB per launch | algorithmic MB |",
            "|---|---|---|---|"]
     for tag, pat, alg in (("", SIM, e["roofline"]["alg_bytes_per_launch"]),

@@ -33,6 +33,7 @@ _SIGS = {
     "ttrl_observe_lidar": ([_P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_reset_highway": ([_P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_reset_highway_seeded": ([_P, _P, _P, _P, _P, C.c_int32, _P, _P], C.c_int),
+    "ttrl_auto_reset_highway": ([_P, _P, _P, _P, _P, C.c_int32, C.c_int32, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_seed_pcg64": ([_P, C.c_int32, _P], C.c_int),
     "ttrl_rewards": ([_P, _P, _P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_rewards_ex": ([_P, _P, _P, _P, _P, _P, _P, _P, _P], C.c_int),

@@ -259,6 +259,11 @@ __device__ __forceinline__ void lane_position(const LaneT<T>& L, T s, T r, T& x,
   x = L.sx + s * L.dx + r * (-L.dy);
   y = L.sy + s * L.dy + r * L.dx;
 }
+template <typename T>
+__device__ __forceinline__ void lane_position_straight(const LaneT<T>& L, T s, T r, T& x, T& y) {
+  x = L.sx + s * L.dx + r * (-L.dy);  // StraightLane.position lane.py:199-204
+  y = L.sy + s * L.dy + r * L.dx;
+}
 
 template <typename T>
 __host__ __device__ inline LaneT<T> make_lane(const ttrl_lane_table_t& R, int l) {
@@ -3076,14 +3081,16 @@ struct SeedSeq {
   }
 };
 
-// RoadNetwork.get_closest_lane_index (road.py:55-71) in float64 over every lane, first minimum.
+// RoadNetwork.get_closest_lane_index (road.py:55-71) in float64 over every lane, first minimum
+// (CV = false: straight lanes along +x only, see lane_local).
+template <bool CV = true>
 __device__ inline int closest_lane_index(const ttrl_lane_table_t& R, double x, double y, double h) {
   int best = 0; double bd = 0;
   for (int l = 0; l < R.n_lanes; ++l) {
     const LaneT<double> L = make_lane<double>(R, l);
     double s, r;
-    lane_local(L, x, y, s, r);
-    const double ang = fabs(wrap_to_pi(h - heading_at(L, s)));
+    lane_local<CV>(L, x, y, s, r);
+    const double ang = fabs(wrap_to_pi(h - heading_at<CV>(L, s)));
     double a = s - R.length[l]; if (!(a > 0)) a = 0;
     double c = 0 - s; if (!(c > 0)) c = 0;
     const double d = fabs(r) + a + c + 1.0 * ang;
@@ -3152,22 +3159,23 @@ __device__ void reset_env_serial(const ttrl_state_t& st, const ttrl_lane_table_t
   }
 }
 
-// numpy pcg64_advance (pcg_advance_lcg_128): the LCG state `delta` steps ahead, by
-// square-and-multiply of the affine map s -> M s + inc.
-__device__ __forceinline__ U128 pcg_advance(U128 st, U128 inc, unsigned long long delta) {
-  U128 acc_mult = {0ull, 1ull}, acc_plus = {0ull, 0ull};
-  U128 cur_mult = {0x2360ED051FC65DA4ull, 0x4385DF649FCCF645ull}, cur_plus = inc;
-  while (delta) {
-    if (delta & 1ull) {
-      acc_mult = mul128(acc_mult, cur_mult);
-      acc_plus = add128(mul128(acc_plus, cur_mult), cur_plus);
-    }
-    cur_plus = mul128(add128(cur_mult, U128{0ull, 1ull}), cur_plus);
-    cur_mult = mul128(cur_mult, cur_mult);
-    delta >>= 1;
-  }
-  return add128(mul128(acc_mult, st), acc_plus);
+// A double of lane `l` (wave-uniform index) of the wavefront, as a uniform value.
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+
+__device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int src) {
+  const unsigned lo = (unsigned)__shfl((int)(unsigned)v, src & 63, 64);
+  const unsigned hi = (unsigned)__shfl((int)(unsigned)(v >> 32), src & 63, 64);
+  return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ double shfl_d(double v, int src) {
+  return __longlong_as_double((long long)shfl_u64((unsigned long long)__double_as_longlong(v), src));
+}
+
 __device__ __forceinline__ unsigned long long pcg_output(U128 st) {  // pcg_next64's output of a state
   const unsigned long long x = st.hi ^ st.lo;
   const unsigned rot = (unsigned)(st.hi >> 58);
@@ -3181,20 +3189,48 @@ __device__ __forceinline__ double pcg_unit(unsigned long long o) {
 // auto-reset on the critical path of env.step.  numpy's draw order is sequential, but its stream
 // is not: vehicle i (1-based) consumes the 64-bit outputs from index c(i) = 3 (i - 1) + i / 2 on
 // (odd i: one output for integers(0, lanes) -- its high half buffered -- and three for the
-// uniforms; even i: the buffered half, then three), so every lane jumps its own generator copy
-// to c(i) (pcg_advance) and draws its vehicle's lane, speed, gap and DELTA in parallel.  Only the
-// placement is a recurrence (x0 = the max s on the drawn lane so far + the gap): one lane walks
-// it over the drawn gaps in LDS with reset_env_serial's exact arithmetic; then every lane assigns its
-// vehicle's lane and timer and the rows are written coalesced.  A Lemire rejection in
+// uniforms; even i: the buffered half, then three).  The LCG step s -> M s + inc is affine, so a
+// scan of the vehicles' k-step maps (M^k, 1 + M + .. + M^(k-1)) over the wavefront gives every lane
+// its generator state at c(i) (numpy pcg64_advance, in parallel), and each lane draws its
+// vehicle's lane, speed, gap and DELTA.  Only the placement is a recurrence (x0 = the max s on the
+// drawn lane so far + the gap): it runs wave-uniformly with reset_env_serial's exact arithmetic --
+// on the highway (straight +x lanes from one start x) as one chain of float64 adds -- then every
+// lane assigns its vehicle's pose, lane and timer and the rows are written coalesced.  A Lemire rejection in
 // integers() (probability < 2^-31 per draw, never for a power-of-two lane count) would shift the
 // stream: such an env is regenerated by the sequential replay (reset_env_serial).
-template <typename T>
+// AutoReset: the env.step auto-reset bookkeeping folded into the reset launch (ttrl_auto_reset_highway):
+// done = terminated | truncated, written to done_out; a done env bumps its entropy word `ep_word`
+// (the episode counter), seeds from the bumped words and gets time = 0.
+struct AutoReset {
+  const uint8_t* term;
+  const uint8_t* trunc;
+  double* time;
+  uint8_t* done_out;
+  int ep_word;
+};
+
+template <typename T, bool CV>
 __global__ void __launch_bounds__(64) reset_wave_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P,
                                                         ttrl_reset_cfg_t cfg, const unsigned long long* __restrict__ pcg,
-                                                        const unsigned* __restrict__ words, int n_words,
-                                                        const uint8_t* __restrict__ mask) {
+                                                        unsigned* __restrict__ words, int n_words,
+                                                        const uint8_t* __restrict__ mask, AutoReset ar) {
   const int env = blockIdx.x, lane = threadIdx.x;
-  if (env >= st.n_envs || (mask && !mask[env])) return;
+  if (env >= st.n_envs) return;
+  if (ar.term) {  // auto-reset: the done mask, episode counter and time in the same launch
+    const bool done = ar.term[env] || ar.trunc[env];
+    if (lane == 0) ar.done_out[env] = (uint8_t)done;
+    if (!done) return;
+  } else if (mask && !mask[env]) {
+    return;
+  }
+#ifdef TTRL_RESET_TRACE  // -DTTRL_RESET_TRACE: phase clocks of a few envs (tools/reset_phases.py)
+  long long tr[8];
+  int ntr = 0;
+#define RT() tr[ntr++] = wall_clock64()
+  RT();
+#else
+#define RT()
+#endif
   const int N = st.n_veh, nl = R.n_lanes, nv = min(cfg.n_vehicles, N);
   const size_t b = (size_t)env * N;
   T* X = (T*)st.x; T* Y = (T*)st.y; T* Hh = (T*)st.heading; T* Vv = (T*)st.speed; T* TS = (T*)st.target_speed;
@@ -3202,30 +3238,48 @@ __global__ void __launch_bounds__(64) reset_wave_kernel(ttrl_state_t st, ttrl_la
   unsigned long long s4[4];
   if (pcg) {
     for (int k = 0; k < 4; ++k) s4[k] = pcg[4 * env + k];
+  } else if (ar.term) {  // (n_words <= 8; the bumped word picked by selects: no scratch array)
+    unsigned w[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      w[q] = q < n_words ? words[(size_t)env * n_words + q] + (q == ar.ep_word ? 1u : 0u) : 0u;
+    SeedSeq::pcg64_seed(w, n_words, s4);
+    if (lane == 0) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (q == ar.ep_word) words[(size_t)env * n_words + q] = w[q];
+      ar.time[env] = 0.0;
+    }
   } else {
     SeedSeq::pcg64_seed(words + (size_t)env * n_words, n_words, s4);
   }
   const U128 s0 = {s4[0], s4[1]}, inc = {s4[2], s4[3]};
-  __shared__ double s_d[64], s_px[64], s_py[64], s_ph[64];
-  __shared__ int s_lid[64];
-  __shared__ double smax[LMAX];  // the max s per lane of the vehicles placed so far (lane 0)
-  // the ego MDPVehicle (lane 0 of the first chunk)
+  RT();
+  // lane k < nl keeps lane k's geometry and the max s on lane k of the vehicles placed so far
+  LaneT<double> myL;
+  if (lane < nl) myL = make_lane<double>(R, lane);
+  double my_smax = 0;
+  // the ego MDPVehicle (slot 0)
   double ex = 0, ey = 0, eh = 0;
   {
     const LaneT<double> L = make_lane<double>(R, cfg.ego_lane);
     lane_position(L, cfg.ego_x, 0.0, ex, ey);
     eh = heading_at(L, cfg.ego_x);
-    if (lane == 0)
-      for (int l = 0; l < nl; ++l) {
-        double s, r;
-        lane_local(make_lane<double>(R, l), ex, ey, s, r);
-        smax[l] = s;
-      }
+    if (lane < nl) {
+      double s, r;
+      lane_local<CV>(myL, ex, ey, s, r);
+      my_smax = s;
+    }
   }
+  // straight +x lanes from one start x (the highway): one running max of s for every lane
+  const double sx0 = readlane_d(myL.sx, 0);
+  const bool same_start = !CV && !__any(lane < nl && myL.sx != sx0);
+  double run_max = readlane_d(my_smax, 0);
   const unsigned rng_ = (unsigned)nl - 1;
   const unsigned long long rexcl = (unsigned long long)rng_ + 1;
   const unsigned thr = nl > 1 ? (unsigned)((0xFFFFFFFFull - rng_) % rexcl) : 0u;
   unsigned carry_hi = 0;  // the buffered half of the previous chunk's last (odd) vehicle
+  U128 chunk_state = s0, next_state = s0;  // the LCG state at the chunk's first draw
   bool reject = false;
   for (int c0 = 0; c0 < N; c0 += 64) {
     const int i = c0 + lane;
@@ -3235,19 +3289,47 @@ __global__ void __launch_bounds__(64) reset_wave_kernel(ttrl_state_t st, ttrl_la
     int lid = 0;
     unsigned u32 = 0, hi32 = 0;
     unsigned long long o1 = 0, o2 = 0, o3 = 0;
-    if (drawn) {
-      const U128 M = {0x2360ED051FC65DA4ull, 0x4385DF649FCCF645ull};
-      const unsigned long long ci = 3ull * (unsigned long long)(i - 1) + (unsigned long long)(i / 2);
-      U128 g = pcg_advance(s0, inc, ci);
-      if (i & 1) {  // integers(0, lanes) draws a fresh output: low half now, high half buffered
-        g = add128(mul128(g, M), inc);
-        const unsigned long long o = pcg_output(g);
-        u32 = (unsigned)o;
-        hi32 = (unsigned)(o >> 32);
+    {
+      // the LCG state before vehicle i: the chunk's start state advanced by the exclusive prefix of
+      // the vehicles' output counts (4 odd, 3 even, 0 the ego), as a scan of affine maps
+      // s -> A s + C inc over the wave (A, C: powers and partial sums of the multiplier)
+      const int len = drawn ? ((i & 1) ? 4 : 3) : 0;
+      U128 A = {0ull, 1ull}, Cs = {0ull, 0ull};  // identity
+      // M^3, 1 + M + M^2 and M^4, 1 + M + M^2 + M^3 (mod 2^128), M the PCG64 multiplier
+      if (len == 3) { A = {0x25f041404bd80e82ull, 0xeb5ae837ed42153dull}; Cs = {0x3b1dd060ff2fd1e0ull, 0x9624b94fc0ada4dfull}; }
+      if (len == 4) { A = {0xf4dd417327db7a9bull, 0xd194dfbe42d45771ull}; Cs = {0x610e11a14b07e063ull, 0x817fa187adefba1cull}; }
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {  // inclusive scan: (A, Cs) <- own o earlier
+        U128 Ap, Cp;
+        Ap.hi = shfl_u64(A.hi, lane - off); Ap.lo = shfl_u64(A.lo, lane - off);
+        Cp.hi = shfl_u64(Cs.hi, lane - off); Cp.lo = shfl_u64(Cs.lo, lane - off);
+        if (lane >= off) {
+          Cs = add128(mul128(A, Cp), Cs);
+          A = mul128(A, Ap);
+        }
       }
-      g = add128(mul128(g, M), inc); o1 = pcg_output(g);
-      g = add128(mul128(g, M), inc); o2 = pcg_output(g);
-      g = add128(mul128(g, M), inc); o3 = pcg_output(g);
+      // exclusive: the maps of the lanes below; the chunk's start state from the carry
+      U128 Ae, Ce;
+      Ae.hi = shfl_u64(A.hi, lane - 1); Ae.lo = shfl_u64(A.lo, lane - 1);
+      Ce.hi = shfl_u64(Cs.hi, lane - 1); Ce.lo = shfl_u64(Cs.lo, lane - 1);
+      if (lane == 0) { Ae = {0ull, 1ull}; Ce = {0ull, 0ull}; }
+      U128 g = add128(mul128(Ae, chunk_state), mul128(Ce, inc));
+      U128 An, Cn;  // the whole chunk (lane 63's inclusive map): the next chunk's start state
+      An.hi = shfl_u64(A.hi, 63); An.lo = shfl_u64(A.lo, 63);
+      Cn.hi = shfl_u64(Cs.hi, 63); Cn.lo = shfl_u64(Cs.lo, 63);
+      next_state = add128(mul128(An, chunk_state), mul128(Cn, inc));
+      if (drawn) {
+        const U128 M = {0x2360ED051FC65DA4ull, 0x4385DF649FCCF645ull};
+        if (i & 1) {  // integers(0, lanes) draws a fresh output: low half now, high half buffered
+          g = add128(mul128(g, M), inc);
+          const unsigned long long o = pcg_output(g);
+          u32 = (unsigned)o;
+          hi32 = (unsigned)(o >> 32);
+        }
+        g = add128(mul128(g, M), inc); o1 = pcg_output(g);
+        g = add128(mul128(g, M), inc); o2 = pcg_output(g);
+        g = add128(mul128(g, M), inc); o3 = pcg_output(g);
+      }
     }
     // even vehicles take the previous (odd) vehicle's buffered half: lane - 1, or the carry
     const unsigned prev_hi = (unsigned)__shfl((int)hi32, (lane + 63) & 63, 64);
@@ -3264,28 +3346,64 @@ __global__ void __launch_bounds__(64) reset_wave_kernel(ttrl_state_t st, ttrl_la
       delta = cfg.delta_lo + (cfg.delta_hi - cfg.delta_lo) * pcg_unit(o3);
     }
     carry_hi = (unsigned)__shfl((int)hi32, 63, 64);
-    s_d[lane] = d;
-    s_lid[lane] = lid;
-    __syncthreads();
-    // ---- the placement recurrence (one lane; reset_env_serial's arithmetic)
-    if (lane == 0) {
-      const int n = min(64, nv - c0);
+    chunk_state = next_state;
+    if (c0 == 0) RT();
+    // ---- the placement recurrence, in draw order: x0 = (max s on the drawn lane) + gap; the
+    // vehicle's pose is computed wave-uniformly, then every lane k < nl folds its own s into its max
+    double px = 0, py = 0, ph = 0;
+    const int n = min(64, nv - c0);
+    if (!CV && same_start) {
+      // every lane straight along +x from one start x: a vehicle's s is the same on every lane, so
+      // the per-lane maxima are one running max and the recurrence is a chain of float64 adds
+      // (the same operations as the general path, hence the same bits)
+      double x0_own = 0;
+#pragma unroll 8
       for (int q = c0 == 0 ? 1 : 0; q < n; ++q) {
-        const int l = s_lid[q];
-        double x0 = smax[l];
-        x0 += s_d[q];
-        const LaneT<double> L = make_lane<double>(R, l);
-        double px, py;
-        lane_position(L, x0, 0.0, px, py);
-        s_px[q] = px; s_py[q] = py; s_ph[q] = heading_at(L, x0);
-        for (int k = 0; k < nl; ++k) {
+        double x0 = run_max;
+        x0 += readlane_d(d, q);
+        const double qx = sx0 + x0 * 1.0 + 0.0 * (-0.0);  // lane_position_straight's x
+        const double sq = qx - sx0;                        // lane_local's s
+        if (sq > run_max) run_max = sq;
+        if (lane == q) x0_own = x0;
+      }
+      // the pose on the drawn lane, from that lane's geometry (shuffles with every lane active:
+      // a bpermute from an inactive lane returns 0)
+      LaneT<double> L = {};
+      L.sx = shfl_d(myL.sx, lid); L.sy = shfl_d(myL.sy, lid);
+      L.dx = shfl_d(myL.dx, lid); L.dy = shfl_d(myL.dy, lid);
+      L.hd = shfl_d(myL.hd, lid);
+      if (i < nv && i >= 1) {
+        lane_position_straight(L, x0_own, 0.0, px, py);
+        ph = L.hd;
+      }
+    } else {
+      for (int q = c0 == 0 ? 1 : 0; q < n; ++q) {
+        const int lq = __builtin_amdgcn_readlane(lid, q);
+        double x0 = readlane_d(my_smax, lq);
+        x0 += readlane_d(d, q);
+        double qx, qy, qh;
+        if constexpr (!CV) {  // straight +x lanes: the drawn lane's geometry from the lane holding it
+          LaneT<double> L = {};
+          L.type = TTRL_LANE_STRAIGHT;
+          L.sx = readlane_d(myL.sx, lq); L.sy = readlane_d(myL.sy, lq);
+          L.dx = readlane_d(myL.dx, lq); L.dy = readlane_d(myL.dy, lq);
+          L.hd = readlane_d(myL.hd, lq);
+          lane_position_straight(L, x0, 0.0, qx, qy);
+          qh = L.hd;
+        } else {
+          const LaneT<double> L = make_lane<double>(R, lq);
+          lane_position(L, x0, 0.0, qx, qy);
+          qh = heading_at(L, x0);
+        }
+        if (lane == q) { px = qx; py = qy; ph = qh; }
+        if (lane < nl) {
           double s, r;
-          lane_local(make_lane<double>(R, k), px, py, s, r);
-          if (s > smax[k]) smax[k] = s;
+          lane_local<CV>(myL, qx, qy, s, r);
+          if (s > my_smax) my_smax = s;
         }
       }
     }
-    __syncthreads();
+    if (c0 == 0) RT();
     // ---- every slot of the chunk, coalesced
     if (i < N) {
       const size_t k = b + i;
@@ -3295,17 +3413,16 @@ __global__ void __launch_bounds__(64) reset_wave_kernel(ttrl_state_t st, ttrl_la
       if (i == 0) {
         st.kind[k] = TTRL_MDP; st.lane_change[k] = 0;
         X[k] = T(ex); Y[k] = T(ey); Hh[k] = T(eh); Vv[k] = T(cfg.ego_speed);
-        const int ln = closest_lane_index(R, ex, ey, eh);
+        const int ln = closest_lane_index<CV>(R, ex, ey, eh);
         st.lane[k] = st.target_lane[k] = ln;
         const int si = speed_to_index(P, cfg.ego_speed);
         st.speed_index[k] = si;
         TS[k] = T(P.target_speeds[si]);
         TM[k] = z; DL[k] = T(4);
       } else if (i < nv) {
-        const double px = s_px[lane], py = s_py[lane], ph = s_ph[lane];
         st.kind[k] = TTRL_IDM; st.lane_change[k] = (uint8_t)cfg.lane_change;
         X[k] = T(px); Y[k] = T(py); Hh[k] = T(ph); Vv[k] = T(sp); TS[k] = T(sp);
-        const int ln = closest_lane_index(R, px, py, ph);
+        const int ln = closest_lane_index<CV>(R, px, py, ph);
         st.lane[k] = st.target_lane[k] = ln;
         st.speed_index[k] = -1;
         TM[k] = T(pymod((px + py) * 3.141592653589793, P.lane_change_delay));
@@ -3316,9 +3433,16 @@ __global__ void __launch_bounds__(64) reset_wave_kernel(ttrl_state_t st, ttrl_la
         DL[k] = T(4); st.lane[k] = st.target_lane[k] = 0; st.speed_index[k] = -1;
       }
     }
-    __syncthreads();
   }
+#ifdef TTRL_RESET_TRACE
+  RT();
+  if (lane == 0 && (env % 512) == 7)
+    printf("reset env %d: seed %lld draws %lld place %lld store %lld (wall clocks, 100 MHz)\n", env, tr[1] - tr[0],
+           tr[2] - tr[1], tr[3] - tr[2], tr[4] - tr[3]);
+#endif
+#undef RT
   if (__any(reject)) {  // a rejected integers() draw shifts the stream: replay this env in order
+    __threadfence_block();
     __syncthreads();
     if (lane == 0) {
       Pcg g;
@@ -3328,8 +3452,6 @@ __global__ void __launch_bounds__(64) reset_wave_kernel(ttrl_state_t st, ttrl_la
   }
 }
 
-// IntersectionEnv._agent_reward / _is_terminated / _is_truncated (intersection_env.py:78-119) and
-// has_arrived (:364-369) for the env's controlled vehicle (its first MDP slot).
 // IntersectionEnv._agent_reward / _is_terminated / _is_truncated (intersection_env.py:78-119) for one
 // env's ego (has_ego false: no controlled vehicle) and AbstractEnv.step's time += 1 / policy
 // frequency (abstract.py:239); ego_speed / ego_crashed: the info's speed / crashed (abstract.py:169-186),
@@ -3741,6 +3863,22 @@ int check_state(const ttrl_state_t* s, const ttrl_lane_table_t* R) {
 
 int slots_for(int n) { return n <= 32 ? 32 : n <= 64 ? 64 : n <= 128 ? 128 : 256; }
 
+// The reset instance for a road: CV = false when every lane is straight along +x (the highway).
+template <typename T>
+void launch_reset(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P,
+                  const ttrl_reset_cfg_t& cfg, const unsigned long long* pcg, unsigned* words, int n_words,
+                  const uint8_t* mask, const AutoReset& ar, hipStream_t st) {
+  bool curved = false;
+  for (int l = 0; l < R.n_lanes; ++l)
+    curved |= R.type[l] != TTRL_LANE_STRAIGHT || R.dir_x[l] != 1.0 || R.dir_y[l] != 0.0;
+  if (curved)
+    hipLaunchKernelGGL((reset_wave_kernel<T, true>), dim3(s.n_envs), dim3(64), 0, st, s, R, P, cfg, pcg, words,
+                       n_words, mask, ar);
+  else
+    hipLaunchKernelGGL((reset_wave_kernel<T, false>), dim3(s.n_envs), dim3(64), 0, st, s, R, P, cfg, pcg, words,
+                       n_words, mask, ar);
+}
+
 int launch_status() { return hipGetLastError() == hipSuccess ? TTRL_OK : TTRL_E_LAUNCH; }
 
 template <typename T, int NS, int EPW>
@@ -3758,7 +3896,7 @@ int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_par
   const size_t lds = host_view_bytes(sizeof(T) == 8 ? TTRL_F64 : TTRL_F32, EPW, NS,
                                      graph || curved ? R.n_lanes : STRAIGHT_LANE_CAP, graph,
                                      !graph && !curved && sorted_view(NS, EPW, NET_STRAIGHT));
-  if (ob.obs) {  // the observation's scratch must fit the act phase's block it overlays (it does for every NS)
+  if (ob.obs || ob.reward) {  // the tail's scratch must fit the act phase's block it overlays (it does for every NS)
     const ViewLayout o = view_layout<T>(EPW, NS, graph || curved ? R.n_lanes : STRAIGHT_LANE_CAP, graph,
                                         !graph && !curved && sorted_view(NS, EPW, NET_STRAIGHT));
     const size_t M = (size_t)EPW * NS;
@@ -4028,11 +4166,9 @@ int ttrl_reset_highway(const ttrl_state_t* s, const ttrl_lane_table_t* road, con
   if (s->n_envs == 0) return TTRL_OK;
   hipStream_t st = (hipStream_t)stream;
   if (s->dtype == TTRL_F64)
-    hipLaunchKernelGGL(reset_wave_kernel<double>, dim3(s->n_envs), dim3(64), 0, st, *s, *road, *p, *cfg,
-                       (const unsigned long long*)pcg, (const unsigned*)nullptr, 0, (const uint8_t*)nullptr);
+    launch_reset<double>(*s, *road, *p, *cfg, (const unsigned long long*)pcg, nullptr, 0, nullptr, AutoReset{}, st);
   else
-    hipLaunchKernelGGL(reset_wave_kernel<float>, dim3(s->n_envs), dim3(64), 0, st, *s, *road, *p, *cfg,
-                       (const unsigned long long*)pcg, (const unsigned*)nullptr, 0, (const uint8_t*)nullptr);
+    launch_reset<float>(*s, *road, *p, *cfg, (const unsigned long long*)pcg, nullptr, 0, nullptr, AutoReset{}, st);
   return launch_status();
 }
 
@@ -4047,11 +4183,29 @@ int ttrl_reset_highway_seeded(const ttrl_state_t* s, const ttrl_lane_table_t* ro
   if (s->n_envs == 0) return TTRL_OK;
   hipStream_t st = (hipStream_t)stream;
   if (s->dtype == TTRL_F64)
-    hipLaunchKernelGGL(reset_wave_kernel<double>, dim3(s->n_envs), dim3(64), 0, st, *s, *road, *p, *cfg,
-                       (const unsigned long long*)nullptr, (const unsigned*)entropy, (int)n_words, mask);
+    launch_reset<double>(*s, *road, *p, *cfg, nullptr, (unsigned*)entropy, (int)n_words, mask, AutoReset{}, st);
   else
-    hipLaunchKernelGGL(reset_wave_kernel<float>, dim3(s->n_envs), dim3(64), 0, st, *s, *road, *p, *cfg,
-                       (const unsigned long long*)nullptr, (const unsigned*)entropy, (int)n_words, mask);
+    launch_reset<float>(*s, *road, *p, *cfg, nullptr, (unsigned*)entropy, (int)n_words, mask, AutoReset{}, st);
+  return launch_status();
+}
+
+int ttrl_auto_reset_highway(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                            const ttrl_reset_cfg_t* cfg, uint32_t* entropy, int32_t n_words, int32_t episode_word,
+                            const uint8_t* terminated, const uint8_t* truncated, double* time, uint8_t* done,
+                            void* stream) {
+  int rc = check_state(s, road);
+  if (rc) return rc < 0 ? rc : TTRL_OK;
+  if (!p || !cfg || !entropy || !terminated || !truncated || !time || !done || n_words < 1 || n_words > 8 ||
+      episode_word < 0 || episode_word >= n_words || cfg->n_vehicles < 1 || cfg->n_vehicles > s->n_veh ||
+      cfg->ego_lane < 0 || cfg->ego_lane >= road->n_lanes || p->n_target_speeds < 1 || p->n_target_speeds > 8)
+    return TTRL_E_ARG;
+  if (s->n_envs == 0) return TTRL_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const AutoReset ar{terminated, truncated, time, done, episode_word};
+  if (s->dtype == TTRL_F64)
+    launch_reset<double>(*s, *road, *p, *cfg, nullptr, (unsigned*)entropy, (int)n_words, nullptr, ar, st);
+  else
+    launch_reset<float>(*s, *road, *p, *cfg, nullptr, (unsigned*)entropy, (int)n_words, nullptr, ar, st);
   return launch_status();
 }
 

@@ -304,6 +304,34 @@ void reset_highway_seeded_(at::TensorList state, const at::Tensor& lanes, const 
      "ttrl_reset_highway_seeded");
 }
 
+void check_time(const at::Tensor& time, const ttrl_state_t& s, const at::Tensor& like);
+
+// VecHighwayEnv.step's auto-reset: done = terminated | truncated (returned), the done envs' episode
+// word bumped, their scenes regenerated from the bumped entropy and their time zeroed.
+at::Tensor auto_reset_highway_(at::TensorList state, const at::Tensor& lanes, const at::Tensor& params,
+                               const at::Tensor& cfg, const at::Tensor& entropy, int64_t episode_word,
+                               const at::Tensor& terminated, const at::Tensor& truncated, const at::Tensor& time) {
+  check_hip(state[0]);
+  ttrl_state_t s = state_of(state);
+  TORCH_CHECK(entropy.dim() == 2 && entropy.size(0) == s.n_envs && entropy.scalar_type() == at::kInt &&
+                  entropy.is_contiguous() && entropy.device() == state[0].device(),
+              "ttrl: entropy must be a contiguous int32 [n_envs, n_words] tensor on the state's device");
+  for (const at::Tensor* t : {&terminated, &truncated})
+    TORCH_CHECK(t->device() == state[0].device() && t->numel() == s.n_envs && t->is_contiguous() &&
+                    (t->scalar_type() == at::kBool || t->scalar_type() == at::kByte),
+                "ttrl: terminated / truncated must be contiguous bool [n_envs] tensors on the state's device");
+  check_time(time, s, state[0]);
+  at::Tensor done = at::empty({s.n_envs}, opts(state[0], at::kBool));
+  ok(ttrl_auto_reset_highway(&s, as_struct<ttrl_lane_table_t>(lanes, "lanes"), as_struct<ttrl_params_t>(params, "params"),
+                             as_struct<ttrl_reset_cfg_t>(cfg, "cfg"), reinterpret_cast<uint32_t*>(entropy.data_ptr()),
+                             static_cast<int32_t>(entropy.size(1)), static_cast<int32_t>(episode_word),
+                             static_cast<const uint8_t*>(terminated.data_ptr()),
+                             static_cast<const uint8_t*>(truncated.data_ptr()), time.data_ptr<double>(),
+                             static_cast<uint8_t*>(done.data_ptr()), stream_of(state[0])),
+     "ttrl_auto_reset_highway");
+  return done;
+}
+
 void ix_reset_(at::TensorList state, const at::Tensor& lanes, const at::Tensor& params, const at::Tensor& cfg,
                const at::Tensor& entropy, const c10::optional<at::Tensor>& mask) {
   check_hip(state[0]);
@@ -466,6 +494,10 @@ void meta_reset_seeded(at::TensorList, const at::Tensor&, const at::Tensor&, con
 void meta_clear_spawn(at::TensorList, const at::Tensor&, const at::Tensor&, const at::Tensor&,
                       const c10::optional<at::Tensor>&) {}
 void meta_copy_envs(at::TensorList, at::TensorList, const at::Tensor&) {}
+at::Tensor meta_auto_reset(at::TensorList state, const at::Tensor&, const at::Tensor&, const at::Tensor&,
+                           const at::Tensor&, int64_t, const at::Tensor&, const at::Tensor&, const at::Tensor&) {
+  return at::empty({meta_x(state).size(0)}, opts(meta_x(state), at::kBool));
+}
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor> meta_rewards(at::TensorList state, const at::Tensor&,
                                                             const at::Tensor&, const at::Tensor&) {
@@ -515,6 +547,8 @@ TORCH_LIBRARY(ttrl, m) {
   m.def("reset_highway_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor pcg) -> ()");
   m.def("reset_highway_seeded_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor entropy, "
         "Tensor? mask) -> ()");
+  m.def("auto_reset_highway_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor(b!) entropy, "
+        "int episode_word, Tensor terminated, Tensor truncated, Tensor(c!) time) -> Tensor done");
   m.def("ix_reset_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor entropy, Tensor? mask) -> ()");
   m.def("ix_clear_spawn_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor? mask) -> ()");
   m.def("copy_envs_(Tensor(a!)[] dst, Tensor[] src, Tensor mask) -> ()");
@@ -541,6 +575,7 @@ TORCH_LIBRARY_IMPL(ttrl, CUDA, m) {  // the HIP device of ROCm PyTorch
   m.impl("observe_lidar", &observe_lidar);
   m.impl("reset_highway_", &reset_highway_);
   m.impl("reset_highway_seeded_", &reset_highway_seeded_);
+  m.impl("auto_reset_highway_", &auto_reset_highway_);
   m.impl("ix_reset_", &ix_reset_);
   m.impl("ix_clear_spawn_", &ix_clear_spawn_);
   m.impl("copy_envs_", &copy_envs_);
@@ -564,6 +599,7 @@ TORCH_LIBRARY_IMPL(ttrl, Meta, m) {
   m.impl("observe_lidar", &meta_lidar);
   m.impl("reset_highway_", &meta_reset);
   m.impl("reset_highway_seeded_", &meta_reset_seeded);
+  m.impl("auto_reset_highway_", &meta_auto_reset);
   m.impl("ix_reset_", &meta_reset_seeded);
   m.impl("ix_clear_spawn_", &meta_clear_spawn);
   m.impl("copy_envs_", &meta_copy_envs);

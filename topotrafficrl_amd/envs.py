@@ -239,9 +239,8 @@ class VecHighwayEnv:
             # finished envs restart on the device; obs is the new episode's first observation and
             # info["final_observation"] the finished episode's last (no host round trip): only the
             # finished envs are regenerated and re-observed (masked launches)
-            done = terminated | truncated
+            done = self._auto_reset_step(terminated, truncated)
             info["final_observation"], info["final_mask"] = obs, done
-            self._auto_reset(done)
             if isinstance(self.observation_type, BatchedKinematicObservation):
                 obs = self.observation_type.observe(mask=done, out=obs.clone())
             else:
@@ -282,6 +281,14 @@ class VecHighwayEnv:
         terms of the last _rewards_and_dones (AbstractEnv._rewards)."""
         return {"speed": self._ego_speed, "crashed": self._ego_crashed,
                 "action": action, "rewards": _reward_terms(self.REWARD_TERMS, self._components)}
+
+    def _auto_reset_step(self, terminated: torch.Tensor, truncated: torch.Tensor) -> torch.Tensor:
+        """The step's auto-reset in one launch (ttrl::auto_reset_highway_): done = terminated |
+        truncated; the done envs' episode counters (entropy word 2) advance, their scenes are
+        regenerated from default_rng([seed lo, seed hi, episode]) and their time zeroed."""
+        _device_only(self.state)
+        return ops.T.auto_reset_highway_(self.state.tensors(), ops.st(self.network.table), ops.st(self.params),
+                                         ops.st(self.reset_cfg), self._entropy, 2, terminated, truncated, self.time)
 
     def _auto_reset(self, done: torch.Tensor) -> None:
         """Masked auto-reset of finished envs on the device."""

@@ -115,7 +115,8 @@ class BatchedKinematicObservation(BatchedObservationType):
         # a fresh output per call (the caching allocator makes it free): like the reference's
         # df.values.copy(), a returned observation is never overwritten by a later step
         # a masked call writes only the masked rows: the others keep their previous slot ids
-        ids = self._ids.clone() if mask is not None and self._ids is not None else None
+        # (in place: the ids are this step's fresh tensor, and become the new episodes' for the masked envs)
+        ids = self._ids if mask is not None and self._ids is not None else None
         self._out, self._ids = kinematics(road.state, road.network, road.params, self.cfg, out=out, ids=ids,
                                           mask=mask)
         return self._out
