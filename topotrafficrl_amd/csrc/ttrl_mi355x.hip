@@ -2227,14 +2227,18 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
         int best_gt = -1, best_lt = -1;
         T gx = T(0), gy = T(0), lx = T(0), ly = T(0);
         if (npairs <= NS) {
+          // the queue's row base, opaque to loop-invariant hoisting: hoisted out of the frame loop,
+          // the three queue pointers were spilled to scratch (12 B per lane written back per launch)
+          int qb = le * NS;
+          asm volatile("" : "+v"(qb));
           for (int q = 0; q < npairs; ++q) {
-            const int ij = V.pq_ij[le * NS + q], ri = ij & 0xff, rj = (ij >> 8) & 0xff, res = ij >> 16;
+            const int ij = V.pq_ij[qb + q], ri = ij & 0xff, rj = (ij >> 8) & 0xff, res = ij >> 16;
             if (ri == i) {
               if (res & 1) crash = true;
-              if ((res & 2) && rj > best_gt) { best_gt = rj; gx = V.pq_tx[le * NS + q] / T(2); gy = V.pq_ty[le * NS + q] / T(2); }
+              if ((res & 2) && rj > best_gt) { best_gt = rj; gx = V.pq_tx[qb + q] / T(2); gy = V.pq_ty[qb + q] / T(2); }
             } else if (rj == i) {
               if (res & 1) crash = true;
-              if ((res & 2) && ri > best_lt) { best_lt = ri; lx = -V.pq_tx[le * NS + q] / T(2); ly = -V.pq_ty[le * NS + q] / T(2); }
+              if ((res & 2) && ri > best_lt) { best_lt = ri; lx = -V.pq_tx[qb + q] / T(2); ly = -V.pq_ty[qb + q] / T(2); }
             }
           }
         } else {  // overflow: every vehicle sweeps all its partners in index order
@@ -2256,8 +2260,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             if (lo ? sat_separated(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt)
                    : sat_separated(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt))
               continue;
-            if (lo) sat_pair_ool(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt, inter, will, tx, ty);
-            else sat_pair_ool(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt, inter, will, tx, ty);
+            if (lo) sat_pair(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt, inter, will, tx, ty);
+            else sat_pair(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt, inter, will, tx, ty);
             if (will) {
               if (lo) { best_gt = j; gx = tx / T(2); gy = ty / T(2); }
               else { best_lt = j; lx = -tx / T(2); ly = -ty / T(2); }
@@ -2275,6 +2279,21 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
     PH(10);
   }
   __syncthreads();
+  {
+  // The thread's row indices and flags, re-derived from the (laundered) thread id after the frame
+  // loop: kept live through the loop they were spilled to scratch, whose lines are written back
+  // to HBM (~14 MB per 4096 x 64 launch).  The names shadow the prologue's.
+  int tid_r = tid;
+  asm volatile("" : "+v"(tid_r));
+  const int le = tid_r / NS, i = tid_r % NS;
+  const int env = blockIdx.x * EPW + le;
+  const bool env_on = env < st.n_envs && (!env_mask || env_mask[env]);
+  const bool slot = env_on && i < N;
+  const size_t k = (size_t)env * N + i;
+  const int me = le * NS + i;
+  const int eb = le * NS;
+  const int kind = V.kind[me];  // the view holds ABSENT for absent and out-of-range slots
+  const bool present = kind != TTRL_ABSENT;
   if (slot) {  // LDS -> HBM, once per launch
     Veh<T> a;
     a.x = V.x[me]; a.y = V.y[me]; a.h = V.h[me]; a.v = V.v[me]; a.ts = V.ts[me]; a.timer = my_timer;
@@ -2332,6 +2351,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
                      (T*)so.ego_speed, so.ego_crashed);
       }
     }
+  }
   }
   PH_FLUSH
 }
@@ -3357,7 +3377,6 @@ __global__ void __launch_bounds__(64) reset_wave_kernel(ttrl_state_t st, ttrl_la
       // the per-lane maxima are one running max and the recurrence is a chain of float64 adds
       // (the same operations as the general path, hence the same bits)
       double x0_own = 0;
-#pragma unroll 8
       for (int q = c0 == 0 ? 1 : 0; q < n; ++q) {
         double x0 = run_max;
         x0 += readlane_d(d, q);
