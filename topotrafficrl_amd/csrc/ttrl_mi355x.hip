@@ -989,8 +989,11 @@ __device__ int g_dbg_count = 0;
 // The results equal project_all's: the on-lane lists are rebuilt per lane in slot order from the
 // on-lane masks, and the closest lane is the lexicographic (d, lane) minimum -- the first minimum
 // of get_closest_lane_index.  All threads must call it.
-// (With the float32 road-network instance at a 128-VGPR budget -- 102 VGPRs and 132 SGPRs spilled
-// -- this phase produced non-finite states or hung; at the 2-wave budget nothing spills.)
+// (Round 2 noted non-finite states / hangs here for the float32 road-network instance at a 4-wave
+// (128-VGPR) budget.  Not reproducible from any committed source: the commit that wrote the note,
+// rebuilt at 4 waves, passes its intersection GPU tests and 40 finite steps, and so does this
+// source at 4 waves with TTRL_CHECK_ITEMS silent (profiles/r03/netgraph_4wave/).  The
+// 2-wave budget of the road networks is a tuning choice, not a correctness one.)
 #ifndef TTRL_ITEMS_NOINLINE
 #define TTRL_ITEMS_ATTR __forceinline__
 #else
@@ -2260,8 +2263,13 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             if (lo ? sat_separated(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt)
                    : sat_separated(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt))
               continue;
+#ifdef TTRL_SAT_OOL  // round 2's out-of-line call (A/B only: see DESIGN.md "the NET_GRAPH 4-wave fault")
+            if (lo) sat_pair_ool(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt, inter, will, tx, ty);
+            else sat_pair_ool(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt, inter, will, tx, ty);
+#else
             if (lo) sat_pair(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt, inter, will, tx, ty);
             else sat_pair(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt, inter, will, tx, ty);
+#endif
             if (will) {
               if (lo) { best_gt = j; gx = tx / T(2); gy = ty / T(2); }
               else { best_lt = j; lx = -tx / T(2); ly = -ty / T(2); }
