@@ -111,6 +111,29 @@ def test_observations(name, cases):
 
 
 @pytest.mark.parametrize("name", [IDS(p) for p in golden_files()])
+def test_observation_fixtures_equal_the_reference_observers(name, cases):
+    """The observation fixtures above (gen_golden.py restates the observers' pandas assembly) equal,
+    bit for bit, what the reference's own KinematicObservation / OccupancyGridObservation /
+    TimeToCollisionObservation / LidarObservation.observe return on the same scenes
+    (oracle/gen_golden_obs.py, observation.py:126-151, 233-275, 353-483, 694-768)."""
+    d = cases[name]
+    ref = load_golden(golden_files(f"obsref_{name}.npz")[0])
+    for k in ("kin5", "kin15", "grid7", "grid_onroad", "ttc", "lidar"):
+        assert ref[k].shape == d[k].shape, k
+        assert np.array_equal(ref[k].astype(d[k].dtype), d[k]), k
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_intersection_observation_fixtures_equal_the_reference_observer(seed):
+    """The intersection episodes' observations (absolute Kinematics 15x7, order "shuffled" drawing
+    env.np_random.shuffle(obs[1:])) equal the reference KinematicObservation's on the same episode,
+    including the generator draws (oracle/gen_golden_obs.py::ix_episode)."""
+    d = load_golden(golden_files(f"ix_s{seed}.npz")[0])
+    ref = load_golden(golden_files(f"obsref_ix_s{seed}.npz")[0])
+    assert np.array_equal(ref["obs0"], d["obs0"]) and np.array_equal(ref["obs"], d["obs"])
+
+
+@pytest.mark.parametrize("name", [IDS(p) for p in golden_files()])
 def test_ttc_and_lidar_observations(name, cases):
     """TimeToCollision (the reference's own compute_ttc_grid, finite_mdp.py:104-167) exact;
     Lidar (LidarObservation.trace over utils.rect_corners / distance_to_rect) to float32."""
