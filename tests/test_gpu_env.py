@@ -295,3 +295,32 @@ def test_fused_step_observation_equals_separate_observe(road, N, dtype, order, h
         assert torch.equal(ra, rb) and torch.equal(ta, tb) and torch.equal(ua, ub)
         assert torch.equal(ia["speed"], ib["speed"]) and torch.equal(ia["crashed"], ib["crashed"])
         assert torch.equal(a._components, b._components) and torch.equal(a.time, b.time)
+
+
+GRID = {"type": "OccupancyGrid", "features": ["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"],
+        "features_range": {"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]},
+        "grid_size": [[-32, 32], [-32, 32]], "grid_step": [2, 2]}
+
+
+@pytest.mark.parametrize("obs_cfg,N,dtype", [(GRID, 128, "f64"), (GRID, 128, "f32"), (GRID, 48, "f64"),
+                                             ({"type": "TimeToCollision", "horizon": 10}, 64, "f64")])
+def test_fused_step_tail_without_kinematics(obs_cfg, N, dtype, hip_device):
+    """With a non-Kinematics observation env.step runs the simulate launch with the reward-only step
+    tail (the ego found and read from the on-chip final state) and the observer separately; it must
+    equal ttrl_simulate followed by ttrl_rewards_step bit for bit (rewards, dones, terms, info, time)."""
+    a, b = make(16, N, obs=obs_cfg, dtype=dtype), make(16, N, obs=obs_cfg, dtype=dtype)
+    a.reset(seed=8)
+    b.reset(seed=8)
+    rng = np.random.default_rng(6)
+    for _ in range(4):
+        act = torch.from_numpy(rng.integers(0, 5, size=16))
+        oa, ra, ta, ua, ia = a.step(act)
+        b._simulate(act)
+        ob = b.observation_type.observe()
+        rb, tb, ub = b._rewards_and_dones(1.0)
+        ib = b._info(ob, act)
+        assert torch.equal(oa, ob)
+        assert torch.equal(a.state["x"], b.state["x"]) and torch.equal(a.state["crashed"], b.state["crashed"])
+        assert torch.equal(ra, rb) and torch.equal(ta, tb) and torch.equal(ua, ub)
+        assert torch.equal(ia["speed"], ib["speed"]) and torch.equal(ia["crashed"], ib["crashed"])
+        assert torch.equal(a._components, b._components) and torch.equal(a.time, b.time)

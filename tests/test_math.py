@@ -85,6 +85,14 @@ def test_log_exp_pow(lib):
     y = np.empty(N)
     lib.v_exp(_p(e), _p(y), N)
     assert ulps(y, np.exp(e.astype(np.longdouble))) <= 1.0
+    # the range edges: the top binade up to overflow, and the gradual-underflow tail (one rounding
+    # to the subnormal grid, whose spacing is 2^-1074)
+    e = np.concatenate([rng.uniform(700, 709.78, N // 10), rng.uniform(-745.13, -708, N // 10)])
+    y = np.empty(len(e))
+    lib.v_exp(_p(e), _p(y), len(e))
+    ref = np.exp(e.astype(np.longdouble))
+    err = np.abs(y.astype(np.longdouble) - ref) / np.maximum(np.spacing(ref.astype(np.float64)), 2.0 ** -1074)
+    assert float(np.max(err)) <= 1.0 and np.isfinite(y).all() and (y > 0).all()
     # the IDM free-road term: (v / v0) ^ DELTA, ratio in [0, 1.5], DELTA in [3.5, 4.5]; exp(y log x)
     # carries the rounding of y log x into the result, ~|y log x| ulps (the kernel's pow before this
     # header was the same composition of ocml's exp and log)

@@ -15,6 +15,12 @@ class BatchedDiscreteMetaAction:
     _CODE = {"LANE_LEFT": _abi.LANE_LEFT, "IDLE": _abi.IDLE, "LANE_RIGHT": _abi.LANE_RIGHT,
              "FASTER": _abi.FASTER, "SLOWER": _abi.SLOWER}
 
+    # Out-of-range action indices: the reference raises KeyError (self.actions[int(a)]).  CPU inputs
+    # are always checked here.  Device-resident inputs are checked only when check_device_actions is
+    # set (an asynchronous device assert, a few small launches per step); otherwise a device index
+    # outside [0, n) is undefined (the kernel matches none of its meta-action branches: IDLE).
+    check_device_actions = False
+
     def __init__(self, env, longitudinal: bool = True, lateral: bool = True, target_speeds=None, **kwargs):
         self.env = env
         self.longitudinal, self.lateral = longitudinal, lateral
@@ -42,6 +48,9 @@ class BatchedDiscreteMetaAction:
             an = a.numpy()
             if an.size and (an.min() < 0 or an.max() >= len(self.actions)):
                 raise KeyError(f"action out of range [0, {len(self.actions)})")  # self.actions[int(a)] raises
+        elif self.check_device_actions and a.numel():
+            lo, hi = torch.aminmax(a)
+            torch._assert_async((lo >= 0) & (hi < len(self.actions)), "action out of range")
         if self._identity:
             return a.to(device=dev, dtype=torch.int32).reshape(-1)
         return self._lut[a.to(dev).long().reshape(-1)]

@@ -143,7 +143,8 @@ TTRL_HD double exp_d(double y) {
                P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
                P5 = 4.13813679705723846039e-08;
   const double LN2_HI = 6.93147180369123816490e-01, LN2_LO = 1.90821492927058770002e-10;
-  const double yc = y > 709.0 ? 709.0 : (y < -745.0 ? -745.0 : (y == y ? y : 0.0));
+  // the clamp only keeps k in range (|k| <= 1075); inside (-745.14, 709.79) yc == y
+  const double yc = y > 709.8 ? 709.8 : (y < -745.2 ? -745.2 : (y == y ? y : 0.0));
   const double k = rint(yc * 1.44269504088896338700e+00);
   const double hi = fma(-k, LN2_HI, yc);
   const double lo = k * LN2_LO;
@@ -151,7 +152,10 @@ TTRL_HD double exp_d(double y) {
   const double t = r * r;
   const double c = r - t * fma(t, fma(t, fma(t, fma(t, P5, P4), P3), P2), P1);
   const double e = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
-  const double res = ldexp(e, (int)k);
+  // 2^k in two exact halves: e * 2^1024 (top binade, e < 1) and the subnormal tail (one rounding,
+  // in the second step) stay correct where a single ldexp would overflow or underflow its exponent
+  const int k1 = (int)k / 2;
+  const double res = ldexp(ldexp(e, k1), (int)k - k1);
   return y > 709.782712893384 ? __builtin_inf() : (y < -745.1332191019412 ? 0.0 : (y == y ? res : y));
 }
 
