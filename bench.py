@@ -244,14 +244,14 @@ def main():
     def one_step(t):
         nonlocal obs
         if sg is not None:
-            if ix and t >= args.warmup:
+            if ix:
                 live.add_((env.state["kind"] != 0).sum())
             if policy is None:
                 sg.set_actions(acts[t])
             sg.replay()
             return
         a = policy.act(obs, t) if policy is not None else acts[t]
-        if ix and t >= args.warmup:
+        if ix:  # counted in the warm-up steps too, so the count's kernels are loaded before t0
             live.add_((env.state["kind"] != 0).sum())
         obs, rew, term, trunc, info = env.step(a)
 
@@ -269,6 +269,7 @@ def main():
             env.state.copy_(snap)
     for t in range(args.warmup):
         one_step(t)
+    live.zero_()  # only the timed steps' live vehicles count
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -29,6 +29,7 @@
  *                            (_make_vehicles :251-318, _spawn_vehicle :320-348, AbstractEnv.reset abstract.py:188-214)
  *   ttrl_ix_clear_spawn      IntersectionEnv.step tail     ttrl_env/envs/intersection_env.py:135-139
  *                            (_clear_vehicles :350-362, _spawn_vehicle :320-348)
+ *   ttrl_ix_step_tail        the step tail + auto-reset from spare scenes (AbstractEnv.reset abstract.py:188-214)
  */
 #ifndef TTRL_MI355X_H
 #define TTRL_MI355X_H
@@ -283,7 +284,8 @@ int ttrl_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road,
  * state the Kinematics observation (ttrl_observe_kinematics; skipped when obs_cfg is NULL) and the
  * step tail of ttrl_rewards_step (time += time_inc, reward, terminated, truncated, components, the
  * info's ego speed / crashed; skipped when reward_cfg is NULL).  Same outputs as the separate
- * calls; not for road networks with routes (TTRL_E_ARG). */
+ * calls, on every road (the intersection's network with routes included, where an
+ * order_shuffled == 2 observation draws from state.rng as ttrl_observe_kinematics does). */
 int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                   const int32_t* actions, int32_t frames, double dt,
                   const ttrl_kin_cfg_t* obs_cfg, float* obs, int32_t* obs_ids,
@@ -371,6 +373,22 @@ int ttrl_copy_envs(const ttrl_state_t* dst, const ttrl_state_t* src, const uint8
  * then _spawn_vehicle(spawn_probability) drawing from state.rng; envs with mask[e] != 0. */
 int ttrl_ix_clear_spawn(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                         const ttrl_ix_cfg_t* cfg, const uint8_t* mask, void* stream);
+/* VecIntersectionEnv.step after ttrl_env_step (fused frames, observation, rewards), with the
+ * auto-reset from scenes reset ahead of time, in one launch.  spare: 2E rows (slot q of env e is
+ * row q * E + e), reset by ttrl_ix_reset from spare_entropy.  An env with terminated | truncated
+ * == 0 runs the IntersectionEnv.step tail (as ttrl_ix_clear_spawn) and copies its observation row
+ * obs_in -> obs_out; a finished env instead takes the spare row of slot spare_parity[e] (every
+ * field, rng and regulation words included), flips spare_parity[e], adds 1 to its episode word
+ * entropy[e][n_words - 1] and 2 to spare_entropy[row][n_words - 1], zeroes time[e] and writes its
+ * first observation into obs_out / obs_ids_out (obs_cfg: Kinematics, n_veh <= 64).  done[E] =
+ * terminated | truncated; spare_mask[2E] flags the consumed spare rows (to be reset again).
+ * Reference: intersection_env.py:135-139, :350-362, :320-348; abstract.py:188-214. */
+int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                      const ttrl_ix_cfg_t* cfg, const ttrl_state_t* spare, const uint8_t* terminated,
+                      const uint8_t* truncated, uint8_t* spare_parity, uint32_t* entropy, uint32_t* spare_entropy,
+                      int32_t n_words, double* time, uint8_t* done, uint8_t* spare_mask,
+                      const ttrl_kin_cfg_t* obs_cfg, const float* obs_in, float* obs_out, const int32_t* obs_ids_in,
+                      int32_t* obs_ids_out, void* stream);
 /* Per-env reward [E] float32, terminated/truncated [E] uint8, given time [E] float64, for the
  * env's controlled vehicle (its first TTRL_MDP slot). */
 int ttrl_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* road,

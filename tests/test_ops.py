@@ -15,7 +15,7 @@ LANES = ops.struct_tensor(_abi.straight_lane_table(4))
 PARAMS = ops.struct_tensor(_abi.default_params())
 MUTATES = {"simulate_", "road_act_", "road_step_", "meta_action_", "env_step_", "kinematics_obs",
            "kinematics_obs_masked_", "reset_highway_", "reset_highway_seeded_", "auto_reset_highway_", "ix_reset_",
-           "ix_clear_spawn_", "copy_envs_"}
+           "ix_clear_spawn_", "ix_step_tail_", "copy_envs_"}
 
 
 def test_every_device_entry_point_is_an_operator():
@@ -27,7 +27,8 @@ def test_every_device_entry_point_is_an_operator():
                           "observe_lidar": "observe_lidar", "reset_highway_": "reset_highway",
                           "reset_highway_seeded_": "reset_highway_seeded",
                           "auto_reset_highway_": "auto_reset_highway", "ix_reset_": "ix_reset",
-                          "ix_clear_spawn_": "ix_clear_spawn", "copy_envs_": "copy_envs", "rewards": "rewards",
+                          "ix_clear_spawn_": "ix_clear_spawn", "ix_step_tail_": "ix_step_tail",
+                          "copy_envs_": "copy_envs", "rewards": "rewards",
                           "rewards_ex": "rewards_ex", "rewards_step_": "rewards_step",
                           "ego_attention_q": "ego_attention_q"}[o] for o in ops.OPS}
     assert covered == abi
@@ -44,7 +45,7 @@ def test_schemas_declare_mutation(name):
 
 
 def test_time_is_mutated_by_the_step_ops():
-    for name in ("env_step_", "rewards_step_", "auto_reset_highway_"):
+    for name in ("env_step_", "rewards_step_", "auto_reset_highway_", "ix_step_tail_"):
         s = getattr(torch.ops.ttrl, name).default._schema
         t = [a for a in s.arguments if a.name == "time"][0]
         assert t.alias_info is not None and t.alias_info.is_write
@@ -75,6 +76,14 @@ def test_meta_shapes():
     assert lid.shape == (6, 16, 2)
     q = torch.ops.ttrl.ego_attention_q(torch.zeros(9, 15, 7, device="meta"), torch.zeros(10, device="meta"), 2, 5)
     assert q.shape == (9, 5)
+    spare = BatchState(12, 64, device="meta")
+    u8 = torch.zeros(6, dtype=torch.uint8, device="meta")
+    done, smask, o2, i2 = torch.ops.ttrl.ix_step_tail_(
+        st.tensors(), LANES, PARAMS, ops.struct_tensor(_abi.IxCfg()), spare.tensors(), u8.bool(), u8.bool(), u8,
+        torch.zeros(6, 3, dtype=torch.int32, device="meta"), torch.zeros(12, 3, dtype=torch.int32, device="meta"), t,
+        ops.struct_tensor(kin), o, i)
+    assert done.shape == (6,) and done.dtype == torch.bool and smask.shape == (12,)
+    assert o2.shape == (6, 15, 7) and i2.shape == (6, 14)
 
 
 def test_struct_tensors_are_checked():

@@ -28,16 +28,15 @@ def run(mode: str, steps: int = 60, warm: int = 10) -> float:
     if mode == "no_wait":
         def prepare(mask):
             main = torch.cuda.current_stream(dev)
-            ent = torch.cat([env._spare_words, env._spare_ep.unsqueeze(1)], 1)
-            m = mask
-            env._side.wait_stream(main)
+            side = env._sides[env._side_i]
+            env._side_i = (env._side_i + 1) % len(env._sides)
+            side.wait_stream(main)
             ev = torch.cuda.Event()
-            ev.record(env._side)  # before the work: the main stream does not wait for it
-            with torch.cuda.stream(env._side):
-                ix_reset(env._spare, env.network, env.params, env.ix, ent, m)
-            ent.record_stream(env._side)
-            if m is not None:
-                m.record_stream(env._side)
+            ev.record(side)  # before the work: the main stream does not wait for it
+            with torch.cuda.stream(side):
+                ix_reset(env._spare, env.network, env.params, env.ix, env._spare_ent, mask)
+            if mask is not None:
+                mask.record_stream(side)
             env._spare_prev, env._spare_ready = env._spare_ready, ev
         env._prepare_spares = prepare
     env.reset(seed=12345)

@@ -40,6 +40,8 @@ _SIGS = {
     "ttrl_rewards_step": ([_P, _P, _P, _P, C.c_double, _P, _P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_ix_reset": ([_P, _P, _P, _P, _P, C.c_int32, _P, _P], C.c_int),
     "ttrl_ix_clear_spawn": ([_P, _P, _P, _P, _P, _P], C.c_int),
+    "ttrl_ix_step_tail": ([_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, C.c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+                          C.c_int),
     "ttrl_copy_envs": ([_P, _P, _P, _P], C.c_int),
     "ttrl_ego_attention_sizes": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P], C.c_int64),
     "ttrl_ego_attention_q": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, C.c_int32, _P, _P, _P], C.c_int),

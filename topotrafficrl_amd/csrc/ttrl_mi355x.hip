@@ -2326,8 +2326,9 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
     if (i == 0 && env_on) st.reg_steps[env] = reg;
   }
   PH(16);
-  if constexpr (!GR) {
-    // ttrl_env_step's tail, from LDS; scratch over the act phase's (dead) block
+  {
+    // ttrl_env_step's tail, from LDS; scratch over the act phase's (dead) block (on a road network
+    // that block also held the RegulatedRoad predictions, dead after the last frame as well)
     constexpr int M = EPW * NS;
     char* scr = (char*)V.afree;
     T* s_key = (T*)scr;
@@ -3806,10 +3807,8 @@ __global__ void __launch_bounds__(64) ix_finish_kernel(ttrl_state_t st, ttrl_lan
 // controlled vehicle and every vehicle neither leaving (an "il"->"o" lane within 4 lengths of its
 // end) nor without a route, in list order; then _spawn_vehicle(spawn_probability).
 template <typename T>
-__global__ void __launch_bounds__(64) ix_clear_spawn_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P,
-                                                            ttrl_ix_cfg_t C, const uint8_t* __restrict__ mask) {
-  const int env = blockIdx.x, lane = threadIdx.x;
-  if (mask && !mask[env]) return;
+__device__ void ix_clear_spawn_env(const ttrl_state_t& st, const ttrl_lane_table_t& R, const ttrl_params_t& P,
+                                   const ttrl_ix_cfg_t& C, int env, int lane) {
   const size_t base = (size_t)env * st.n_veh;
   unsigned long long keep[4] = {~0ull, ~0ull, ~0ull, ~0ull};
   for (int c0 = 0; c0 < st.n_veh; c0 += 64) {
@@ -3832,31 +3831,135 @@ __global__ void __launch_bounds__(64) ix_clear_spawn_kernel(ttrl_state_t st, ttr
   if (lane == 0) rng_store(g, w);
 }
 
+template <typename T>
+__global__ void __launch_bounds__(64) ix_clear_spawn_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P,
+                                                            ttrl_ix_cfg_t C, const uint8_t* __restrict__ mask) {
+  const int env = blockIdx.x, lane = threadIdx.x;
+  if (mask && !mask[env]) return;
+  ix_clear_spawn_env<T>(st, R, P, C, env, lane);
+}
+
+// One row of every field (per-env route / regulation / rng words included) from src row ks to dst
+// row kd, the slots on the lanes of one wavefront.
+template <typename T>
+__device__ __forceinline__ void copy_env_rows(const ttrl_state_t& dst, const ttrl_state_t& src, int env_dst,
+                                              int env_src, int lane) {
+  const size_t bd = (size_t)env_dst * dst.n_veh, bs = (size_t)env_src * src.n_veh;
+  const bool net = dst.route_road && src.route_road;
+  for (int j = lane; j < dst.n_veh; j += 64) {
+    const size_t kd = bd + j, ks = bs + j;
+#pragma unroll
+    for (int q = 0; q < 11; ++q) real_field<T>(dst, q)[kd] = real_field<T>(src, q)[ks];
+    dst.lane[kd] = src.lane[ks]; dst.target_lane[kd] = src.target_lane[ks]; dst.speed_index[kd] = src.speed_index[ks];
+    dst.kind[kd] = src.kind[ks]; dst.crashed[kd] = src.crashed[ks]; dst.has_impact[kd] = src.has_impact[ks];
+    dst.lane_change[kd] = src.lane_change[ks];
+    if (net) {
+      ((int32_t*)dst.route_road)[kd] = ((const int32_t*)src.route_road)[ks];
+      ((int32_t*)dst.route_lane)[kd] = ((const int32_t*)src.route_lane)[ks];
+      dst.route_n[kd] = src.route_n[ks];
+      dst.yielding[kd] = src.yielding[ks];
+    }
+  }
+  if (lane == 0 && dst.reg_steps && src.reg_steps) dst.reg_steps[env_dst] = src.reg_steps[env_src];
+  if (lane < TTRL_RNG_WORDS && dst.rng && src.rng)
+    dst.rng[(size_t)env_dst * TTRL_RNG_WORDS + lane] = src.rng[(size_t)env_src * TTRL_RNG_WORDS + lane];
+}
+
+// VecIntersectionEnv.step after the fused simulate / observation / reward launch, with auto-reset
+// from scenes reset ahead of time (the spare rows), in one launch, one wavefront per env:
+// - an env that goes on runs IntersectionEnv.step's tail (_clear_vehicles, _spawn_vehicle;
+//   intersection_env.py:135-139) and keeps its observation row (obs_in -> obs_out);
+// - a finished env (terminated | truncated) is reset (AbstractEnv.reset, abstract.py:188-214): it
+//   takes the spare scene of its parity slot (prepared from default_rng([seed words, episode]) by
+//   ttrl_ix_reset), so its clear / spawn -- which the reset discards with the rest of the finished
+//   scene, rows and np_random alike -- is skipped; its episode counter advances, the consumed spare
+//   row's counter advances by two (that row's next scene is two episodes on) and is flagged in
+//   spare_mask for the side stream's reset, the parity flips, time is zeroed, and the first
+//   observation of the new scene is written to obs_out / ids_out (kin_observe, one slot per lane).
+struct IxTail {
+  ttrl_state_t spare;  // 2E rows: slot p of env e is row p * E + e
+  const uint8_t* term;
+  const uint8_t* trunc;
+  uint8_t* par;        // [E] the next slot each env takes
+  uint32_t* ent;       // [E][nw] entropy words, the episode counter last
+  uint32_t* spare_ent; // [2E][nw]
+  int nw;
+  double* time;
+  uint8_t* done;       // [E] out
+  uint8_t* spare_mask; // [2E] out
+  ttrl_kin_cfg_t kcfg;
+  bool obs;
+  const float* obs_in;
+  float* obs_out;
+  const int32_t* ids_in;
+  int32_t* ids_out;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(64) ix_step_tail_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P,
+                                                          ttrl_ix_cfg_t C, IxTail t) {
+  __shared__ T s_key[64];
+  __shared__ int s_cnt[1], s_ego[1];
+  __shared__ int s_perm[1][64], s_p[1][64];
+  __shared__ LaneT<T> s_lanes[LMAX];
+  const int env = blockIdx.x, lane = threadIdx.x;
+  const int E = st.n_envs, N = st.n_veh;
+  const bool d = t.term[env] || t.trunc[env];
+  const int V = t.kcfg.vehicles_count, F = t.kcfg.n_features;
+  if (!d) {
+    if (lane == 0) { t.done[env] = 0; t.spare_mask[env] = 0; t.spare_mask[E + env] = 0; }
+    if (t.obs) {  // the row observed by the fused launch stays this step's observation
+      for (int q = lane; q < V * F; q += 64) t.obs_out[(size_t)env * V * F + q] = t.obs_in[(size_t)env * V * F + q];
+      if (t.ids_out)
+        for (int q = lane; q < V - 1; q += 64) t.ids_out[(size_t)env * (V - 1) + q] = t.ids_in[(size_t)env * (V - 1) + q];
+    }
+    ix_clear_spawn_env<T>(st, R, P, C, env, lane);
+    return;
+  }
+  const int p = t.par[env];
+  const int row = p * E + env;
+  copy_env_rows<T>(st, t.spare, env, row, lane);
+  if (lane == 0) {
+    t.done[env] = 1;
+    t.ent[(size_t)env * t.nw + t.nw - 1] += 1u;
+    t.spare_ent[(size_t)row * t.nw + t.nw - 1] += 2u;
+    t.spare_mask[row] = 1;
+    t.spare_mask[(1 - p) * E + env] = 0;
+    t.par[env] = (uint8_t)(p ^ 1);
+    t.time[env] = 0.0;
+  }
+  if (!t.obs) return;
+  if (lane < R.n_lanes) s_lanes[lane] = make_lane<T>(R, lane);
+  __syncthreads();  // the copied rows (and rng words) are the block's own writes: visible after the barrier
+  const size_t k = (size_t)env * N + lane;
+  T x = T(0), y = T(0), h = T(0), v = T(0);
+  int ln = 0;
+  bool present = false, mdp = false;
+  if (lane < N) {
+    x = ((const T*)st.x)[k]; y = ((const T*)st.y)[k]; h = ((const T*)st.heading)[k];
+    v = ((const T*)st.speed)[k]; ln = st.lane[k];
+    present = st.kind[k] != TTRL_ABSENT;
+    mdp = st.kind[k] == TTRL_MDP;
+  }
+  auto ego_of = [&](int ego, T& ex, T& ey, T& eh, T& ev, T& ec, T& es, int& elane) {
+    const size_t k0 = (size_t)env * N + ego;
+    ex = ((const T*)st.x)[k0]; ey = ((const T*)st.y)[k0]; eh = ((const T*)st.heading)[k0];
+    ev = ((const T*)st.speed)[k0]; elane = st.lane[k0];
+    const SinCos<T> sc = k_sincos(eh);
+    ec = sc.c; es = sc.s;
+  };
+  const SinCos<T> sc = k_sincos(h);
+  kin_observe<T, 64, 1>(st, s_lanes, P, t.kcfg, true, env, x, y, h, v, sc.c, sc.s, ln, present, mdp, ego_of, s_key,
+                        s_cnt, s_ego, s_perm, s_p, t.obs_out, t.ids_out);
+}
+
 // Masked whole-env copy (double-buffered resets): one workgroup per env, the slots on the lanes.
 template <typename T>
 __global__ void __launch_bounds__(64) copy_envs_kernel(ttrl_state_t dst, ttrl_state_t src,
                                                        const uint8_t* __restrict__ mask) {
   const int env = blockIdx.x, lane = threadIdx.x;
   if (!mask[env]) return;
-  const size_t base = (size_t)env * dst.n_veh;
-  const bool net = dst.route_road && src.route_road;
-  for (int j = lane; j < dst.n_veh; j += 64) {
-    const size_t k = base + j;
-#pragma unroll
-    for (int q = 0; q < 11; ++q) real_field<T>(dst, q)[k] = real_field<T>(src, q)[k];
-    dst.lane[k] = src.lane[k]; dst.target_lane[k] = src.target_lane[k]; dst.speed_index[k] = src.speed_index[k];
-    dst.kind[k] = src.kind[k]; dst.crashed[k] = src.crashed[k]; dst.has_impact[k] = src.has_impact[k];
-    dst.lane_change[k] = src.lane_change[k];
-    if (net) {
-      ((int32_t*)dst.route_road)[k] = ((const int32_t*)src.route_road)[k];
-      ((int32_t*)dst.route_lane)[k] = ((const int32_t*)src.route_lane)[k];
-      dst.route_n[k] = src.route_n[k];
-      dst.yielding[k] = src.yielding[k];
-    }
-  }
-  if (lane == 0 && dst.reg_steps && src.reg_steps) dst.reg_steps[env] = src.reg_steps[env];
-  if (lane < TTRL_RNG_WORDS && dst.rng && src.rng)
-    dst.rng[(size_t)env * TTRL_RNG_WORDS + lane] = src.rng[(size_t)env * TTRL_RNG_WORDS + lane];
+  copy_env_rows<T>(dst, src, env, env, lane);
 }
 
 // ------------------------------------------------------------------- launch helpers
@@ -3932,7 +4035,7 @@ int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_par
   }
   if (graph)
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_GRAPH>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, P,
-                       actions, mask, frames, dt, mode, ablate, StepOut{});
+                       actions, mask, frames, dt, mode, ablate, ob);
   else if (curved)
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_CURVED>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R,
                        P, actions, mask, frames, dt, mode, ablate, ob);
@@ -4059,7 +4162,7 @@ int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
                   void* stream) {
   int rc = check_state(s, road);
   if (rc) return rc < 0 ? rc : TTRL_OK;
-  if (is_graph(*road) || (!obs_cfg) != (!obs) || (obs_cfg && check_kin_cfg(s, obs_cfg))) return TTRL_E_ARG;
+  if ((!obs_cfg) != (!obs) || (obs_cfg && check_kin_cfg(s, obs_cfg))) return TTRL_E_ARG;
   if (reward_cfg && (!time || !reward || !terminated || !truncated || (!ego_speed) != (!ego_crashed)))
     return TTRL_E_ARG;
   StepOut so{};
@@ -4330,6 +4433,45 @@ int ttrl_ix_clear_spawn(const ttrl_state_t* s, const ttrl_lane_table_t* road, co
     hipLaunchKernelGGL(ix_clear_spawn_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg, mask);
   else
     hipLaunchKernelGGL(ix_clear_spawn_kernel<float>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg, mask);
+  return launch_status();
+}
+
+int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                      const ttrl_ix_cfg_t* cfg, const ttrl_state_t* spare, const uint8_t* terminated,
+                      const uint8_t* truncated, uint8_t* spare_parity, uint32_t* entropy, uint32_t* spare_entropy,
+                      int32_t n_words, double* time, uint8_t* done, uint8_t* spare_mask,
+                      const ttrl_kin_cfg_t* obs_cfg, const float* obs_in, float* obs_out, const int32_t* obs_ids_in,
+                      int32_t* obs_ids_out, void* stream) {
+  int rc = check_ix(s, road, p, cfg);
+  if (rc) return rc < 0 ? rc : TTRL_OK;
+  if (!spare || !terminated || !truncated || !spare_parity || !entropy || !spare_entropy || n_words < 1 ||
+      n_words > 65 || !time || !done || !spare_mask)
+    return TTRL_E_ARG;
+  if (spare->n_envs != 2 * s->n_envs || spare->n_veh != s->n_veh || spare->dtype != s->dtype || !spare->rng ||
+      !spare->reg_steps || !spare->route_road || !spare->route_lane || !spare->route_n || !spare->yielding)
+    return TTRL_E_ARG;
+  const void* sp[] = {spare->x, spare->y, spare->heading, spare->speed, spare->target_speed, spare->timer,
+                      spare->delta, spare->steer, spare->acc, spare->impact_x, spare->impact_y, spare->lane,
+                      spare->target_lane, spare->speed_index, spare->kind, spare->crashed, spare->has_impact,
+                      spare->lane_change};
+  for (const void* q : sp)
+    if (!q) return TTRL_E_ARG;
+  if (obs_cfg) {  // the re-observation puts one slot on each lane of the env's wavefront
+    if (check_kin_cfg(s, obs_cfg) || !obs_in || !obs_out || (!obs_ids_in) != (!obs_ids_out) || s->n_veh > 64)
+      return obs_cfg && s->n_veh > 64 ? TTRL_E_UNSUPPORTED : TTRL_E_ARG;
+  }
+  IxTail t{};
+  t.spare = *spare; t.term = terminated; t.trunc = truncated; t.par = spare_parity; t.ent = entropy;
+  t.spare_ent = spare_entropy; t.nw = n_words; t.time = time; t.done = done; t.spare_mask = spare_mask;
+  if (obs_cfg) {
+    t.kcfg = *obs_cfg; t.obs = true; t.obs_in = obs_in; t.obs_out = obs_out; t.ids_in = obs_ids_in;
+    t.ids_out = obs_ids_out;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  if (s->dtype == TTRL_F64)
+    hipLaunchKernelGGL(ix_step_tail_kernel<double>, dim3(s->n_envs), dim3(64), 0, st, *s, *road, *p, *cfg, t);
+  else
+    hipLaunchKernelGGL(ix_step_tail_kernel<float>, dim3(s->n_envs), dim3(64), 0, st, *s, *road, *p, *cfg, t);
   return launch_status();
 }
 

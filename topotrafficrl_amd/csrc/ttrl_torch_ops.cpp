@@ -355,6 +355,66 @@ void ix_clear_spawn_(at::TensorList state, const at::Tensor& lanes, const at::Te
      "ttrl_ix_clear_spawn");
 }
 
+// VecIntersectionEnv.step after env_step_: clear / spawn for the envs that go on, the auto-reset of
+// the finished ones from the spare scenes (2E rows) and their first observation.  Returns
+// (done [E] bool, spare_mask [2E] uint8: the spare rows to reset again, obs [E, V, F], ids).
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ix_step_tail_(
+    at::TensorList state, const at::Tensor& lanes, const at::Tensor& params, const at::Tensor& cfg,
+    at::TensorList spare, const at::Tensor& terminated, const at::Tensor& truncated, const at::Tensor& spare_parity,
+    const at::Tensor& entropy, const at::Tensor& spare_entropy, const at::Tensor& time,
+    const c10::optional<at::Tensor>& kin_cfg, const c10::optional<at::Tensor>& obs,
+    const c10::optional<at::Tensor>& ids) {
+  check_hip(state[0]);
+  ttrl_state_t s = state_of(state), sp = state_of(spare);
+  const auto& x = state[0];
+  TORCH_CHECK(spare[0].device() == x.device() && sp.n_envs == 2 * s.n_envs && sp.n_veh == s.n_veh &&
+                  sp.dtype == s.dtype,
+              "ttrl: spare must be a state of 2 * n_envs rows of the same width and dtype on the state's device");
+  for (const at::Tensor* t : {&terminated, &truncated})
+    TORCH_CHECK(t->device() == x.device() && t->numel() == s.n_envs && t->is_contiguous() &&
+                    (t->scalar_type() == at::kBool || t->scalar_type() == at::kByte),
+                "ttrl: terminated / truncated must be contiguous bool [n_envs] tensors on the state's device");
+  TORCH_CHECK(spare_parity.device() == x.device() && spare_parity.scalar_type() == at::kByte &&
+                  spare_parity.is_contiguous() && spare_parity.numel() == s.n_envs,
+              "ttrl: spare_parity must be a contiguous uint8 [n_envs] tensor on the state's device");
+  TORCH_CHECK(entropy.dim() == 2 && entropy.size(0) == s.n_envs && entropy.scalar_type() == at::kInt &&
+                  entropy.is_contiguous() && entropy.device() == x.device(),
+              "ttrl: entropy must be a contiguous int32 [n_envs, n_words] tensor on the state's device");
+  TORCH_CHECK(spare_entropy.dim() == 2 && spare_entropy.size(0) == 2 * s.n_envs &&
+                  spare_entropy.size(1) == entropy.size(1) && spare_entropy.scalar_type() == at::kInt &&
+                  spare_entropy.is_contiguous() && spare_entropy.device() == x.device(),
+              "ttrl: spare_entropy must be a contiguous int32 [2 * n_envs, n_words] tensor on the state's device");
+  check_time(time, s, x);
+  const ttrl_kin_cfg_t* kc = kin_cfg && kin_cfg->defined() ? as_struct<ttrl_kin_cfg_t>(*kin_cfg, "kin_cfg") : nullptr;
+  at::Tensor obs_out, ids_out, oin, iin;
+  if (kc) {
+    TORCH_CHECK(obs && obs->defined() && ids && ids->defined(), "ttrl: a kin_cfg needs the step's obs and ids");
+    std::tie(obs_out, ids_out) = kin_outputs(x, kc);
+    oin = obs->contiguous();
+    iin = ids->contiguous();
+    TORCH_CHECK(oin.device() == x.device() && oin.scalar_type() == at::kFloat && oin.sizes() == obs_out.sizes(),
+                "ttrl: obs must be the step's float32 [E, V, F] observation");
+    TORCH_CHECK(iin.device() == x.device() && iin.scalar_type() == at::kInt && iin.sizes() == ids_out.sizes(),
+                "ttrl: ids must be the step's int32 [E, V-1] observed ids");
+  } else {
+    obs_out = at::empty({0}, opts(x, at::kFloat));
+    ids_out = at::empty({0}, opts(x, at::kInt));
+  }
+  at::Tensor done = at::empty({s.n_envs}, opts(x, at::kBool));
+  at::Tensor smask = at::empty({2 * s.n_envs}, opts(x, at::kByte));
+  ok(ttrl_ix_step_tail(&s, as_struct<ttrl_lane_table_t>(lanes, "lanes"), as_struct<ttrl_params_t>(params, "params"),
+                       as_struct<ttrl_ix_cfg_t>(cfg, "cfg"), &sp, static_cast<const uint8_t*>(terminated.data_ptr()),
+                       static_cast<const uint8_t*>(truncated.data_ptr()),
+                       static_cast<uint8_t*>(spare_parity.data_ptr()), reinterpret_cast<uint32_t*>(entropy.data_ptr()),
+                       reinterpret_cast<uint32_t*>(spare_entropy.data_ptr()), static_cast<int32_t>(entropy.size(1)),
+                       time.data_ptr<double>(), static_cast<uint8_t*>(done.data_ptr()),
+                       static_cast<uint8_t*>(smask.data_ptr()), kc, kc ? oin.data_ptr<float>() : nullptr,
+                       kc ? obs_out.data_ptr<float>() : nullptr, kc ? iin.data_ptr<int32_t>() : nullptr,
+                       kc ? ids_out.data_ptr<int32_t>() : nullptr, stream_of(x)),
+     "ttrl_ix_step_tail");
+  return {done, smask, obs_out, ids_out};
+}
+
 void copy_envs_(at::TensorList dst, at::TensorList src, const at::Tensor& mask) {
   check_hip(dst[0]);
   ttrl_state_t d = state_of(dst), s = state_of(src);
@@ -494,6 +554,16 @@ void meta_reset_seeded(at::TensorList, const at::Tensor&, const at::Tensor&, con
 void meta_clear_spawn(at::TensorList, const at::Tensor&, const at::Tensor&, const at::Tensor&,
                       const c10::optional<at::Tensor>&) {}
 void meta_copy_envs(at::TensorList, at::TensorList, const at::Tensor&) {}
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> meta_ix_step_tail(
+    at::TensorList state, const at::Tensor&, const at::Tensor&, const at::Tensor&, at::TensorList, const at::Tensor&,
+    const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&,
+    const c10::optional<at::Tensor>& kin_cfg, const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&) {
+  const auto& x = meta_x(state);
+  const int64_t E = x.size(0);
+  at::Tensor o = at::empty({0}, opts(x, at::kFloat)), i = at::empty({0}, opts(x, at::kInt));
+  if (kin_cfg && kin_cfg->defined()) std::tie(o, i) = kin_outputs(x, as_struct<ttrl_kin_cfg_t>(*kin_cfg, "kin_cfg"));
+  return {at::empty({E}, opts(x, at::kBool)), at::empty({2 * E}, opts(x, at::kByte)), o, i};
+}
 at::Tensor meta_auto_reset(at::TensorList state, const at::Tensor&, const at::Tensor&, const at::Tensor&,
                            const at::Tensor&, int64_t, const at::Tensor&, const at::Tensor&, const at::Tensor&) {
   return at::empty({meta_x(state).size(0)}, opts(meta_x(state), at::kBool));
@@ -552,6 +622,10 @@ TORCH_LIBRARY(ttrl, m) {
   m.def("ix_reset_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor entropy, Tensor? mask) -> ()");
   m.def("ix_clear_spawn_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor? mask) -> ()");
   m.def("copy_envs_(Tensor(a!)[] dst, Tensor[] src, Tensor mask) -> ()");
+  m.def("ix_step_tail_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor[] spare, "
+        "Tensor terminated, Tensor truncated, Tensor(b!) spare_parity, Tensor(c!) entropy, Tensor(d!) spare_entropy, "
+        "Tensor(e!) time, Tensor? kin_cfg, Tensor? obs, Tensor? ids) -> (Tensor done, Tensor spare_mask, "
+        "Tensor obs, Tensor ids)");
   m.def("rewards(Tensor[] state, Tensor lanes, Tensor cfg, Tensor time) -> (Tensor reward, Tensor terminated, "
         "Tensor truncated)");
   m.def("rewards_ex(Tensor[] state, Tensor lanes, Tensor cfg, Tensor time) -> (Tensor reward, Tensor terminated, "
@@ -579,6 +653,7 @@ TORCH_LIBRARY_IMPL(ttrl, CUDA, m) {  // the HIP device of ROCm PyTorch
   m.impl("ix_reset_", &ix_reset_);
   m.impl("ix_clear_spawn_", &ix_clear_spawn_);
   m.impl("copy_envs_", &copy_envs_);
+  m.impl("ix_step_tail_", &ix_step_tail_);
   m.impl("rewards", &rewards);
   m.impl("rewards_ex", &rewards_ex);
   m.impl("rewards_step_", &rewards_step_);
@@ -603,6 +678,7 @@ TORCH_LIBRARY_IMPL(ttrl, Meta, m) {
   m.impl("ix_reset_", &meta_reset_seeded);
   m.impl("ix_clear_spawn_", &meta_clear_spawn);
   m.impl("copy_envs_", &meta_copy_envs);
+  m.impl("ix_step_tail_", &meta_ix_step_tail);
   m.impl("rewards", &meta_rewards);
   m.impl("rewards_ex", &meta_rewards_ex);
   m.impl("rewards_step_", &meta_rewards_step);

@@ -24,8 +24,8 @@ import torch
 
 from . import _abi, ops
 from .action import action_factory
-from .envs import _reward_terms, rewards_and_dones
-from .observation import observation_factory
+from .envs import _keep_tail, _reward_terms, rewards_and_dones
+from .observation import BatchedKinematicObservation, observation_factory
 from .road import BatchedRoad, RoadNetwork
 from .state import BatchState
 
@@ -279,6 +279,7 @@ class VecIntersectionEnv:
             # finished env swaps in its next episode's scene, whose 45 warm-up frames ran
             # overlapped with earlier steps, and the following one is prepared in the background
             "overlap_resets": True,
+            "reset_streams": 2,  # side streams the overlapped resets rotate over
         }
 
     def configure(self, config: dict | None) -> None:
@@ -309,21 +310,25 @@ class VecIntersectionEnv:
         self._trunc = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
         self._components = torch.zeros((self.num_envs, 4), dtype=torch.float32, device=self.device)
         self._entropy = None  # [E, words + 1]: seed words, then the auto-reset episode counter
-        # overlap_resets: every env's next two episodes are prepared ahead of time on self._side, in
-        # two spare scenes per env (rows [0, E) and [E, 2E) of self._spare).  An env finishing
+        # overlap_resets: every env's next two episodes are prepared ahead of time on side streams,
+        # in two spare scenes per env (rows [0, E) and [E, 2E) of self._spare).  An env finishing
         # takes its scene from slot _spare_par[e], which was prepared at least two steps earlier
         # (the slots alternate), so the step waits only for the side-stream work launched two steps
-        # back (_spare_prev), while the last step's resets still run beside this step's launches.
+        # back (_spare_prev).  A step's spare resets (45 warm-up frames for a few hundred envs:
+        # a latency chain of about one step) go to the two side streams in turn, so the chains of
+        # consecutive steps overlap instead of queueing behind each other.
         self._spare = None
         if c["auto_reset"] and c["overlap_resets"]:
             E = self.num_envs
             self._spare = BatchState(2 * E, int(c["vehicle_slots"]), device=self.device, dtype=c["dtype"])
             self._spare_slot = (self._spare.rows(0, E), self._spare.rows(E, E))
             self._spare_par = torch.zeros(E, dtype=torch.uint8, device=self.device)
-            self._side = torch.cuda.Stream(self.device)
+            self._sides = tuple(torch.cuda.Stream(self.device) for _ in range(max(1, int(c["reset_streams"]))))
+            self._side_i = 0
             self._spare_ready = self._spare_prev = torch.cuda.Event()
-            self._spare_words = None  # [2E, words]: each spare scene's seed words ...
-            self._spare_ep = None     # [2E]: ... and episode counter
+            # [2E, words + 1]: each spare scene's seed words and episode counter (the last word);
+            # ix_step_tail_ advances the counter of a consumed row by two
+            self._spare_ent = None
         self.define_spaces()
 
     @property
@@ -368,8 +373,9 @@ class VecIntersectionEnv:
         self.done = False
         ix_reset(self.state, self.network, self.params, self.ix, self._entropy[:, :-1])
         if self._spare is not None:  # every env's second and third episodes, in the background
-            self._spare_words = torch.cat([self._entropy[:, :-1], self._entropy[:, :-1]])
-            self._spare_ep = torch.cat([self._entropy[:, -1] + 1, self._entropy[:, -1] + 2])
+            ent = self._entropy
+            self._spare_ent = torch.cat([torch.cat([ent[:, :-1], ent[:, :-1]]),
+                                         torch.cat([ent[:, -1:] + 1, ent[:, -1:] + 2])], 1).contiguous()
             self._spare_par.zero_()
             self._prepare_spares(None)
             self._spare_prev = self._spare_ready
@@ -378,27 +384,29 @@ class VecIntersectionEnv:
         return obs, self._info(obs, None)
 
     def _prepare_spares(self, mask: torch.Tensor | None) -> None:
-        """Reset the spare scenes of ``mask`` ([2E]; all: None) on the side stream, after the main
-        stream's work so far (the swap that consumed them).  The side stream reads its own copy of
-        the seed words and episode counters and a mask the main stream never writes again, so the
-        main stream may go on updating the counters while it runs."""
+        """Reset the spare scenes of ``mask`` ([2E]; all: None) on the next side stream, after the
+        main stream's work so far (the swap that consumed them).  The side stream reads the seed
+        words and episode counters of the masked rows only; the main stream writes a row's counter
+        when it consumes that row again, two steps later at the earliest, after waiting for this
+        reset (_spare_prev), so the rows in flight are never written under it."""
         main = torch.cuda.current_stream(self.device)
-        ent = torch.cat([self._spare_words, self._spare_ep.unsqueeze(1)], 1)
-        m = mask
-        self._side.wait_stream(main)
-        with torch.cuda.stream(self._side):
-            ix_reset(self._spare, self.network, self.params, self.ix, ent, m)
+        side = self._sides[self._side_i]
+        self._side_i = (self._side_i + 1) % len(self._sides)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            ix_reset(self._spare, self.network, self.params, self.ix, self._spare_ent, mask)
             ev = torch.cuda.Event()
-            ev.record(self._side)
-        ent.record_stream(self._side)
-        if m is not None:
-            m.record_stream(self._side)
+            ev.record(side)
+        if mask is not None:
+            mask.record_stream(side)
         self._spare_prev, self._spare_ready = self._spare_ready, ev
 
     def step(self, action):
         """IntersectionEnv.step (intersection_env.py:135-139) over AbstractEnv.step (abstract.py:224-250)."""
         if self.road is None:
             raise NotImplementedError("The road and vehicle must be initialized in the environment implementation")
+        if self._spare is not None:
+            return self._step_overlapped(action)
         self._simulate(action)
         obs = self.observation_type.observe()
         # time += 1 / policy_frequency (abstract.py:239) runs in the rewards launch
@@ -410,6 +418,43 @@ class VecIntersectionEnv:
             info["final_observation"], info["final_mask"] = obs, done
             obs = obs.clone()
             self._auto_reset(done, obs)
+        return obs, reward, terminated, truncated, info
+
+    def _step_overlapped(self, action):
+        """The auto-reset step with overlapped resets in two launches: ttrl::env_step_ (the fused
+        frames, the observation of the final state and the step tail: time += 1 / policy_frequency,
+        rewards, dones, info) and ttrl::ix_step_tail_ (clear / spawn for the envs that go on; the
+        finished ones swap in their spare scene and are re-observed); then the consumed spare rows
+        are reset again on a side stream.  Bit for bit the in-place composition (simulate, observe,
+        rewards, clear / spawn, reset, masked observe; test_overlapped_resets_equal_in_place_resets)."""
+        ot = self.observation_type
+        kin = isinstance(ot, BatchedKinematicObservation)
+        frames = int(self.config["simulation_frequency"] // self.config["policy_frequency"])
+        codes = None
+        if action is not None and not self.config["manual_control"]:
+            codes = self.action_type._codes(action)
+        self.steps += frames
+        obs, ids, *outs = self.road.env_step(codes, frames, 1 / self.config["simulation_frequency"],
+                                             ot.fused_cfg() if kin else None, self.reward_cfg, self.time,
+                                             1 / self.config["policy_frequency"])
+        reward, terminated, truncated = _keep_tail(self, outs)
+        if not kin:
+            obs = ot.observe()
+        info = self._info(obs, action)
+        _device_only(self.state)
+        # the slots this step takes were prepared two steps back at the latest
+        torch.cuda.current_stream(self.device).wait_event(self._spare_prev)
+        done, smask, obs2, ids2 = ops.T.ix_step_tail_(
+            self.state.tensors(), ops.st(self.network.table), ops.st(self.params), ops.st(self.ix),
+            self._spare.tensors(), terminated, truncated, self._spare_par, self._entropy, self._spare_ent, self.time,
+            ops.kin_cfg_tensor(ot.fused_cfg()) if kin else None, obs if kin else None, ids if kin else None)
+        self._prepare_spares(smask)
+        info["final_observation"], info["final_mask"] = obs, done
+        if kin:
+            ot.fused_result(obs2, ids2)
+            obs = obs2
+        else:
+            obs = ot.observe()
         return obs, reward, terminated, truncated, info
 
     def _simulate(self, action=None) -> None:
@@ -432,10 +477,13 @@ class VecIntersectionEnv:
         tensors [E].  One controlled vehicle per env, so agents_rewards / agents_terminated are
         1-tuples: its _agent_reward and crashed-or-arrived."""
         c = self._components
+        # _agent_is_terminal = crashed or arrived, which is _is_terminated itself unless
+        # offroad_terminal adds the off-road term (intersection_env.py:106-116); the step's reward
+        # and flag tensors are fresh per step, so sharing them costs no copy
+        at = self._term if not self.config["offroad_terminal"] else (c[:, 0] != 0) | (c[:, 2] != 0)
         return {"speed": self._ego_speed, "crashed": self._ego_crashed, "action": action,
                 "rewards": _reward_terms(self.REWARD_TERMS, c),
-                "agents_rewards": (self._reward.clone(),),
-                "agents_terminated": ((c[:, 0] != 0) | (c[:, 2] != 0),)}
+                "agents_rewards": (self._reward,), "agents_terminated": (at,)}
 
     def _auto_reset(self, done: torch.Tensor, obs: torch.Tensor) -> None:
         """Finished envs restart on the device with default_rng([seed words..., episode]) and
@@ -444,18 +492,7 @@ class VecIntersectionEnv:
         bit-identical) and the episode after it is prepared in the background."""
         d = done.view(torch.uint8)  # bool storage is one byte per env: the uint8 mask, no launch
         self._entropy[:, -1] += d
-        if self._spare is None:
-            ix_reset(self.state, self.network, self.params, self.ix, self._entropy, d)
-        else:
-            torch.cuda.current_stream(self.device).wait_event(self._spare_prev)
-            m1 = d & self._spare_par
-            m0 = d ^ m1
-            copy_envs(self.state, self._spare_slot[0], m0)
-            copy_envs(self.state, self._spare_slot[1], m1)
-            mask = torch.cat([m0, m1])
-            self._spare_ep.add_(mask, alpha=2)  # the taken slot's next scene: two episodes on
-            self._spare_par.bitwise_xor_(d)
-            self._prepare_spares(mask)
+        ix_reset(self.state, self.network, self.params, self.ix, self._entropy, d)
         self.time.masked_fill_(done, 0.0)
         self.observation_type.observe(mask=d, out=obs)
 
@@ -484,10 +521,10 @@ class VecIntersectionEnv:
             torch.cuda.current_stream(self.device).wait_event(self._spare_ready)
             new._spare = self._spare.clone()
             new._spare_slot = (new._spare.rows(0, self.num_envs), new._spare.rows(self.num_envs, self.num_envs))
-            new._spare_words = self._spare_words.clone()
-            new._spare_ep = self._spare_ep.clone()
+            new._spare_ent = self._spare_ent.clone()
             new._spare_par = self._spare_par.clone()
-            new._side = torch.cuda.Stream(self.device)
+            new._sides = tuple(torch.cuda.Stream(self.device) for _ in self._sides)
+            new._side_i = 0
             new._spare_ready = torch.cuda.Event()
             new._spare_ready.record(torch.cuda.current_stream(self.device))
             new._spare_prev = new._spare_ready
