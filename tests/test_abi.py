@@ -112,3 +112,17 @@ def test_device_seeding_matches_numpy_seedsequence():
         assert lib.ttrl_seed_pcg64(w.ctypes.data, len(w), out.ctypes.data) == 0
         assert np.array_equal(out, _abi.pcg64_states([[int(v) for v in ent]])[0]), ent
     assert lib.ttrl_seed_pcg64(None, 1, None) == -1
+
+
+def test_view_budgets_fit_the_residency_they_are_sized_for():
+    """LDS bytes per workgroup of the simulate kernel's views (ttrl_diag_view_bytes): the straight
+    highway's float64 64-slot env fits 16 workgroups per CU (4 waves per SIMD, 160 KB LDS), the
+    intersection's float64 road network (2 envs x 32 slots, 20 lanes; capped list rows and float32
+    trajectory prefilters) fits 8 (2 waves per SIMD: a 4096-env batch in one round)."""
+    lib = _lib.load()
+    f = lib.ttrl_diag_view_bytes
+    f.restype = C.c_long
+    f.argtypes = [C.c_int32] * 6
+    assert f(_abi.F64, 1, 64, 4, 0, 1) * 16 <= 160 * 1024
+    assert f(_abi.F64, 2, 32, 20, 1, 0) * 8 <= 160 * 1024
+    assert f(_abi.F32, 2, 32, 20, 1, 0) * 8 <= 160 * 1024

@@ -521,7 +521,9 @@ template <typename T> struct View {
   int8_t* rn;                    // [EPW*NS] route lengths (-1 None)
   uint8_t* ynew;                 // [EPW*NS] RegulatedRoad: yields decided this enforcement
   RoadTab* rt;                   // road topology
-  T *px, *py, *ph;               // [EPW*NS][PRED_T] predicted poses (is_conflict_possible)
+  float *px, *py;                // [EPW*NS][PRED_T] predicted positions, float32 (is_conflict_possible's
+                                 // distance prefilter; poses that pass are recomputed in float64)
+  T* ps0;                        // [EPW*NS] the prediction's start: s along the current lane
   unsigned long long* onm;       // [LMAX] (vehicle, lane) projection: on-lane slot masks
   uint8_t* live;                 // [EPW*NS] present slots in slot order
   int8_t* lperm;                 // [LMAX] lanes, straight ones first
@@ -537,6 +539,16 @@ template <typename T> struct View {
   T *steer, *acc, *ix, *iy;      // [EPW*NS] the action and the pending impact (only the vehicle reads them)
 };
 constexpr int PRED_T = 11;       // np.arange(0.25, 3, 0.25) (regulation.py:86)
+// Per-lane list capacity of the one-wavefront road-network instance: key / idx rows hold the first
+// GRAPH_LIST_CAP vehicles of a lane in list order (an intersection scene has ~8 live vehicles per
+// env over 20 lanes); the rest of a longer list is walked from the lane's on-lane slot mask with
+// its s recomputed (the same lane_local bits).  With the predictions in float32 this keeps the
+// float64 view <= 20 KB: 8 workgroups per CU, a 4096-env batch in one round.
+constexpr int GRAPH_LIST_CAP = 14;
+// Capacity of a list row: every slot of the env on the other instances.
+__host__ __device__ constexpr int list_cap(int NS, int EPW, bool graph) {
+  return graph && NS * EPW == 64 ? GRAPH_LIST_CAP : NS;
+}
 
 // Byte offsets of the view's arrays in the dynamic LDS block (host: sizing; device: carve).
 constexpr int N_REALS = 8;  // x, y, v, ch, sh, ts, h, delta
@@ -588,9 +600,10 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, 
     o.sord = take(M, 4);
     o.spos = take(M, 4);
   } else {
-    o.key = take(sizeof(T) * (size_t)n_lanes * EPW * (NS + 1), 16);
+    const size_t LS = list_cap(NS, EPW, graph) + 1;
+    o.key = take(sizeof(T) * (size_t)n_lanes * EPW * LS, 16);
     o.mypos = take(sizeof(short) * (size_t)n_lanes * M, 4);
-    o.idx = take((size_t)n_lanes * EPW * (NS + 1), 4);
+    o.idx = take((size_t)n_lanes * EPW * LS, 4);
   }
   const size_t u0 = take(0, 16);
   o.afree = take(sizeof(T) * M, 16);
@@ -607,8 +620,8 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, 
   o.pq_ij = take(sizeof(int) * M, 4);
   if (p < u1) p = u1;
   if (graph) {
-    o.pred = t0;
-    const size_t pred_end = t0 + sizeof(T) * 3 * PRED_T * M;
+    o.pred = t0;  // float px, py [M][PRED_T], then ps0 [M]
+    const size_t pred_end = t0 + ((sizeof(float) * 2 * PRED_T * M + 15) & ~(size_t)15) + sizeof(T) * M;
     if (p < pred_end) p = pred_end;
     o.rroad = take(TTRL_ROUTE_MAX * M, 4);
     o.rlane = take(TTRL_ROUTE_MAX * M, 4);
@@ -660,9 +673,9 @@ __device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lane
   V.tgt = (int8_t*)(smem + o.tgt);
   if (graph) {
     const size_t M = (size_t)EPW * NS;
-    V.px = (T*)(smem + o.pred);
+    V.px = (float*)(smem + o.pred);
     V.py = V.px + PRED_T * M;
-    V.ph = V.py + PRED_T * M;
+    V.ps0 = (T*)(smem + o.pred + ((sizeof(float) * 2 * PRED_T * M + 15) & ~(size_t)15));
     V.rroad = (int8_t*)(smem + o.rroad);
     V.rlane = (int8_t*)(smem + o.rlane);
     V.rn = (int8_t*)(smem + o.rn);
@@ -755,10 +768,12 @@ __device__ __forceinline__ void store_veh(const Veh<T>& a, const ttrl_state_t& s
 // slot order (ballot + popcount prefix), so neighbour scans visit only real candidates in
 // the reference's list order; returns the closest lane (RoadNetwork.get_closest_lane_index
 // road.py:55-71, distance_with_heading lane.py:132-147).  All threads must call it.
-template <typename T, int NS, int EPW, bool CV = true, bool LISTS = true>
+// LC < NS (the one-wavefront road network): rows keep the first LC entries, and V.onm[l] gets the
+// lane's on-lane mask of the whole wavefront (the rest of a longer list is walked from it).
+template <typename T, int NS, int EPW, bool CV = true, bool LISTS = true, int LC = NS>
 __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t& P, int nl, int tid, int le, int i,
                                            bool present, T x, T y, T h, bool want_closest, int* onb_out = nullptr) {
-  constexpr int NSP = NS + 1;
+  constexpr int NSP = LC + 1;
   const T vl = T(P.lane_vehicle_length);
   int best = 0, mx = 0;
   T bd = T(0), ang = T(0), prev_hd = T(0);
@@ -799,9 +814,13 @@ __device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t
       }
       const bool on = full && present && fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl;
       if constexpr (LISTS) {
-        const unsigned long long m = (__ballot(on) >> sh) & seg;
+        const unsigned long long wm = __ballot(on);
+        if constexpr (LC < NS) {
+          if (tid == 0) V.onm[l] = wm;
+        }
+        const unsigned long long m = (wm >> sh) & seg;
         const int pos = on ? __popcll(m & ((1ull << i) - 1)) : -1;
-        if (on) {
+        if (on && pos < LC) {
           V.key[((size_t)l * EPW + le) * NSP + pos] = s;
           V.idx[((size_t)l * EPW + le) * NSP + pos] = (uint8_t)i;
         }
@@ -999,11 +1018,12 @@ __device__ int g_dbg_count = 0;
 #else
 #define TTRL_ITEMS_ATTR __noinline__
 #endif
-template <typename T, int NS, int EPW>
+template <typename T, int NS, int EPW, int LC>
 __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const ttrl_params_t& P, int nl, int tid, int le, int i,
                              bool present, bool want_closest) {
   static_assert(NS * EPW == 64, "one wavefront per workgroup");
-  constexpr int NSP = NS + 1;
+  constexpr int NSP = LC + 1;
+  constexpr unsigned long long SEG = NS == 64 ? ~0ull : ((1ull << NS) - 1);
   const T vl = T(P.lane_vehicle_length);
   const unsigned long long below = (1ull << tid) - 1;
   const unsigned long long live = __ballot(present);
@@ -1017,10 +1037,14 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const ttrl_params
   const int g = total > 0 ? tid / total : 1;
   T bd = T(0), prev_hd = T(0), ang = T(0);
   int best = -1;
+  // pass 1: on-lane masks and the closest lane; the first two on-lane s of the thread's items are
+  // kept for pass 2 (the others are recomputed there: lane_local gives the same bits)
+  int v = 0, la = -1, lb = -1;
+  T sa = T(0), sb = T(0), x = T(0), y = T(0);
   if (g < G) {
-    const int v = V.live[tid - g * total];
-    const int vbase = (v / NS) * NSP + v % NS;
-    const T x = V.x[v], y = V.y[v], h = V.h[v];
+    v = V.live[tid - g * total];
+    x = V.x[v]; y = V.y[v];
+    const T h = V.h[v];
     for (int kk = g; kk < nl; kk += G) {
       int l = V.lperm[kk];
 #ifdef TTRL_CHECK_ITEMS
@@ -1034,7 +1058,8 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const ttrl_params
       lane_local<true>(L, x, y, s, r);
       if (fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl) {  // AbstractLane.on_lane margin 1
         atomicOr(&V.onm[l], 1ull << v);
-        V.key[(size_t)l * EPW * NSP + vbase] = s;  // at the slot; compacted below
+        if (la < 0) { la = l; sa = s; }
+        else if (lb < 0) { lb = l; sb = s; }
       }
       if (want_closest) {
         const T hdl = heading_at<true>(L, s);  // distance_with_heading lane.py:132-147
@@ -1061,21 +1086,34 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const ttrl_params
       if (cl < 0 || du < cd || (du == cd && lu < cl)) { cd = du; cl = lu; }
     }
   }
-  // one thread per (lane, env) list: its on-lane slots in slot order, keys compacted in place
-  // (position <= slot), slots, each vehicle's position and the list lengths
+  // pass 2: each on-lane item writes its vehicle's list position (slot order = list order) and,
+  // within the row's capacity, its key and slot
+  if (g < G) {
+    const int e = v / NS, sl = v % NS;
+    for (int kk = g; kk < nl; kk += G) {
+      const int l = V.lperm[kk];
+      const unsigned long long m = V.onm[l];
+      if (!((m >> v) & 1ull)) continue;
+      const int pos = __popcll((m >> (e * NS)) & SEG & ((1ull << sl) - 1));
+      V.mypos[(size_t)l * EPW * NS + v] = (short)pos;
+      if (pos < LC) {
+        T s = l == la ? sa : sb;
+        if (l != la && l != lb) {
+          T r;
+          lane_local<true>(V.lanes[l], x, y, s, r);
+        }
+        const size_t base = ((size_t)l * EPW + e) * NSP;
+        V.key[base + pos] = s;
+        V.idx[base + pos] = (uint8_t)sl;
+      }
+    }
+  }
+  // the list lengths, one thread per (lane, env)
   if (tid < nl * EPW) {
     const int l = tid / EPW, e = tid - l * EPW;
-    constexpr unsigned long long SEG = NS == 64 ? ~0ull : ((1ull << NS) - 1);
-    const size_t base = ((size_t)l * EPW + e) * NSP;
-    int pos = 0;
-    for (unsigned long long m = (V.onm[l] >> (e * NS)) & SEG; m; m &= m - 1, ++pos) {
-      const int v = __builtin_ctzll(m);
-      V.key[base + pos] = V.key[base + v];
-      V.idx[base + pos] = (uint8_t)v;
-      V.mypos[(size_t)l * EPW * NS + e * NS + v] = (short)pos;
-    }
-    V.cnt[e * (LMAX + 1) + l] = pos;
-    atomicMax(&V.cnt[e * (LMAX + 1) + LMAX], pos);
+    const int c = __popcll((V.onm[l] >> (e * NS)) & SEG);
+    V.cnt[e * (LMAX + 1) + l] = c;
+    atomicMax(&V.cnt[e * (LMAX + 1) + LMAX], c);
   }
 #ifdef TTRL_CHECK_ITEMS
   __syncthreads();
@@ -1094,7 +1132,7 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const ttrl_params
       const bool on1 = (m >> i) & 1ull;
       const int pos = __popcll(m & ((1ull << i) - 1));
       const size_t base = ((size_t)l * EPW + le) * NSP;
-      if (on != on1 || (on && (V.key[base + pos] != s || V.idx[base + pos] != i)))
+      if (on != on1 || (on && pos < LC && (V.key[base + pos] != s || V.idx[base + pos] != i)))
         if (atomicAdd(&g_dbg_count, 1) < 20)
           printf("items: blk %d tid %d lane %d on %d/%d pos %d key %g/%g idx %d total %d\n", (int)blockIdx.x, tid,
                  l, (int)on, (int)on1, pos, (double)V.key[base + pos], (double)s, (int)V.idx[base + pos], total);
@@ -1124,10 +1162,10 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const ttrl_params
 // The vehicle's longitudinal position along lane l: from the lane's candidate list when the vehicle
 // is on it (the projection after the last kinematics stored exactly lane_local's s for the same
 // position), else lane_local itself -- saves the turns' atan2 in the act phase.
-template <typename T, int NS, int EPW>
+template <typename T, int NS, int EPW, int LC = NS>
 __device__ __forceinline__ T lane_s(const View<T>& V, int l, int le, int i, T x, T y) {
   const int pos = V.mypos[(size_t)l * EPW * NS + le * NS + i];
-  if (pos >= 0) return V.key[((size_t)l * EPW + le) * (NS + 1) + pos];
+  if (pos >= 0 && pos < LC) return V.key[((size_t)l * EPW + le) * (LC + 1) + pos];
   T s, r;
   lane_local(V.lanes[l], x, y, s, r);
   return s;
@@ -1215,29 +1253,39 @@ __device__ TTRL_NET_ATTR int follow_road(const LaneT<T>* lanes, const RoadTab& R
 }
 
 // ControlledVehicle.predict_trajectory_constant_speed controller.py:228-247 through
-// RoadNetwork.position_heading_along_route road.py:352-389: the poses at t = 0.25 .. 2.75 s
-// along the route (route None or empty: the current lane), written to p*[0 .. PRED_T).
+// RoadNetwork.position_heading_along_route road.py:352-389: the pose at t = 0.25 (step + 1) s
+// along the route (route None or empty: the current lane) from s0, the position along the
+// current lane; the heading only when eh is given.
 template <typename T>
-__device__ TTRL_NET_ATTR void predict_poses(const LaneT<T>* lanes, const RoadTab& R, int cur, T x, T y, T v,
-                                           const int8_t* rr, const int8_t* rl, int rn, T* px, T* py, T* ph) {
-  T s0, r0;
-  lane_local(lanes[cur], x, y, s0, r0);
+__device__ TTRL_NET_ATTR void pose_at(const LaneT<T>* lanes, const RoadTab& R, int cur, T s0, T v, const int8_t* rr,
+                                     const int8_t* rl, int rn, int step, T& ex, T& ey, T* eh) {
   const bool route = rn > 0;
   const int n = route ? rn : 1;
   const int cid = lanes[cur].lid < lanes[cur].rn ? lanes[cur].lid : 0;  // None -> the current lane id
+  T L = s0 + v * (T(0.25) + T(step) * T(0.25));
+  int idx = 0;
+  int lane = route ? R.first[rr[0]] + (rl[0] >= 0 ? rl[0] : cid) : cur;
+  while (n - idx > 1 && L > lanes[lane].len) {
+    L -= lanes[lane].len;
+    ++idx;
+    lane = R.first[rr[idx]] + (rl[idx] >= 0 ? rl[idx] : cid);
+  }
+  lane_position(lanes[lane], L, T(0), ex, ey);
+  if (eh) *eh = heading_at(lanes[lane], L);
+}
+
+// The predicted positions at t = 0.25 .. 2.75 s, stored in float32 for is_conflict_possible's
+// distance prefilter (px / py[0 .. PRED_T)); s0 for the float64 poses recomputed where it passes.
+template <typename T>
+__device__ TTRL_NET_ATTR void predict_poses(const LaneT<T>* lanes, const RoadTab& R, int cur, T x, T y, T v,
+                                           const int8_t* rr, const int8_t* rl, int rn, float* px, float* py, T* ps0) {
+  T s0, r0;
+  lane_local(lanes[cur], x, y, s0, r0);
+  *ps0 = s0;
   for (int t = 0; t < PRED_T; ++t) {
-    T L = s0 + v * (T(0.25) + T(t) * T(0.25));
-    int idx = 0;
-    int lane = route ? R.first[rr[0]] + (rl[0] >= 0 ? rl[0] : cid) : cur;
-    while (n - idx > 1 && L > lanes[lane].len) {
-      L -= lanes[lane].len;
-      ++idx;
-      lane = R.first[rr[idx]] + (rl[idx] >= 0 ? rl[idx] : cid);
-    }
     T ex, ey;
-    lane_position(lanes[lane], L, T(0), ex, ey);
-    px[t] = ex; py[t] = ey;
-    ph[t] = heading_at(lanes[lane], L);
+    pose_at(lanes, R, cur, s0, v, rr, rl, rn, t, ex, ey, (T*)nullptr);
+    px[t] = (float)ex; py[t] = (float)ey;
   }
 }
 
@@ -1315,14 +1363,36 @@ __device__ __forceinline__ T idm_acc(const View<T>& V, const ttrl_params_t& P, i
 // One pass answering up to 3 Road.neighbour_vehicles queries per thread (road.py:480-513)
 // over the compacted per-lane candidate lists: front = min s_v >= s (ties: later slot),
 // rear = max s_v < s (ties: earlier slot), visiting candidates in slot (= list) order.
+// The entries of lane l's list (env le) from position `from` on, walked from the lane's on-lane
+// slot mask in slot (= list) order with s recomputed by lane_local (the bits the projection
+// stored), continuing a scan's front (s <= x <= sf: later wins ties) and rear (x < s, x > sr:
+// earlier wins) updates, with slots in f / r.  The one-wavefront road network's rows hold
+// GRAPH_LIST_CAP entries; longer lists are rare.
+template <typename T, int NS>
+__device__ __forceinline__ void overflow_scan(const View<T>& V, int le, int self, int l, int from, T s, T& sf, int& f,
+                                           bool rear, T& sr, int& r) {
+  constexpr unsigned long long SEG = NS == 64 ? ~0ull : ((1ull << NS) - 1);
+  unsigned long long m = (V.onm[l] >> (le * NS)) & SEG;
+  for (int c = 0; c < from && m; ++c) m &= m - 1;
+  const LaneT<T> L = V.lanes[l];
+  for (; m; m &= m - 1) {
+    const int j = __builtin_ctzll(m);
+    if (j == self) continue;
+    T x, rr;
+    lane_local<true>(L, V.x[le * NS + j], V.y[le * NS + j], x, rr);
+    if (s <= x && x <= sf) { sf = x; f = j; }
+    if (rear && x < s && x > sr) { sr = x; r = j; }
+  }
+}
+
 // Bit q of RM asks for query q's rear (the caller may need only fronts).  The updates are
 // selects, so the loop body is straight-line code.
-template <typename T, int NQ, int NS, int EPW, unsigned RM = 7u>
+template <typename T, int NQ, int NS, int EPW, unsigned RM = 7u, int LC = NS>
 __device__ __forceinline__ void scan_neighbours(const View<T>& V, int le, int self, const int (&ql)[NQ],
                                                 const T (&s)[NQ], int (&f)[NQ], int (&r)[NQ]) {
-  constexpr int NSP = NS + 1;
+  constexpr int NSP = LC + 1;
   const int* cnt = V.cnt + le * (LMAX + 1);
-  const int mx = cnt[LMAX];
+  const int mx = cnt[LMAX] < LC ? cnt[LMAX] : LC;
   T sf[NQ], sr[NQ];
   int n[NQ], me[NQ], fp[NQ], rp[NQ];
   const T* row[NQ];
@@ -1331,7 +1401,7 @@ __device__ __forceinline__ void scan_neighbours(const View<T>& V, int le, int se
     sf[q] = K<T>::inf(); sr[q] = -K<T>::inf(); fp[q] = -1; rp[q] = -1;
     const int l = ql[q] < 0 ? 0 : ql[q];
     row[q] = V.key + ((size_t)l * EPW + le) * NSP;
-    n[q] = ql[q] < 0 ? 0 : cnt[l];
+    n[q] = ql[q] < 0 ? 0 : (cnt[l] < LC ? cnt[l] : LC);
     me[q] = V.mypos[(size_t)l * EPW * NS + le * NS + self];  // self is skipped by position
   }
   constexpr int U = NQ == 1 ? 8 : 4;
@@ -1364,6 +1434,13 @@ __device__ __forceinline__ void scan_neighbours(const View<T>& V, int le, int se
     const uint8_t* ix = V.idx + ((size_t)(ql[q] < 0 ? 0 : ql[q]) * EPW + le) * NSP;
     f[q] = fp[q] >= 0 ? (int)ix[fp[q]] : -1;
     r[q] = rp[q] >= 0 ? (int)ix[rp[q]] : -1;
+  }
+  if constexpr (LC < NS) {  // lists beyond the row capacity: the rest, in list order, from the lane mask
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (ql[q] < 0 || cnt[ql[q]] <= LC) continue;
+      overflow_scan<T, NS>(V, le, self, ql[q], LC, s[q], sf[q], f[q], (RM & (1u << q)) != 0, sr[q], r[q]);
+    }
   }
 }
 
@@ -1513,6 +1590,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   // The straight-road instance carves a compile-time layout (LANE_CAP lanes): every view array
   // is then the LDS base plus an immediate offset, so no base addresses occupy registers.
   constexpr bool SO = sorted_view(NS, EPW, NET);
+  constexpr int LC = list_cap(NS, EPW, GR);  // list row capacity (GRAPH_LIST_CAP on one-wave networks)
   View<T> V = carve<T>(smem, EPW, NS, NET == NET_STRAIGHT ? STRAIGHT_LANE_CAP : nl, GR, SO);
   PH_INIT
   stage_lanes(V, R, tid);
@@ -1573,7 +1651,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
   {
     int ob = 0;
     const T x0 = V.x[me];
-    project_all<T, NS, EPW, CV, !SO>(V, P, nl, tid, le, i, present, x0, V.y[me], T(0), false, &ob);
+    project_all<T, NS, EPW, CV, !SO, LC>(V, P, nl, tid, le, i, present, x0, V.y[me], T(0), false, &ob);
     if constexpr (SO) sort_order<T, NS, EPW>(V, nl, tid, le, i, true, my_sorted, x0, ob);
   }
   const int kind = V.kind[me];
@@ -1588,7 +1666,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
       int tgt = V.tgt[me];
       if constexpr (GR)  // ControlledVehicle.act starts with follow_road (controller.py:98)
         tgt = follow_road(V.lanes, *V.rt, T(P.lane_vehicle_length), tgt, x, y, V.rroad + me * TTRL_ROUTE_MAX,
-                          V.rlane + me * TTRL_ROUTE_MAX, V.rn + me, lane_s<T, NS, EPW>(V, tgt, le, i, x, y));
+                          V.rlane + me * TTRL_ROUTE_MAX, V.rn + me, lane_s<T, NS, EPW, LC>(V, tgt, le, i, x, y));
       if (act == TTRL_FASTER || act == TTRL_SLOWER) {  // MDPVehicle.act controller.py:304-315
         int si = speed_to_index(P, v) + (act == TTRL_FASTER ? 1 : -1);
         si = si < 0 ? 0 : (si > P.n_target_speeds - 1 ? P.n_target_speeds - 1 : si);
@@ -1625,7 +1703,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
           if (present && (kind == TTRL_MDP || !(V.flags[me] & FL_CRASHED))) {
             tgt_new = follow_road(V.lanes, *V.rt, T(P.lane_vehicle_length), tgt_new, V.x[me], V.y[me],
                                   V.rroad + me * TTRL_ROUTE_MAX, V.rlane + me * TTRL_ROUTE_MAX, V.rn + me,
-                                  lane_s<T, NS, EPW>(V, tgt_new, le, i, V.x[me], V.y[me]));
+                                  lane_s<T, NS, EPW, LC>(V, tgt_new, le, i, V.x[me], V.y[me]));
             V.tgt[me] = (int8_t)tgt_new;
           }
         }
@@ -1661,7 +1739,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           if constexpr (GR) {
-            s2[q] = lane_s<T, NS, EPW>(V, ql[q] < 0 ? 0 : ql[q], le, i, x, y);
+            s2[q] = lane_s<T, NS, EPW, LC>(V, ql[q] < 0 ? 0 : ql[q], le, i, x, y);
           } else {
             T rr;
             lane_local<CV>(V.lanes[ql[q] < 0 ? 0 : ql[q]], x, y, s2[q], rr);
@@ -1682,14 +1760,14 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
           }
         } else if (!(ablate & A_NO_SCAN)) {
           if (__any(ql[1] >= 0)) {
-            if (polite) scan_neighbours<T, 2, NS, EPW, 1u>(V, le, i, ql, s2, f2, r2);
-            else scan_neighbours<T, 2, NS, EPW, 0u>(V, le, i, ql, s2, f2, r2);
+            if (polite) scan_neighbours<T, 2, NS, EPW, 1u, LC>(V, le, i, ql, s2, f2, r2);
+            else scan_neighbours<T, 2, NS, EPW, 0u, LC>(V, le, i, ql, s2, f2, r2);
           } else {
             const int ql1[1] = {ql[0]};
             const T s1[1] = {s2[0]};
             int f1[1], r1[1];
-            if (polite) scan_neighbours<T, 1, NS, EPW, 1u>(V, le, i, ql1, s1, f1, r1);
-            else scan_neighbours<T, 1, NS, EPW, 0u>(V, le, i, ql1, s1, f1, r1);
+            if (polite) scan_neighbours<T, 1, NS, EPW, 1u, LC>(V, le, i, ql1, s1, f1, r1);
+            else scan_neighbours<T, 1, NS, EPW, 0u, LC>(V, le, i, ql1, s1, f1, r1);
             f2[0] = f1[0]; r2[0] = r1[0];
           }
         }
@@ -1744,7 +1822,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             T sf = K<T>::inf(), sr = -K<T>::inf();
             int fp = -1, rp = -1;
             int np_ = -1, nf = -1;  // the side lane's front / rear of the item's vehicle
-            const size_t rowb = SO ? 0 : ((size_t)ln * EPW + le) * (NS + 1);
+            const size_t rowb = SO ? 0 : ((size_t)ln * EPW + le) * (LC + 1);
             if constexpr (SO) {
               if (!(ablate & A_NO_SCAN)) {
                 if (V.stie[le] == 0) sorted_nbrs<T, NS>(V, le, ln, V.spos[ve], np_, nf);
@@ -1752,7 +1830,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
               }
             } else if (!(ablate & A_NO_SCAN)) {
               const T* row = V.key + rowb;
-              const int n = V.cnt[le * (LMAX + 1) + ln];
+              const int n = V.cnt[le * (LMAX + 1) + ln] < LC ? V.cnt[le * (LMAX + 1) + ln] : LC;
               const int mep = V.mypos[(size_t)ln * EPW * NS + le * NS + vi];  // the item's vehicle is skipped
               for (int kk = g; kk < n; kk += G) {
                 const T xk = row[kk];
@@ -1776,6 +1854,10 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             if constexpr (!SO) {
               np_ = fp >= 0 ? (int)V.idx[rowb + fp] : -1;
               nf = rp >= 0 ? (int)V.idx[rowb + rp] : -1;
+              if constexpr (LC < NS) {  // the list beyond the row capacity (every lane of the group alike)
+                if (!(ablate & A_NO_SCAN) && V.cnt[le * (LMAX + 1) + ln] > LC)
+                  overflow_scan<T, NS>(V, le, vi, ln, LC, sq, sf, np_, true, sr, nf);
+              }
             }
             const int op = V.f0[ve], of = V.r0[ve];
             const T delta = V.delta[ve];
@@ -1937,7 +2019,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
               }
               predict_poses(V.lanes, *V.rt, (int)V.lane[me], V.x[me], V.y[me], V.v[me], V.rroad + me * TTRL_ROUTE_MAX,
                             V.rlane + me * TTRL_ROUTE_MAX, (int)V.rn[me], V.px + me * PRED_T, V.py + me * PRED_T,
-                            V.ph + me * PRED_T);
+                            V.ps0 + me);
             }
             V.ynew[me] = 0;
             __syncthreads();
@@ -1946,12 +2028,24 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
             // (a < b) of the env at LDS base ebp; a yield only ever sets ynew, so pairs commute
             auto reg_pair = [&](int ebp, int a, int b) {
               bool conflict = false;
+              const int ka = ebp + a, kb = ebp + b;
               for (int t = 0; t < PRED_T && !conflict; ++t) {
-                const int pa = (ebp + a) * PRED_T + t, pb = (ebp + b) * PRED_T + t;
-                const T dx = V.px[pb] - V.px[pa], dy = V.py[pb] - V.py[pa];
+                const int pa = ka * PRED_T + t, pb = kb * PRED_T + t;
+                // float32 prefilter: a pair farther apart than LENGTH + the conversion and rounding
+                // error bound (4e-7 of the coordinates' magnitude, 1 mm) is farther than LENGTH in
+                // float64 too (NaN / inf fall through to the exact test)
+                const float fxa = V.px[pa], fya = V.py[pa], fxb = V.px[pb], fyb = V.py[pb];
+                const float fdx = fxb - fxa, fdy = fyb - fya;
+                const float thr = float(P.length) + 1e-3f + 4e-7f * (fabsf(fxa) + fabsf(fxb) + fabsf(fya) + fabsf(fyb));
+                if (fdx * fdx + fdy * fdy > thr * thr) continue;
+                T xa, ya, ha, xb, yb, hb;  // the float64 poses, as predict_trajectory_constant_speed gives them
+                pose_at(V.lanes, *V.rt, (int)V.lane[ka], V.ps0[ka], V.v[ka], V.rroad + ka * TTRL_ROUTE_MAX,
+                        V.rlane + ka * TTRL_ROUTE_MAX, (int)V.rn[ka], t, xa, ya, &ha);
+                pose_at(V.lanes, *V.rt, (int)V.lane[kb], V.ps0[kb], V.v[kb], V.rroad + kb * TTRL_ROUTE_MAX,
+                        V.rlane + kb * TTRL_ROUTE_MAX, (int)V.rn[kb], t, xb, yb, &hb);
+                const T dx = xb - xa, dy = yb - ya;
                 if (sqrt(dx * dx + dy * dy) > T(P.length)) continue;
-                conflict = rects_intersect(V.px[pa], V.py[pa], V.ph[pa], V.px[pb], V.py[pb], V.ph[pb],
-                                           T(1.5) * T(P.length), T(0.9) * T(P.width));
+                conflict = rects_intersect(xa, ya, ha, xb, yb, hb, T(1.5) * T(P.length), T(0.9) * T(P.width));
               }
               if (!conflict) return;
               const int qa = V.lanes[V.lane[ebp + a]].prio, qb = V.lanes[V.lane[ebp + b]].prio;
@@ -2051,10 +2145,10 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int
 #else
       if constexpr (false)
 #endif
-        cl = project_items<T, NS, EPW>(V, P, nl, tid, le, i, present, !(ablate & A_NO_LANE));
+        cl = project_items<T, NS, EPW, LC>(V, P, nl, tid, le, i, present, !(ablate & A_NO_LANE));
       else {
         int ob = 0;
-        cl = project_all<T, NS, EPW, CV, !SO>(V, P, nl, tid, le, i, present, x, y, h, !(ablate & A_NO_LANE), &ob);
+        cl = project_all<T, NS, EPW, CV, !SO, LC>(V, P, nl, tid, le, i, present, x, y, h, !(ablate & A_NO_LANE), &ob);
         // this frame's order: the collision window below, the next frame's act
         if constexpr (SO) sort_order<T, NS, EPW>(V, nl, tid, le, i, false, my_sorted, x, ob);
       }
@@ -4172,6 +4266,11 @@ int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
     so.trunc = truncated; so.comp = components; so.ego_speed = ego_speed; so.ego_crashed = ego_crashed;
   }
   return run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream, 0, nullptr, &so);
+}
+
+/* Diagnostic only (not in include/): the simulate kernel's LDS view bytes per workgroup. */
+long ttrl_diag_view_bytes(int32_t dtype, int32_t epw, int32_t ns, int32_t n_lanes, int32_t graph, int32_t sorted) {
+  return (long)host_view_bytes(dtype, epw, ns, n_lanes, graph != 0, sorted != 0);
 }
 
 /* Diagnostic only (not in include/): the fused loop with phases ablated, for profiling. */
