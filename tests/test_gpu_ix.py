@@ -89,3 +89,92 @@ def test_ix_batch_of_episodes(hip_device):
             assert np.array_equal(out[k][e, :n], g[k][0, :n]), (e, k)
         assert out["reg_steps"][e] == g["reg_steps"][0]
         assert np.max(np.abs(out["x"][e, :n] - g["x"][0, :n])) < 1e-5
+
+
+def crowded_lane_state(n_extra: int = 22):
+    """A golden intersection scene with n_extra copies of an IDM vehicle spread along its straight
+    inbound lane (5.2 m apart, same route and speed): the lane's list then holds more vehicles than
+    the road-network instance's list rows (GRAPH_LIST_CAP = 14)."""
+    d = load_golden(golden_files("ix_*")[0])
+    h = HostState.from_ix(d, "pre", 0, pad_to=32)
+    t = ix_lanes(d)
+    n = int((h["kind"][0] > 0).sum())
+    j = next(q for q in range(n) if h["kind"][0, q] == 2 and t.type[h["lane"][0, q]] == 0)
+    l = int(h["lane"][0, j])
+    s0 = (h["x"][0, j] - t.start_x[l]) * t.dir_x[l] + (h["y"][0, j] - t.start_y[l]) * t.dir_y[l]
+    ss = [s for s in s0 + 5.2 * np.arange(-20, 20) if 1.0 <= s <= t.length[l] - 1.0 and abs(s - s0) > 1][:n_extra]
+    assert n + len(ss) <= 32
+    for q, s in enumerate(ss):
+        r = n + q
+        for k in h.a:
+            if h.a[k].ndim >= 2 and h.a[k].shape[1] == 32:
+                h.a[k][0, r] = h.a[k][0, j]
+        h["x"][0, r] = t.start_x[l] + s * t.dir_x[l]
+        h["y"][0, r] = t.start_y[l] + s * t.dir_y[l]
+        h["crashed"][0, r] = 0
+        h["has_impact"][0, r] = 0
+    return d, h, l, n + len(ss)
+
+
+def test_crowded_lane_beyond_list_capacity(hip_device):
+    """More vehicles on one lane than a list row holds: the neighbour and MOBIL scans continue from
+    the lane's on-lane mask (s recomputed, list order kept); frames and a fused step equal the oracle."""
+    from oracle.oracle import Oracle
+    d, h, l, n = crowded_lane_state()
+    t = ix_lanes(d)
+    on = sum(1 for q in range(n) if h["lane"][0, q] == l)
+    assert on > 14, on
+    o = Oracle(t, P_IX)
+    dev = to_dev(h, hip_device)
+    road = BatchedRoad(RoadNetwork(t), dev, P_IX)
+    g = h.copy()
+    for f in range(4):  # frame by frame
+        road.act()
+        o.road_act(g)
+        compare(dev, g, 1e-9, n)
+        road.step(1 / 15)
+        o.road_step(g, 1 / 15)
+        compare(dev, g, 1e-9, n)
+    road.simulate(torch.tensor([LONGI[1]]), 15, 1 / 15)  # and a fused step
+    o.simulate(g, [LONGI[1]], 15, 1 / 15)
+    compare(dev, g, 1e-6, n)
+
+
+def test_crowded_lane_mobil_on_a_regulated_road(hip_device):
+    """A 3-lane road with RegulatedRoad enforcement (so the road-network instance runs it, with its
+    capped list rows): 22 vehicles on the middle lane, 8 on the outer lanes whose lane-change timers
+    are due, so MOBIL scans the crowded middle lane beyond the row capacity; frames and a fused
+    step equal the oracle."""
+    from oracle.oracle import Oracle
+    from topotrafficrl_amd import _abi
+    t = _abi.straight_lane_table(3, length=400.0)
+    t.regulation_frequency = 2
+    rng = np.random.default_rng(3)
+    h = HostState(1, 32)
+    lanes = [1] * 23 + [0] * 4 + [2] * 4
+    xs = np.concatenate([20 + 8.0 * np.arange(23), 30 + 40.0 * np.arange(4), 50 + 40.0 * np.arange(4)])
+    for q, (ln, x) in enumerate(zip(lanes, xs)):
+        h["kind"][0, q] = _abi.MDP if q == 0 else _abi.IDM
+        h["x"][0, q] = x + rng.uniform(-0.5, 0.5)
+        h["y"][0, q] = 4.0 * ln + rng.uniform(-0.2, 0.2)
+        h["speed"][0, q] = rng.uniform(18, 26)
+        h["target_speed"][0, q] = rng.uniform(22, 30)
+        h["lane"][0, q] = h["target_lane"][0, q] = ln
+        h["timer"][0, q] = 0.99 if ln != 1 else rng.uniform(0, 1)
+        h["lane_change"][0, q] = 0 if q == 0 else 1
+    h["speed_index"][0, 0] = 1
+    n = len(lanes)
+    o = Oracle(t, P_IX)
+    dev = to_dev(h, hip_device)
+    road = BatchedRoad(RoadNetwork(t), dev, P_IX)
+    g = h.copy()
+    for f in range(6):
+        road.act()
+        o.road_act(g)
+        compare(dev, g, 1e-9, n)
+        road.step(1 / 15)
+        o.road_step(g, 1 / 15)
+        compare(dev, g, 1e-9, n)
+    road.simulate(torch.tensor([LONGI[1]]), 15, 1 / 15)
+    o.simulate(g, [LONGI[1]], 15, 1 / 15)
+    compare(dev, g, 1e-6, n)

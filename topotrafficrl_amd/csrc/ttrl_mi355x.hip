@@ -181,6 +181,39 @@ template <typename T> struct LaneT {
   int road, lid, rfirst, rn, prio;  // network: road, id within it, the road's first lane and lane count
 };
 
+// The behaviour constants as the float32 kernels use them: ttrl_params_t rounded once on the host,
+// so the launch's kernel arguments are float32 and every use reads a scalar register.  Converted
+// inside the kernel, the constants were hoisted out of the frame loop as VGPRs and spilled (the
+// float32 straight instance's scratch segment, written back to HBM every launch).  Same values as
+// T(P.x) in the kernel: float(double) rounds to nearest on the host as on the device.
+struct ParamsF {
+  float acc_max, comfort_acc_max, comfort_acc_min, distance_wanted, time_wanted, gap_denom, politeness,
+      lane_change_min_acc_gain, lane_change_max_braking, lane_change_delay, tau_pursuit, kp_a, kp_heading, kp_lateral,
+      max_steering, length, width, diagonal, max_speed, min_speed, lane_vehicle_length;
+  float target_speeds[8];
+  int32_t n_target_speeds;
+};
+template <typename T> struct ParamsSel { using type = ttrl_params_t; };
+template <> struct ParamsSel<float> { using type = ParamsF; };
+template <typename T> using ParamsT = typename ParamsSel<T>::type;
+inline ParamsF params_f(const ttrl_params_t& p) {
+  ParamsF f{};
+  f.acc_max = (float)p.acc_max; f.comfort_acc_max = (float)p.comfort_acc_max; f.comfort_acc_min = (float)p.comfort_acc_min;
+  f.distance_wanted = (float)p.distance_wanted; f.time_wanted = (float)p.time_wanted; f.gap_denom = (float)p.gap_denom;
+  f.politeness = (float)p.politeness; f.lane_change_min_acc_gain = (float)p.lane_change_min_acc_gain;
+  f.lane_change_max_braking = (float)p.lane_change_max_braking; f.lane_change_delay = (float)p.lane_change_delay;
+  f.tau_pursuit = (float)p.tau_pursuit; f.kp_a = (float)p.kp_a; f.kp_heading = (float)p.kp_heading;
+  f.kp_lateral = (float)p.kp_lateral; f.max_steering = (float)p.max_steering; f.length = (float)p.length;
+  f.width = (float)p.width; f.diagonal = (float)p.diagonal; f.max_speed = (float)p.max_speed;
+  f.min_speed = (float)p.min_speed; f.lane_vehicle_length = (float)p.lane_vehicle_length;
+  for (int k = 0; k < 8; ++k) f.target_speeds[k] = (float)p.target_speeds[k];
+  f.n_target_speeds = p.n_target_speeds;
+  return f;
+}
+template <typename T> inline ParamsT<T> params_for(const ttrl_params_t& p);
+template <> inline ttrl_params_t params_for<double>(const ttrl_params_t& p) { return p; }
+template <> inline ParamsF params_for<float>(const ttrl_params_t& p) { return params_f(p); }
+
 // Scalar arguments (a struct argument would be materialised in scratch); compiled out of the
 // straight-road instance, so the curved lanes' trigonometry stays off its register budget.
 template <typename T> struct Pair { T a, b; };
@@ -289,8 +322,8 @@ __device__ __forceinline__ bool reachable(const LaneT<T>& L, T vl, T px, T py) {
 }
 
 // ControlledVehicle.steering_control controller.py:145-187
-template <bool CV = true, typename T>
-__device__ __forceinline__ T steering_control(const LaneT<T>& L, const ttrl_params_t& P, T x, T y, T h, T v) {
+template <bool CV = true, typename T, typename PP>
+__device__ __forceinline__ T steering_control(const LaneT<T>& L, const PP& P, T x, T y, T h, T v) {
   T s, r;
   lane_local<CV>(L, x, y, s, r);
   const T lfh = heading_at<CV>(L, s + v * T(P.tau_pursuit));  // lane_future_heading
@@ -306,8 +339,8 @@ __device__ __forceinline__ T steering_control(const LaneT<T>& L, const ttrl_para
 }
 
 // MDPVehicle.speed_to_index controller.py:326-344 (np.round: half to even)
-template <typename T>
-__device__ __forceinline__ int speed_to_index(const ttrl_params_t& P, T v) {
+template <typename T, typename PP>
+__device__ __forceinline__ int speed_to_index(const PP& P, T v) {
   const int n = P.n_target_speeds;
   const T x = (v - T(P.target_speeds[0])) / (T(P.target_speeds[n - 1]) - T(P.target_speeds[0]));
   return (int)clip(rint(x * T(n - 1)), T(0), T(n - 1));
@@ -324,8 +357,8 @@ __device__ __forceinline__ int speed_to_index(const ttrl_params_t& P, T v) {
 
 // utils.are_polygons_intersecting utils.py:194-239 on the closed 5-point rectangles of
 // RoadObject.polygon objects.py:168-180.  a = lower-index vehicle (the reference's self).
-template <typename T>
-__device__ TTRL_SAT_ATTR void sat_pair(const ttrl_params_t& P, T ax, T ay, T ac, T as, T av, T bx, T by, T bc, T bs, T bv,
+template <typename T, typename PP>
+__device__ TTRL_SAT_ATTR void sat_pair(const PP& P, T ax, T ay, T ac, T as, T av, T bx, T by, T bc, T bs, T bv,
                          T dt, bool& inter, bool& will, T& tx, T& ty) {
   const T hl = T(P.length) / T(2), hw = T(P.width) / T(2);
   const T lx[4] = {-hl, -hl, +hl, +hl}, ly[4] = {-hw, +hw, +hw, -hw};
@@ -400,8 +433,8 @@ template <typename T> __device__ __forceinline__ T sat_margin(T ax, T ay, T bx, 
   return T(SepTol<T>::abs) + T(SepTol<T>::rel) * X + T(SepTol<T>::quad) * X * X;
 }
 
-template <typename T>
-__device__ __forceinline__ bool sat_separated(const ttrl_params_t& P, T ax, T ay, T ac, T as, T av, T bx, T by, T bc,
+template <typename T, typename PP>
+__device__ __forceinline__ bool sat_separated(const PP& P, T ax, T ay, T ac, T as, T av, T bx, T by, T bc,
                                               T bs, T bv, T dt) {
   const T hl = T(P.length) / T(2), hw = T(P.width) / T(2);
   const T dx = bx - ax, dy = by - ay;
@@ -421,8 +454,8 @@ __device__ __forceinline__ bool sat_separated(const ttrl_params_t& P, T ax, T ay
 // same normal normalisation, same projection, branch and sweep arithmetic): axis k < 4 is
 // edge k of a's polygon, k >= 4 edge k-4 of b's.  Returns the static and swept interval
 // distances and the normal oriented along the centre difference (the translation axis).
-template <typename T>
-__device__ __forceinline__ void sat_axis(const ttrl_params_t& P, int k, T ax, T ay, T ac, T as, T av, T bx, T by,
+template <typename T, typename PP>
+__device__ __forceinline__ void sat_axis(const PP& P, int k, T ax, T ay, T ac, T as, T av, T bx, T by,
                                          T bc, T bs, T bv, T dt, T& dd, T& dist, T& axx, T& axy) {
   const T hl = T(P.length) / T(2), hw = T(P.width) / T(2);
   const T lx[4] = {-hl, -hl, +hl, +hl}, ly[4] = {-hw, +hw, +hw, -hw};
@@ -472,8 +505,8 @@ __device__ __forceinline__ void sat_axis(const ttrl_params_t& P, int k, T ax, T 
 }
 
 // Out-of-line copy for the rare overflow sweep (keeps the hot path's register budget).
-template <typename T>
-__device__ __noinline__ void sat_pair_ool(const ttrl_params_t& P, T ax, T ay, T ac, T as, T av, T bx, T by, T bc,
+template <typename T, typename PP>
+__device__ __noinline__ void sat_pair_ool(const PP& P, T ax, T ay, T ac, T as, T av, T bx, T by, T bc,
                                           T bs, T bv, T dt, bool& inter, bool& will, T& tx, T& ty) {
   sat_pair(P, ax, ay, ac, as, av, bx, by, bc, bs, bv, dt, inter, will, tx, ty);
 }
@@ -770,8 +803,8 @@ __device__ __forceinline__ void store_veh(const Veh<T>& a, const ttrl_state_t& s
 // road.py:55-71, distance_with_heading lane.py:132-147).  All threads must call it.
 // LC < NS (the one-wavefront road network): rows keep the first LC entries, and V.onm[l] gets the
 // lane's on-lane mask of the whole wavefront (the rest of a longer list is walked from it).
-template <typename T, int NS, int EPW, bool CV = true, bool LISTS = true, int LC = NS>
-__device__ __forceinline__ int project_all(const View<T>& V, const ttrl_params_t& P, int nl, int tid, int le, int i,
+template <typename T, int NS, int EPW, bool CV = true, bool LISTS = true, int LC = NS, typename PP>
+__device__ __forceinline__ int project_all(const View<T>& V, const PP& P, int nl, int tid, int le, int i,
                                            bool present, T x, T y, T h, bool want_closest, int* onb_out = nullptr) {
   constexpr int NSP = LC + 1;
   const T vl = T(P.lane_vehicle_length);
@@ -1018,8 +1051,8 @@ __device__ int g_dbg_count = 0;
 #else
 #define TTRL_ITEMS_ATTR __noinline__
 #endif
-template <typename T, int NS, int EPW, int LC>
-__device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const ttrl_params_t& P, int nl, int tid, int le, int i,
+template <typename T, int NS, int EPW, int LC, typename PP>
+__device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int nl, int tid, int le, int i,
                              bool present, bool want_closest) {
   static_assert(NS * EPW == 64, "one wavefront per workgroup");
   constexpr int NSP = LC + 1;
@@ -1320,8 +1353,8 @@ __device__ __forceinline__ T idm_ratio(T v, T ts, T lim) {
   if (!(vv > T(0))) vv = (T(0) > vv) ? T(0) : vv;  // Python max(v, 0)
   return vv / fabs(not_zero(ts));
 }
-template <typename T>
-__device__ __forceinline__ T idm_free(const ttrl_params_t& P, T v, T ts, T lim, T delta) {
+template <typename T, typename PP>
+__device__ __forceinline__ T idm_free(const PP& P, T v, T ts, T lim, T delta) {
   return T(P.comfort_acc_max) * (T(1) - k_pow(idm_ratio(v, ts, lim), delta));
 }
 // The power split in two, so a vehicle's base can be shared: the act phase stores every vehicle's
@@ -1334,8 +1367,8 @@ __device__ __forceinline__ float pow_from_base(float b, float delta) { return t_
 
 // IDM interaction term  COMFORT_ACC_MAX * (desired_gap(e, f) / not_zero(d))^2 (behavior.py:185-189,
 // desired_gap :192-217, lane_distance_to objects.py:182-197 along e's current lane).
-template <bool CV = true, typename T>
-__device__ __forceinline__ T idm_interact(const View<T>& V, const ttrl_params_t& P, int eb, int e, int f) {
+template <bool CV = true, typename T, typename PP>
+__device__ __forceinline__ T idm_interact(const View<T>& V, const PP& P, int eb, int e, int f) {
   const LaneT<T> L = V.lanes[V.lane[eb + e]];
   T s1, r1, s0, r0;
   lane_local<CV>(L, V.x[eb + f], V.y[eb + f], s1, r1);
@@ -1351,8 +1384,8 @@ __device__ __forceinline__ T idm_interact(const View<T>& V, const ttrl_params_t&
 }
 
 // Full IDMVehicle.acceleration(ego=e, front=f) with the caller's DELTA (behavior.py:150-190).
-template <bool CV = true, typename T>
-__device__ __forceinline__ T idm_acc(const View<T>& V, const ttrl_params_t& P, int eb, int e, int f, T delta) {
+template <bool CV = true, typename T, typename PP>
+__device__ __forceinline__ T idm_acc(const View<T>& V, const PP& P, int eb, int e, int f, T delta) {
   if (e < 0) return T(0);
   const LaneT<T> L = V.lanes[V.lane[eb + e]];
   T a = idm_free(P, V.v[eb + e], V.ts[eb + e], L.lim, delta);
@@ -1504,8 +1537,8 @@ __device__ unsigned g_wphase[WTRACE_MAX][20];  // PHASE_TIMING: each wave's phas
 #define PH_FLUSH
 #endif
 
-template <typename T, int NS, int EPW, typename EgoFn>
-__device__ __forceinline__ void kin_observe(const ttrl_state_t& st, const LaneT<T>* lanes, const ttrl_params_t& P,
+template <typename T, int NS, int EPW, typename EgoFn, typename PP>
+__device__ __forceinline__ void kin_observe(const ttrl_state_t& st, const LaneT<T>* lanes, const PP& P,
                                             const ttrl_kin_cfg_t& cfg, bool env_ok, int env, T x, T y, T h, T v,
                                             T hc, T hs, int lane, bool present, bool mdp, EgoFn ego_of, T* s_key,
                                             int* s_cnt, int* s_ego, int (*s_perm)[64], int (*s_p)[64],
@@ -1563,8 +1596,17 @@ template <typename T, int NS, int EPW, int NET>
 __global__ void __launch_bounds__(NS* EPW, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES
                                                                : (NET == NET_STRAIGHT ? 4
                                                                   : (sizeof(T) == 8 || NET == NET_GRAPH ? 2 : 4)))
-simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, const int32_t* __restrict__ actions,
-                const uint8_t* __restrict__ env_mask, int frames, double dt_d, int mode, int ablate, StepOut so) {
+simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_t* __restrict__ actions,
+                const uint8_t* __restrict__ env_mask, int frames, double dt_d, int mode, int ablate_arg, StepOut so) {
+  // The diagnostic phase ablations (ttrl_diag_simulate) exist only in -DTTRL_DIAG_ABLATE builds: as a
+  // run-time argument their ~20 tests held SGPR masks for the whole launch (spilled to VGPR lanes),
+  // and the product passes 0 anyway.
+#ifdef TTRL_DIAG_ABLATE
+  const int ablate = ablate_arg;
+#else
+  constexpr int ablate = 0;
+  (void)ablate_arg;
+#endif
   constexpr bool CV = NET != NET_STRAIGHT;  // curved lane classes possible
   constexpr bool GR = NET == NET_GRAPH;     // roads, routes, RegulatedRoad
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2646,8 +2688,8 @@ __device__ __forceinline__ uint4 philox(uint4 c, uint2 key) {
 // and ego_of(ego, ex, ey, eh, ev, ec, es, elane) fetches the ego's.  The scratch arrays are
 // s_key[EPW * NS], s_cnt[EPW], s_ego[EPW], s_perm[EPW][64], s_p[EPW][64].  Used by kinematics_obs_kernel and,
 // fused after the last frame, by simulate_kernel (ttrl_env_step).
-template <typename T, int NS, int EPW, typename EgoFn>
-__device__ __forceinline__ void kin_observe(const ttrl_state_t& st, const LaneT<T>* lanes, const ttrl_params_t& P,
+template <typename T, int NS, int EPW, typename EgoFn, typename PP>
+__device__ __forceinline__ void kin_observe(const ttrl_state_t& st, const LaneT<T>* lanes, const PP& P,
                                             const ttrl_kin_cfg_t& cfg, bool env_ok, int env, T x, T y, T h, T v,
                                             T hc, T hs, int lane, bool present, bool mdp, EgoFn ego_of, T* s_key,
                                             int* s_cnt, int* s_ego, int (*s_perm)[64], int (*s_p)[64],
@@ -3225,8 +3267,8 @@ __device__ inline int closest_lane_index(const ttrl_lane_table_t& R, double x, d
 // Scene generation: ego MDPVehicle, then n-1 x IDMVehicle.create_random
 // (kinematics.py:50-104) + randomize_behavior (behavior.py:66-69), the numpy RNG stream
 // reproduced bit for bit, one env in draw order.
-template <typename T>
-__device__ void reset_env_serial(const ttrl_state_t& st, const ttrl_lane_table_t& R, const ttrl_params_t& P,
+template <typename T, typename PP>
+__device__ void reset_env_serial(const ttrl_state_t& st, const ttrl_lane_table_t& R, const PP& P,
                                  const ttrl_reset_cfg_t& cfg, Pcg g, int env) {
   const int N = st.n_veh, nl = R.n_lanes;
   const size_t b = (size_t)env * N;
@@ -3769,8 +3811,8 @@ __device__ __forceinline__ void plan_route(const ttrl_lane_table_t& R, const ttr
 // IntersectionEnv._spawn_vehicle intersection_env.py:320-348 (IDMVehicle.make_on_lane
 // objects.py:68-89, IDMVehicle.__init__ behavior.py:48-64, randomize_behavior :66-69).
 // Uniform across the wave: every lane holds the same generator and makes the same draws.
-template <typename T>
-__device__ void wave_spawn(const ttrl_state_t& st, const ttrl_lane_table_t& R, const ttrl_params_t& P,
+template <typename T, typename PP>
+__device__ void wave_spawn(const ttrl_state_t& st, const ttrl_lane_table_t& R, const PP& P,
                            const ttrl_ix_cfg_t& C, Pcg& g, size_t base, int lane, double longitudinal, double pos_dev,
                            double speed_dev, double prob, bool go_straight) {
   if (pcg_double(g) > prob) return;
@@ -3900,8 +3942,8 @@ __global__ void __launch_bounds__(64) ix_finish_kernel(ttrl_state_t st, ttrl_lan
 // IntersectionEnv.step tail (intersection_env.py:135-139): _clear_vehicles (:350-362) keeps the
 // controlled vehicle and every vehicle neither leaving (an "il"->"o" lane within 4 lengths of its
 // end) nor without a route, in list order; then _spawn_vehicle(spawn_probability).
-template <typename T>
-__device__ void ix_clear_spawn_env(const ttrl_state_t& st, const ttrl_lane_table_t& R, const ttrl_params_t& P,
+template <typename T, typename PP>
+__device__ void ix_clear_spawn_env(const ttrl_state_t& st, const ttrl_lane_table_t& R, const PP& P,
                                    const ttrl_ix_cfg_t& C, int env, int lane) {
   const size_t base = (size_t)env * st.n_veh;
   unsigned long long keep[4] = {~0ull, ~0ull, ~0ull, ~0ull};
@@ -4127,15 +4169,16 @@ int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_par
     const size_t need = ((sizeof(T) * M + 15) & ~(size_t)15) + 2 * sizeof(int) * 64 * EPW + 2 * sizeof(int) * EPW;
     if (o.afree + need > o.item + sizeof(short) * 2 * M) return TTRL_E_UNSUPPORTED;
   }
+  const ParamsT<T> PT = params_for<T>(P);
   if (graph)
-    hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_GRAPH>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, P,
+    hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_GRAPH>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, PT,
                        actions, mask, frames, dt, mode, ablate, ob);
   else if (curved)
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_CURVED>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R,
-                       P, actions, mask, frames, dt, mode, ablate, ob);
+                       PT, actions, mask, frames, dt, mode, ablate, ob);
   else
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_STRAIGHT>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R,
-                       P, actions, mask, frames, dt, mode, ablate, ob);
+                       PT, actions, mask, frames, dt, mode, ablate, ob);
   return launch_status();
 }
 
@@ -4276,6 +4319,9 @@ long ttrl_diag_view_bytes(int32_t dtype, int32_t epw, int32_t ns, int32_t n_lane
 /* Diagnostic only (not in include/): the fused loop with phases ablated, for profiling. */
 int ttrl_diag_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                        const int32_t* actions, int32_t frames, double dt, int32_t ablate, void* stream) {
+#ifndef TTRL_DIAG_ABLATE
+  if (ablate != 0) return TTRL_E_UNSUPPORTED;  // a -DTTRL_DIAG_ABLATE build of the library ablates phases
+#endif
   return run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream, ablate);
 }
 
