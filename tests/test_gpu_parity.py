@@ -271,7 +271,7 @@ def test_random_batch_rollout_vs_oracle(n, hip_device):
         compare(dev, h, 1e-6)
 
 
-@pytest.mark.parametrize("n", [24, 64])
+@pytest.mark.parametrize("n", [24, 64, 100, 128])
 def test_tied_positions_vs_oracle(n, hip_device):
     """Vehicles sharing x exactly (the ego included, same and different lanes): the sorted-order
     neighbour lookups of the straight instance cannot rank them, so those envs take the slot-order
@@ -409,10 +409,12 @@ def test_ttc_and_lidar_random_batch_vs_oracle(hip_device):
         assert np.array_equal(time_to_collision(dev, net, P, tc).cpu().numpy(), o.observe_ttc(h, tc))
 
 
-def test_collision_pair_queue_overflow_vs_oracle(hip_device):
+@pytest.mark.parametrize("n", [60, 120])
+def test_collision_pair_queue_overflow_vs_oracle(n, hip_device):
     """Pile-ups with more close pairs than slots (> NS queued pairs in an env) take the
-    per-vehicle sweep fallback; results must still equal the oracle."""
-    E, n = 64, 60
+    per-vehicle sweep fallback; results must still equal the oracle (n = 120: the two-wave
+    128-slot instance, whose sorted window feeds the queue)."""
+    E = 64
     rng = np.random.default_rng(11)
     h = HostState(E, n)
     h["x"][:] = 500 + rng.uniform(-12, 12, (E, n))

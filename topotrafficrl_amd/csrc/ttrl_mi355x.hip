@@ -627,7 +627,7 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, 
   const size_t t0 = take(0, 16);
   if (sorted) {  // the sorted order replaces the lists (the projection writes it, the act reads it)
     o.sxf = take(sizeof(float) * M, 16);
-    o.lmask = take(sizeof(unsigned long long) * EPW * n_lanes, 8);
+    o.lmask = take(sizeof(unsigned long long) * EPW * n_lanes * ((NS + 63) / 64), 8);
     o.stie = take(sizeof(int) * EPW, 4);
     o.onb = take(M, 4);
     o.sord = take(M, 4);
@@ -811,8 +811,8 @@ __device__ __forceinline__ int project_all(const View<T>& V, const PP& P, int nl
   int best = 0, mx = 0;
   T bd = T(0), ang = T(0), prev_hd = T(0);
   int* cnt = V.cnt + le * (LMAX + 1);
-  if constexpr (NS <= 64) {
-    const int sh = (tid & 63) / NS * NS;
+  if constexpr (NS <= 64 || !LISTS) {  // !LISTS: per-thread on-lane bits, any NS
+    const int sh = NS <= 64 ? (tid & 63) / NS * NS : 0;
     const unsigned long long seg = NS == 64 ? ~0ull : ((1ull << NS) - 1);
     bool have = false;  // bd / best hold a lane
     int onbits = 0;     // !LISTS: the lanes this vehicle is on
@@ -1004,14 +1004,113 @@ __device__ __forceinline__ void sort_order(const View<T>& V, int nl, int tid, in
   if (i == 0) V.stie[le] = tb != 0;
 }
 
+// sort_order for one 128-slot env over two wavefronts (NS = 128, EPW = 1): sorted position p lives
+// in thread p, which carries the slot at p in my_slot.  The slots' x and on-lane bits are read
+// from the view (written by the kinematics and project_all before the call); the exchanges across
+// the wave boundary -- the bitonic j = 64 stage of a launch's first order, the odd-even pair
+// (63, 64), the sortedness and tie checks -- go through LDS (the act phase's scratch, dead here).
+template <typename T>
+__device__ void sort_order128(const View<T>& V, int nl, int tid, bool init, int& my_slot) {
+  constexpr int NS = 128;
+  T* xk = V.afree;          // [128] keys for the cross-wave exchanges
+  int* xp = (int*)V.mob;    // [128] payloads
+  __syncthreads();  // every slot's x and on-lane bits are in the view
+  if (init) my_slot = tid;
+  T key = V.x[my_slot];
+  const int ob = V.onb[my_slot];
+  const bool nan = key != key;
+  if (nan) key = K<T>::inf();
+  int pay = my_slot | ob << 8;
+  const int lane = tid & 63;
+  auto less = [](T ka, int pa, T kb, int pb) { return ka < kb || (ka == kb && (pa & 0xff) < (pb & 0xff)); };
+  auto apply = [&](int pt, T pk, int pp, bool valid, bool up) {
+    const bool pl = less(pk, pp, key, pay);
+    const bool take = valid && ((tid < pt) == up ? pl : !pl);
+    key = take ? pk : key;
+    pay = take ? pp : pay;
+  };
+  if (init) {
+#pragma unroll
+    for (int k = 2; k <= NS; k <<= 1)
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        if (j == 64) {
+          xk[tid] = key; xp[tid] = pay;
+          __syncthreads();
+          const T pk = xk[tid ^ 64];
+          const int pp = xp[tid ^ 64];
+          __syncthreads();
+          apply(tid ^ 64, pk, pp, true, (tid & k) == 0);
+        } else {
+          apply(tid ^ j, __shfl(key, lane ^ j), __shfl(pay, lane ^ j), true, (tid & k) == 0);
+        }
+      }
+  }
+  T nk;
+  int np;
+  for (int pass = 0;; ++pass) {  // the previous frame's order, restored by odd-even transposition
+    if (tid == 64) { xk[0] = key; xp[0] = pay; }
+    __syncthreads();
+    nk = __shfl(key, lane < 63 ? lane + 1 : lane);
+    np = __shfl(pay, lane < 63 ? lane + 1 : lane);
+    if (tid == 63) { nk = xk[0]; np = xp[0]; }
+    const bool ok = tid + 1 >= NS || less(key, pay, nk, np);
+    if (__syncthreads_and(ok) || pass == NS) break;
+    apply(tid ^ 1, __shfl(key, lane ^ 1), __shfl(pay, lane ^ 1), true, true);
+    if (tid == 63 || tid == 64) { xk[1 + tid - 63] = key; xp[1 + tid - 63] = pay; }
+    __syncthreads();
+    const int po = (tid & 1) ? tid + 1 : tid - 1;
+    T pk = __shfl(key, (po & 63));
+    int pp = __shfl(pay, (po & 63));
+    if (tid == 63) { pk = xk[2]; pp = xp[2]; }
+    if (tid == 64) { pk = xk[1]; pp = xp[1]; }
+    apply(po >= 0 && po < NS ? po : tid, pk, pp, po >= 0 && po < NS, true);
+    __syncthreads();  // the boundary slots are rewritten by the next pass
+  }
+  const int sl = pay & 0xff;
+  my_slot = sl;
+  V.sord[tid] = (uint8_t)sl;
+  V.spos[sl] = (uint8_t)tid;
+  V.sxf[tid] = (float)key;
+#pragma unroll
+  for (int l = 0; l < STRAIGHT_LANE_CAP; ++l) {
+    const unsigned long long m = __ballot((pay >> (8 + l)) & 1);
+    if (lane == 0 && l < nl) V.lmask[l * 2 + (tid >> 6)] = m;
+  }
+  bool tie = nan;
+  if (tid + 1 < NS && key < T(FAR) && nk < T(FAR)) {
+    tie |= !less(key, pay, nk, np) || nk == key;  // unsorted at the pass cap (not expected) / equal x
+#pragma unroll
+    for (int l = 0; l < STRAIGHT_LANE_CAP; ++l)
+      if (l < nl) tie |= (key - V.lanes[l].sx) == (nk - V.lanes[l].sx);
+  }
+  const bool any_tie = __syncthreads_or(tie);
+  if (tid == 0) V.stie[0] = any_tie;
+}
+
 // Road.neighbour_vehicles (road.py:480-513) on lane l for the vehicle at sorted position p, from
 // the lane's position mask (no ties: positions order the keys strictly); slots, -1 for none.
 template <typename T, int NS>
 __device__ __forceinline__ void sorted_nbrs(const View<T>& V, int le, int l, int p, int& f, int& r) {
-  const unsigned long long m = V.lmask[le * STRAIGHT_LANE_CAP + l] & ~(1ull << p);
-  const unsigned long long up = m & ~((2ull << p) - 1), dn = m & ((1ull << p) - 1);
-  f = up ? (int)V.sord[le * NS + __ffsll((long long)up) - 1] : -1;
-  r = dn ? (int)V.sord[le * NS + 63 - __clzll((long long)dn)] : -1;
+  if constexpr (NS <= 64) {
+    const unsigned long long m = V.lmask[le * STRAIGHT_LANE_CAP + l] & ~(1ull << p);
+    const unsigned long long up = m & ~((2ull << p) - 1), dn = m & ((1ull << p) - 1);
+    f = up ? (int)V.sord[le * NS + __ffsll((long long)up) - 1] : -1;
+    r = dn ? (int)V.sord[le * NS + 63 - __clzll((long long)dn)] : -1;
+  } else {  // 128 positions in two words (sort_order128)
+    static_assert(NS == 128, "two mask words");
+    const unsigned long long* w = V.lmask + (le * STRAIGHT_LANE_CAP + l) * 2;
+    const int wp = p >> 6, b = p & 63;
+    const unsigned long long own = w[wp] & ~(1ull << b);
+    const unsigned long long up = own & ~((2ull << b) - 1), dn = own & ((1ull << b) - 1);
+    int fp = -1, rp = -1;
+    if (up) fp = (wp << 6) + __ffsll((long long)up) - 1;
+    else if (wp == 0 && w[1]) fp = 64 + __ffsll((long long)w[1]) - 1;
+    if (dn) rp = (wp << 6) + 63 - __clzll((long long)dn);
+    else if (wp == 1 && w[0]) rp = 63 - __clzll((long long)w[0]);
+    f = fp >= 0 ? (int)V.sord[le * NS + fp] : -1;
+    r = rp >= 0 ? (int)V.sord[le * NS + rp] : -1;
+  }
 }
 
 // The same in the reference's list (slot) order, for envs whose sorted order has ties: front =
@@ -1211,7 +1310,9 @@ enum { NET_STRAIGHT = 0, NET_CURVED = 1, NET_GRAPH = 2 };
 // The straight instance on one wavefront per workgroup keeps each env's vehicles in (x, slot) order
 // (sort_order) instead of per-lane candidate lists: on lanes along +x every lane's s is x minus a
 // constant, so that one order ranks the candidates of every lane.
-constexpr bool sorted_view(int NS, int EPW, int NET) { return NET == NET_STRAIGHT && NS * EPW == 64; }
+constexpr bool sorted_view(int NS, int EPW, int NET) {
+  return NET == NET_STRAIGHT && (NS * EPW == 64 || (NS == 128 && EPW == 1));
+}
 
 // AbstractLane.distance lane.py:127-130
 template <typename T>
@@ -1694,7 +1795,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
     int ob = 0;
     const T x0 = V.x[me];
     project_all<T, NS, EPW, CV, !SO, LC>(V, P, nl, tid, le, i, present, x0, V.y[me], T(0), false, &ob);
-    if constexpr (SO) sort_order<T, NS, EPW>(V, nl, tid, le, i, true, my_sorted, x0, ob);
+    if constexpr (SO && NS == 128) sort_order128<T>(V, nl, tid, true, my_sorted);
+    else if constexpr (SO) sort_order<T, NS, EPW>(V, nl, tid, le, i, true, my_sorted, x0, ob);
   }
   const int kind = V.kind[me];
 
@@ -2192,7 +2294,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
         int ob = 0;
         cl = project_all<T, NS, EPW, CV, !SO, LC>(V, P, nl, tid, le, i, present, x, y, h, !(ablate & A_NO_LANE), &ob);
         // this frame's order: the collision window below, the next frame's act
-        if constexpr (SO) sort_order<T, NS, EPW>(V, nl, tid, le, i, false, my_sorted, x, ob);
+        if constexpr (SO && NS == 128) sort_order128<T>(V, nl, tid, false, my_sorted);
+        else if constexpr (SO) sort_order<T, NS, EPW>(V, nl, tid, le, i, false, my_sorted, x, ob);
       }
       if (present && !(ablate & A_NO_LANE)) V.lane[me] = (int8_t)cl;  // on_state_update kinematics.py:170-177
       if (i == 0) V.pq_n[le] = 0;
@@ -2278,34 +2381,53 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
         // float window: |xf_j - xf_i| in float errs by < 1.2e-7 (|x_i| + |x_j|), far below the slack
         const float xfi = V.xf[me];
         const float Rwf = (float)Rw * 1.0001f + 1e-5f * fabsf(xfi) + 1e-3f;
-#pragma unroll
-        for (int c0 = 0; c0 < NS; c0 += CH) {
-          if (c0 + CH <= i + 1) continue;  // only partners j > i
-          unsigned long long m = 0;
-#pragma unroll
-          for (int j1 = 0; j1 < CH; j1 += 8) {
-            float xs[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) xs[u] = V.xf[eb + c0 + j1 + u];
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-              if (!(fabsf(xs[u] - xfi) > Rwf)) m |= 1ull << (j1 + u);
+        auto test_push = [&](int j) {
+          const T dx = V.x[eb + j] - xi, dy = V.y[eb + j] - yi;
+          const T d2 = dx * dx + dy * dy;
+          if (d2 > (thr + T(1)) * (thr + T(1))) return;  // far: skip the exact test
+          // objects.py:123-133 exact: norm > thr; inside thr - 1 it provably is not (no sqrt)
+          if (!(thr > T(1) && d2 < (thr - T(1)) * (thr - T(1))) && sqrt(d2) > thr) return;
+          if (sat_separated(P, xi, yi, V.ch[me], V.sh[me], vi, V.x[eb + j], V.y[eb + j], V.ch[eb + j], V.sh[eb + j],
+                            V.v[eb + j], dt))
+            return;  // provably (false, false): contributes nothing
+          const int q = atomicAdd(&V.pq_n[le], 1);
+          if (q < NS) V.pq_ij[le * NS + q] = pair_pack(i, j, 0);
+        };
+        if (SO && V.stie[le] == 0) {
+          // the 128-slot sorted view: walk out from this vehicle's sorted position while inside the
+          // window (the queue's order is free: pass 3 folds each vehicle's pairs by their indices)
+          if (!(ablate & A_NO_PREF)) {
+            const int p = V.spos[me];
+            for (int q = p + 1; q < NS && !(V.sxf[eb + q] - xfi > Rwf); ++q) {
+              const int j = V.sord[eb + q];
+              if (j > i) test_push(j);
+            }
+            for (int q = p - 1; q >= 0 && !(xfi - V.sxf[eb + q] > Rwf); --q) {
+              const int j = V.sord[eb + q];
+              if (j > i) test_push(j);
+            }
           }
-          if (i >= c0) m &= ~((2ull << (i - c0)) - 1);  // keep j > i
-          if (ablate & A_NO_PREF) m = 0;
-          while (m) {
-            const int j = c0 + __ffsll((long long)m) - 1;
-            m &= m - 1;
-            const T dx = V.x[eb + j] - xi, dy = V.y[eb + j] - yi;
-            const T d2 = dx * dx + dy * dy;
-            if (d2 > (thr + T(1)) * (thr + T(1))) continue;  // far: skip the exact test
-            // objects.py:123-133 exact: norm > thr; inside thr - 1 it provably is not (no sqrt)
-            if (!(thr > T(1) && d2 < (thr - T(1)) * (thr - T(1))) && sqrt(d2) > thr) continue;
-            if (sat_separated(P, xi, yi, V.ch[me], V.sh[me], vi, V.x[eb + j], V.y[eb + j], V.ch[eb + j], V.sh[eb + j],
-                              V.v[eb + j], dt))
-              continue;  // provably (false, false): contributes nothing
-            const int q = atomicAdd(&V.pq_n[le], 1);
-            if (q < NS) V.pq_ij[le * NS + q] = pair_pack(i, j, 0);
+        } else {
+#pragma unroll
+          for (int c0 = 0; c0 < NS; c0 += CH) {
+            if (c0 + CH <= i + 1) continue;  // only partners j > i
+            unsigned long long m = 0;
+#pragma unroll
+            for (int j1 = 0; j1 < CH; j1 += 8) {
+              float xs[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) xs[u] = V.xf[eb + c0 + j1 + u];
+#pragma unroll
+              for (int u = 0; u < 8; ++u)
+                if (!(fabsf(xs[u] - xfi) > Rwf)) m |= 1ull << (j1 + u);
+            }
+            if (i >= c0) m &= ~((2ull << (i - c0)) - 1);  // keep j > i
+            if (ablate & A_NO_PREF) m = 0;
+            while (m) {
+              const int j = c0 + __ffsll((long long)m) - 1;
+              m &= m - 1;
+              test_push(j);
+            }
           }
         }
       }
