@@ -1,0 +1,55 @@
+"""Timing of the reference's own Python frame loop -- TEST INFRASTRUCTURE, build container only.
+
+Imports the unmodified reference simulation core exactly as oracle/gen_golden.py does (the
+package __init__s that need gymnasium are bypassed) and times Road.act + Road.step(1/15) on the
+synthetic 64-vehicle straight highway of SURVEY.md §3.C, single-threaded, next to the float64 C
+oracle (oracle/ttrl_oracle.c) on the same scenes and one core.  /root/reference does not exist
+on the GPU box, so bench.py's cpu_baseline is the C port; this records the reference itself.
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python oracle/time_reference.py [seconds]
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("OMP_NUM_THREADS", "1")
+
+
+def main(seconds: float = 20.0, n: int = 64) -> None:
+    from oracle import gen_golden as G
+    from oracle.oracle import HostState, Oracle
+    from topotrafficrl_amd import _abi
+    frames, el, scenes = 0, 0.0, 0
+    while el < seconds:
+        road = G.make_highway(n, 1000 + scenes)
+        scenes += 1
+        s = time.perf_counter()
+        for _ in range(15 * 5):  # 5 env steps of 15 frames per scene (scene building not timed)
+            road.act()
+            road.step(1 / 15)
+            frames += 1
+        el += time.perf_counter() - s
+    ref = frames * n / el
+    lanes = _abi.straight_lane_table(4)
+    o = Oracle(lanes, _abi.default_params())
+    E = 64
+    h = HostState(E, n)
+    o.reset_highway(h, _abi.reset_cfg(n, lanes), list(range(E)))
+    steps, t1 = 0, time.perf_counter()
+    while time.perf_counter() - t1 < 5.0:
+        o.simulate(h, np.ones(E, dtype=np.int32), 15, 1 / 15)
+        steps += 1
+    port = steps * 15 * E * n / (time.perf_counter() - t1)
+    print(f"reference Python (Road.act + Road.step, {n} vehicles, 1 core): {ref:.4g} vehicle-frames/s "
+          f"({frames} frames over {scenes} scenes, {el:.1f} s)")
+    print(f"float64 C oracle, same workload shape, 1 core (OMP_NUM_THREADS=1): {port:.4g} vehicle-frames/s "
+          f"({port / ref:.0f}x the reference)")
+
+
+if __name__ == "__main__":
+    main(float(sys.argv[1]) if len(sys.argv) > 1 else 20.0)
