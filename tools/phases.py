@@ -76,7 +76,7 @@ def main(dtype="f64", steps=30, frames=15, ix=False, E=4096):
           f"p50 {np.percentile(span, 50):.0f} p90 {np.percentile(span, 90):.0f} max {span.max()}")
     st = t0 - lo[inv]
     print(f"wave start offset within its SIMD: mean {st.mean():.0f} max {st.max()}")
-    if os.environ.get("TIMING_LIB", "lib_timing.so") == "lib_timing.so":  # per-wave phase cycles
+    if os.environ.get("TIMING_LIB", "lib_timing.so").endswith("lib_timing.so"):  # per-wave phase cycles
         wp = np.zeros((nw, 20), dtype=np.uint32)
         lib.ttrl_diag_wave_phases.argtypes = [C.c_void_p, C.c_int]
         lib.ttrl_diag_wave_phases(wp.ctypes.data, nw)
