@@ -213,12 +213,15 @@ def test_dqn_training_on_the_intersection(hip_device):
     assert len(L.memory) == 512 and L.steps == 8 and torch.isfinite(L.last_loss)
 
 
-@pytest.mark.parametrize("duration", [1, 3])
-def test_overlapped_resets_equal_in_place_resets(duration, hip_device):
-    """overlap_resets (each env's next two episodes prepared on a side stream, swapped in from
-    alternating spare slots when an env finishes) gives the same trajectories, bit for bit, as
-    resetting in place; duration 1 finishes every env at every step (both slots in turn)."""
-    cfg = {**ENV_JSON, "num_envs": 48, "device": hip_device, "auto_reset": True, "duration": duration}
+@pytest.mark.parametrize("duration,dtype,streams", [(1, "f64", 2), (3, "f64", 2), (3, "f32", 2), (2, "f64", 1)])
+def test_overlapped_resets_equal_in_place_resets(duration, dtype, streams, hip_device):
+    """overlap_resets (each env's next two episodes prepared on side streams, swapped in from
+    alternating spare slots by ix_step_tail when an env finishes, the new episode observed in the
+    same launch) gives the same trajectories, bit for bit, as the in-place composition of separate
+    launches (simulate, observe, rewards, clear / spawn, reset, masked observe); duration 1
+    finishes every env at every step (both slots in turn)."""
+    cfg = {**ENV_JSON, "num_envs": 48, "device": hip_device, "auto_reset": True, "duration": duration,
+           "dtype": dtype, "reset_streams": streams}
     a = VecIntersectionEnv({**cfg, "overlap_resets": True})
     b = VecIntersectionEnv({**cfg, "overlap_resets": False})
     oa, _ = a.reset(seed=21)
