@@ -316,3 +316,22 @@ def test_masked_observation_keeps_the_other_envs_ids(hip_device):
     ot.observe(mask=mask, out=torch.empty((16, ot.vehicles_count, len(ot.features)), device=hip_device))
     keep = torch.arange(16, device=hip_device) != 3
     assert torch.equal(ot.observed_ids[keep], full[keep])
+
+
+def test_overlapped_resets_with_an_occupancy_grid(hip_device):
+    """A non-Kinematics observation with overlapped resets: the finished envs' rows are their new
+    scenes' grids, the others' the grid observed before clear / spawn -- as the in-place path."""
+    grid = {"type": "OccupancyGrid", "features": ["presence", "vx", "vy"], "grid_size": [[-27.5, 27.5], [-27.5, 27.5]],
+            "grid_step": [5, 5]}
+    cfg = {"observation": grid, "num_envs": 32, "device": hip_device, "auto_reset": True, "duration": 2}
+    a = VecIntersectionEnv({**cfg, "overlap_resets": True})
+    b = VecIntersectionEnv({**cfg, "overlap_resets": False})
+    a.reset(seed=5)
+    b.reset(seed=5)
+    g = torch.Generator(device=hip_device).manual_seed(9)
+    for t in range(5):
+        act = torch.randint(0, 3, (32,), device=hip_device, generator=g)
+        ra, rb = a.step(act), b.step(act)
+        for x, y in zip(ra[:4], rb[:4]):
+            assert torch.equal(x, y), t
+        assert torch.equal(ra[4]["final_observation"], rb[4]["final_observation"])

@@ -25,6 +25,12 @@ def run(mode: str, steps: int = 60, warm: int = 10) -> float:
     env = VecIntersectionEnv({"num_envs": C["num_envs"], "vehicle_slots": C["vehicles"], "observation": C["obs"],
                               "device": str(dev), "dtype": "f64", "auto_reset": True,
                               "overlap_resets": mode != "in_place"})
+    if mode == "no_side":  # the spare resets skipped entirely: the step without the side work (bound)
+        def prepare(mask):
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            env._spare_prev, env._spare_ready = env._spare_ready, ev
+        env._prepare_spares = prepare
     if mode == "no_wait":
         def prepare(mask):
             main = torch.cuda.current_stream(dev)
@@ -55,5 +61,5 @@ def run(mode: str, steps: int = 60, warm: int = 10) -> float:
 
 
 if __name__ == "__main__":
-    for m in ("shipped", "no_wait", "in_place", "shipped"):
+    for m in ("shipped", "no_wait", "no_side", "in_place", "shipped"):
         print(f"{m:10s} {run(m):.3f} ms per env.step", flush=True)

@@ -453,8 +453,9 @@ class VecIntersectionEnv:
         if kin:
             ot.fused_result(obs2, ids2)
             obs = obs2
-        else:
-            obs = ot.observe()
+        else:  # the other observers draw nothing: observe the new scenes, keep the others' rows
+            new = ot.observe()
+            obs = torch.where(done.view(-1, *([1] * (new.dim() - 1))), new, obs)
         return obs, reward, terminated, truncated, info
 
     def _simulate(self, action=None) -> None:
@@ -486,15 +487,19 @@ class VecIntersectionEnv:
                 "agents_rewards": (self._reward,), "agents_terminated": (at,)}
 
     def _auto_reset(self, done: torch.Tensor, obs: torch.Tensor) -> None:
-        """Finished envs restart on the device with default_rng([seed words..., episode]) and
-        their first observation is written into ``obs``; the others are untouched.  With
-        overlap_resets the new scene is swapped in from the spare buffer (reset ahead of time,
-        bit-identical) and the episode after it is prepared in the background."""
+        """In-place auto-reset (overlap_resets off): finished envs restart on the device with
+        default_rng([seed words..., episode]) and their first observation is written into
+        ``obs``; the others are untouched.  (With overlap_resets, _step_overlapped swaps in scenes
+        reset ahead of time instead, bit-identical.)"""
         d = done.view(torch.uint8)  # bool storage is one byte per env: the uint8 mask, no launch
         self._entropy[:, -1] += d
         ix_reset(self.state, self.network, self.params, self.ix, self._entropy, d)
         self.time.masked_fill_(done, 0.0)
-        self.observation_type.observe(mask=d, out=obs)
+        if isinstance(self.observation_type, BatchedKinematicObservation):
+            self.observation_type.observe(mask=d, out=obs)
+        else:  # the other observers draw nothing: observe all, keep the others' rows
+            new = self.observation_type.observe()
+            obs.copy_(torch.where(done.view(-1, *([1] * (new.dim() - 1))), new, obs))
 
     @property
     def vehicle(self):
