@@ -10,14 +10,22 @@ Default workload (config 4, per GPU): 4096 envs x 64 vehicles, Kinematics 15x7
 (env.json ranges, absolute=false, sorted), synthetic straight 4-lane highway,
 random-seeded scenes and uniformly random ego actions (pre-drawn on the device).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype f64|f32] [--config 1..6] [--auto-reset]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype f64|f32] [--config 1..6] [--auto-reset] [--strong]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+--gpus N > 1 without a torch.distributed.run environment: this process touches no GPU, starts
+``python -m torch.distributed.run --nproc-per-node N ... bench.py`` as a CHILD process (one rank
+per GPU), relays rank 0's JSON line and exits non-zero unless it reports n_gpus == N.
+--strong: a fixed global batch (default 8 x the config's per-GPU envs: 32,768 at config 4) split
+over the ranks by sharding.shard, instead of the default weak scaling (the config's envs per GPU).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -172,9 +180,80 @@ def read_pmc(dtype: str, cfg_id: int) -> tuple[dict | None, str]:
     return e, f"profiles/pmc_traffic.json ({e.get('profile', '?')}, libttrl_mi355x.so {e['so_sha16']})"
 
 
+def launch_ranks(n: int, argv: list) -> int:
+    """``bench.py --gpus n`` outside torch.distributed.run: run the ranks as a child
+    ``torch.distributed.run`` job on 127.0.0.1 (a subprocess, never an exec: this process has not
+    touched the GPU and does not), relay rank 0's JSON line with a ``launcher`` note, and return
+    non-zero if the child fails or its line does not report n_gpus == n."""
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL on this host needs dmabuf IPC
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    lines = []
+    for line in p.stdout.splitlines():
+        if line.startswith("{"):
+            lines.append(line)
+        else:
+            print(line, file=sys.stderr)
+    if p.returncode != 0:
+        print(f"bench.py: the {n}-rank child job failed (exit {p.returncode})", file=sys.stderr)
+        return p.returncode
+    if len(lines) != 1:
+        print(f"bench.py: expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr)
+        return 1
+    out = json.loads(lines[0])
+    if out.get("n_gpus") != n:
+        print(f"bench.py: --gpus {n} but the ranks report n_gpus = {out.get('n_gpus')}", file=sys.stderr)
+        return 3
+    out["launcher"] = {"ranks": n, "cmd": "python -m torch.distributed.run --nnodes=1 --nproc-per-node "
+                       f"{n} --master-addr 127.0.0.1 bench.py ...", "parent_imported_torch": "torch" in sys.modules}
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+def dry_run(args, rank: int, world: int) -> None:
+    """The rank logic without a GPU (tests/test_bench.py): gloo process group, the shard of every
+    rank, the max-over-ranks reduction; rank 0 prints the line's rank fields."""
+    import torch.distributed as dist
+    from topotrafficrl_amd import sharding
+    if world > 1:
+        dist.init_process_group("gloo")
+    offset, count, g = shard_of(args, rank, world)
+    shards = [(offset, count)]
+    if world > 1:
+        shards = [None] * world
+        dist.all_gather_object(shards, (offset, count))
+    elapsed = sharding.max_over_ranks(0.001 * (rank + 1))
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "scaling": "strong" if args.strong else "weak",
+                          "global_envs": g, "shards": shards, "max_elapsed": elapsed}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def shard_of(args, rank: int, world: int) -> tuple:
+    """(global env offset, envs on this rank, global envs) for weak or strong scaling."""
+    from topotrafficrl_amd import sharding
+    E = CONFIGS[args.config]["num_envs"]
+    if args.strong:
+        g = args.global_envs or 8 * E
+        off, cnt = sharding.shard(g, rank, world)
+        return off, cnt, g
+    off, cnt = sharding.weak_shard(E, rank)
+    return off, cnt, world * E
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: --global-envs (default 8 x the config's envs) split over the ranks")
+    ap.add_argument("--global-envs", type=int, default=None)
+    ap.add_argument("--dry-run", action="store_true", help="the rank / shard logic only, no GPU (tests)")
     ap.add_argument("--steps", type=int, default=None, help="default 20 (config 6: 100)")
     ap.add_argument("--warmup", type=int, default=None, help="default 3 (config 6: 10)")
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
@@ -192,13 +271,24 @@ def main():
         args.steps = 100 if args.config in (1, 6) else 20
     if args.warmup is None:
         args.warmup = 10 if args.config == 6 else 3
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+
+    from topotrafficrl_amd import sharding
+    rank, local, world = sharding.world()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:
+        dry_run(args, rank, world)
+        return
 
     import torch
     import torch.distributed as dist
     from topotrafficrl_amd.envs import VecHighwayEnv
 
-    from topotrafficrl_amd import sharding
-    rank, local, world = sharding.world()
     # TTRL_BENCH_SHARED_GPU=1 (rehearsal on a one-GPU box): every rank on cuda:0, gloo for the
     # barrier and the max-over-ranks reduction; the real multi-GPU run uses one GPU per rank + RCCL
     shared = os.environ.get("TTRL_BENCH_SHARED_GPU") == "1"
@@ -215,8 +305,10 @@ def main():
     torch.cuda.set_device(dev)
 
     C = CONFIGS[args.config]
-    E, N = C["num_envs"], C["vehicles"]
-    offset, _ = sharding.weak_shard(E, rank)  # weak scaling: E envs per GPU, global ids [rank*E, (rank+1)*E)
+    N = C["vehicles"]
+    # weak scaling: the config's envs per GPU, global ids [rank*E, (rank+1)*E); strong: the rank's
+    # contiguous block of the global batch (sharding.shard)
+    offset, E, global_envs = shard_of(args, rank, world)
     ix = args.config == 6
     if ix:
         from topotrafficrl_amd.intersection import VecIntersectionEnv
@@ -328,9 +420,9 @@ def main():
     kern_ms = float(np.mean(kern_warm)) if sg is not None else float(np.mean([span(r) for r in launches if r]))
     elapsed = sharding.max_over_ranks(elapsed, device=None if shared else dev)
 
-    veh_steps = world * E * N * 15 * args.steps
-    if ix:  # live vehicles, not slots (the rank's own count scaled by the number of ranks)
-        veh_steps = world * int(live.item()) * 15
+    veh_steps = global_envs * N * 15 * args.steps
+    if ix:  # live vehicles, not slots, summed over the ranks
+        veh_steps = int(sharding.sum_over_ranks(float(live.item()), device=None if shared else dev)) * 15
     value = veh_steps / elapsed
     rd, wr = state_bytes(args.dtype)
     alg_bytes = E * N * (rd + wr)  # per fused simulate launch
@@ -353,18 +445,19 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic",
-        "config": {"workload": C["name"], "envs_per_gpu": E, "vehicles_per_env": N, "frames_per_step": 15,
+        "config": {"workload": C["name"], "envs_per_gpu": E, "global_envs": global_envs, "vehicles_per_env": N,
+                   "frames_per_step": 15,
                    "observation": C["obs"]["type"], "parallelism": f"env-sharded x{world}, no collective on the step",
                    "hip_graph": bool(args.graph), "auto_reset": bool(args.auto_reset or ix)},
         # the HBM roofline of the fused launch: algorithmic bytes (state read + written once, the
         # observation written once) over the launch time measured here with HIP events
         "roofline": dict(bound="hbm", **hbm, kernel=kernel, kernel_ms=kern_ms, alg_bytes_per_launch=alg_bytes,
                          alg_bytes_per_vehicle_step=alg_bytes / (E * N * 15.0)),
-        "env_steps_per_s": world * E * args.steps / elapsed,
+        "env_steps_per_s": global_envs * args.steps / elapsed,
     }
     if pmc and pmc.get("valu_active_cycles_per_wave") and pmc.get("sq_waves"):
         # The roofline that binds: the fused kernel is VALU-issue / latency bound,
@@ -398,7 +491,7 @@ def main():
                                "kernel": "grid_obs_kernel (OccupancyGridObservation.observe)", "kernel_ms": g_ms,
                                "alg_bytes_per_launch": g_bytes}
     if ix:
-        out["config"]["live_vehicles_per_env"] = veh_steps / (world * E * 15 * args.steps)
+        out["config"]["live_vehicles_per_env"] = veh_steps / (global_envs * 15 * args.steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = (cpu_baseline_ix(args.cpu_seconds) if ix else
                                cpu_baseline(N, C["obs"] if C["obs"]["type"] == "Kinematics" else GRID7,

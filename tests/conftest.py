@@ -22,7 +22,7 @@ def golden_files(pattern="*.npz"):
     when asked for by name."""
     files = sorted(glob.glob(os.path.join(GOLDEN, pattern)))
     if pattern == "*.npz":
-        files = [f for f in files if not os.path.basename(f).startswith(("ix_", "mdp_", "policy_", "dqn_", "obsref_"))]
+        files = [f for f in files if not os.path.basename(f).startswith(("ix_", "mdp_", "policy_", "dqn_", "obsref_", "envref_"))]
     return files
 
 

@@ -44,3 +44,40 @@ def test_configs_match_baseline_json():
     assert (bench.CONFIGS[5]["num_envs"], bench.CONFIGS[5]["vehicles"]) == (8192, 64)
     assert (bench.CONFIGS[1]["num_envs"], bench.CONFIGS[1]["vehicles"]) == (1, 50)
     assert bench.CONFIGS[3]["obs"]["type"] == "OccupancyGrid"
+
+
+def _run_bench(*argv, env_extra=None):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(bench.ROOT, "bench.py"), *argv], capture_output=True,
+                       text=True, env=env, timeout=240)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+def test_gpus_n_runs_n_ranks_from_a_plain_invocation():
+    """`python bench.py --gpus 2` (how the driver may call it) runs a 2-rank torch.distributed.run
+    child job; the parent imports no torch (so it opens no device) and relays rank 0's line, which
+    reports n_gpus == 2 with the weak-scaling shards [r*E, (r+1)*E)."""
+    rc, out, err = _run_bench("--gpus", "2", "--dry-run")
+    assert rc == 0, err
+    assert out["n_gpus"] == 2 and out["scaling"] == "weak"
+    assert [tuple(s) for s in out["shards"]] == [(0, 4096), (4096, 4096)]
+    assert out["launcher"]["ranks"] == 2 and out["launcher"]["parent_imported_torch"] is False
+    assert out["max_elapsed"] == 0.002  # the max over both ranks
+
+
+def test_strong_scaling_splits_the_global_batch():
+    rc, out, err = _run_bench("--gpus", "2", "--dry-run", "--strong")
+    assert rc == 0, err
+    assert out["scaling"] == "strong" and out["global_envs"] == 32768
+    assert [tuple(s) for s in out["shards"]] == [(0, 16384), (16384, 16384)]
+    rc, out, err = _run_bench("--gpus", "1", "--dry-run", "--strong", "--global-envs", "1000")
+    assert rc == 0 and out["n_gpus"] == 1 and [tuple(s) for s in out["shards"]] == [(0, 1000)]
+
+
+def test_world_size_must_equal_gpus():
+    rc, out, err = _run_bench("--gpus", "2", "--dry-run", env_extra={"WORLD_SIZE": "1"})
+    assert rc == 2 and "WORLD_SIZE=1" in err

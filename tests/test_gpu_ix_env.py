@@ -213,15 +213,17 @@ def test_dqn_training_on_the_intersection(hip_device):
     assert len(L.memory) == 512 and L.steps == 8 and torch.isfinite(L.last_loss)
 
 
-@pytest.mark.parametrize("duration,dtype,streams", [(1, "f64", 2), (3, "f64", 2), (3, "f32", 2), (2, "f64", 1)])
-def test_overlapped_resets_equal_in_place_resets(duration, dtype, streams, hip_device):
+@pytest.mark.parametrize("duration,dtype,streams,slots", [(1, "f64", 2, 32), (3, "f64", 2, 32), (3, "f32", 2, 32),
+                                                         (2, "f64", 1, 32), (1, "f64", 3, 32), (2, "f64", 2, 96)])
+def test_overlapped_resets_equal_in_place_resets(duration, dtype, streams, slots, hip_device):
     """overlap_resets (each env's next two episodes prepared on side streams, swapped in from
     alternating spare slots by ix_step_tail when an env finishes, the new episode observed in the
     same launch) gives the same trajectories, bit for bit, as the in-place composition of separate
     launches (simulate, observe, rewards, clear / spawn, reset, masked observe); duration 1
-    finishes every env at every step (both slots in turn)."""
+    finishes every env at every step (both slots in turn).  96 slots: the new scenes are observed
+    by the masked observation launch instead of the tail launch (one slot per lane there)."""
     cfg = {**ENV_JSON, "num_envs": 48, "device": hip_device, "auto_reset": True, "duration": duration,
-           "dtype": dtype, "reset_streams": streams}
+           "dtype": dtype, "reset_streams": streams, "vehicle_slots": slots}
     a = VecIntersectionEnv({**cfg, "overlap_resets": True})
     b = VecIntersectionEnv({**cfg, "overlap_resets": False})
     oa, _ = a.reset(seed=21)
@@ -242,8 +244,11 @@ def test_deepcopy_forks_an_independent_env(hip_device):
     """copy.deepcopy (the reference's what-if simulations, abstract.py:342-429) forks state, seeds
     and spare scenes: both copies then follow the same trajectory independently."""
     import copy
-    env = VecIntersectionEnv({**ENV_JSON, "num_envs": 16, "device": hip_device, "auto_reset": True, "duration": 2})
+    env = VecIntersectionEnv({**ENV_JSON, "num_envs": 16, "device": hip_device, "auto_reset": True, "duration": 1})
     env.reset(seed=9)
+    a0 = torch.zeros(16, dtype=torch.int64, device=hip_device)
+    env.step(a0)
+    env.step(a0)  # spare resets in flight on both side streams when the fork clones them
     fork = copy.deepcopy(env)
     a = torch.ones(16, dtype=torch.int64, device=hip_device)
     for _ in range(4):
@@ -282,15 +287,18 @@ def test_slot_classes_match_the_oracle(slots, hip_device):
         assert np.max(np.abs(obs.cpu().numpy() - want)) <= 1e-4
 
 
-def test_reset_right_after_step_joins_the_background_resets(hip_device):
-    """reset() straight after a step, while the side stream may still be resetting the spare
-    scenes: it waits for them before replacing the spare buffers (or rebuilding with a new config),
-    so the result equals a fresh env's."""
-    cfg = {**ENV_JSON, "num_envs": 32, "device": hip_device, "auto_reset": True, "duration": 2}
+@pytest.mark.parametrize("streams", [2, 3])
+def test_reset_right_after_step_joins_the_background_resets(streams, hip_device):
+    """reset() straight after steps whose auto-resets keep every side stream busy: it waits for
+    all of them (not only the latest) before replacing the spare buffers (or rebuilding with a new
+    config), so the result equals a fresh env's."""
+    cfg = {**ENV_JSON, "num_envs": 32, "device": hip_device, "auto_reset": True, "duration": 1,
+           "reset_streams": streams}
     env = VecIntersectionEnv(cfg)
     env.reset(seed=3)
     a = torch.ones(32, dtype=torch.int64, device=hip_device)
-    env.step(a)
+    for _ in range(streams + 1):  # duration 1: every env finishes, every step launches spare resets
+        env.step(a)
     obs, _ = env.reset(seed=11, options={"config": {"initial_vehicle_count": 8}})
     fresh = VecIntersectionEnv({**cfg, "initial_vehicle_count": 8})
     want, _ = fresh.reset(seed=11)
@@ -335,3 +343,52 @@ def test_overlapped_resets_with_an_occupancy_grid(hip_device):
         for x, y in zip(ra[:4], rb[:4]):
             assert torch.equal(x, y), t
         assert torch.equal(ra[4]["final_observation"], rb[4]["final_observation"])
+
+
+def test_single_vehicle_observation_has_padding_ids(hip_device):
+    """vehicles_count 1 (the ego alone): observed_ids' placeholder column is -1, also for the envs
+    the overlapped auto-reset re-observes."""
+    obs1 = dict(ENV_JSON["observation"], vehicles_count=1)
+    env = VecIntersectionEnv({"observation": obs1, "num_envs": 16, "device": hip_device, "auto_reset": True,
+                              "duration": 1})
+    env.reset(seed=2)
+    assert torch.equal(env.observation_type.observed_ids.cpu(), torch.full((16, 1), -1, dtype=torch.int32))
+    for _ in range(3):
+        env.step(torch.ones(16, dtype=torch.int64, device=hip_device))
+        assert torch.equal(env.observation_type.observed_ids.cpu(), torch.full((16, 1), -1, dtype=torch.int32))
+
+
+def test_device_episodes_match_the_reference_env(hip_device):
+    """All 18 episodes of the reference's own IntersectionEnv (envref fixtures: reset(seed) and 13
+    env.json steps, crashes, arrivals and rejected spawns among them) replayed in one batch from
+    their seeds: observation, reward, flags, the info dict, the state after clear / spawn, and
+    each env's np_random state word for word after every step."""
+    from test_ix_env_oracle import ENVREF, INFO_TERMS
+    refs = [load_golden(p) for p in ENVREF]
+    E = len(refs)
+    env = VecIntersectionEnv({**ENV_JSON, "num_envs": E, "device": hip_device})
+    obs, info = env.reset(seed=[int(d["meta"][0]) for d in refs])
+    st = env.state.to_numpy()
+    for e, d in enumerate(refs):
+        same_state(env_view(st, e), HostState.from_ix(d, "pre", 0, pad_to=32), 1e-9, f"reset {e}")
+        assert np.max(np.abs(obs[e].cpu().numpy() - d["obs0"])) <= 1e-6, e
+    steps = int(refs[0]["meta"][1])
+    acts = np.stack([d["actions"] for d in refs], 1)
+    for p in range(steps):
+        obs, rew, term, trunc, info = env.step(torch.from_numpy(acts[p]).to(hip_device))
+        st = env.state.to_numpy()
+        terms = np.stack([info["rewards"][n].cpu().numpy() for n in INFO_TERMS], 1)
+        speed, crashed = info["speed"].cpu().numpy(), info["crashed"].cpu().numpy()
+        ar, at = info["agents_rewards"][0].cpu().numpy(), info["agents_terminated"][0].cpu().numpy()
+        for e, d in enumerate(refs):
+            tol = obs_tol(HostState.from_ix(d, "end", p, pad_to=32), EPISODE_TOL)
+            assert np.max(np.abs(obs[e].cpu().numpy() - d["obs"][p])) <= tol, (e, p)
+            assert abs(float(rew[e]) - d["reward"][p]) <= tol, (e, p)
+            assert bool(term[e]) == bool(d["terminated"][p]) and bool(trunc[e]) == bool(d["truncated"][p]), (e, p)
+            want = d["info"][p]
+            assert abs(float(speed[e]) - want[0]) <= tol * (1 + abs(want[0])) and bool(crashed[e]) == bool(want[1])
+            assert terms[e, 0] == want[2] and terms[e, 2] == want[4] and terms[e, 3] == want[5], (e, p)
+            assert abs(terms[e, 1] - want[3]) <= tol and abs(float(ar[e]) - want[6]) <= tol, (e, p)
+            assert bool(at[e]) == bool(want[7]), (e, p)
+            same_state(env_view(st, e), HostState.from_ix(d, "post", p, pad_to=32), EPISODE_TOL, f"env {e} step {p}")
+            assert np.array_equal(st["rng"][e], d["rng"][p]), (e, p, "np_random state")

@@ -4,7 +4,12 @@ _make_vehicles with its 45 warm-up frames, challenger, ego, removal of nearby ve
 iterating), then per step the fused frames, the np_random-shuffled Kinematics observation,
 reward / terminated / truncated, _clear_vehicles and _spawn_vehicle.  Every draw comes from
 one np_random per env, as gymnasium seeds it.  Also pins the product's host-side restatement of
-_make_road and the BFS routes against the reference's own network.  CPU only."""
+_make_road and the BFS routes against the reference's own network.
+
+The envref_ix_s* fixtures (oracle/gen_golden_envref.py) are the reference's own IntersectionEnv
+run under gymnasium / pygame stand-ins (reset(seed), 13 steps of env.json): the committed ix goldens
+are held to them bit for bit, and the oracle replays all 18 of their episodes from the seed, the
+info dict and np_random's state included.  CPU only."""
 import numpy as np
 import pytest
 
@@ -159,3 +164,90 @@ def test_make_and_register():
     with pytest.raises(KeyError):
         make("merge-v0")
     assert register() in (True, False)
+
+
+ENVREF = golden_files("envref_ix_s*.npz")
+INFO_TERMS = ["collision_reward", "high_speed_reward", "arrived_reward", "on_road_reward"]
+
+
+def test_envref_fixtures_cover_the_episode_events():
+    """The reference-run episodes hold crashes, arrivals (the exit reward and termination),
+    truncations and spawns rejected by the 15 m test after their draws."""
+    ds = [load_golden(p) for p in ENVREF]
+    assert len(ds) == 18
+    assert sum(int(d["info"][:, 1].max()) for d in ds) >= 5            # crashed
+    assert sum(int((d["info"][:, 4] > 0).any()) for d in ds) >= 3      # arrived
+    assert sum(int(d["truncated"].any()) for d in ds) >= 1
+    assert sum(int(d["spawns"][1]) for d in ds) >= 10                  # rejected spawns
+    assert all(np.array_equal(d["rng0"], _abi.rng_states([int(d["meta"][0])])[0]) for d in ds)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_ix_goldens_equal_the_reference_env(seed):
+    """gen_golden_ix's IxEnv episodes (every intersection golden the oracle and the device are held
+    to) equal the reference IntersectionEnv's on the same seed and actions, bit for bit: reset,
+    the state after the frames, after clear / spawn, observations, rewards and flags."""
+    ix = load_golden(golden_files(f"ix_s{seed}.npz")[0])
+    ref = load_golden(golden_files(f"envref_ix_s{seed}.npz")[0])
+    assert np.array_equal(ix["actions"], ref["actions"])
+    for k in ("obs0", "obs", "reward", "terminated", "truncated"):
+        assert np.array_equal(ix[k], ref[k]), k
+    steps = int(ref["meta"][1])
+    for p in range(steps):
+        for mine, theirs in ((HostState.from_ix(ix, "pre", p), HostState.from_ix(ref, "pre", p)),
+                             (HostState.from_ix(ix, "frame", (p, 14)), HostState.from_ix(ref, "end", p)),
+                             (HostState.from_ix(ix, "post", p), HostState.from_ix(ref, "post", p))):
+            n = int((theirs["kind"] > 0).sum())
+            assert int((mine["kind"] > 0).sum()) == n, p
+            for k, v in theirs.a.items():
+                if k == "rng":
+                    continue
+                w = mine.a[k]
+                assert np.array_equal(w[:, :n] if w.ndim > 1 else w, v[:, :n] if v.ndim > 1 else v), (p, k)
+
+
+def _info_of(h: HostState, comp: np.ndarray) -> np.ndarray:
+    """The fixture's info row from the oracle state: ego speed, crashed, the four reward terms,
+    agents_rewards (filled by the caller), agents_terminated (crashed or arrived)."""
+    ego = int(np.argmax(h["kind"][0] == _abi.MDP))
+    return np.array([h["speed"][0, ego], float(h["crashed"][0, ego]), *comp[0].astype(np.float64), 0.0,
+                     float(bool(h["crashed"][0, ego]) or comp[0, 2] != 0)])
+
+
+@pytest.mark.parametrize("path", ENVREF, ids=IDS)
+def test_reference_env_episode_from_seed(path):
+    """The float64 oracle replays the reference IntersectionEnv's episode from its seed: reset,
+    the frames, the shuffled observation, reward / terminated / truncated, the info dict, clear /
+    spawn -- and np_random's state after every step is the reference's, word for word (every
+    spawn, rejection and shuffle drew exactly the reference's draws)."""
+    d = load_golden(path)
+    seed, steps = int(d["meta"][0]), int(d["meta"][1])
+    net = intersection_network()
+    o = Oracle(net.table, P_IX)
+    cfg = ix_cfg(net, CFG, P_IX)
+    h = HostState(1, 32)
+    o.ix_reset(h, cfg, [seed])
+    same_state(h, HostState.from_ix(d, "pre", 0, pad_to=32), 1e-9, "reset")
+    obs, _ = o.observe_kinematics(h, KIN)
+    assert np.max(np.abs(obs[0] - d["obs0"])) <= 1e-6
+    _, _, _, comp = o.rewards(h, REW, 0.0, components=True)
+    want = d["info0"]
+    got = _info_of(h, comp)
+    assert np.allclose(got[[0, 2, 3, 4, 5]], want[[0, 2, 3, 4, 5]], rtol=0, atol=1e-6) and got[1] == want[1]
+    for p in range(steps):
+        o.simulate(h, [LONGI[int(d["actions"][p])]], 15, 1 / 15)
+        end = HostState.from_ix(d, "end", p, pad_to=32)
+        same_state(h, end, EPISODE_TOL, f"frames {p}")
+        obs, _ = o.observe_kinematics(h, KIN)
+        tol = obs_tol(end, EPISODE_TOL)
+        assert np.max(np.abs(obs[0] - d["obs"][p])) <= tol, p
+        rew, term, trunc, comp = o.rewards(h, REW, float(p + 1), components=True)
+        assert abs(rew[0] - d["reward"][p]) <= tol and term[0] == d["terminated"][p] and trunc[0] == d["truncated"][p], p
+        got, want = _info_of(h, comp), d["info"][p]
+        got[6] = rew[0]
+        assert abs(got[0] - want[0]) <= tol * (1 + abs(want[0])), (p, "speed")
+        assert got[1] == want[1] and got[7] == want[7] and got[4] == want[4] and got[5] == want[5], (p, got, want)
+        assert abs(got[3] - want[3]) <= tol and got[2] == want[2] and abs(got[6] - want[6]) <= tol, (p, got, want)
+        o.ix_clear_spawn(h, cfg)
+        same_state(h, HostState.from_ix(d, "post", p, pad_to=32), EPISODE_TOL, f"post {p}")
+        assert np.array_equal(h["rng"][0], d["rng"][p]), (p, "np_random state")

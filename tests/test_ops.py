@@ -86,6 +86,21 @@ def test_meta_shapes():
     assert o2.shape == (6, 15, 7) and i2.shape == (6, 14)
 
 
+def test_cached_struct_bytes_follow_in_place_changes():
+    """ops.st caches a struct's bytes, keyed on the bytes themselves: an in-place change of a field
+    (scalar or array element) after the first use reaches the next call."""
+    p = _abi.default_params()
+    t0 = ops.st(p)
+    assert ops.st(p) is t0  # unchanged: the cached tensor
+    p.politeness = 0.25
+    t1 = ops.st(p)
+    assert t1 is not t0 and bytes(t1.numpy()) == bytes(p)
+    lanes = _abi.straight_lane_table(4)
+    ops.st(lanes)
+    lanes.length[2] = 123.0
+    assert bytes(ops.st(lanes).numpy()) == bytes(lanes)
+
+
 def test_struct_tensors_are_checked():
     st = BatchState(2, 8, device="meta")
     with pytest.raises(RuntimeError, match="uint8 CPU tensor"):

@@ -4169,7 +4169,7 @@ __global__ void __launch_bounds__(64) ix_step_tail_kernel(ttrl_state_t st, ttrl_
     if (t.obs) {  // the row observed by the fused launch stays this step's observation
       for (int q = lane; q < V * F; q += 64) t.obs_out[(size_t)env * V * F + q] = t.obs_in[(size_t)env * V * F + q];
       if (t.ids_out)
-        for (int q = lane; q < V - 1; q += 64) t.ids_out[(size_t)env * (V - 1) + q] = t.ids_in[(size_t)env * (V - 1) + q];
+        for (int q = lane, W = V > 1 ? V - 1 : 1; q < W; q += 64) t.ids_out[(size_t)env * W + q] = t.ids_in[(size_t)env * W + q];
     }
     ix_clear_spawn_env<T>(st, R, P, C, env, lane);
     return;

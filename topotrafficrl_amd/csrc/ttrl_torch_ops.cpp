@@ -191,8 +191,11 @@ std::tuple<at::Tensor, at::Tensor> neighbours(at::TensorList state, const at::Te
 // ------------------------------------------------------------------------------------ observers
 std::tuple<at::Tensor, at::Tensor> kin_outputs(const at::Tensor& x, const ttrl_kin_cfg_t* c) {
   const int64_t E = x.size(0);
+  // one observed vehicle (the ego alone) has no id column: the kernels write none, so the
+  // placeholder column holds the padding id -1 instead of uninitialised memory
+  const int64_t w = std::max<int64_t>(c->vehicles_count - 1, 1);
   return {at::empty({E, c->vehicles_count, c->n_features}, opts(x, at::kFloat)),
-          at::empty({E, std::max<int64_t>(c->vehicles_count - 1, 1)}, opts(x, at::kInt))};
+          c->vehicles_count > 1 ? at::empty({E, w}, opts(x, at::kInt)) : at::full({E, w}, -1, opts(x, at::kInt))};
 }
 
 std::tuple<at::Tensor, at::Tensor> kinematics_obs(at::TensorList state, const at::Tensor& lanes,

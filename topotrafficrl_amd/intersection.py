@@ -359,9 +359,10 @@ class VecIntersectionEnv:
         """AbstractEnv.reset (abstract.py:188-214) + IntersectionEnv._reset: env e is
         ``IntersectionEnv.reset(seed=seed + env_id_offset + e)``."""
         if self._spare is not None:
-            # the side stream may still be resetting the spares (it writes _spare and reads
-            # the spare counters): join it before either buffer is replaced or freed below
-            torch.cuda.current_stream(self.device).wait_event(self._spare_ready)
+            # the side streams may still be resetting the spares (they write _spare and read the
+            # spare counters): join every one of them before either buffer is replaced or freed
+            # below -- with two or more side streams, _spare_ready covers only the latest
+            self._join_sides()
         if options and "config" in options:
             self.configure(options["config"])
             self._build()
@@ -382,6 +383,13 @@ class VecIntersectionEnv:
         obs = self.observation_type.observe()
         self._rewards_and_dones()  # abstract.py:211 reset's _info evaluates _rewards too
         return obs, self._info(obs, None)
+
+    def _join_sides(self) -> None:
+        """Order the main stream after all side-stream work enqueued so far (every spare reset in
+        flight, on whichever side stream it runs)."""
+        main = torch.cuda.current_stream(self.device)
+        for side in self._sides:
+            main.wait_stream(side)
 
     def _prepare_spares(self, mask: torch.Tensor | None) -> None:
         """Reset the spare scenes of ``mask`` ([2E]; all: None) on the next side stream, after the
@@ -444,14 +452,24 @@ class VecIntersectionEnv:
         _device_only(self.state)
         # the slots this step takes were prepared two steps back at the latest
         torch.cuda.current_stream(self.device).wait_event(self._spare_prev)
+        # the tail launch re-observes a new scene with one slot per lane of a wavefront: wider rows
+        # (vehicle_slots > 64) take the masked observation launch instead, which draws the same
+        # shuffles from the same generators (test_overlapped_resets_equal_in_place_resets[96])
+        fused_obs = kin and self.state.n_veh <= 64
         done, smask, obs2, ids2 = ops.T.ix_step_tail_(
             self.state.tensors(), ops.st(self.network.table), ops.st(self.params), ops.st(self.ix),
             self._spare.tensors(), terminated, truncated, self._spare_par, self._entropy, self._spare_ent, self.time,
-            ops.kin_cfg_tensor(ot.fused_cfg()) if kin else None, obs if kin else None, ids if kin else None)
+            ops.kin_cfg_tensor(ot.fused_cfg()) if fused_obs else None, obs if fused_obs else None,
+            ids if fused_obs else None)
         self._prepare_spares(smask)
         info["final_observation"], info["final_mask"] = obs, done
-        if kin:
+        if fused_obs:
             ot.fused_result(obs2, ids2)
+            obs = obs2
+        elif kin:
+            obs2, ids2 = obs.clone(), ids.clone()
+            ot.fused_result(obs2, ids2)
+            ot.observe(mask=done.view(torch.uint8), out=obs2)
             obs = obs2
         else:  # the other observers draw nothing: observe the new scenes, keep the others' rows
             new = ot.observe()
@@ -522,8 +540,8 @@ class VecIntersectionEnv:
         new.time = self.time.clone()
         if self._entropy is not None:
             new._entropy = self._entropy.clone()
-        if self._spare is not None:  # its own spare scenes, side stream and events
-            torch.cuda.current_stream(self.device).wait_event(self._spare_ready)
+        if self._spare is not None:  # its own spare scenes, side streams and events
+            self._join_sides()  # every in-flight spare reset (not only the latest) lands before the clone
             new._spare = self._spare.clone()
             new._spare_slot = (new._spare.rows(0, self.num_envs), new._spare.rows(self.num_envs, self.num_envs))
             new._spare_ent = self._spare_ent.clone()

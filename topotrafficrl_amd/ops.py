@@ -49,13 +49,17 @@ def struct_tensor(s: C.Structure) -> torch.Tensor:
 
 
 def st(s: C.Structure) -> torch.Tensor:
-    """``struct_tensor(s)`` cached on the struct: for the structs that do not change after they
-    are built (lane tables, params, reward / reset / grid / intersection configs)."""
-    t = getattr(s, "_ttrl_bytes", None)
-    if t is None:
-        t = struct_tensor(s)
-        s._ttrl_bytes = t
-    return t
+    """``struct_tensor(s)`` cached on the struct (lane tables, params, reward / reset / grid /
+    intersection configs are passed on every step).  The cache is keyed on the struct's current
+    bytes, so a field changed in place after the first use (``params.politeness = ...``,
+    ``cfg.init_longitudinal[3] = ...``) reaches the next call: a snapshot and a compare of a few
+    KB, no tensor rebuilt unless the bytes moved."""
+    b = bytes(s)
+    cached = getattr(s, "_ttrl_bytes", None)
+    if cached is None or cached[0] != b:
+        cached = (b, torch.frombuffer(bytearray(b), dtype=torch.uint8))
+        s._ttrl_bytes = cached
+    return cached[1]
 
 
 def kin_cfg_tensor(cfg) -> torch.Tensor:
