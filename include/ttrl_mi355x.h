@@ -357,6 +357,17 @@ int64_t ttrl_ego_attention_sizes(int32_t n_features, int32_t n_actions, int32_t 
 int ttrl_ego_attention_q(const float* obs, int32_t batch, int32_t n_entities, int32_t n_features,
                          int32_t heads, const float* weights, int32_t n_actions, float* scratch, float* q,
                          void* stream);
+/* AbstractDQNAgent.act (dqn/abstract.py:65-83) with EpsilonGreedy (epsilon_greedy.py:32-48) for a
+ * batch, in the same launch as the forward above: q [batch][n_actions] (as ttrl_ego_attention_q)
+ * and actions [batch] int64 = np.argmax(q[e]) (first maximum), replaced with probability epsilon by
+ * a uniform action -- the reference's action distribution.  The draws are Philox4x32-10 keyed on
+ * seed, counter (env, step): reproducible per (seed, env, step) whatever the batch.  epsilon_dev /
+ * step_dev (device scalars, optional) override epsilon / step, for captured graphs.  epsilon must
+ * lie in [0, 1]. */
+int ttrl_ego_attention_act(const float* obs, int32_t batch, int32_t n_entities, int32_t n_features,
+                           int32_t heads, const float* weights, int32_t n_actions, float epsilon,
+                           const float* epsilon_dev, uint64_t seed, int64_t step, const int64_t* step_dev,
+                           float* q, int64_t* actions, void* stream);
 /* IntersectionEnv._reset for the envs with mask[e] != 0 (mask NULL: all): np_random =
  * default_rng(SeedSequence(entropy[e][0..n_words-1])) into state.rng, then _make_vehicles:
  * initial spawns, warmup_frames of Road.act/step (RegulatedRoad), the challenger, the ego

@@ -30,7 +30,8 @@ def test_every_device_entry_point_is_an_operator():
                           "ix_clear_spawn_": "ix_clear_spawn", "ix_step_tail_": "ix_step_tail",
                           "copy_envs_": "copy_envs", "rewards": "rewards",
                           "rewards_ex": "rewards_ex", "rewards_step_": "rewards_step",
-                          "ego_attention_q": "ego_attention_q"}[o] for o in ops.OPS}
+                          "ego_attention_q": "ego_attention_q", "ego_attention_act": "ego_attention_act"}[o]
+               for o in ops.OPS}
     assert covered == abi
     for o in ops.OPS:
         assert hasattr(torch.ops.ttrl, o), o
@@ -338,3 +339,10 @@ def test_ego_attention_op_equals_the_c_abi(hip_device):
     q2 = torch.ops.ttrl.ego_attention_q(x, w, 2, 5)
     torch.cuda.synchronize()
     assert torch.equal(q1, q2)
+    act1 = torch.empty(100, dtype=torch.int64, device=hip_device)
+    q3 = torch.empty((100, 5), device=hip_device)
+    assert lib.ttrl_ego_attention_act(x.data_ptr(), 100, 15, 7, 2, w.data_ptr(), 5, 0.3, None, 77, 5, None,
+                                      q3.data_ptr(), act1.data_ptr(), _stream()) == 0
+    act2, q4 = torch.ops.ttrl.ego_attention_act(x, w, 2, 5, 0.3, 77, 5)
+    torch.cuda.synchronize()
+    assert torch.equal(q3, q1) and torch.equal(q4, q1) and torch.equal(act1, act2)

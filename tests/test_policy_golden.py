@@ -83,6 +83,96 @@ def test_fused_hip_forward_matches_reference_network(name, hip_device):
         assert (q.argmax(1)[clear] == ref.argmax(1)[clear]).all()
 
 
+def test_acting_steps_the_exploration_time_first():
+    """AbstractDQNAgent.act (dqn/abstract.py:77-83) steps EpsilonGreedy.time before update: the
+    k-th act of a fresh agent acts with epsilon(k); the schedule at the fixture's times."""
+    z = load_golden(os.path.join(GOLDEN, "dqn_memory.npz"))
+    pol = EgoAttentionPolicy("cpu", tau=float(z["eps/tau"]), temperature=float(z["eps/temperature"]),
+                             final_temperature=float(z["eps/final_temperature"]), fused=False)
+    x = torch.from_numpy(load_golden(os.path.join(GOLDEN, "policy_2h_a5.npz"))["x"][:8])
+    for t, e in zip(z["eps/time"], z["eps/epsilon"]):
+        if t == 0:
+            continue  # no act runs at time 0: the first act is at time 1
+        pol.time = int(t) - 1
+        pol.act(x)
+        assert pol.time == int(t) and abs(pol.last_epsilon - e) <= 1e-15
+
+
+@pytest.mark.gpu
+def test_fused_epsilon_greedy(hip_device):
+    """The epsilon-greedy draw fused into the forward launch (ttrl::ego_attention_act):
+    epsilon 0 is the reference network's argmax (where its top two Q-values are apart), epsilon 1
+    is uniform over the actions (chi-square), epsilon 0.3 leaves the greedy action with probability
+    0.3 (1 - 1/A); draws are a pure function of (seed, env, step); Q equals the plain forward."""
+    from topotrafficrl_amd import ops
+    z = load_golden(os.path.join(GOLDEN, "policy_2h_a5.npz"))
+    net = _network(z, hip_device)
+    w, A = net.packed_weights(), int(z["n_actions"])
+    x = torch.from_numpy(z["x"][:1000]).to(hip_device)
+    a0, q0 = ops.T.ego_attention_act(x, w, 2, A, 0.0, 3, 1)
+    assert torch.equal(q0, net.fused_q(x))
+    ref = z["q_b1000"]
+    srt = np.sort(ref, axis=1)
+    clear = (srt[:, -1] - srt[:, -2]) > 1e-4
+    assert (a0.cpu().numpy()[clear] == ref.argmax(1)[clear]).all()
+    assert torch.equal(a0, q0.argmax(1))  # first maximum, as np.argmax
+    big = x.repeat(8, 1, 1)  # 8000 envs
+    counts = np.zeros(A)
+    for step in range(5):
+        a1, _ = ops.T.ego_attention_act(big, w, 2, A, 1.0, 3, step)
+        counts += np.bincount(a1.cpu().numpy(), minlength=A)
+    n = counts.sum()
+    chi2 = float(((counts - n / A) ** 2 / (n / A)).sum())
+    assert chi2 < 20.5, (counts, chi2)  # p = 0.0004 at 4 degrees of freedom
+    greedy = q0.argmax(1).repeat(8)
+    moved = 0
+    for step in range(5):
+        a3, _ = ops.T.ego_attention_act(big, w, 2, A, 0.3, 3, step)
+        moved += int((a3 != greedy).sum())
+    p = 0.3 * (1 - 1 / A)
+    m = 5 * big.shape[0]
+    assert abs(moved / m - p) < 5 * np.sqrt(p * (1 - p) / m)
+    r1, _ = ops.T.ego_attention_act(big, w, 2, A, 0.5, 11, 7)
+    r2, _ = ops.T.ego_attention_act(big, w, 2, A, 0.5, 11, 7)
+    r3, _ = ops.T.ego_attention_act(big, w, 2, A, 0.5, 11, 8)
+    assert torch.equal(r1, r2) and not torch.equal(r1, r3)
+    # env e's draw does not depend on the batch it is in
+    r4, _ = ops.T.ego_attention_act(big[:1000], w, 2, A, 0.5, 11, 7)
+    assert torch.equal(r4, r1[:1000])
+    # device scalars override epsilon / step (the captured-graph path)
+    eps = torch.tensor(0.5, device=hip_device)
+    stp = torch.tensor(7, dtype=torch.int64, device=hip_device)
+    r5, _ = ops.T.ego_attention_act(big, w, 2, A, 0.0, 11, 0, eps, stp)
+    assert torch.equal(r5, r1)
+
+
+@pytest.mark.gpu
+def test_policy_act_is_one_launch_in_a_graph(hip_device):
+    """EgoAttentionPolicy.act on the GPU: the fused launch; inside a StepGraph the replays draw
+    with the schedule's epsilon and a fresh step each time, equal to eager acting."""
+    from topotrafficrl_amd.envs import VecHighwayEnv
+    from topotrafficrl_amd.graph import StepGraph
+    KIN = {"type": "Kinematics", "vehicles_count": 15,
+           "features": ["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"],
+           "features_range": {"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]},
+           "absolute": False, "order": "sorted"}
+    cfg = {"num_envs": 64, "vehicles_count": 32, "observation": KIN, "device": hip_device}
+    e1, e2 = VecHighwayEnv(cfg), VecHighwayEnv(cfg)
+    o1, _ = e1.reset(seed=3)
+    o2, _ = e2.reset(seed=3)
+    p1 = EgoAttentionPolicy(hip_device, seed=0, tau=2.0)
+    p2 = EgoAttentionPolicy(hip_device, seed=0, tau=2.0)
+    sg = StepGraph(e2, o2, p2)
+    assert p2.time == 0
+    for t in range(4):
+        a = p1.act(o1)
+        o1, r1, *_ = e1.step(a)
+        o2g, r2, *_ = sg.replay()
+        assert torch.equal(a, sg.actions), t
+        assert torch.equal(o1, o2g) and torch.equal(r1, r2), t
+    assert p1.time == p2.time == 4
+
+
 def _learner(z, device):
     net = EgoAttentionNetwork(5).to(device)
     net.load_state_dict({k: v.to(device) for k, v in _state_dict(z, "w0/").items()}, strict=True)

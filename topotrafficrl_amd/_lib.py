@@ -45,6 +45,8 @@ _SIGS = {
     "ttrl_copy_envs": ([_P, _P, _P, _P], C.c_int),
     "ttrl_ego_attention_sizes": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P], C.c_int64),
     "ttrl_ego_attention_q": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, C.c_int32, _P, _P, _P], C.c_int),
+    "ttrl_ego_attention_act": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, C.c_int32, C.c_float, _P,
+                                C.c_uint64, C.c_int64, _P, _P, _P, _P], C.c_int),
 }
 EXPORTS = [k for k in _SIGS]
 

@@ -153,27 +153,49 @@ class EgoAttentionPolicy:
         self.tau, self.t0, self.t1 = tau, temperature, final_temperature
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed + 1)
-        self.time = 0
+        self.seed = int(seed) + 1  # the fused acting's Philox key
+        self.time = 0  # EpsilonGreedy.time: the number of act() calls so far
+        self.last_epsilon = None  # the epsilon of the latest act() (EpsilonGreedy.epsilon)
 
     def epsilon(self, t: int) -> float:
-        """EpsilonGreedy.update (epsilon_greedy.py:37-48)."""
+        """EpsilonGreedy.update (epsilon_greedy.py:37-48): epsilon at exploration time t."""
         return self.t1 + (self.t0 - self.t1) * math.exp(-t / self.tau)
+
+    def fused_acting(self, obs: torch.Tensor) -> bool:
+        return self.fused and obs.device.type == "cuda" and self.value_net.fused_supported()
 
     @torch.no_grad()
     def q_values(self, obs: torch.Tensor) -> torch.Tensor:
-        if self.fused and obs.device.type == "cuda" and self.value_net.fused_supported():
+        if self.fused_acting(obs):
             return self.value_net.fused_q(obs)
         return self.value_net(obs)
 
     @torch.no_grad()
-    def act(self, obs: torch.Tensor, t: int | None = None, epsilon: torch.Tensor | None = None) -> torch.Tensor:
-        """Greedy on Q with probability 1 - epsilon(t), uniform otherwise.  ``epsilon`` (a device
-        scalar) overrides the schedule: a captured graph refreshes it before every replay."""
-        if epsilon is None:
-            t = self.time if t is None else t
-            self.time = t + 1
-            epsilon = self.epsilon(t)
-        q = self.q_values(obs)
+    def act(self, obs: torch.Tensor, t: int | None = None, epsilon: torch.Tensor | None = None,
+            step: torch.Tensor | None = None) -> torch.Tensor:
+        """AbstractDQNAgent.act (dqn/abstract.py:65-83) for a batch: the exploration time is stepped
+        first (step_time, :77-78), then EpsilonGreedy.update sets epsilon from it and the greedy
+        action (np.argmax, first maximum), then the action is drawn from {a: epsilon / A +
+        (1 - epsilon) [a == greedy]} (epsilon_greedy.py:32-48).  ``t``: the exploration time before
+        this call (default: the policy's own counter).  ``epsilon`` / ``step`` (device scalars, float32 /
+        int64) override the schedule and the draw counter: a captured graph refreshes them before
+        every replay.
+
+        On a GPU the forward, argmax and draw are ONE launch (ttrl::ego_attention_act, Philox
+        keyed on (seed, env, step)); elsewhere the torch forward with torch's generator."""
+        t = self.time if t is None else int(t)
+        self.time = t + 1
+        self.last_epsilon = self.epsilon(self.time) if epsilon is None else epsilon
+        if self.fused_acting(obs):
+            from . import ops
+            net = self.value_net
+            act, _ = ops.T.ego_attention_act(obs.float(), net.packed_weights(), net.attention_layer.h,
+                                             net.output_layer.predict.out_features,
+                                             self.last_epsilon if epsilon is None else 0.0, self.seed, self.time,
+                                             epsilon, step)
+            return act
+        epsilon = self.last_epsilon
+        q = self.value_net(obs)
         greedy = q.argmax(dim=1)
         e = obs.shape[0]
         u = torch.rand(e, device=self.device, generator=self.gen)

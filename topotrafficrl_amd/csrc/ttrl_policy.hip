@@ -119,7 +119,7 @@ __host__ __device__ inline PolLds pol_lds(int NE, int F, int H) {
   P.es = P.ob + ((EPWV * NE * F + 3) & ~3);
   P.qk = P.es + HD * 4;
   P.s0 = P.qk + H * HD * 4;
-  P.total = P.s0 + EPWV * H;
+  P.total = P.s0 + EPWV * (H > 16 ? H : 16);  // the ego scores, later the Q rows of the argmax (A <= 16)
   return P;
 }
 
@@ -129,6 +129,33 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // B[l >> 4][l & 15] and D[4 (l >> 4) + r][l & 15] in register r.
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// EpsilonGreedy acting fused into the forward (epsilon_greedy.py:32-48 with DiscreteDistribution.sample,
+// exploration/abstract.py:20-25; AbstractDQNAgent.act, dqn/abstract.py:65-83): the greedy action is
+// np.argmax(Q) (the first maximum; a NaN wins, as in numpy), and with probability epsilon a uniform
+// action replaces it -- the distribution {a: epsilon / A + (1 - epsilon) [a == greedy]} the reference
+// samples.  The draws are counter-based, Philox4x32-10 keyed on the seed with counter (env, step):
+// any batch split or replay order gives each env the same action.  epsilon / step come from device
+// scalars when given (a captured HIP graph refreshes them between replays).
+struct Explore {
+  int64_t* act;            // [B] actions out; null: Q-values only
+  float eps;
+  const float* eps_dev;    // overrides eps when set
+  long long step;
+  const int64_t* step_dev; // overrides step when set
+  unsigned seed_lo, seed_hi;
+};
+
+__device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 key) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const unsigned long long p0 = (unsigned long long)0xD2511F53u * c.x;
+    const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c.z;
+    c = make_uint4((unsigned)(p1 >> 32) ^ c.y ^ key.x, (unsigned)p1, (unsigned)(p0 >> 32) ^ c.w ^ key.y, (unsigned)p0);
+    key.x += 0x9E3779B9u; key.y += 0xBB67AE85u;
+  }
+  return c;
 }
 
 // One wave per EPWV envs, lane k = feature k. Linearity moves the key and value projections
@@ -151,7 +178,7 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 template <int F, int H>
 __global__ void __launch_bounds__(64, 2) ego_attention_kernel(const float* __restrict__ obs, int B, int NE,
                                                               const float* __restrict__ W, int A,
-                                                              float* __restrict__ Q) {
+                                                              float* __restrict__ Q, Explore ex) {
   constexpr int DPH = HD / H, NV = EPWV * H;
   const PolicyLayout L = policy_layout(F, A);
   const PolLds P = pol_lds(NE, F, H);
@@ -396,8 +423,30 @@ __global__ void __launch_bounds__(64, 2) ego_attention_kernel(const float* __res
       a[3] = fmaf(w, v.w, a[3]);
     }
 #pragma unroll
-    for (int u = 0; u < EPWV; ++u)
+    for (int u = 0; u < EPWV; ++u) {
       if (b0 + u < B) Q[(b0 + u) * A + k] = a[u];
+      if (ex.act) s0s[u * 16 + k] = a[u];  // the ego scores' LDS is dead: the env's Q row for the argmax
+    }
+  }
+  if (ex.act) {  // 4. epsilon-greedy: lane u acts for env b0 + u
+    __syncthreads();
+    if (k < EPWV && b0 + k < B) {
+      const float* qrow = s0s + k * 16;
+      int best = 0;
+      float bq = qrow[0];
+      for (int i = 1; i < A; ++i) {
+        const float v = qrow[i];
+        if (bq == bq && (v > bq || v != v)) { bq = v; best = i; }  // np.argmax: first max, first NaN
+      }
+      const float eps = ex.eps_dev ? *ex.eps_dev : ex.eps;
+      const unsigned long long step = ex.step_dev ? (unsigned long long)*ex.step_dev : (unsigned long long)ex.step;
+      const unsigned long long env = (unsigned long long)(b0 + k);
+      const uint4 r = philox4x32(make_uint4((unsigned)env, (unsigned)(env >> 32), (unsigned)step, (unsigned)(step >> 32)),
+                                 make_uint2(ex.seed_lo, ex.seed_hi));
+      const float uni = (float)(r.x >> 8) * 0x1p-24f;                       // U[0, 1)
+      const int rnd = (int)(((unsigned long long)r.y * (unsigned)A) >> 32);  // U{0 .. A-1}
+      ex.act[b0 + k] = uni < eps ? rnd : best;
+    }
   }
   POL_T(8);
 #ifdef TTRL_POL_CLOCKS
@@ -407,21 +456,37 @@ __global__ void __launch_bounds__(64, 2) ego_attention_kernel(const float* __res
 }
 
 template <int F, int H>
-int launch(const float* obs, int B, int NE, const float* W, int A, float* Q, hipStream_t st) {
+int launch(const float* obs, int B, int NE, const float* W, int A, float* Q, const Explore& ex, hipStream_t st) {
   const size_t lds = pol_lds(NE, F, H).total * sizeof(float);
   hipLaunchKernelGGL((ego_attention_kernel<F, H>), dim3((B + EPWV - 1) / EPWV), dim3(64), lds, st, obs, B, NE,
-                     W, A, Q);
+                     W, A, Q, ex);
   return hipGetLastError() == hipSuccess ? TTRL_OK : TTRL_E_LAUNCH;
 }
 
 template <int F>
-int launch_heads(const float* obs, int B, int NE, int heads, const float* W, int A, float* Q, hipStream_t st) {
+int launch_heads(const float* obs, int B, int NE, int heads, const float* W, int A, float* Q, const Explore& ex,
+                 hipStream_t st) {
   switch (heads) {
-    case 1: return launch<F, 1>(obs, B, NE, W, A, Q, st);
-    case 2: return launch<F, 2>(obs, B, NE, W, A, Q, st);
-    case 4: return launch<F, 4>(obs, B, NE, W, A, Q, st);
-    case 8: return launch<F, 8>(obs, B, NE, W, A, Q, st);
+    case 1: return launch<F, 1>(obs, B, NE, W, A, Q, ex, st);
+    case 2: return launch<F, 2>(obs, B, NE, W, A, Q, ex, st);
+    case 4: return launch<F, 4>(obs, B, NE, W, A, Q, ex, st);
+    case 8: return launch<F, 8>(obs, B, NE, W, A, Q, ex, st);
     default: return TTRL_E_ARG;
+  }
+}
+
+int forward(const float* obs, int32_t batch, int32_t n_entities, int32_t n_features, int32_t heads,
+            const float* weights, int32_t n_actions, float* q, const Explore& ex, void* stream) {
+  if (!obs || !weights || !q || batch < 0 || n_entities < 2 || n_entities > 32 || n_actions < 1 ||
+      n_actions > 16 || (heads != 1 && heads != 2 && heads != 4 && heads != 8) || heads * n_entities > 64)
+    return TTRL_E_ARG;
+  if (batch == 0) return TTRL_OK;
+  hipStream_t st = (hipStream_t)stream;
+  switch (n_features) {
+    case 5: return launch_heads<5>(obs, batch, n_entities, heads, weights, n_actions, q, ex, st);
+    case 7: return launch_heads<7>(obs, batch, n_entities, heads, weights, n_actions, q, ex, st);
+    case 8: return launch_heads<8>(obs, batch, n_entities, heads, weights, n_actions, q, ex, st);
+    default: return TTRL_E_UNSUPPORTED;
   }
 }
 
@@ -438,17 +503,19 @@ int64_t ttrl_ego_attention_sizes(int32_t n_features, int32_t n_actions, int32_t 
 
 int ttrl_ego_attention_q(const float* obs, int32_t batch, int32_t n_entities, int32_t n_features, int32_t heads,
                          const float* weights, int32_t n_actions, float* scratch, float* q, void* stream) {
-  if (!obs || !weights || !scratch || !q || batch < 0 || n_entities < 2 || n_entities > 32 || n_actions < 1 ||
-      n_actions > 16 || (heads != 1 && heads != 2 && heads != 4 && heads != 8) || heads * n_entities > 64)
-    return TTRL_E_ARG;
-  if (batch == 0) return TTRL_OK;
-  hipStream_t st = (hipStream_t)stream;
-  switch (n_features) {
-    case 5: return launch_heads<5>(obs, batch, n_entities, heads, weights, n_actions, q, st);
-    case 7: return launch_heads<7>(obs, batch, n_entities, heads, weights, n_actions, q, st);
-    case 8: return launch_heads<8>(obs, batch, n_entities, heads, weights, n_actions, q, st);
-    default: return TTRL_E_UNSUPPORTED;
-  }
+  if (!scratch) return TTRL_E_ARG;
+  return forward(obs, batch, n_entities, n_features, heads, weights, n_actions, q, Explore{}, stream);
+}
+
+int ttrl_ego_attention_act(const float* obs, int32_t batch, int32_t n_entities, int32_t n_features, int32_t heads,
+                           const float* weights, int32_t n_actions, float epsilon, const float* epsilon_dev,
+                           uint64_t seed, int64_t step, const int64_t* step_dev, float* q, int64_t* actions,
+                           void* stream) {
+  if (!actions || !(epsilon >= 0.0f && epsilon <= 1.0f)) return TTRL_E_ARG;
+  Explore ex{};
+  ex.act = actions; ex.eps = epsilon; ex.eps_dev = epsilon_dev; ex.step = step; ex.step_dev = step_dev;
+  ex.seed_lo = (unsigned)seed; ex.seed_hi = (unsigned)(seed >> 32);
+  return forward(obs, batch, n_entities, n_features, heads, weights, n_actions, q, ex, stream);
 }
 
 #ifdef TTRL_POL_CLOCKS

@@ -500,6 +500,42 @@ at::Tensor ego_attention_q(const at::Tensor& obs, const at::Tensor& weights, int
   return q;
 }
 
+// EgoAttention Q-values and the epsilon-greedy actions in one launch (ttrl_ego_attention_act):
+// returns (actions [B] int64, q [B, A] float32).  epsilon_dev / step_dev: optional device scalars
+// (float32 / int64) that override epsilon / step inside the kernel (captured graphs).
+std::tuple<at::Tensor, at::Tensor> ego_attention_act(const at::Tensor& obs, const at::Tensor& weights, int64_t heads,
+                                                     int64_t n_actions, double epsilon, int64_t seed, int64_t step,
+                                                     const c10::optional<at::Tensor>& epsilon_dev,
+                                                     const c10::optional<at::Tensor>& step_dev) {
+  check_hip(obs);
+  TORCH_CHECK(obs.dim() == 3 && obs.scalar_type() == at::kFloat, "ttrl: obs must be float32 [B, entities, features]");
+  TORCH_CHECK(weights.device() == obs.device() && weights.scalar_type() == at::kFloat && weights.is_contiguous(),
+              "ttrl: weights must be a contiguous float32 tensor on the obs device (packed layout)");
+  TORCH_CHECK(epsilon >= 0.0 && epsilon <= 1.0, "ttrl: epsilon must lie in [0, 1]");
+  const bool ed = epsilon_dev && epsilon_dev->defined(), sd = step_dev && step_dev->defined();
+  if (ed)
+    TORCH_CHECK(epsilon_dev->device() == obs.device() && epsilon_dev->scalar_type() == at::kFloat &&
+                    epsilon_dev->numel() == 1,
+                "ttrl: epsilon_dev must be a float32 scalar on the obs device");
+  if (sd)
+    TORCH_CHECK(step_dev->device() == obs.device() && step_dev->scalar_type() == at::kLong && step_dev->numel() == 1,
+                "ttrl: step_dev must be an int64 scalar on the obs device");
+  at::Tensor x = obs.contiguous();
+  const int32_t B = x.size(0), NE = x.size(1), F = x.size(2);
+  int64_t n_scratch = 0;
+  const int64_t n_w = ttrl_ego_attention_sizes(F, static_cast<int32_t>(n_actions), B, NE, &n_scratch);
+  TORCH_CHECK(n_w > 0 && weights.numel() == n_w, "ttrl: packed weights need ", n_w, " floats, got ", weights.numel());
+  at::Tensor q = at::empty({B, n_actions}, opts(x, at::kFloat));
+  at::Tensor act = at::empty({B}, opts(x, at::kLong));
+  ok(ttrl_ego_attention_act(x.data_ptr<float>(), B, NE, F, static_cast<int32_t>(heads), weights.data_ptr<float>(),
+                            static_cast<int32_t>(n_actions), static_cast<float>(epsilon),
+                            ed ? epsilon_dev->data_ptr<float>() : nullptr, static_cast<uint64_t>(seed), step,
+                            sd ? step_dev->data_ptr<int64_t>() : nullptr, q.data_ptr<float>(),
+                            act.data_ptr<int64_t>(), stream_of(x)),
+     "ttrl_ego_attention_act");
+  return {act, q};
+}
+
 // ------------------------------------------------------------------------------------ Meta kernels
 const at::Tensor& meta_x(at::TensorList ts) {
   TORCH_CHECK(ts.size() == kFields, "ttrl: state must hold ", kFields, " tensors in _abi.ALL_FIELDS order, got ",
@@ -598,6 +634,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
 at::Tensor meta_ego_attention(const at::Tensor& obs, const at::Tensor&, int64_t, int64_t n_actions) {
   return at::empty({obs.size(0), n_actions}, opts(obs, at::kFloat));
 }
+std::tuple<at::Tensor, at::Tensor> meta_ego_attention_act(const at::Tensor& obs, const at::Tensor&, int64_t,
+                                                          int64_t n_actions, double, int64_t, int64_t,
+                                                          const c10::optional<at::Tensor>&,
+                                                          const c10::optional<at::Tensor>&) {
+  return {at::empty({obs.size(0)}, opts(obs, at::kLong)), at::empty({obs.size(0), n_actions}, opts(obs, at::kFloat))};
+}
 
 }  // namespace
 
@@ -636,6 +678,8 @@ TORCH_LIBRARY(ttrl, m) {
   m.def("rewards_step_(Tensor[] state, Tensor lanes, Tensor cfg, Tensor(a!) time, float time_inc) -> (Tensor reward, "
         "Tensor terminated, Tensor truncated, Tensor components, Tensor ego_speed, Tensor ego_crashed)");
   m.def("ego_attention_q(Tensor obs, Tensor weights, int heads, int n_actions) -> Tensor");
+  m.def("ego_attention_act(Tensor obs, Tensor weights, int heads, int n_actions, float epsilon, int seed, int step, "
+        "Tensor? epsilon_dev=None, Tensor? step_dev=None) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(ttrl, CUDA, m) {  // the HIP device of ROCm PyTorch
@@ -661,6 +705,7 @@ TORCH_LIBRARY_IMPL(ttrl, CUDA, m) {  // the HIP device of ROCm PyTorch
   m.impl("rewards_ex", &rewards_ex);
   m.impl("rewards_step_", &rewards_step_);
   m.impl("ego_attention_q", &ego_attention_q);
+  m.impl("ego_attention_act", &ego_attention_act);
 }
 
 TORCH_LIBRARY_IMPL(ttrl, Meta, m) {
@@ -686,4 +731,5 @@ TORCH_LIBRARY_IMPL(ttrl, Meta, m) {
   m.impl("rewards_ex", &meta_rewards_ex);
   m.impl("rewards_step_", &meta_rewards_step);
   m.impl("ego_attention_q", &meta_ego_attention);
+  m.impl("ego_attention_act", &meta_ego_attention_act);
 }

@@ -8,8 +8,8 @@ policy forward) disappears from the step time.  This is the MI355X replacement f
 tracing compiler on this path.
 
 Graph semantics: the tensors a replay returns are static buffers overwritten by the next
-replay (clone what you keep); ``epsilon`` is a device scalar refreshed before each replay,
-so the exploration schedule keeps advancing.  ``VecHighwayEnv`` must not auto-reset inside a
+replay (clone what you keep); ``epsilon`` and the exploration ``step`` are device scalars
+refreshed before each replay, so the exploration schedule and the policy's draws keep advancing.  ``VecHighwayEnv`` must not auto-reset inside a
 graph (use ``auto_reset=False``); ``VecIntersectionEnv`` may (``GRAPH_AUTO_RESET``): its
 done mask, episode counters, seeds and masked resets are all device tensors and launches, so a
 replay resets exactly the envs an eager step would.
@@ -33,7 +33,9 @@ class StepGraph:
         self.obs = obs.clone()
         self.actions = torch.zeros(env.num_envs, dtype=torch.int64, device=dev)
         self.epsilon = torch.zeros((), dtype=torch.float32, device=dev)
+        self.step = torch.zeros((), dtype=torch.int64, device=dev)
         self.t = 0
+        time0 = policy.time if policy is not None else 0  # warm-up and capture do not count as acts
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # warm up allocator pools and lazy initialisation off-graph
@@ -53,10 +55,12 @@ class StepGraph:
             self.graph.register_generator_state(policy.gen)
         with torch.cuda.graph(self.graph):
             self.out = self._body()
+        if policy is not None:
+            policy.time = time0
 
     def _body(self):
         if self.policy is not None:
-            a = self.policy.act(self.obs, epsilon=self.epsilon)
+            a = self.policy.act(self.obs, epsilon=self.epsilon, step=self.step)
             self.actions.copy_(a)
         obs, reward, terminated, truncated, _ = self.env.step(self.actions)
         self.obs.copy_(obs)
@@ -66,9 +70,10 @@ class StepGraph:
         self.actions.copy_(actions)
 
     def replay(self):
-        if self.policy is not None:
-            self.epsilon.fill_(self.policy.epsilon(self.policy.time))
+        if self.policy is not None:  # AbstractDQNAgent.act steps the exploration time first
             self.policy.time += 1
+            self.epsilon.fill_(self.policy.epsilon(self.policy.time))
+            self.step.fill_(self.policy.time)
         self.graph.replay()
         self.t += 1
         return self.out
