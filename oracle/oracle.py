@@ -121,6 +121,7 @@ _SIGS = {
     "oracle_ix_clear_spawn": [C.c_void_p] * 5,
     "oracle_rng_ops": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p],
     "oracle_frame_margins": [C.c_void_p] * 4 + [C.c_double, C.c_int32, C.c_void_p, C.c_void_p],
+    "oracle_frame_links": [C.c_void_p] * 4 + [C.c_double, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32],
 }
 
 
@@ -160,19 +161,27 @@ class Oracle:
         self._ok(self.lib.oracle_simulate(C.byref(s), C.byref(self.lanes), C.byref(self.params),
                                           None if a is None else a.ctypes.data, frames, dt, None))
 
+    LINK_MAX = 32
+
     def frame_margins(self, h: HostState, actions=None, dt: float = 1 / 15, sites: bool = False,
-                      act: bool = True, step: bool = True):
+                      act: bool = True, step: bool = True, links: bool = False):
         """One frame (meta-action when ``actions`` is given, then Road.act and / or Road.step) applied
         to ``h`` in place; returns [E, N] float64: each vehicle's smallest relative decision margin
-        (and, with ``sites``, the oracle source line of that decision, [E, N] int32)."""
+        (and, with ``sites``, the oracle source line of that decision, [E, N] int32; with ``links``,
+        [E, N, LINK_MAX] int32: the slots whose same-frame results the vehicle's decisions read --
+        the abort rule's earlier vehicles within the desired gap, collision partners -- -1 padded,
+        a row ending in -2 overflowed; see oracle_frame_links)."""
         s = h.struct()
         a = None if actions is None else np.ascontiguousarray(actions, dtype=np.int32)
         m = np.empty((h.E, h.N), dtype=np.float64)
         line = np.zeros((h.E, h.N), dtype=np.int32)
-        self._ok(self.lib.oracle_frame_margins(C.byref(s), C.byref(self.lanes), C.byref(self.params),
-                                               None if a is None else a.ctypes.data, dt,
-                                               int(act) | 2 * int(step), m.ctypes.data, line.ctypes.data))
-        return (m, line) if sites else m
+        lk = np.full((h.E, h.N, self.LINK_MAX), -1, dtype=np.int32) if links else None
+        self._ok(self.lib.oracle_frame_links(C.byref(s), C.byref(self.lanes), C.byref(self.params),
+                                             None if a is None else a.ctypes.data, dt,
+                                             int(act) | 2 * int(step), m.ctypes.data, line.ctypes.data,
+                                             None if lk is None else lk.ctypes.data, self.LINK_MAX))
+        out = (m,) + ((line,) if sites else ()) + ((lk,) if links else ())
+        return out if len(out) > 1 else m
 
     def neighbours(self, h: HostState, query_lane=None):
         s = h.struct()

@@ -32,6 +32,8 @@ typedef struct {
   uint64_t* rng;                /* [E][TTRL_RNG_WORDS] np_random */
   double* mg;                   /* [E*N] decision margins (oracle_frame_margins), NULL otherwise */
   int32_t* mgsite;              /* [E*N] source line of each vehicle's smallest margin */
+  int32_t* lk;                  /* [E*N][lkmax] causal links (oracle_frame_links), NULL otherwise */
+  int lkmax;
 } S;
 
 static S view(const ttrl_state_t* s) {
@@ -44,7 +46,7 @@ static S view(const ttrl_state_t* s) {
   o.kind = s->kind; o.crashed = s->crashed; o.hasimp = s->has_impact; o.lc = s->lane_change;
   o.rroad = s->route_road; o.rlane = s->route_lane; o.rn = s->route_n; o.yield = s->yielding; o.reg = s->reg_steps;
   o.rng = s->rng;
-  o.mg = NULL; o.mgsite = NULL;
+  o.mg = NULL; o.mgsite = NULL; o.lk = NULL; o.lkmax = 0;
   return o;
 }
 
@@ -58,6 +60,23 @@ static void mg_at(const S* o, int k, double m, double scale, int line) {
   if (r < o->mg[k]) { o->mg[k] = r; if (o->mgsite) o->mgsite[k] = line; }
 }
 #define mg(o, k, m, scale) mg_at(o, k, m, scale, __LINE__)
+
+/* Causal links (oracle_frame_links only): within one frame, vehicle k's discrete outcomes read
+ * another vehicle j's results of the SAME frame in two places only -- the lane-change abort reads
+ * the targets that vehicles earlier in the list set this frame (behavior.py:229-244), and the
+ * collision pass reads every vehicle's post-step pose (objects.py:91-137).  Every j whose changed
+ * result could change k's outcome there is recorded in k's row (slots within the env, -1 padded;
+ * a full row ends in -2).  Reads of frame-start state (neighbour scans, MOBIL, IDM) are not links:
+ * both precisions start the frame from the same inputs. */
+static void link_at(const S* o, int k, int j) {
+  if (!o->lk) return;
+  int32_t* row = o->lk + (size_t)k * o->lkmax;
+  for (int q = 0; q < o->lkmax; ++q) {
+    if (row[q] == j) return;
+    if (row[q] == -1) { row[q] = j; return; }
+  }
+  row[o->lkmax - 1] = -2;
+}
 
 static const double PI = 3.141592653589793;
 
@@ -399,6 +418,10 @@ static void change_lane_policy(S* o, const ttrl_lane_table_t* R, const ttrl_para
     if (R->road[lane] != R->road[tgt]) return;                 /* not the same road: no abort (:231) */
     for (int j = 0; j < o->N; ++j) {
       if (j == self || o->kind[base + j] == TTRL_ABSENT) continue;
+      if (o->lk && j < self) {  /* j acted before self: a changed target of j could abort self here */
+        double d = lane_distance(o, R, base, self, j);
+        if (-1.0 < d && d < desired_gap(o, P, base, self, j) + 1.0) link_at(o, base + self, j);
+      }
       if (o->lane[base + j] != tgt && o->tgt[base + j] == tgt) {
         double d = lane_distance(o, R, base, self, j);
         double ds = desired_gap(o, P, base, self, j);
@@ -628,6 +651,10 @@ static void handle_collisions(S* o, const ttrl_params_t* P, int base, int i, int
     mg(o, a, sqrt(dx * dx + dy * dy) - thr, o->x[a]);
     mg(o, b, sqrt(dx * dx + dy * dy) - thr, o->x[a]);
   }
+  if (o->lk && sqrt(dx * dx + dy * dy) <= thr + 1.0) {  /* a pair the prefilter may pass: each reads the other */
+    link_at(o, a, j);
+    link_at(o, b, i);
+  }
   if (sqrt(dx * dx + dy * dy) > thr) return;
   double pa[5][2], pb[5][2];
   polygon(P, o->x[a], o->y[a], o->h[a], pa);
@@ -816,12 +843,17 @@ int oracle_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttr
  * Road.step(dt) if phases & 2) with every discrete decision's float64 margin recorded per vehicle
  * into margin[E*N] (see mg()) and its source line into site[E*N]: the classifier of float32
  * decision flips (SURVEY.md §8(d) parity tolerance). */
-int oracle_frame_margins(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
-                         const int32_t* actions, double dt, int32_t phases, double* margin, int32_t* site) {
-  if (check(s) || !margin) return TTRL_E_ARG;
+int oracle_frame_links(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                       const int32_t* actions, double dt, int32_t phases, double* margin, int32_t* site,
+                       int32_t* links, int32_t link_max) {
+  if (check(s) || !margin || (links && link_max < 1)) return TTRL_E_ARG;
   S o = view(s);
   for (int k = 0; k < o.E * o.N; ++k) { margin[k] = INFINITY; if (site) site[k] = 0; }
   o.mg = margin; o.mgsite = site;
+  if (links) {
+    for (size_t q = 0; q < (size_t)o.E * o.N * link_max; ++q) links[q] = -1;
+    o.lk = links; o.lkmax = link_max;
+  }
   for (int e = 0; e < o.E; ++e)
     if (actions && (actions[e] < 0 || actions[e] > 4)) return TTRL_E_ARG;
 #pragma omp parallel for schedule(static)
@@ -834,6 +866,11 @@ int oracle_frame_margins(const ttrl_state_t* s, const ttrl_lane_table_t* R, cons
     if (phases & 2) step_env(&o, R, P, e, dt);
   }
   return 0;
+}
+
+int oracle_frame_margins(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                         const int32_t* actions, double dt, int32_t phases, double* margin, int32_t* site) {
+  return oracle_frame_links(s, R, P, actions, dt, phases, margin, site, NULL, 0);
 }
 
 int oracle_neighbours(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,

@@ -127,17 +127,19 @@ def f32_inputs(h: HostState) -> HostState:
 
 F32_TOL = 1e-4     # continuous state, one frame: |d| <= 1e-4 * (1 + |x|)
 F32_MARGIN = 1e-5  # a discrete flip must sit at a float64 decision margin below this (relative)
-F32_REACH = 60.0   # m: how far one vehicle's flip can reach another's decisions within one frame
-                   # (the lane-change abort's desired gap, 10 + 1.5 v; a collision partner)
 
 
-def check_f32_flips(dev: BatchState, h: HostState, margin: np.ndarray, what: str) -> int:
+def check_f32_flips(dev: BatchState, h: HostState, margin: np.ndarray, links: np.ndarray, what: str) -> int:
     """float32 result vs the float64 oracle on the same (rounded) inputs.  A vehicle "flips" when a
     discrete field differs or a continuous one exceeds F32_TOL.  Every flip must trace back to a
-    decision whose float64 margin (oracle_frame_margins) is below F32_MARGIN: the vehicle's own,
-    or, transitively, a flipped vehicle's within F32_REACH in the same env.  Returns the count."""
+    decision whose float64 margin (oracle_frame_links) is below F32_MARGIN: the vehicle's own, or,
+    transitively, that of a flipped vehicle it is causally linked to in this frame -- one whose
+    same-frame result its decisions read (an earlier vehicle's target within the lane-change
+    abort's desired gap, a collision partner's post-step pose; oracle_frame_links).  Returns the
+    count of flips."""
     d = dev.to_numpy()
     n = h.N
+    assert not np.any(links == -2), f"{what}: a causal-link row overflowed"
     flip = np.zeros((h.E, n), dtype=bool)
     for k in DISC:
         flip |= d[k][:, :n] != h[k][:, :n]
@@ -149,17 +151,16 @@ def check_f32_flips(dev: BatchState, h: HostState, margin: np.ndarray, what: str
         flip |= imp & (np.abs(d[k][:, :n] - h[k][:, :n]) > F32_TOL * (1 + np.abs(h[k][:, :n])))
     ok = flip & (margin < F32_MARGIN)
     changed = True
-    while changed:  # transitive closure over nearby flipped vehicles
+    while changed:  # transitive closure over the causal links to excused flips
         changed = False
         for e, i in zip(*np.nonzero(flip & ~ok)):
-            src = np.nonzero(ok[e])[0]
-            dx = h["x"][e, src] - h["x"][e, i]
-            dy = h["y"][e, src] - h["y"][e, i]
-            if len(src) and np.min(dx * dx + dy * dy) <= F32_REACH ** 2:
+            src = links[e, i][links[e, i] >= 0]
+            if len(src) and ok[e, src].any():
                 ok[e, i] = changed = True
     bad = np.argwhere(flip & ~ok)
     assert len(bad) == 0, (f"{what}: float32 flips with no small float64 decision margin at (env, slot) "
-                           f"{bad[:5].tolist()}; margins {[float(margin[e, i]) for e, i in bad[:5]]}")
+                           f"{bad[:5].tolist()}; margins {[float(margin[e, i]) for e, i in bad[:5]]}; "
+                           f"links {[links[e, i][links[e, i] >= 0].tolist() for e, i in bad[:5]]}")
     return int(flip.sum())
 
 
@@ -180,9 +181,9 @@ def test_single_frames_f32(path, hip_device):
             road.meta_action(torch.tensor(act))
         road.act()
         road.step(1 / 15)
-        m = o.frame_margins(g, act)
+        m, lk = o.frame_margins(g, act, links=True)
         torch.cuda.synchronize()
-        flips += check_f32_flips(dev, g, m, f"frame {f}")
+        flips += check_f32_flips(dev, g, m, lk, f"frame {f}")
     assert flips <= max(2, frames // 10), flips  # flips are rare, not merely excused
 
 
@@ -329,7 +330,7 @@ def test_close_pairs_collisions_vs_oracle(dtype, hip_device):
     flips = 0
     for _ in range(3):
         if dtype == "f32":
-            m = o.frame_margins(h, None, 1 / 15, act=False, step=True)
+            m, lk = o.frame_margins(h, None, 1 / 15, act=False, step=True, links=True)
         else:
             o.road_step(h, 1 / 15)
         road.step(1 / 15)
@@ -344,7 +345,7 @@ def test_close_pairs_collisions_vs_oracle(dtype, hip_device):
                 sel = imp if k.startswith("impact") else slice(None)
                 assert np.max(np.abs(d[k][sel] - h[k][sel])) < 1e-9, k
         else:
-            flips += check_f32_flips(dev, h, m, "collision step")
+            flips += check_f32_flips(dev, h, m, lk, "collision step")
             h = f32_inputs(h)
             dev.load_numpy(h.a)  # re-sync on the rounded oracle state so one step's flips do not compound
     assert flips <= E * n * 2e-3, flips

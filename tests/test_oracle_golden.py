@@ -75,6 +75,34 @@ def test_frame_margins_leave_the_frame_unchanged(name, cases):
 
 
 @pytest.mark.parametrize("name", [IDS(p) for p in golden_files()])
+def test_frame_links_are_local_and_leave_the_frame_unchanged(name, cases):
+    """oracle_frame_links (the causal links of the float32 flip classifier) steps the frame
+    exactly as oracle_frame_margins does, never overflows its rows, and links a vehicle only to
+    vehicles of its own env near it: an earlier vehicle within the abort's desired gap
+    (d0 + v T + v dv / (2 sqrt(a b)) < 200 m at these speeds) or a collision partner."""
+    d = cases[name]
+    o = Oracle(_abi.lane_table_from_arrays(d["lane_table"]), P)
+    n_links = 0
+    for f in range(d["x"].shape[0] - 1):
+        h = HostState.from_golden(d, f)
+        h0 = h.copy()
+        act = [int(d["actions"][f // 15])] if f % 15 == 0 else None
+        m1, lk = o.frame_margins(h, act, links=True)
+        g = h0.copy()
+        m0 = o.frame_margins(g, act)
+        assert np.array_equal(m0, m1)
+        for k in h.a:
+            assert np.array_equal(h.a[k], g.a[k], equal_nan=True), k
+        assert not np.any(lk == -2) and np.all(lk < h.N)
+        for e, i, q in zip(*np.nonzero(lk >= 0)):
+            j = lk[e, i, q]
+            assert j != i and h0["kind"][e, j] != 0
+            assert abs(h0["x"][e, j] - h0["x"][e, i]) < 200.0
+        n_links += int((lk >= 0).sum())
+    assert n_links > 0 or not name.startswith("dense")  # the pile-up scenes always have partners
+
+
+@pytest.mark.parametrize("name", [IDS(p) for p in golden_files()])
 def test_policy_step_rollout(name, cases):
     d = cases[name]
     o = Oracle(_abi.lane_table_from_arrays(d["lane_table"]), P)
