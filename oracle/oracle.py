@@ -120,6 +120,9 @@ _SIGS = {
     "oracle_ix_reset": [C.c_void_p] * 5,
     "oracle_ix_clear_spawn": [C.c_void_p] * 5,
     "oracle_rng_ops": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p],
+    "oracle_observe_grid_m": [C.c_void_p] * 6,
+    "oracle_observe_ttc_m": [C.c_void_p] * 6,
+    "oracle_observe_lidar_m": [C.c_void_p] * 6,
     "oracle_frame_margins": [C.c_void_p] * 4 + [C.c_double, C.c_int32, C.c_void_p, C.c_void_p],
     "oracle_frame_links": [C.c_void_p] * 4 + [C.c_double, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32],
 }
@@ -229,29 +232,36 @@ class Oracle:
             raise RuntimeError("oracle_rng_ops: bad op")
         return out[:n]
 
-    def observe_ttc(self, h: HostState, cfg: _abi.TtcCfg):
+    # ``margins=True`` also returns, per output cell (ray for the Lidar), the smallest float64
+    # relative margin of a discrete decision that could move content into or out of it (+inf:
+    # none): the float32 observation classifier of tests/test_gpu_parity.py (ttrl_oracle.c mg_cell)
+
+    def observe_ttc(self, h: HostState, cfg: _abi.TtcCfg, margins: bool = False):
         s = h.struct()
         if cfg.obs_speeds == 0 and cfg.obs_lanes == 0:  # raw compute_ttc_grid
             out = np.zeros((h.E, self.params.n_target_speeds, self.lanes.n_lanes, cfg.horizon_bins), dtype=np.float32)
         else:
             out = np.zeros((h.E, cfg.obs_speeds, cfg.obs_lanes, cfg.horizon_bins), dtype=np.float32)
-        self._ok(self.lib.oracle_observe_ttc(C.byref(s), C.byref(self.lanes), C.byref(self.params), C.byref(cfg),
-                                             out.ctypes.data))
-        return out
+        m = np.empty(out.shape, dtype=np.float64) if margins else None
+        self._ok(self.lib.oracle_observe_ttc_m(C.byref(s), C.byref(self.lanes), C.byref(self.params), C.byref(cfg),
+                                               out.ctypes.data, None if m is None else m.ctypes.data))
+        return (out, m) if margins else out
 
-    def observe_lidar(self, h: HostState, cfg: _abi.LidarCfg):
+    def observe_lidar(self, h: HostState, cfg: _abi.LidarCfg, margins: bool = False):
         s = h.struct()
         out = np.zeros((h.E, cfg.cells, 2), dtype=np.float32)
-        self._ok(self.lib.oracle_observe_lidar(C.byref(s), C.byref(self.lanes), C.byref(self.params), C.byref(cfg),
-                                               out.ctypes.data))
-        return out
+        m = np.empty((h.E, cfg.cells), dtype=np.float64) if margins else None
+        self._ok(self.lib.oracle_observe_lidar_m(C.byref(s), C.byref(self.lanes), C.byref(self.params),
+                                                 C.byref(cfg), out.ctypes.data, None if m is None else m.ctypes.data))
+        return (out, m) if margins else out
 
-    def observe_grid(self, h: HostState, cfg: _abi.GridCfg):
+    def observe_grid(self, h: HostState, cfg: _abi.GridCfg, margins: bool = False):
         s = h.struct()
         out = np.zeros((h.E, cfg.n_features, cfg.shape_x, cfg.shape_y), dtype=np.float32)
-        self._ok(self.lib.oracle_observe_grid(C.byref(s), C.byref(self.lanes), C.byref(self.params),
-                                              C.byref(cfg), out.ctypes.data))
-        return out
+        m = np.empty(out.shape, dtype=np.float64) if margins else None
+        self._ok(self.lib.oracle_observe_grid_m(C.byref(s), C.byref(self.lanes), C.byref(self.params),
+                                                C.byref(cfg), out.ctypes.data, None if m is None else m.ctypes.data))
+        return (out, m) if margins else out
 
     def reset_highway(self, h: HostState, cfg: _abi.ResetCfg, seeds):
         s = h.struct()

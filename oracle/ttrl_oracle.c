@@ -318,6 +318,10 @@ static int next_lane(S* o, const ttrl_lane_table_t* R, int k, int cur, double x,
 /* ControlledVehicle.follow_road controller.py:135-143 */
 static void follow_road(S* o, const ttrl_lane_table_t* R, const ttrl_params_t* P, int base, int i) {
   const int k = base + i;
+  if (o->mg) {
+    double s, r; local(R, o->tgt[k], o->x[k], o->y[k], &s, &r);
+    mg(o, k, s - (R->length[o->tgt[k]] - P->lane_vehicle_length / 2), s);
+  }
   if (after_end(R, P, o->tgt[k], o->x[k], o->y[k])) o->tgt[k] = next_lane(o, R, k, o->tgt[k], o->x[k], o->y[k]);
 }
 
@@ -730,6 +734,42 @@ static int conflict(const ttrl_params_t* P, const double* ax, const double* ay, 
   }
   return 0;
 }
+/* The signed decision value of conflict() (>= 0 iff a conflict): per time step, min(LENGTH - the
+ * centre distance, the larger corner-inside value of the two rectangles), where a rectangle's
+ * corner-inside value is the max over its 9 points of min(l/2 - |u|, w/2 - |v|) in the other's
+ * frame -- its magnitude is the margin of the float64 decision (oracle_frame_margins only). */
+static double inside_value(double c1x, double c1y, double l1, double w1, double a1, double c2x, double c2y, double l2,
+                           double w2, double a2) {
+  const double hl = l1 / 2, hw = w1 / 2;
+  const double px[9] = {-hl, -hl, hl, hl, 0, -hl, hl, 0, 0};
+  const double py[9] = {-hw, hw, hw, -hw, 0, 0, 0, -hw, hw};
+  double c = cos(a1), s = sin(a1), best = -INFINITY;
+  for (int q = 0; q < 9; ++q) {
+    double x = c * px[q] + (-s) * py[q] + c1x, y = s * px[q] + c * py[q] + c1y;
+    double c2 = cos(a2), s2 = sin(a2), dx = x - c2x, dy = y - c2y;
+    double u = c2 * dx + (-s2) * dy, v = s2 * dx + c2 * dy;
+    double du = l2 / 2 - fabs(u), dv = w2 / 2 - fabs(v);
+    double m = du < dv ? du : dv;
+    if (m > best) best = m;
+  }
+  return best;
+}
+static double conflict_value(const ttrl_params_t* P, const double* ax, const double* ay, const double* ah,
+                             const double* bx, const double* by, const double* bh) {
+  const double l = 1.5 * P->length, w = 0.9 * P->width;
+  double best = -INFINITY;
+  for (int t = 0; t < PRED_T; ++t) {
+    double dx = bx[t] - ax[t], dy = by[t] - ay[t];
+    double g = P->length - sqrt(dx * dx + dy * dy);
+    double ci = inside_value(ax[t], ay[t], l, w, ah[t], bx[t], by[t], l, w, bh[t]);
+    double cj = inside_value(bx[t], by[t], l, w, bh[t], ax[t], ay[t], l, w, ah[t]);
+    double c = ci > cj ? ci : cj;
+    if (c < g) g = c;
+    if (g > best) best = g;
+  }
+  return best;
+}
+
 /* RegulatedRoad.respect_priorities regulation.py:62-77 (front_distance_to objects.py:204-205) */
 static int respect(const S* o, const ttrl_lane_table_t* R, int a, int b) {
   const int pa = R->priority[o->lane[a]], pb = R->priority[o->lane[b]];
@@ -755,6 +795,20 @@ static void enforce_road_rules(S* o, const ttrl_lane_table_t* R, const ttrl_para
     if (o->kind[base + i] == TTRL_ABSENT) continue;
     for (int j = i + 1; j < N; ++j) {
       if (o->kind[base + j] == TTRL_ABSENT) continue;
+      if (o->mg) {  /* the conflict test and the front-distance comparison decide for both vehicles */
+        const double cv = conflict_value(P, px + PRED_T * i, py + PRED_T * i, ph + PRED_T * i, px + PRED_T * j,
+                                         py + PRED_T * j, ph + PRED_T * j);
+        const double sc = fabs(o->x[base + i]) + fabs(o->y[base + i]);
+        mg(o, base + i, cv, sc);
+        mg(o, base + j, cv, sc);
+        const int a = base + i, b = base + j;
+        if (cv >= 0 && R->priority[o->lane[a]] == R->priority[o->lane[b]]) {  /* respect() runs */
+          double fab = cos(o->h[a]) * (o->x[b] - o->x[a]) + sin(o->h[a]) * (o->y[b] - o->y[a]);
+          double fba = cos(o->h[b]) * (o->x[a] - o->x[b]) + sin(o->h[b]) * (o->y[a] - o->y[b]);
+          mg(o, a, fab - fba, sc);
+          mg(o, b, fab - fba, sc);
+        }
+      }
       if (!conflict(P, px + PRED_T * i, py + PRED_T * i, ph + PRED_T * i, px + PRED_T * j, py + PRED_T * j,
                     ph + PRED_T * j))
         continue;
@@ -992,12 +1046,36 @@ int oracle_observe_kinematics(const ttrl_state_t* s, const ttrl_lane_table_t* R,
   return 0;
 }
 
-/* OccupancyGridObservation.observe observation.py:353-434 (+ fill_road_layer_by_lanes :453-483) */
-int oracle_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
-                        const ttrl_grid_cfg_t* cfg, float* out) {
+/* Observation decision margins (the float32 observation classifier, tests/test_gpu_parity.py):
+ * every output cell records the smallest relative margin of a discrete decision that could move
+ * content into or out of it (a floor() cell index, a range test, a min comparison); +inf where
+ * none.  Like mg(), a float32 observer may differ from the float64 one in a cell only where this
+ * margin is below the float32 working precision. */
+static void mg_cell(double* m, size_t q, double v) { if (m && v < m[q]) m[q] = v; }
+
+/* The cell (floor(ux), floor(uy)) of a layer [W][H], its neighbour across the nearer boundary of
+ * each axis, and the diagonal one: the cells a small error in (ux, uy) can move an item between.
+ * Margins in metres (distance to the boundary) relative to `scale`. */
+static void grid_item_mg(double* m, int W, int H, double ux, double uy, double sx, double sy, double scale) {
+  const double cx = floor(ux), cy = floor(uy), fx = ux - cx, fy = uy - cy;
+  const double mx = (fx < 0.5 ? fx : 1 - fx) * sx / scale, my = (fy < 0.5 ? fy : 1 - fy) * sy / scale;
+  const int dx = fx < 0.5 ? -1 : 1, dy = fy < 0.5 ? -1 : 1;
+  const double cand[4][3] = {{cx, cy, mx < my ? mx : my}, {cx + dx, cy, mx}, {cx, cy + dy, my},
+                             {cx + dx, cy + dy, mx > my ? mx : my}};
+  for (int q = 0; q < 4; ++q)
+    if (0 <= cand[q][0] && cand[q][0] < W && 0 <= cand[q][1] && cand[q][1] < H)
+      mg_cell(m, (size_t)cand[q][0] * H + (size_t)cand[q][1], cand[q][2]);
+}
+
+/* OccupancyGridObservation.observe observation.py:353-434 (+ fill_road_layer_by_lanes :453-483);
+ * margin (optional, [E][F][W][H]): see grid_item_mg */
+int oracle_observe_grid_m(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                          const ttrl_grid_cfg_t* cfg, float* out, double* margin) {
   (void)P; if (check(s)) return TTRL_E_ARG;
   S o = view(s);
   const int F = cfg->n_features, W = cfg->shape_x, H = cfg->shape_y;
+  if (margin)
+    for (size_t q = 0; q < (size_t)o.E * F * W * H; ++q) margin[q] = INFINITY;
 #pragma omp parallel
   {
   double* grid = (double*)malloc(sizeof(double) * F * W * H);
@@ -1023,10 +1101,14 @@ int oracle_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* R, const
             wp = clipd(wp, 0, R->length[l]);
             double px, py;
             position(R, l, wp, 0, &px, &py);
+            const double scale = 1 + fabs(px) + fabs(py);
             px -= o.x[ego]; py -= o.y[ego];
             long cx = (long)floor((px - cfg->grid_min_x) / cfg->step_x);
             long cy = (long)floor((py - cfg->grid_min_y) / cfg->step_y);
             if (0 <= cx && cx < W && 0 <= cy && cy < H) grid[(c * W + cx) * H + cy] = 1;
+            if (margin)
+              grid_item_mg(margin + ((size_t)e * F + c) * W * H, W, H, (px - cfg->grid_min_x) / cfg->step_x,
+                           (py - cfg->grid_min_y) / cfg->step_y, cfg->step_x, cfg->step_y, scale);
           }
         }
         continue;
@@ -1049,6 +1131,10 @@ int oracle_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* R, const
         long cx = (long)floor((x - cfg->grid_min_x) / cfg->step_x);
         long cy = (long)floor((y - cfg->grid_min_y) / cfg->step_y);
         if (0 <= cx && cx < W && 0 <= cy && cy < H) grid[(c * W + cx) * H + cy] = val;
+        if (margin)
+          grid_item_mg(margin + ((size_t)e * F + c) * W * H, W, H, (x - cfg->grid_min_x) / cfg->step_x,
+                       (y - cfg->grid_min_y) / cfg->step_y, cfg->step_x, cfg->step_y,
+                       1 + fabs(o.x[k]) + fabs(o.y[k]) + fabs(o.x[ego]) + fabs(o.y[ego]));
       }
     }
     float* ob = out + (size_t)e * F * W * H;
@@ -1061,6 +1147,11 @@ int oracle_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* R, const
   free(grid);
   }
   return 0;
+}
+
+int oracle_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                        const ttrl_grid_cfg_t* cfg, float* out) {
+  return oracle_observe_grid_m(s, R, P, cfg, out, NULL);
 }
 
 /* ---------------------------------------------------------------- scene generation */
@@ -1343,34 +1434,61 @@ int oracle_rng_ops(uint64_t* state5, const int32_t* ops, const int32_t* args, in
  * (finite_mdp.py:104-167), on the single straight road: every vehicle is on the ego's road
  * with the same lane count, so `lane = [other.lane_index[2]]` (finite_mdp.py:142-149).
  */
-int oracle_observe_ttc(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
-                       const ttrl_ttc_cfg_t* cfg, float* out) {
+/* margin (optional, shaped as out): a contribution's decisions -- the equal-speed skip, the sign
+ * of the time to collision (distance and closing speed, not_zero's switch), its bin (int() and
+ * ceil of t / quantization) and the horizon test -- recorded into the bins around its time. */
+int oracle_observe_ttc_m(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                         const ttrl_ttc_cfg_t* cfg, float* out, double* margin) {
   if (check(s) || !cfg || !out) return TTRL_E_ARG;
   S o = view(s);
   const int NS = P->n_target_speeds, NL = R->n_lanes, T = cfg->horizon_bins;
   const int OL = cfg->obs_lanes, OS = cfg->obs_speeds;
+  const int raw = OS == 0 && OL == 0;
+  if (margin)
+    for (size_t q = 0; q < (size_t)o.E * (raw ? NS * NL : OS * OL) * T; ++q) margin[q] = INFINITY;
 #pragma omp parallel
   {
   double* grid = (double*)malloc(sizeof(double) * NS * NL * T);
+  double* gm = (double*)malloc(sizeof(double) * NS * NL * T);
 #pragma omp for schedule(static)
   for (int e = 0; e < o.E; ++e) {
     const int base = e * o.N, ego = base;
-    for (int k = 0; k < NS * NL * T; ++k) grid[k] = 0;
+    for (int k = 0; k < NS * NL * T; ++k) { grid[k] = 0; gm[k] = INFINITY; }
     const double ec = cos(o.h[ego]), es = sin(o.h[ego]);
     for (int si = 0; si < NS; ++si) {
       const double ego_speed = P->target_speeds[si];             /* index_to_speed controller.py:317-324 */
       for (int j = 0; j < o.N; ++j) {                             /* env.road.vehicles, list order */
         const int k = base + j;
-        if (j == 0 || o.kind[k] == TTRL_ABSENT || ego_speed == o.v[k]) continue;
-        const double margin = P->length / 2 + P->length / 2;
-        const double pts[3][2] = {{0, 1}, {-margin, 0.5}, {margin, 0.5}};
+        if (j == 0 || o.kind[k] == TTRL_ABSENT) continue;
+        const double m_eq = fabs(ego_speed - o.v[k]) / (1 + fabs(ego_speed));
+        if (ego_speed == o.v[k] && !margin) continue;
+        const double margin_len = P->length / 2 + P->length / 2;
+        const double pts[3][2] = {{0, 1}, {-margin_len, 0.5}, {margin_len, 0.5}};
         for (int c = 0; c < 3; ++c) {
           const double distance = lane_distance(&o, R, base, 0, j) + pts[c][0];
           const double proj = o.v[k] * (cos(o.h[k]) * ec + sin(o.h[k]) * es);
           const double ttc = distance / not_zero(ego_speed - proj);
-          if (ttc < 0) continue;
           const int l = o.lane[k];
           const double q = ttc / cfg->time_quantization;
+          if (margin) {
+            const double den = ego_speed - proj, sc = 1 + fabs(ego_speed) + fabs(proj);
+            double m = m_eq;
+            const double pos = 1 + fabs(o.x[k]) + fabs(o.y[k]) + fabs(o.x[ego]) + fabs(o.y[ego]);
+            if (fabs(distance) / pos < m) m = fabs(distance) / pos;
+            if (fabs(den) / sc < m) m = fabs(den) / sc;
+            if (fabs(fabs(den) - 1e-2) / sc < m) m = fabs(fabs(den) - 1e-2) / sc;
+            const double aq = fabs(q), fq = aq - floor(aq);
+            const double mq = (fq < 0.5 ? fq : 1 - fq) / (1 + aq);
+            if (mq < m) m = mq;
+            if (fabs(T - aq) / (1 + aq) < m) m = fabs(T - aq) / (1 + aq);
+            for (double t = floor(aq) - 1; t <= ceil(aq) + 1; ++t)
+              if (0 <= t && t < T) {
+                double* g = &gm[(si * NL + l) * T + (int)t];
+                if (m < *g) *g = m;
+              }
+          }
+          if (ego_speed == o.v[k]) continue;
+          if (ttc < 0) continue;
           const double times[2] = {q, ceil(q)};                   /* int() of a non-negative value */
           for (int u = 0; u < 2; ++u) {
             if (!(times[u] < (double)T)) continue;
@@ -1383,6 +1501,8 @@ int oracle_observe_ttc(const ttrl_state_t* s, const ttrl_lane_table_t* R, const 
     }
     if (OS == 0 && OL == 0) {                                     /* raw grid (finite_mdp.py:48) */
       for (int k = 0; k < NS * NL * T; ++k) out[(size_t)e * NS * NL * T + k] = (float)grid[k];
+      if (margin)
+        for (int k = 0; k < NS * NL * T; ++k) margin[(size_t)e * NS * NL * T + k] = gm[k];
       continue;
     }
     /* observation.py:136-151: pad lanes with ones, window of obs_lanes around the ego's
@@ -1394,14 +1514,24 @@ int oracle_observe_ttc(const ttrl_state_t* s, const ttrl_lane_table_t* R, const 
       int sp = row < 1 + NS ? 0 : (row >= 2 * NS ? NS - 1 : row - NS);
       for (int b = 0; b < OL; ++b) {
         const int l = lane - OL / 2 + b;
-        for (int t = 0; t < T; ++t)
+        for (int t = 0; t < T; ++t) {
           ob[(a * OL + b) * T + t] = (l < 0 || l >= NL) ? 1.0f : (float)grid[(sp * NL + l) * T + t];
+          if (margin)
+            margin[(size_t)e * OS * OL * T + (a * OL + b) * T + t] = (l < 0 || l >= NL) ? INFINITY
+                                                                                       : gm[(sp * NL + l) * T + t];
+        }
       }
     }
   }
   free(grid);
+  free(gm);
   }
   return TTRL_OK;
+}
+
+int oracle_observe_ttc(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                       const ttrl_ttc_cfg_t* cfg, float* out) {
+  return oracle_observe_ttc_m(s, R, P, cfg, out, NULL);
 }
 
 /* utils.distance_to_rect utils.py:386-413 for the ray [r, q] and rectangle corners a, b, c, d */
@@ -1428,19 +1558,39 @@ static int angle_to_index(double angle, double step, int cells) {  /* observatio
   return (int)(k < 0 ? k + cells : k);
 }
 
-/* LidarObservation.trace observation.py:704-752 (obstacles: the other vehicles, list order) */
-int oracle_observe_lidar(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
-                         const ttrl_lidar_cfg_t* cfg, float* out) {
+/* The ray index of an angle (angle_to_index) and its margin: the arc length in metres, at
+ * `dist` from the observer, to the nearer sector boundary, relative to `scale`. */
+static double ray_mg(double angle, double step, double dist, double scale) {
+  const double u = angle / step, f = u - floor(u);
+  return (f < 0.5 ? f : 1 - f) * step * dist / scale;
+}
+static void mg_rays(double* m, int C, int from, int to, double v) {  /* rays from..to (wrapping), +-1 */
+  if (!m) return;
+  const int n = ((to - from) % C + C) % C + 3;
+  for (int u = 0; u < n && u < C; ++u) mg_cell(m, (size_t)(((from - 1 + u) % C + C) % C), v);
+}
+
+/* LidarObservation.trace observation.py:704-752 (obstacles: the other vehicles, list order);
+ * margin (optional, [E][cells]): each ray's decisions -- a vehicle's range test, the sector of its
+ * centre and of its corners' angular extent, the ray-rectangle hit test, and the nearest-hit
+ * comparison between vehicles. */
+int oracle_observe_lidar_m(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                           const ttrl_lidar_cfg_t* cfg, float* out, double* margin) {
   (void)R;
   if (check(s) || !cfg || !out || cfg->cells < 1 || cfg->cells > 64) return TTRL_E_ARG;
   S o = view(s);
   const int C = cfg->cells;
   const double range = cfg->maximum_range, step = 2 * PI / C;
+  if (margin)
+    for (size_t q = 0; q < (size_t)o.E * C; ++q) margin[q] = INFINITY;
 #pragma omp parallel for schedule(static)
   for (int e = 0; e < o.E; ++e) {
     const int base = e * o.N, ei = ego_of(&o, base), ego = base + ei;
     double grid[64][2];
-    for (int c = 0; c < C; ++c) grid[c][0] = grid[c][1] = range;
+    double best2[64][2];  /* the two smallest hit distances of each ray, for the comparison margin */
+    int who[64];
+    double* rm = margin ? margin + (size_t)e * C : NULL;
+    for (int c = 0; c < C; ++c) { grid[c][0] = grid[c][1] = range; best2[c][0] = best2[c][1] = INFINITY; who[c] = -1; }
     if (ei < 0) {
       for (int c = 0; c < C; ++c) out[(size_t)e * C * 2 + 2 * c] = out[(size_t)e * C * 2 + 2 * c + 1] = (float)(cfg->normalize ? 1.0 : range);
       continue;
@@ -1452,10 +1602,27 @@ int oracle_observe_lidar(const ttrl_state_t* s, const ttrl_lane_table_t* R, cons
       if (j == ei || o.kind[k] == TTRL_ABSENT) continue;
       const double dx = o.x[k] - ox, dy = o.y[k] - oy;
       const double center_distance = sqrt(dx * dx + dy * dy);
-      if (center_distance > range) continue;
+      const double scale = 1 + fabs(o.x[k]) + fabs(o.y[k]) + fabs(ox) + fabs(oy);
+      const double m_range = fabs(center_distance - range) / scale;
+      if (center_distance > range) {
+        if (rm && m_range < 1e-3) mg_rays(rm, C, 0, C - 1, m_range);  /* at the range: any of its rays */
+        continue;
+      }
       const double vx = o.v[k] * cos(o.h[k]) - ovx, vy = o.v[k] * sin(o.h[k]) - ovy;
       const int ci = angle_to_index(atan2(dy, dx) + step / 2, step, C);
       const double distance = center_distance - P->width / 2;
+      if (rm) {
+        mg_rays(rm, C, ci, ci, ray_mg(atan2(dy, dx) + step / 2, step, center_distance, scale));
+        if (m_range < 1e-3) mg_rays(rm, C, 0, C - 1, m_range);
+      }
+#define HIT(c_, d_)                                                                               \
+  do {                                                                                            \
+    if (who[c_] != j) {                                                                           \
+      if ((d_) < best2[c_][0]) { best2[c_][1] = best2[c_][0]; best2[c_][0] = (d_); who[c_] = j; } \
+      else if ((d_) < best2[c_][1]) best2[c_][1] = (d_);                                          \
+    } else if ((d_) < best2[c_][0]) best2[c_][0] = (d_);                                          \
+  } while (0)
+      HIT(ci, distance);
       if (distance <= grid[ci][0]) {
         grid[ci][0] = distance;
         grid[ci][1] = vx * cos(ci * step) + vy * sin(ci * step);
@@ -1479,17 +1646,38 @@ int oracle_observe_lidar(const ttrl_state_t* s, const ttrl_lane_table_t* R, cons
       }
       const int start = angle_to_index(amin, step, C), end = angle_to_index(amax, step, C);
       const int n = start < end ? end - start + 1 : (C - start) + end + 1;
+      if (rm) {  /* the corners' sectors, the wrap test: the vehicle's whole span of rays */
+        double m = ray_mg(amin, step, center_distance, scale);
+        const double m2 = ray_mg(amax, step, center_distance, scale);
+        if (m2 < m) m = m2;
+        const double mw = fmin(fabs(amin + PI / 2), fabs(amax - PI / 2)) * center_distance / scale;
+        if (mw < m) m = mw;
+        mg_rays(rm, C, start, end, m);
+      }
       for (int u = 0; u < n; ++u) {
         const int idx = start < end ? start + u : (u < C - start ? start + u : u - (C - start));
         const double dirx = cos(idx * step), diry = sin(idx * step);
         const double r[2] = {ox, oy}, qq[2] = {ox + range * dirx, oy + range * diry};
         const double d = distance_to_rect(r, qq, corners);
+        if (rm) {  /* the hit test: the ray's distance to the rectangle's nearest edge line */
+          double mh = INFINITY;
+          for (int q = 0; q < 4; ++q) {  /* the corners' signed distances to the ray's line */
+            const double cd = fabs((corners[q][0] - ox) * diry - (corners[q][1] - oy) * dirx);
+            if (cd / scale < mh) mh = cd / scale;
+          }
+          mg_cell(rm, (size_t)idx, mh);
+        }
+        if (d < INFINITY) HIT(idx, d);
         if (d <= grid[idx][0]) {
           grid[idx][0] = d;
           grid[idx][1] = vx * dirx + vy * diry;
         }
       }
     }
+#undef HIT
+    if (rm)  /* the nearest hit of each ray against the runner-up vehicle's */
+      for (int c = 0; c < C; ++c)
+        if (best2[c][1] < INFINITY) mg_cell(rm, (size_t)c, fabs(best2[c][1] - best2[c][0]) / (1 + range));
     float* ob = out + (size_t)e * C * 2;
     for (int c = 0; c < C; ++c) {
       ob[2 * c] = (float)(cfg->normalize ? grid[c][0] / range : grid[c][0]);
@@ -1497,4 +1685,9 @@ int oracle_observe_lidar(const ttrl_state_t* s, const ttrl_lane_table_t* R, cons
     }
   }
   return TTRL_OK;
+}
+
+int oracle_observe_lidar(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P,
+                         const ttrl_lidar_cfg_t* cfg, float* out) {
+  return oracle_observe_lidar_m(s, R, P, cfg, out, NULL);
 }

@@ -199,3 +199,21 @@ def test_golden_covers_the_hard_cases(cases):
         impacts += int(np.isfinite(d["impact_x"]).sum())
         crashes += int(d["crashed"][-1].sum())
     assert changes > 50 and aborts > 0 and impacts > 100 and crashes > 50, (changes, aborts, impacts, crashes)
+
+
+@pytest.mark.parametrize("name", [IDS(p) for p in golden_files()])
+def test_observation_margins_leave_the_observations_unchanged(name, cases):
+    """The observation margins (the float32 observation classifier) come with outputs equal to the
+    plain observers', and are small in few cells: a cell is excused only near a floor / range /
+    nearest-hit decision."""
+    d = cases[name]
+    lanes = _abi.lane_table_from_arrays(d["lane_table"])
+    o = Oracle(lanes, P)
+    h = HostState.from_golden(d, 15)
+    grid = _abi.grid_cfg(["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"], [[-32, 32], [-32, 32]], [2, 2],
+                         {"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]})
+    for obs, cfg in ((o.observe_grid, grid), (o.observe_ttc, _abi.ttc_cfg()), (o.observe_lidar, _abi.lidar_cfg())):
+        a = obs(h, cfg)
+        b, m = obs(h, cfg, margins=True)
+        assert np.array_equal(a, b) and m.shape[:2] == a.shape[:2]
+        assert np.all(m >= 0) and np.mean(m < 1e-5) < 0.02, (cfg, np.mean(m < 1e-5))
