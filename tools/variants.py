@@ -107,4 +107,4 @@ if __name__ == "__main__":
     if sys.argv[1] == "build":
         build()
     else:
-        run(sys.argv[2:] or ["f64", "f32"])
+        run(sys.argv[2:] or ["f64", "f32"], E=int(os.environ.get("E", "4096")), N=int(os.environ.get("N", "64")))

@@ -554,6 +554,9 @@ template <typename T> struct View {
   int8_t* rn;                    // [EPW*NS] route lengths (-1 None)
   uint8_t* ynew;                 // [EPW*NS] RegulatedRoad: yields decided this enforcement
   RoadTab* rt;                   // road topology
+  int* rq;                       // [rq_cap] RegulatedRoad (pair, time step) items past the float prefilter,
+  uint8_t* rqf;                  // [RQ_PAIRS] and the pairs' conflict flags: the dead transient block
+  int rq_cap;                    // beyond the predictions (0: no room, the serial pair loop runs)
   float *px, *py;                // [EPW*NS][PRED_T] predicted positions, float32 (is_conflict_possible's
                                  // distance prefilter; poses that pass are recomputed in float64)
   T* ps0;                        // [EPW*NS] the prediction's start: s along the current lane
@@ -585,10 +588,11 @@ __host__ __device__ constexpr int list_cap(int NS, int EPW, bool graph) {
 
 // Byte offsets of the view's arrays in the dynamic LDS block (host: sizing; device: carve).
 constexpr int N_REALS = 8;  // x, y, v, ch, sh, ts, h, delta
+constexpr int RQ_PAIRS = 256;  // RegulatedRoad pairs of a wave the flattened enforcement takes (else serial)
 struct ViewLayout {
   size_t lanes, reals[N_REALS], xf, key, afree, powb, pq_tx, pq_ty, pq_ij, bal, cnt, wcnt, nitem, pq_n, mypos, f0, r0, ft,
       mob, item, idx, kind, flags, lane, tgt, pred, rroad, rlane, rn, ynew, rt, onm, live, lperm, pd, pl, onb, sord,
-      spos, sxf, lmask, stie, own, total;
+      spos, sxf, lmask, stie, own, rq, rqf, rq_cap, total;
 };
 
 template <typename T>
@@ -656,6 +660,10 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, 
     o.pred = t0;  // float px, py [M][PRED_T], then ps0 [M]
     const size_t pred_end = t0 + ((sizeof(float) * 2 * PRED_T * M + 15) & ~(size_t)15) + sizeof(T) * M;
     if (p < pred_end) p = pred_end;
+    // beyond the predictions, the rest of the transient block is dead during the enforcement as well
+    o.rqf = (pred_end + 15) & ~(size_t)15;
+    o.rq = o.rqf + RQ_PAIRS;
+    o.rq_cap = p > o.rq + 4 * 64 ? (p - o.rq) / 4 : 0;
     o.rroad = take(TTRL_ROUTE_MAX * M, 4);
     o.rlane = take(TTRL_ROUTE_MAX * M, 4);
     o.rn = take(M, 4);
@@ -714,6 +722,9 @@ __device__ __forceinline__ View<T> carve(char* smem, int EPW, int NS, int n_lane
     V.rn = (int8_t*)(smem + o.rn);
     V.ynew = (uint8_t*)(smem + o.ynew);
     V.rt = (RoadTab*)(smem + o.rt);
+    V.rq = (int*)(smem + o.rq);
+    V.rqf = (uint8_t*)(smem + o.rqf);
+    V.rq_cap = (int)o.rq_cap;
     V.onm = (unsigned long long*)(smem + o.onm);
     V.pd = (T*)(smem + o.pd);
     V.live = (uint8_t*)(smem + o.live);
@@ -2161,11 +2172,34 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
                 V.ts[me] = V.lanes[V.lane[me]].lim;
                 V.flags[me] = (uint8_t)(fl & ~FL_YIELD);
               }
-              predict_poses(V.lanes, *V.rt, (int)V.lane[me], V.x[me], V.y[me], V.v[me], V.rroad + me * TTRL_ROUTE_MAX,
-                            V.rlane + me * TTRL_ROUTE_MAX, (int)V.rn[me], V.px + me * PRED_T, V.py + me * PRED_T,
-                            V.ps0 + me);
+              if constexpr (NS * EPW != 64)
+                predict_poses(V.lanes, *V.rt, (int)V.lane[me], V.x[me], V.y[me], V.v[me], V.rroad + me * TTRL_ROUTE_MAX,
+                              V.rlane + me * TTRL_ROUTE_MAX, (int)V.rn[me], V.px + me * PRED_T, V.py + me * PRED_T,
+                              V.ps0 + me);
             }
             V.ynew[me] = 0;
+            if constexpr (NS * EPW == 64) {
+              // One wavefront: the predictions as (vehicle, time step) items over all its lanes (a scene
+              // has ~8 live vehicles in 32 slots: one vehicle per lane walked its 11 poses serially)
+              const bool pv = doreg && present;
+              if (pv) {
+                T s0, r0;
+                lane_local(V.lanes[V.lane[me]], V.x[me], V.y[me], s0, r0);
+                V.ps0[me] = s0;
+              }
+              const unsigned long long pm = __ballot(pv);
+              if (pv) V.live[__popcll(pm & ((1ull << tid) - 1))] = (uint8_t)tid;
+              __syncthreads();
+              const int nitems = __popcll(pm) * PRED_T;
+              for (int q = tid; q < nitems; q += 64) {
+                const int vv = V.live[q / PRED_T], t = q - (q / PRED_T) * PRED_T;
+                T ex, ey;
+                pose_at(V.lanes, *V.rt, (int)V.lane[vv], V.ps0[vv], V.v[vv], V.rroad + vv * TTRL_ROUTE_MAX,
+                        V.rlane + vv * TTRL_ROUTE_MAX, (int)V.rn[vv], t, ex, ey, (T*)nullptr);
+                V.px[vv * PRED_T + t] = (float)ex;
+                V.py[vv * PRED_T + t] = (float)ey;
+              }
+            }
             __syncthreads();
             PH(18);
             // is_conflict_possible (regulation.py:80-103) then respect_priorities (:62-77) for the pair
@@ -2219,15 +2253,91 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
                 tot += np[e];
               }
               __syncthreads();
-              for (int k = tid; k < tot; k += 64) {
-                int e = 0, kk = k;
+              // pair k of the wave -> (env, lower live index, upper live index), pairs ordered by the upper
+              auto decode = [&](int k, int& e, int& a, int& b) {
+                int kk = k;
+                e = 0;
                 while (kk >= np[e]) { kk -= np[e]; ++e; }
-                int rb = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)kk)) * 0.5f);  // pairs ordered by rb
+                int rb = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)kk)) * 0.5f);
                 while (rb * (rb - 1) / 2 > kk) --rb;
                 while ((rb + 1) * rb / 2 <= kk) ++rb;
-                const int ra = kk - rb * (rb - 1) / 2;
-                reg_pair(e * NS, V.live[e * NS + ra], V.live[e * NS + rb]);
+                a = V.live[e * NS + kk - rb * (rb - 1) / 2];
+                b = V.live[e * NS + rb];
+              };
+              bool flat = false;
+              if (tot <= RQ_PAIRS && V.rq_cap > 0) {
+                // Flattened: is_conflict_possible is an OR over the 11 time steps, so (pair, step) items
+                // are independent.  (A) the float32 distance prefilter over all items, survivors queued
+                // (ballot slots); (B) the exact float64 test of the survivors, one per lane (a close pair
+                // no longer walks its steps serially on one lane); (C) respect_priorities of the pairs
+                // that conflict.  Queue overflow: the serial per-pair loop below.
+                for (int k = tid; k < tot; k += 64) V.rqf[k] = 0;
+                const float thr_len = float(P.length) + 1e-3f;
+                int nq = 0;
+                for (int k0 = 0; k0 < tot * PRED_T; k0 += 64) {
+                  const int k = k0 + tid;
+                  bool pass = false;
+                  int pid = 0, t = 0;
+                  if (k < tot * PRED_T) {
+                    pid = k / PRED_T;
+                    t = k - pid * PRED_T;
+                    int e, a, b;
+                    decode(pid, e, a, b);
+                    const int pa = (e * NS + a) * PRED_T + t, pb = (e * NS + b) * PRED_T + t;
+                    const float fxa = V.px[pa], fya = V.py[pa], fxb = V.px[pb], fyb = V.py[pb];
+                    const float fdx = fxb - fxa, fdy = fyb - fya;
+                    const float thr = thr_len + 4e-7f * (fabsf(fxa) + fabsf(fxb) + fabsf(fya) + fabsf(fyb));
+                    pass = !(fdx * fdx + fdy * fdy > thr * thr);  // as reg_pair's prefilter (NaN passes)
+                  }
+                  const unsigned long long bal = __ballot(pass);
+                  const int pos = nq + __popcll(bal & ((1ull << tid) - 1));
+                  if (pass && pos < V.rq_cap) V.rq[pos] = pid << 4 | t;
+                  nq += __popcll(bal);
+                }
+                if (nq <= V.rq_cap) {
+                  flat = true;
+                  __syncthreads();
+                  for (int k = tid; k < nq; k += 64) {
+                    const int pid = V.rq[k] >> 4, t = V.rq[k] & 15;
+                    int e, a, b;
+                    decode(pid, e, a, b);
+                    const int ka = e * NS + a, kb = e * NS + b;
+                    T xa, ya, ha, xb, yb, hb;
+                    pose_at(V.lanes, *V.rt, (int)V.lane[ka], V.ps0[ka], V.v[ka], V.rroad + ka * TTRL_ROUTE_MAX,
+                            V.rlane + ka * TTRL_ROUTE_MAX, (int)V.rn[ka], t, xa, ya, &ha);
+                    pose_at(V.lanes, *V.rt, (int)V.lane[kb], V.ps0[kb], V.v[kb], V.rroad + kb * TTRL_ROUTE_MAX,
+                            V.rlane + kb * TTRL_ROUTE_MAX, (int)V.rn[kb], t, xb, yb, &hb);
+                    const T dx = xb - xa, dy = yb - ya;
+                    if (!(sqrt(dx * dx + dy * dy) > T(P.length)) &&
+                        rects_intersect(xa, ya, ha, xb, yb, hb, T(1.5) * T(P.length), T(0.9) * T(P.width)))
+                      V.rqf[pid] = 1;
+                  }
+                  __syncthreads();
+                  for (int k = tid; k < tot; k += 64) {
+                    if (!V.rqf[k]) continue;
+                    int e, a, b;
+                    decode(k, e, a, b);
+                    const int ebp = e * NS;
+                    const int qa = V.lanes[V.lane[ebp + a]].prio, qb = V.lanes[V.lane[ebp + b]].prio;
+                    int yv;
+                    if (qa > qb) yv = b;
+                    else if (qa < qb) yv = a;
+                    else {
+                      const int ka = ebp + a, kb = ebp + b;
+                      const T fab = V.ch[ka] * (V.x[kb] - V.x[ka]) + V.sh[ka] * (V.y[kb] - V.y[ka]);
+                      const T fba = V.ch[kb] * (V.x[ka] - V.x[kb]) + V.sh[kb] * (V.y[ka] - V.y[kb]);
+                      yv = fab > fba ? a : b;
+                    }
+                    if (V.kind[ebp + yv] == TTRL_IDM) V.ynew[ebp + yv] = 1;  // ControlledVehicle, not MDPVehicle
+                  }
+                }
               }
+              if (!flat)
+                for (int k = tid; k < tot; k += 64) {
+                  int e, a, b;
+                  decode(k, e, a, b);
+                  reg_pair(e * NS, a, b);
+                }
             } else if (doreg) {  // every pair (a < b) once: thread i takes (i, i + d mod NS), d = 1 .. NS/2
               for (int d = 1; d <= NS / 2; ++d) {
                 if (d == NS / 2 && i >= NS / 2) break;
@@ -4436,6 +4546,13 @@ int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
 /* Diagnostic only (not in include/): the simulate kernel's LDS view bytes per workgroup. */
 long ttrl_diag_view_bytes(int32_t dtype, int32_t epw, int32_t ns, int32_t n_lanes, int32_t graph, int32_t sorted) {
   return (long)host_view_bytes(dtype, epw, ns, n_lanes, graph != 0, sorted != 0);
+}
+
+/* Diagnostic only (not in include/): the flattened enforcement's queue capacity of a road-network
+ * view (0: the serial pair loop runs). */
+long ttrl_diag_rq_cap(int32_t dtype, int32_t epw, int32_t ns, int32_t n_lanes) {
+  return (long)(dtype == TTRL_F64 ? view_layout<double>(epw, ns, n_lanes, true, false).rq_cap
+                                  : view_layout<float>(epw, ns, n_lanes, true, false).rq_cap);
 }
 
 /* Diagnostic only (not in include/): the fused loop with phases ablated, for profiling. */
