@@ -312,6 +312,36 @@ __host__ __device__ inline LaneT<T> make_lane(const ttrl_lane_table_t& R, int l)
   return L;
 }
 
+// The bounding box of a lane's centre line, in float32 rounded outwards (a margin of 1e-3 m +
+// 1e-6 of the coordinates): straight lanes their two ends, circular lanes their two ends and the
+// cardinal points the arc passes; a sine lane gets no box (+-inf: never pruned).  A lower bound of
+// distance_with_heading for project_items' pruning.
+template <typename T>
+__device__ inline float4 lane_box(const LaneT<T>& L) {
+  T x0, y0, x1, y1;
+  if (L.type == TTRL_LANE_STRAIGHT) {
+    const T ex = L.sx + L.len * L.dx, ey = L.sy + L.len * L.dy;
+    x0 = fmin(L.sx, ex); x1 = fmax(L.sx, ex);
+    y0 = fmin(L.sy, ey); y1 = fmax(L.sy, ey);
+  } else if (L.type == TTRL_LANE_CIRCULAR) {
+    const T a0 = L.sph, a1 = a0 + L.dirn * L.len / L.rad;
+    const T lo = fmin(a0, a1), hi = fmax(a0, a1);
+    x0 = x1 = L.cx + L.rad * cos(a0);
+    y0 = y1 = L.cy + L.rad * sin(a0);
+    const T ex = L.cx + L.rad * cos(a1), ey = L.cy + L.rad * sin(a1);
+    x0 = fmin(x0, ex); x1 = fmax(x1, ex); y0 = fmin(y0, ey); y1 = fmax(y1, ey);
+    const T q = T(1.5707963267948966);
+    for (T a = ceil(lo / q) * q; a <= hi; a += q) {  // cardinal points within the arc
+      const T px = L.cx + L.rad * cos(a), py = L.cy + L.rad * sin(a);
+      x0 = fmin(x0, px); x1 = fmax(x1, px); y0 = fmin(y0, py); y1 = fmax(y1, py);
+    }
+  } else {
+    return make_float4(-INFINITY, -INFINITY, INFINITY, INFINITY);
+  }
+  const float m = 1e-3f + 1e-6f * (float)(fabs(x0) + fabs(x1) + fabs(y0) + fabs(y1));
+  return make_float4((float)x0 - m, (float)y0 - m, (float)x1 + m, (float)y1 + m);
+}
+
 // AbstractLane.is_reachable_from lane.py:104-118
 template <bool CV = true, typename T>
 __device__ __forceinline__ bool reachable(const LaneT<T>& L, T vl, T px, T py) {
@@ -1161,9 +1191,14 @@ __device__ int g_dbg_count = 0;
 #else
 #define TTRL_ITEMS_ATTR __noinline__
 #endif
+#ifndef TTRL_NO_PROJ_PRUNE
+constexpr bool PROJ_PRUNE = true;
+#else
+constexpr bool PROJ_PRUNE = false;
+#endif
 template <typename T, int NS, int EPW, int LC, typename PP>
 __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int nl, int tid, int le, int i,
-                             bool present, bool want_closest) {
+                             bool present, bool want_closest, float4 my_box, float onb) {
   static_assert(NS * EPW == 64, "one wavefront per workgroup");
   constexpr int NSP = LC + 1;
   constexpr unsigned long long SEG = NS == 64 ? ~0ull : ((1ull << NS) - 1);
@@ -1175,7 +1210,125 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int 
   if (tid < nl) V.onm[tid] = 0ull;
   for (int k = tid; k < nl * EPW * NS / 2; k += 64) ((int*)V.mypos)[k] = -1;  // not on the lane
   if (tid < EPW) V.cnt[tid * (LMAX + 1) + LMAX] = 0;
+  // Pruned projection (exact).  distance_with_heading d = |r| + max(s - len, 0) + max(-s, 0) +
+  // |angle| is at least the Euclidean distance to the lane's centre line (radially to the line or
+  // its extension, then along it to its end), so at least the distance to the line's bounding box
+  // (lane_box).  An item whose box lies farther than (a) the on-lane reach (|r| <= w/2 + 1 and
+  // -LENGTH <= s < len + LENGTH keep a point within w/2 + 1 + LENGTH of the line) and (b) the
+  // vehicle's distance to its previous lane (an upper bound of its minimum, the same arithmetic)
+  // is neither on the lane nor the closest lane nor tied with it.  (A) box tests over all (vehicle,
+  // lane) items, the survivors compacted in (vehicle, lperm) order; (B) their projections spread
+  // over all lanes of the wave; (C) each vehicle's first minimum over its run of survivors;
+  // (D) the on-lane survivors' list entries.  A scene whose survivors exceed the queue takes the
+  // unpruned passes below.  Scratch: the act block, dead here (boxes, run starts, the queue), and
+  // the lists' key rows (each survivor's d and lane), dead until (D) rewrites them.
+  char* pscr = (char*)V.afree;
+  float4* lbox = (float4*)pscr;                     // [nl]
+  short* pstart = (short*)(lbox + nl);              // [65] run start of each live vehicle
+  short* psv = pstart + 66;                         // [cap] survivors: slot << 5 | lperm position
+  constexpr int ACT_BYTES = EPW * NS * (2 * (int)sizeof(T) + 14);  // afree .. item (view_layout)
+  const int key_bytes = nl * EPW * NSP * (int)sizeof(T);
+  const int cap = min((ACT_BYTES - 16 * nl - 2 * 66) / 2, key_bytes / (1 + (int)sizeof(T))) - 1;
+  T* pd_ = V.key;                                   // [cap] d of each survivor
+  int8_t* pl_ = (int8_t*)(pd_ + cap);               // [cap] and its lane
+  if constexpr (PROJ_PRUNE) {
+    if (tid < nl) lbox[tid] = my_box;
+    T ub = K<T>::inf();
+    if (present && want_closest) {
+      const int l0 = V.lane[tid];
+      if (l0 >= 0 && l0 < nl) {
+        const LaneT<T> L = V.lanes[l0];
+        const T x0 = V.x[tid], y0 = V.y[tid];
+        T s0, r0;
+        lane_local<true>(L, x0, y0, s0, r0);
+        T a = s0 - L.len; if (!(a > T(0))) a = T(0);
+        T b = T(0) - s0; if (!(b > T(0))) b = T(0);
+        ub = fabs(r0) + a + b + T(1) * fabs(wrap_to_pi(V.h[tid] - heading_at<true>(L, s0)));
+      }
+    }
+    V.pd[tid] = ub;
+  }
   __syncthreads();
+  int cl = 0;
+  bool pruned = false;
+  if constexpr (PROJ_PRUNE) {
+    // (A) box tests, (vehicle, lperm position) items in vehicle-major order
+    const int nitems = total * nl;
+    int nsv = 0;
+    for (int k0 = 0; k0 < nitems; k0 += 64) {
+      const int k = k0 + tid;
+      bool keep = false;
+      int q = 0, kk = 0, vv = 0;
+      if (k < nitems) {
+        q = k / nl;
+        kk = k - q * nl;
+        vv = V.live[q];
+        const float fx = (float)V.x[vv], fy = (float)V.y[vv];
+        const T ubv = V.pd[vv];
+        // the float32 rounding of the box test: 1e-3 m + 1e-6 of the coordinates
+        const float bound = fmaxf(onb, ubv < T(3.0e38f) ? (float)ubv * 1.000001f : INFINITY) + 1e-3f +
+                            1e-6f * (fabsf(fx) + fabsf(fy));
+        const float4 bx = lbox[V.lperm[kk]];
+        const float ex = fmaxf(fmaxf(bx.x - fx, fx - bx.z), 0.0f), ey = fmaxf(fmaxf(bx.y - fy, fy - bx.w), 0.0f);
+        keep = !(ex * ex + ey * ey > bound * bound);  // NaN positions are kept
+      }
+      const unsigned long long bal = __ballot(keep);
+      const int pos = nsv + __popcll(bal & below);
+      if (k < nitems && kk == 0) pstart[q] = (short)pos;  // the survivors before vehicle q's run
+      if (keep && pos < cap) psv[pos] = (short)(vv << 5 | kk);
+      nsv += __popcll(bal);
+    }
+    if (nsv <= cap) {
+      pruned = true;
+      if (tid == 0) pstart[total] = (short)nsv;
+      __syncthreads();
+      // (B) the survivors' projections
+      for (int k = tid; k < nsv; k += 64) {
+        const int vv = psv[k] >> 5, l = V.lperm[psv[k] & 31];
+        const LaneT<T> L = V.lanes[l];
+        T s, r;
+        lane_local<true>(L, V.x[vv], V.y[vv], s, r);
+        if (fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl)  // AbstractLane.on_lane margin 1
+          atomicOr(&V.onm[l], 1ull << vv);
+        if (want_closest) {  // distance_with_heading lane.py:132-147
+          T a = s - L.len; if (!(a > T(0))) a = T(0);
+          T b = T(0) - s; if (!(b > T(0))) b = T(0);
+          pd_[k] = fabs(r) + a + b + T(1) * fabs(wrap_to_pi(V.h[vv] - heading_at<true>(L, s)));
+          pl_[k] = (int8_t)l;
+        }
+      }
+      __syncthreads();
+      // (C) the first minimum of each vehicle over its run (lperm order, ties to the lower lane)
+      if (want_closest && present) {
+        const int q = __popcll(live & below);
+        T cd = T(0);
+        cl = -1;
+        for (int k = pstart[q], k1 = pstart[q + 1]; k < k1; ++k) {
+          const int lu = pl_[k];
+          const T du = pd_[k];
+          if (cl < 0 || du < cd || (du == cd && lu < cl)) { cd = du; cl = lu; }
+        }
+      }
+      __syncthreads();  // (C)'s reads of the key rows before (D) writes them
+      // (D) each on-lane survivor's list position (slot order = list order), key and slot
+      for (int k = tid; k < nsv; k += 64) {
+        const int vv = psv[k] >> 5, l = V.lperm[psv[k] & 31];
+        const unsigned long long m = V.onm[l];
+        if (!((m >> vv) & 1ull)) continue;
+        const int e = vv / NS, sl = vv % NS;
+        const int pos = __popcll((m >> (e * NS)) & SEG & ((1ull << sl) - 1));
+        V.mypos[(size_t)l * EPW * NS + vv] = (short)pos;
+        if (pos < LC) {
+          T sq, rq;
+          lane_local<true>(V.lanes[l], V.x[vv], V.y[vv], sq, rq);
+          const size_t base = ((size_t)l * EPW + e) * NSP;
+          V.key[base + pos] = sq;
+          V.idx[base + pos] = (uint8_t)sl;
+        }
+      }
+    }
+  }
+  if (!pruned) {
   const int G = total > 0 ? 64 / total : 1;  // lane groups per vehicle
   const int g = total > 0 ? tid / total : 1;
   T bd = T(0), prev_hd = T(0), ang = T(0);
@@ -1217,7 +1370,6 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int 
   }
   if (want_closest) { V.pd[tid] = bd; V.pl[tid] = (int8_t)best; }
   __syncthreads();
-  int cl = 0;
   if (want_closest && present) {  // the vehicle's groups, combined as (d, lane)
     const int q = __popcll(live & below);
     T cd = T(0);
@@ -1251,6 +1403,7 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int 
       }
     }
   }
+  }  // !pruned
   // the list lengths, one thread per (lane, env)
   if (tid < nl * EPW) {
     const int l = tid / EPW, e = tid - l * EPW;
@@ -1802,6 +1955,14 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
   PH(15);
   if (i == 0) V.nitem[le] = 0;
   __syncthreads();  // lane table + view staged
+  // project_items' pruning: each thread < nl keeps its lane's box for the launch; the on-lane reach
+  // is the widest lane's w / 2 + 1 + LENGTH (AbstractLane.on_lane, margin 1)
+  float4 my_box = make_float4(0.f, 0.f, 0.f, 0.f);
+  float onb_all = 0.0f;
+  if constexpr (GR && NS * EPW == 64) {
+    if (tid < nl) my_box = lane_box(V.lanes[tid]);
+    for (int l = 0; l < nl; ++l) onb_all = fmaxf(onb_all, (float)(R.width[l] / 2 + 1 + P.lane_vehicle_length));
+  }
   {
     int ob = 0;
     const T x0 = V.x[me];
@@ -2399,7 +2560,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
 #else
       if constexpr (false)
 #endif
-        cl = project_items<T, NS, EPW, LC>(V, P, nl, tid, le, i, present, !(ablate & A_NO_LANE));
+        cl = project_items<T, NS, EPW, LC>(V, P, nl, tid, le, i, present, !(ablate & A_NO_LANE), my_box, onb_all);
       else {
         int ob = 0;
         cl = project_all<T, NS, EPW, CV, !SO, LC>(V, P, nl, tid, le, i, present, x, y, h, !(ablate & A_NO_LANE), &ob);
