@@ -326,7 +326,12 @@ def main():
     g.manual_seed(1000 + rank)
     n_act = env.action_space.n
     acts = torch.randint(0, n_act, (args.warmup + args.steps, E), device=dev, generator=g, dtype=torch.int32)
-    live = torch.zeros((), dtype=torch.int64, device=dev)  # live vehicles summed over the timed steps
+    # config 6 counts live vehicles, not slots: every step's tail launch (ttrl_ix_step_tail) adds the
+    # vehicles present after it -- the next step's live vehicles -- to this counter, so the timed
+    # steps' count is (live at the first timed step) + counter - (live after the last one)
+    live = torch.zeros((), dtype=torch.int64, device=dev)
+    if ix:
+        env.live_counter = live
 
     sg = None
     if args.graph:
@@ -336,15 +341,11 @@ def main():
     def one_step(t):
         nonlocal obs
         if sg is not None:
-            if ix:
-                live.add_((env.state["kind"] != 0).sum())
             if policy is None:
                 sg.set_actions(acts[t])
             sg.replay()
             return
-        a = policy.act(obs, t) if policy is not None else acts[t]
-        if ix:  # counted in the warm-up steps too, so the count's kernels are loaded before t0
-            live.add_((env.state["kind"] != 0).sum())
+        a = policy.act(obs, t, dtype=torch.int32) if policy is not None else acts[t]
         obs, rew, term, trunc, info = env.step(a)
 
     kern_warm = []
@@ -361,7 +362,9 @@ def main():
             env.state.copy_(snap)
     for t in range(args.warmup):
         one_step(t)
-    live.zero_()  # only the timed steps' live vehicles count
+    torch.cuda.synchronize()
+    live0 = int((env.state["kind"] != 0).sum()) if ix else 0  # the first timed step's live vehicles
+    live.zero_()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -410,6 +413,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if ix:  # the counter holds the tails of the timed steps: the last one counts the step after them
+        live_steps = live0 + int(live.item()) - int((env.state["kind"] != 0).sum())
     BatchedRoad.simulate, BatchedRoad.env_step = orig_sim, orig_env_step
     BatchedOccupancyGridObservation.observe = orig_grid
 
@@ -422,7 +427,7 @@ def main():
 
     veh_steps = global_envs * N * 15 * args.steps
     if ix:  # live vehicles, not slots, summed over the ranks
-        veh_steps = int(sharding.sum_over_ranks(float(live.item()), device=None if shared else dev)) * 15
+        veh_steps = int(sharding.sum_over_ranks(float(live_steps), device=None if shared else dev)) * 15
     value = veh_steps / elapsed
     rd, wr = state_bytes(args.dtype)
     alg_bytes = E * N * (rd + wr)  # per fused simulate launch

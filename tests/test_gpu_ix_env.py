@@ -231,23 +231,77 @@ def test_overlapped_resets_equal_in_place_resets(duration, dtype, streams, slots
     same launch) gives the same trajectories, bit for bit, as the in-place composition of separate
     launches (simulate, observe, rewards, clear / spawn, reset, masked observe); duration 1
     finishes every env at every step (both slots in turn).  96 slots: the new scenes are observed
-    by the masked observation launch instead of the tail launch (one slot per lane there)."""
+    by the masked observation launch instead of the tail launch (one slot per lane there).  The
+    tail's live-vehicle counter (the config-6 bench's count) equals the vehicles present after
+    every step."""
     cfg = {**ENV_JSON, "num_envs": 48, "device": hip_device, "auto_reset": True, "duration": duration,
            "dtype": dtype, "reset_streams": streams, "vehicle_slots": slots}
     a = VecIntersectionEnv({**cfg, "overlap_resets": True})
     b = VecIntersectionEnv({**cfg, "overlap_resets": False})
+    a.live_counter = torch.zeros((), dtype=torch.int64, device=hip_device)
     oa, _ = a.reset(seed=21)
     ob, _ = b.reset(seed=21)
     assert torch.equal(oa, ob)
     g = torch.Generator(device=hip_device).manual_seed(2)
+    present = 0
     for t in range(8):
         act = torch.randint(0, 3, (48,), device=hip_device, generator=g)
         ra = a.step(act)
         rb = b.step(act)
+        present += int((a.state["kind"] != 0).sum())
         for x, y in zip(ra[:4], rb[:4]):
             assert torch.equal(x, y), t
     for k in a.state.t:
         assert torch.equal(a.state[k], b.state[k]), k
+    assert int(a.live_counter) == present
+    # the next step's dispatch order: the envs in workgroup groups, heaviest group first
+    order = a._order[:48].cpu()
+    assert torch.equal(order.sort().values, torch.arange(48, dtype=torch.int32))
+    G = 2 if slots <= 32 else 1
+    assert torch.equal(order.view(-1, G), order.view(-1, G)[:, :1] + torch.arange(G, dtype=torch.int32))
+    w = (a.state["kind"] != 0).sum(1).cpu()[order.long()].view(-1, G).sum(1)
+    assert bool((w[:-1] >= w[1:]).all()), w
+
+
+@pytest.mark.parametrize("E", [64, 63])
+def test_dispatch_order_leaves_results_unchanged(E, hip_device):
+    """The step launch's dispatch order (workgroup slot -> env) changes only which workgroup runs an
+    env: every output and the state after the launch are the same for any permutation (63 envs: the
+    last workgroup holds one env)."""
+    env = VecIntersectionEnv({**ENV_JSON, "num_envs": E, "device": hip_device})
+    env.reset(seed=5)
+    g = torch.Generator(device=hip_device).manual_seed(4)
+    for _ in range(3):
+        env.step(torch.randint(0, 3, (E,), device=hip_device, generator=g))
+    snap, t0 = env.state.clone(), env.time.clone()
+    codes = env.action_type._codes(torch.randint(0, 3, (E,), device=hip_device, generator=g))
+    kc = env.observation_type.fused_cfg()  # one cfg (shuffle words included) for the three launches
+    runs = []
+    for order in (None, torch.randperm(E, generator=torch.Generator().manual_seed(1)).to(torch.int32).to(hip_device),
+                  torch.arange(E - 1, -1, -1, dtype=torch.int32, device=hip_device)):
+        env.state.copy_(snap)
+        env.time.copy_(t0)
+        outs = env.road.env_step(codes, 15, 1 / 15, kc, env.reward_cfg, env.time, 1.0, order)
+        runs.append(([o.clone() for o in outs], env.state.clone(), env.time.clone()))
+    for outs, st, t in runs[1:]:
+        for x, y in zip(outs, runs[0][0]):
+            assert torch.equal(x, y)
+        for k in st.t:
+            assert torch.equal(st[k], runs[0][1][k]), k
+        assert torch.equal(t, runs[0][2])
+    # the masked reset's warm-up launch with the masked envs packed first (ix_step_tail_'s spare_order)
+    mask = (torch.rand(E, generator=torch.Generator().manual_seed(2)) < 0.3).to(torch.uint8).to(hip_device)
+    on = torch.nonzero(mask).flatten().to(torch.int32)
+    packed = torch.full((E,), -1, dtype=torch.int32, device=hip_device)
+    packed[:on.numel()] = on.flip(0)
+    ent = torch.randint(0, 2 ** 31 - 1, (E, 2), dtype=torch.int32, generator=torch.Generator().manual_seed(3))
+    outs = []
+    for order in (None, packed):
+        env.state.copy_(snap)
+        ix_reset(env.state, env.network, env.params, env.ix, ent.to(hip_device), mask, order)
+        outs.append(env.state.clone())
+    for k in outs[0].t:
+        assert torch.equal(outs[0][k], outs[1][k]), k
 
 
 def test_deepcopy_forks_an_independent_env(hip_device):

@@ -53,7 +53,9 @@ class BatchedDiscreteMetaAction:
             torch._assert_async((lo >= 0) & (hi < len(self.actions)), "action out of range")
         if self._identity:
             return a.to(device=dev, dtype=torch.int32).reshape(-1)
-        return self._lut[a.to(dev).long().reshape(-1)]
+        # int32 / int64 indices index the table directly (one gather launch, no cast launch first)
+        a = a.to(dev).reshape(-1)
+        return self._lut[a if a.dtype in (torch.int32, torch.int64) else a.long()]
 
     def act(self, actions) -> None:
         """DiscreteMetaAction.act (action.py:259-260) for every env's ego."""

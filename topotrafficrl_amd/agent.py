@@ -172,14 +172,15 @@ class EgoAttentionPolicy:
 
     @torch.no_grad()
     def act(self, obs: torch.Tensor, t: int | None = None, epsilon: torch.Tensor | None = None,
-            step: torch.Tensor | None = None) -> torch.Tensor:
+            step: torch.Tensor | None = None, dtype: torch.dtype = torch.int64) -> torch.Tensor:
         """AbstractDQNAgent.act (dqn/abstract.py:65-83) for a batch: the exploration time is stepped
         first (step_time, :77-78), then EpsilonGreedy.update sets epsilon from it and the greedy
         action (np.argmax, first maximum), then the action is drawn from {a: epsilon / A +
         (1 - epsilon) [a == greedy]} (epsilon_greedy.py:32-48).  ``t``: the exploration time before
         this call (default: the policy's own counter).  ``epsilon`` / ``step`` (device scalars, float32 /
         int64) override the schedule and the draw counter: a captured graph refreshes them before
-        every replay.
+        every replay.  ``dtype``: the actions' index type (int64, or int32 -- the env's own, which
+        env.step takes without a cast launch).
 
         On a GPU the forward, argmax and draw are ONE launch (ttrl::ego_attention_act, Philox
         keyed on (seed, env, step)); elsewhere the torch forward with torch's generator."""
@@ -192,12 +193,12 @@ class EgoAttentionPolicy:
             act, _ = ops.T.ego_attention_act(obs.float(), net.packed_weights(), net.attention_layer.h,
                                              net.output_layer.predict.out_features,
                                              self.last_epsilon if epsilon is None else 0.0, self.seed, self.time,
-                                             epsilon, step)
-            return act
+                                             epsilon, step, int32_actions=dtype == torch.int32)
+            return act if act.dtype == dtype else act.to(dtype)
         epsilon = self.last_epsilon
         q = self.value_net(obs)
         greedy = q.argmax(dim=1)
         e = obs.shape[0]
         u = torch.rand(e, device=self.device, generator=self.gen)
         rnd = torch.randint(0, self.n_actions, (e,), device=self.device, generator=self.gen)
-        return torch.where(u < epsilon, rnd, greedy)
+        return torch.where(u < epsilon, rnd, greedy).to(dtype)

@@ -1831,7 +1831,19 @@ struct StepOut {
   float* comp;
   void* ego_speed;
   uint8_t* ego_crashed;
+  // road networks: workgroup slot -> env (a permutation of the envs, EPW consecutive entries per
+  // workgroup; null: slot order).  A dispatch order only: every env's result is independent of it.
+  const int32_t* order;
 };
+
+// The env of workgroup slot q: order[q] under a dispatch order, else q.  Slots past the batch (the
+// last workgroup of an odd batch) and -1 entries (a compacted masked launch's padding) map out of
+// range: no env.
+__device__ __forceinline__ int env_at(const int32_t* order, int q, int n_envs) {
+  if (!order || q >= n_envs) return q;
+  const int e = order[q];
+  return e < 0 ? n_envs : e;
+}
 
 // A per-vehicle value only its own thread reads: a register, or (L) its slot in an LDS view array.
 template <bool L, typename T> struct Own {
@@ -1880,12 +1892,14 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
   const int tid = threadIdx.x;
   const int le = tid / NS, i = tid % NS;
   const int N = st.n_veh, nl = R.n_lanes;
-  const int env = blockIdx.x * EPW + le;
+  // road networks take their envs in so.order (heaviest workgroups first, see ix_order_kernel)
+  const int32_t* ord = GR ? so.order : nullptr;
+  const int env = env_at(ord, blockIdx.x * EPW + le, st.n_envs);
   const bool env_on = env < st.n_envs && (!env_mask || env_mask[env]);  // masked-out envs: untouched
   if (env_mask) {  // a workgroup with no active env leaves at once (uniform: before any barrier)
     bool any = false;
     for (int q = 0; q < EPW; ++q) {
-      const int e = blockIdx.x * EPW + q;
+      const int e = env_at(ord, blockIdx.x * EPW + q, st.n_envs);
       any |= e < st.n_envs && env_mask[e];
     }
     if (!any) return;
@@ -2823,7 +2837,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
   int tid_r = tid;
   asm volatile("" : "+v"(tid_r));
   const int le = tid_r / NS, i = tid_r % NS;
-  const int env = blockIdx.x * EPW + le;
+  const int env = env_at(ord, blockIdx.x * EPW + le, st.n_envs);
   const bool env_on = env < st.n_envs && (!env_mask || env_mask[env]);
   const bool slot = env_on && i < N;
   const size_t k = (size_t)env * N + i;
@@ -4422,7 +4436,80 @@ struct IxTail {
   float* obs_out;
   const int32_t* ids_in;
   int32_t* ids_out;
+  unsigned long long* live;  // optional: += the vehicles present after the tail (the next step's)
+  int32_t* live_env;         // optional [E]: each env's vehicles present after the tail
 };
+
+// The env's present vehicles after the tail: added to *t.live (one atomic per env) and / or
+// written to t.live_env[env] (the next step's dispatch order, ix_order_kernel).
+template <typename T>
+__device__ __forceinline__ void ix_count_live(const ttrl_state_t& st, const IxTail& t, int env, int lane) {
+  __syncthreads();  // the tail's writes to kind (clear / spawn, or the copied rows) are the block's own
+  const int N = st.n_veh;
+  int c = 0;
+  for (int q0 = 0; q0 < N; q0 += 64)
+    c += __popcll(__ballot(q0 + lane < N && st.kind[(size_t)env * N + q0 + lane] != TTRL_ABSENT));
+  if (lane == 0) {
+    if (t.live) atomicAdd(t.live, (unsigned long long)c);
+    if (t.live_env) t.live_env[env] = c;
+  }
+}
+
+// The next step's dispatch orders (one workgroup, after the tail).
+// order (optional): the simulate launch's groups of G consecutive envs (its workgroups), heaviest
+// first by the group's live vehicles (a counting sort on 0..kmax; ties in any order).  The hardware
+// dispatches workgroups in slot order, so the long-running groups start first and the cheap ones
+// fill in behind them -- and behind the warm-up waves of the spare resets a step launch finds
+// resident (the slots they hold push the last-dispatched groups into a second round).  [0, E)
+// out, [E, 2E) the tail's live counts.
+// spare_order (optional): the spare rows to reset (spare_mask != 0) first, in any order, then -1:
+// the warm-up launch of those resets packs them G to a workgroup instead of spreading them over
+// ~one workgroup each, halving the warm-up waves that share the chip with the next step launch.
+// Results do not depend on either order (test_dispatch_order_leaves_results_unchanged,
+// test_overlapped_resets_equal_in_place_resets).
+__global__ void __launch_bounds__(1024) ix_order_kernel(int32_t* __restrict__ order, int E, int G, int kmax,
+                                                        const uint8_t* __restrict__ spare_mask,
+                                                        int32_t* __restrict__ spare_order, int n_spare) {
+  constexpr int NB = 320;  // buckets (kmax <= 256), 5 per lane of the scanning wave
+  __shared__ int h[NB];
+  __shared__ int n_on;
+  const int tid = threadIdx.x, P = E / G;
+  if (spare_order) {
+    if (tid == 0) n_on = 0;
+    __syncthreads();
+    for (int r = tid; r < n_spare; r += blockDim.x)
+      if (spare_mask[r]) spare_order[atomicAdd(&n_on, 1)] = r;
+    __syncthreads();
+    for (int r = n_on + tid; r < n_spare; r += blockDim.x) spare_order[r] = -1;
+  }
+  if (!order) return;
+  const int32_t* live = order + E;
+  auto key_of = [&](int p) {
+    int k = 0;
+    for (int q = 0; q < G; ++q) k += live[p * G + q];
+    return kmax - min(max(k, 0), kmax);  // descending
+  };
+  for (int b = tid; b < NB; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  for (int p = tid; p < P; p += blockDim.x) atomicAdd(&h[key_of(p)], 1);
+  __syncthreads();
+  if (tid < 64) {  // exclusive prefix over the buckets
+    int v[5], sum = 0;
+    for (int j = 0; j < 5; ++j) { v[j] = h[tid * 5 + j]; sum += v[j]; }
+    int inc = sum;
+    for (int d = 1; d < 64; d <<= 1) {
+      const int o = __shfl_up(inc, d);
+      if (tid >= d) inc += o;
+    }
+    int run = inc - sum;
+    for (int j = 0; j < 5; ++j) { h[tid * 5 + j] = run; run += v[j]; }
+  }
+  __syncthreads();
+  for (int p = tid; p < P; p += blockDim.x) {
+    const int pos = atomicAdd(&h[key_of(p)], 1);
+    for (int q = 0; q < G; ++q) order[pos * G + q] = p * G + q;
+  }
+}
 
 template <typename T>
 __global__ void __launch_bounds__(64) ix_step_tail_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P,
@@ -4443,6 +4530,7 @@ __global__ void __launch_bounds__(64) ix_step_tail_kernel(ttrl_state_t st, ttrl_
         for (int q = lane, W = V > 1 ? V - 1 : 1; q < W; q += 64) t.ids_out[(size_t)env * W + q] = t.ids_in[(size_t)env * W + q];
     }
     ix_clear_spawn_env<T>(st, R, P, C, env, lane);
+    if (t.live || t.live_env) ix_count_live<T>(st, t, env, lane);
     return;
   }
   const int p = t.par[env];
@@ -4457,6 +4545,7 @@ __global__ void __launch_bounds__(64) ix_step_tail_kernel(ttrl_state_t st, ttrl_
     t.par[env] = (uint8_t)(p ^ 1);
     t.time[env] = 0.0;
   }
+  if (t.live || t.live_env) ix_count_live<T>(st, t, env, lane);
   if (!t.obs) return;
   if (lane < R.n_lanes) s_lanes[lane] = make_lane<T>(R, lane);
   __syncthreads();  // the copied rows (and rng words) are the block's own writes: visible after the barrier
@@ -4689,7 +4778,7 @@ int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
                   int32_t frames, double dt, const ttrl_kin_cfg_t* obs_cfg, float* obs, int32_t* obs_ids,
                   const ttrl_reward_cfg_t* reward_cfg, double* time, double time_inc, float* reward,
                   uint8_t* terminated, uint8_t* truncated, float* components, void* ego_speed, uint8_t* ego_crashed,
-                  void* stream) {
+                  const int32_t* order, void* stream) {
   int rc = check_state(s, road);
   if (rc) return rc < 0 ? rc : TTRL_OK;
   if ((!obs_cfg) != (!obs) || (obs_cfg && check_kin_cfg(s, obs_cfg))) return TTRL_E_ARG;
@@ -4701,6 +4790,7 @@ int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
     so.rcfg = *reward_cfg; so.time = time; so.time_inc = time_inc; so.reward = reward; so.term = terminated;
     so.trunc = truncated; so.comp = components; so.ego_speed = ego_speed; so.ego_crashed = ego_crashed;
   }
+  so.order = order;
   return run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream, 0, nullptr, &so);
 }
 
@@ -4917,7 +5007,7 @@ static int check_ix(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttr
 
 int ttrl_ix_reset(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                   const ttrl_ix_cfg_t* cfg, const uint32_t* entropy, int32_t n_words, const uint8_t* mask,
-                  void* stream) {
+                  const int32_t* order, void* stream) {
   int rc = check_ix(s, road, p, cfg);
   if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!entropy || n_words < 1 || n_words > 64) return TTRL_E_ARG;
@@ -4932,7 +5022,10 @@ int ttrl_ix_reset(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
                        (const unsigned*)entropy, (int)n_words, mask);
   if ((rc = launch_status())) return rc;
   // _make_vehicles' warm-up: 3 s of Road.act / Road.step with no controlled vehicle yet
-  if ((rc = run_sim(s, road, p, nullptr, cfg->warmup_frames, cfg->warmup_dt, MODE_ACT | MODE_STEP, stream, 0, mask)))
+  StepOut wo{};
+  wo.order = order;  // the masked rows packed to the front (ix_order_kernel's spare_order)
+  if ((rc = run_sim(s, road, p, nullptr, cfg->warmup_frames, cfg->warmup_dt, MODE_ACT | MODE_STEP, stream, 0, mask,
+                    &wo)))
     return rc;
   if (s->dtype == TTRL_F64)
     hipLaunchKernelGGL(ix_finish_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg, mask);
@@ -4986,7 +5079,8 @@ int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
                       const uint8_t* truncated, uint8_t* spare_parity, uint32_t* entropy, uint32_t* spare_entropy,
                       int32_t n_words, double* time, uint8_t* done, uint8_t* spare_mask,
                       const ttrl_kin_cfg_t* obs_cfg, const float* obs_in, float* obs_out, const int32_t* obs_ids_in,
-                      int32_t* obs_ids_out, void* stream) {
+                      int32_t* obs_ids_out, int64_t* live_count, int32_t* order, int32_t* spare_order,
+                      void* stream) {
   int rc = check_ix(s, road, p, cfg);
   if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!spare || !terminated || !truncated || !spare_parity || !entropy || !spare_entropy || n_words < 1 ||
@@ -5008,6 +5102,11 @@ int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
   IxTail t{};
   t.spare = *spare; t.term = terminated; t.trunc = truncated; t.par = spare_parity; t.ent = entropy;
   t.spare_ent = spare_entropy; t.nw = n_words; t.time = time; t.done = done; t.spare_mask = spare_mask;
+  t.live = reinterpret_cast<unsigned long long*>(live_count);
+  // the dispatch order groups the envs of one simulate workgroup (EPW: 2 on 32 slots, else 1)
+  const int G = slots_for(s->n_veh) == 32 ? 2 : 1;
+  const bool ordered = order && s->n_envs % G == 0;
+  if (ordered) t.live_env = order + s->n_envs;
   if (obs_cfg) {
     t.kcfg = *obs_cfg; t.obs = true; t.obs_in = obs_in; t.obs_out = obs_out; t.ids_in = obs_ids_in;
     t.ids_out = obs_ids_out;
@@ -5017,6 +5116,9 @@ int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
     hipLaunchKernelGGL(ix_step_tail_kernel<double>, dim3(s->n_envs), dim3(64), 0, st, *s, *road, *p, *cfg, t);
   else
     hipLaunchKernelGGL(ix_step_tail_kernel<float>, dim3(s->n_envs), dim3(64), 0, st, *s, *road, *p, *cfg, t);
+  if (ordered || spare_order)
+    hipLaunchKernelGGL(ix_order_kernel, dim3(1), dim3(1024), 0, st, ordered ? order : nullptr, s->n_envs, G,
+                       G * s->n_veh, spare_mask, spare_order, 2 * s->n_envs);
   return launch_status();
 }
 

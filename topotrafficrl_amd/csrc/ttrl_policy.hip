@@ -139,7 +139,8 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 // any batch split or replay order gives each env the same action.  epsilon / step come from device
 // scalars when given (a captured HIP graph refreshes them between replays).
 struct Explore {
-  int64_t* act;            // [B] actions out; null: Q-values only
+  int64_t* act;            // [B] actions out (int64); both null: Q-values only
+  int32_t* act32;          // [B] the same actions as int32 (the env's action index type)
   float eps;
   const float* eps_dev;    // overrides eps when set
   long long step;
@@ -425,10 +426,10 @@ __global__ void __launch_bounds__(64, 2) ego_attention_kernel(const float* __res
 #pragma unroll
     for (int u = 0; u < EPWV; ++u) {
       if (b0 + u < B) Q[(b0 + u) * A + k] = a[u];
-      if (ex.act) s0s[u * 16 + k] = a[u];  // the ego scores' LDS is dead: the env's Q row for the argmax
+      if (ex.act || ex.act32) s0s[u * 16 + k] = a[u];  // the ego scores' LDS is dead: the env's Q row for the argmax
     }
   }
-  if (ex.act) {  // 4. epsilon-greedy: lane u acts for env b0 + u
+  if (ex.act || ex.act32) {  // 4. epsilon-greedy: lane u acts for env b0 + u
     __syncthreads();
     if (k < EPWV && b0 + k < B) {
       const float* qrow = s0s + k * 16;
@@ -445,7 +446,9 @@ __global__ void __launch_bounds__(64, 2) ego_attention_kernel(const float* __res
                                  make_uint2(ex.seed_lo, ex.seed_hi));
       const float uni = (float)(r.x >> 8) * 0x1p-24f;                       // U[0, 1)
       const int rnd = (int)(((unsigned long long)r.y * (unsigned)A) >> 32);  // U{0 .. A-1}
-      ex.act[b0 + k] = uni < eps ? rnd : best;
+      const int pick = uni < eps ? rnd : best;
+      if (ex.act) ex.act[b0 + k] = pick;
+      if (ex.act32) ex.act32[b0 + k] = pick;
     }
   }
   POL_T(8);
@@ -510,10 +513,11 @@ int ttrl_ego_attention_q(const float* obs, int32_t batch, int32_t n_entities, in
 int ttrl_ego_attention_act(const float* obs, int32_t batch, int32_t n_entities, int32_t n_features, int32_t heads,
                            const float* weights, int32_t n_actions, float epsilon, const float* epsilon_dev,
                            uint64_t seed, int64_t step, const int64_t* step_dev, float* q, int64_t* actions,
-                           void* stream) {
-  if (!actions || !(epsilon >= 0.0f && epsilon <= 1.0f)) return TTRL_E_ARG;
+                           int32_t* actions32, void* stream) {
+  if ((!actions && !actions32) || !(epsilon >= 0.0f && epsilon <= 1.0f)) return TTRL_E_ARG;
   Explore ex{};
-  ex.act = actions; ex.eps = epsilon; ex.eps_dev = epsilon_dev; ex.step = step; ex.step_dev = step_dev;
+  ex.act = actions; ex.act32 = actions32;
+  ex.eps = epsilon; ex.eps_dev = epsilon_dev; ex.step = step; ex.step_dev = step_dev;
   ex.seed_lo = (unsigned)seed; ex.seed_hi = (unsigned)(seed >> 32);
   return forward(obs, batch, n_entities, n_features, heads, weights, n_actions, q, ex, stream);
 }

@@ -155,7 +155,7 @@ env_step_outputs(const at::Tensor& x, const ttrl_kin_cfg_t* kc) {
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> env_step_(
     at::TensorList state, const at::Tensor& lanes, const at::Tensor& params, const c10::optional<at::Tensor>& actions,
     int64_t frames, double dt, const c10::optional<at::Tensor>& kin_cfg, const at::Tensor& reward_cfg,
-    const at::Tensor& time, double time_inc) {
+    const at::Tensor& time, double time_inc, const c10::optional<at::Tensor>& order) {
   check_hip(state[0]);
   ttrl_state_t s = state_of(state);
   const ttrl_kin_cfg_t* kc = kin_cfg && kin_cfg->defined() ? as_struct<ttrl_kin_cfg_t>(*kin_cfg, "kin_cfg") : nullptr;
@@ -163,6 +163,11 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
                   time.numel() == s.n_envs,
               "ttrl: time must be a contiguous float64 [n_envs] tensor on the state's device");
   at::Tensor a = dev_i32(actions, s.n_envs, state[0], "actions");
+  const bool od = order && order->defined();
+  if (od)  // a permutation of the envs (its first n_envs entries; ix_step_tail_'s buffer is 2 n_envs)
+    TORCH_CHECK(order->device() == state[0].device() && order->scalar_type() == at::kInt && order->is_contiguous() &&
+                    order->numel() >= s.n_envs,
+                "ttrl: order must be a contiguous int32 tensor of at least n_envs entries on the state's device");
   auto out = env_step_outputs(state[0], kc);
   auto& [obs, ids, rew, term, trunc, comp, speed, crashed] = out;
   ok(ttrl_env_step(&s, as_struct<ttrl_lane_table_t>(lanes, "lanes"), as_struct<ttrl_params_t>(params, "params"),
@@ -171,7 +176,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
                    as_struct<ttrl_reward_cfg_t>(reward_cfg, "reward_cfg"), time.data_ptr<double>(), time_inc,
                    rew.data_ptr<float>(), static_cast<uint8_t*>(term.data_ptr()),
                    static_cast<uint8_t*>(trunc.data_ptr()), comp.data_ptr<float>(), speed.data_ptr(),
-                   static_cast<uint8_t*>(crashed.data_ptr()), stream_of(state[0])),
+                   static_cast<uint8_t*>(crashed.data_ptr()), od ? order->data_ptr<int32_t>() : nullptr,
+                   stream_of(state[0])),
      "ttrl_env_step");
   return out;
 }
@@ -336,14 +342,21 @@ at::Tensor auto_reset_highway_(at::TensorList state, const at::Tensor& lanes, co
 }
 
 void ix_reset_(at::TensorList state, const at::Tensor& lanes, const at::Tensor& params, const at::Tensor& cfg,
-               const at::Tensor& entropy, const c10::optional<at::Tensor>& mask) {
+               const at::Tensor& entropy, const c10::optional<at::Tensor>& mask,
+               const c10::optional<at::Tensor>& order) {
   check_hip(state[0]);
   ttrl_state_t s = state_of(state);
   at::Tensor w = entropy_words(entropy, s, state[0]);
   at::Tensor m = dev_u8(mask, s.n_envs, state[0], "mask");
+  const bool od = order && order->defined();
+  if (od)  // every masked env once, then -1 (ix_step_tail_'s spare_order)
+    TORCH_CHECK(m.defined() && order->device() == state[0].device() && order->scalar_type() == at::kInt &&
+                    order->is_contiguous() && order->numel() == s.n_envs,
+                "ttrl: order must be a contiguous int32 [n_envs] tensor on the state's device, with a mask");
   ok(ttrl_ix_reset(&s, as_struct<ttrl_lane_table_t>(lanes, "lanes"), as_struct<ttrl_params_t>(params, "params"),
                    as_struct<ttrl_ix_cfg_t>(cfg, "cfg"), reinterpret_cast<const uint32_t*>(w.data_ptr()),
-                   static_cast<int32_t>(w.size(1)), static_cast<const uint8_t*>(ptr(m)), stream_of(state[0])),
+                   static_cast<int32_t>(w.size(1)), static_cast<const uint8_t*>(ptr(m)),
+                   od ? order->data_ptr<int32_t>() : nullptr, stream_of(state[0])),
      "ttrl_ix_reset");
 }
 
@@ -361,12 +374,14 @@ void ix_clear_spawn_(at::TensorList state, const at::Tensor& lanes, const at::Te
 // VecIntersectionEnv.step after env_step_: clear / spawn for the envs that go on, the auto-reset of
 // the finished ones from the spare scenes (2E rows) and their first observation.  Returns
 // (done [E] bool, spare_mask [2E] uint8: the spare rows to reset again, obs [E, V, F], ids).
+// live_count (optional int64 scalar): += the vehicles present after the tail.
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ix_step_tail_(
     at::TensorList state, const at::Tensor& lanes, const at::Tensor& params, const at::Tensor& cfg,
     at::TensorList spare, const at::Tensor& terminated, const at::Tensor& truncated, const at::Tensor& spare_parity,
     const at::Tensor& entropy, const at::Tensor& spare_entropy, const at::Tensor& time,
     const c10::optional<at::Tensor>& kin_cfg, const c10::optional<at::Tensor>& obs,
-    const c10::optional<at::Tensor>& ids) {
+    const c10::optional<at::Tensor>& ids, const c10::optional<at::Tensor>& live_count,
+    const c10::optional<at::Tensor>& order, const c10::optional<at::Tensor>& spare_order) {
   check_hip(state[0]);
   ttrl_state_t s = state_of(state), sp = state_of(spare);
   const auto& x = state[0];
@@ -403,6 +418,21 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ix_step_tail_(
     obs_out = at::empty({0}, opts(x, at::kFloat));
     ids_out = at::empty({0}, opts(x, at::kInt));
   }
+  const bool lc = live_count && live_count->defined();
+  if (lc)
+    TORCH_CHECK(live_count->device() == x.device() && live_count->scalar_type() == at::kLong &&
+                    live_count->numel() == 1,
+                "ttrl: live_count must be an int64 scalar on the state's device");
+  const bool od = order && order->defined();
+  if (od)
+    TORCH_CHECK(order->device() == x.device() && order->scalar_type() == at::kInt && order->is_contiguous() &&
+                    order->numel() == 2 * int64_t(s.n_envs),
+                "ttrl: order must be a contiguous int32 [2 * n_envs] tensor on the state's device");
+  const bool so = spare_order && spare_order->defined();
+  if (so)
+    TORCH_CHECK(spare_order->device() == x.device() && spare_order->scalar_type() == at::kInt &&
+                    spare_order->is_contiguous() && spare_order->numel() == 2 * int64_t(s.n_envs),
+                "ttrl: spare_order must be a contiguous int32 [2 * n_envs] tensor on the state's device");
   at::Tensor done = at::empty({s.n_envs}, opts(x, at::kBool));
   at::Tensor smask = at::empty({2 * s.n_envs}, opts(x, at::kByte));
   ok(ttrl_ix_step_tail(&s, as_struct<ttrl_lane_table_t>(lanes, "lanes"), as_struct<ttrl_params_t>(params, "params"),
@@ -413,7 +443,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ix_step_tail_(
                        time.data_ptr<double>(), static_cast<uint8_t*>(done.data_ptr()),
                        static_cast<uint8_t*>(smask.data_ptr()), kc, kc ? oin.data_ptr<float>() : nullptr,
                        kc ? obs_out.data_ptr<float>() : nullptr, kc ? iin.data_ptr<int32_t>() : nullptr,
-                       kc ? ids_out.data_ptr<int32_t>() : nullptr, stream_of(x)),
+                       kc ? ids_out.data_ptr<int32_t>() : nullptr, lc ? live_count->data_ptr<int64_t>() : nullptr,
+                       od ? order->data_ptr<int32_t>() : nullptr, so ? spare_order->data_ptr<int32_t>() : nullptr,
+                       stream_of(x)),
      "ttrl_ix_step_tail");
   return {done, smask, obs_out, ids_out};
 }
@@ -501,12 +533,14 @@ at::Tensor ego_attention_q(const at::Tensor& obs, const at::Tensor& weights, int
 }
 
 // EgoAttention Q-values and the epsilon-greedy actions in one launch (ttrl_ego_attention_act):
-// returns (actions [B] int64, q [B, A] float32).  epsilon_dev / step_dev: optional device scalars
-// (float32 / int64) that override epsilon / step inside the kernel (captured graphs).
+// returns (actions [B] int64, or int32 with int32_actions -- the env's action index type, so the
+// step takes them without a cast launch; q [B, A] float32).  epsilon_dev / step_dev: optional device
+// scalars (float32 / int64) that override epsilon / step inside the kernel (captured graphs).
 std::tuple<at::Tensor, at::Tensor> ego_attention_act(const at::Tensor& obs, const at::Tensor& weights, int64_t heads,
                                                      int64_t n_actions, double epsilon, int64_t seed, int64_t step,
                                                      const c10::optional<at::Tensor>& epsilon_dev,
-                                                     const c10::optional<at::Tensor>& step_dev) {
+                                                     const c10::optional<at::Tensor>& step_dev,
+                                                     bool int32_actions) {
   check_hip(obs);
   TORCH_CHECK(obs.dim() == 3 && obs.scalar_type() == at::kFloat, "ttrl: obs must be float32 [B, entities, features]");
   TORCH_CHECK(weights.device() == obs.device() && weights.scalar_type() == at::kFloat && weights.is_contiguous(),
@@ -526,12 +560,13 @@ std::tuple<at::Tensor, at::Tensor> ego_attention_act(const at::Tensor& obs, cons
   const int64_t n_w = ttrl_ego_attention_sizes(F, static_cast<int32_t>(n_actions), B, NE, &n_scratch);
   TORCH_CHECK(n_w > 0 && weights.numel() == n_w, "ttrl: packed weights need ", n_w, " floats, got ", weights.numel());
   at::Tensor q = at::empty({B, n_actions}, opts(x, at::kFloat));
-  at::Tensor act = at::empty({B}, opts(x, at::kLong));
+  at::Tensor act = at::empty({B}, opts(x, int32_actions ? at::kInt : at::kLong));
   ok(ttrl_ego_attention_act(x.data_ptr<float>(), B, NE, F, static_cast<int32_t>(heads), weights.data_ptr<float>(),
                             static_cast<int32_t>(n_actions), static_cast<float>(epsilon),
                             ed ? epsilon_dev->data_ptr<float>() : nullptr, static_cast<uint64_t>(seed), step,
                             sd ? step_dev->data_ptr<int64_t>() : nullptr, q.data_ptr<float>(),
-                            act.data_ptr<int64_t>(), stream_of(x)),
+                            int32_actions ? nullptr : act.data_ptr<int64_t>(),
+                            int32_actions ? act.data_ptr<int32_t>() : nullptr, stream_of(x)),
      "ttrl_ego_attention_act");
   return {act, q};
 }
@@ -552,7 +587,8 @@ void meta_none_meta(at::TensorList, const at::Tensor&, const at::Tensor&, const 
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor>
 meta_env_step(at::TensorList state, const at::Tensor&, const at::Tensor&, const c10::optional<at::Tensor>&, int64_t,
-              double, const c10::optional<at::Tensor>& kin_cfg, const at::Tensor&, const at::Tensor&, double) {
+              double, const c10::optional<at::Tensor>& kin_cfg, const at::Tensor&, const at::Tensor&, double,
+              const c10::optional<at::Tensor>&) {
   const ttrl_kin_cfg_t* kc = kin_cfg && kin_cfg->defined() ? as_struct<ttrl_kin_cfg_t>(*kin_cfg, "kin_cfg") : nullptr;
   return env_step_outputs(meta_x(state), kc);
 }
@@ -590,13 +626,16 @@ at::Tensor meta_lidar(at::TensorList state, const at::Tensor&, const at::Tensor&
 void meta_reset(at::TensorList, const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&) {}
 void meta_reset_seeded(at::TensorList, const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&,
                        const c10::optional<at::Tensor>&) {}
+void meta_ix_reset(at::TensorList, const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&,
+                   const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&) {}
 void meta_clear_spawn(at::TensorList, const at::Tensor&, const at::Tensor&, const at::Tensor&,
                       const c10::optional<at::Tensor>&) {}
 void meta_copy_envs(at::TensorList, at::TensorList, const at::Tensor&) {}
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> meta_ix_step_tail(
     at::TensorList state, const at::Tensor&, const at::Tensor&, const at::Tensor&, at::TensorList, const at::Tensor&,
     const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&,
-    const c10::optional<at::Tensor>& kin_cfg, const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&) {
+    const c10::optional<at::Tensor>& kin_cfg, const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&,
+    const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&) {
   const auto& x = meta_x(state);
   const int64_t E = x.size(0);
   at::Tensor o = at::empty({0}, opts(x, at::kFloat)), i = at::empty({0}, opts(x, at::kInt));
@@ -637,8 +676,9 @@ at::Tensor meta_ego_attention(const at::Tensor& obs, const at::Tensor&, int64_t,
 std::tuple<at::Tensor, at::Tensor> meta_ego_attention_act(const at::Tensor& obs, const at::Tensor&, int64_t,
                                                           int64_t n_actions, double, int64_t, int64_t,
                                                           const c10::optional<at::Tensor>&,
-                                                          const c10::optional<at::Tensor>&) {
-  return {at::empty({obs.size(0)}, opts(obs, at::kLong)), at::empty({obs.size(0), n_actions}, opts(obs, at::kFloat))};
+                                                          const c10::optional<at::Tensor>&, bool int32_actions) {
+  return {at::empty({obs.size(0)}, opts(obs, int32_actions ? at::kInt : at::kLong)),
+          at::empty({obs.size(0), n_actions}, opts(obs, at::kFloat))};
 }
 
 }  // namespace
@@ -649,7 +689,8 @@ TORCH_LIBRARY(ttrl, m) {
   m.def("road_step_(Tensor(a!)[] state, Tensor lanes, Tensor params, float dt) -> ()");
   m.def("meta_action_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor actions) -> ()");
   m.def("env_step_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor? actions, int frames, float dt, "
-        "Tensor? kin_cfg, Tensor reward_cfg, Tensor(b!) time, float time_inc) -> (Tensor obs, Tensor ids, "
+        "Tensor? kin_cfg, Tensor reward_cfg, Tensor(b!) time, float time_inc, Tensor? order=None) -> (Tensor obs, "
+        "Tensor ids, "
         "Tensor reward, Tensor terminated, Tensor truncated, Tensor components, Tensor ego_speed, Tensor ego_crashed)");
   m.def("neighbours(Tensor[] state, Tensor lanes, Tensor? query_lane) -> (Tensor front, Tensor rear)");
   // the np_random-shuffled observation (order_shuffled 2) advances state.rng: the state is mutated
@@ -664,13 +705,15 @@ TORCH_LIBRARY(ttrl, m) {
         "Tensor? mask) -> ()");
   m.def("auto_reset_highway_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor(b!) entropy, "
         "int episode_word, Tensor terminated, Tensor truncated, Tensor(c!) time) -> Tensor done");
-  m.def("ix_reset_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor entropy, Tensor? mask) -> ()");
+  m.def("ix_reset_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor entropy, Tensor? mask, "
+        "Tensor? order=None) -> ()");
   m.def("ix_clear_spawn_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor? mask) -> ()");
   m.def("copy_envs_(Tensor(a!)[] dst, Tensor[] src, Tensor mask) -> ()");
   m.def("ix_step_tail_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor[] spare, "
         "Tensor terminated, Tensor truncated, Tensor(b!) spare_parity, Tensor(c!) entropy, Tensor(d!) spare_entropy, "
-        "Tensor(e!) time, Tensor? kin_cfg, Tensor? obs, Tensor? ids) -> (Tensor done, Tensor spare_mask, "
-        "Tensor obs, Tensor ids)");
+        "Tensor(e!) time, Tensor? kin_cfg, Tensor? obs, Tensor? ids, Tensor(f!)? live_count=None, "
+        "Tensor(g!)? order=None, Tensor(h!)? spare_order=None) -> (Tensor done, Tensor spare_mask, Tensor obs, "
+        "Tensor ids)");
   m.def("rewards(Tensor[] state, Tensor lanes, Tensor cfg, Tensor time) -> (Tensor reward, Tensor terminated, "
         "Tensor truncated)");
   m.def("rewards_ex(Tensor[] state, Tensor lanes, Tensor cfg, Tensor time) -> (Tensor reward, Tensor terminated, "
@@ -679,7 +722,7 @@ TORCH_LIBRARY(ttrl, m) {
         "Tensor terminated, Tensor truncated, Tensor components, Tensor ego_speed, Tensor ego_crashed)");
   m.def("ego_attention_q(Tensor obs, Tensor weights, int heads, int n_actions) -> Tensor");
   m.def("ego_attention_act(Tensor obs, Tensor weights, int heads, int n_actions, float epsilon, int seed, int step, "
-        "Tensor? epsilon_dev=None, Tensor? step_dev=None) -> (Tensor, Tensor)");
+        "Tensor? epsilon_dev=None, Tensor? step_dev=None, bool int32_actions=False) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(ttrl, CUDA, m) {  // the HIP device of ROCm PyTorch
@@ -723,7 +766,7 @@ TORCH_LIBRARY_IMPL(ttrl, Meta, m) {
   m.impl("reset_highway_", &meta_reset);
   m.impl("reset_highway_seeded_", &meta_reset_seeded);
   m.impl("auto_reset_highway_", &meta_auto_reset);
-  m.impl("ix_reset_", &meta_reset_seeded);
+  m.impl("ix_reset_", &meta_ix_reset);
   m.impl("ix_clear_spawn_", &meta_clear_spawn);
   m.impl("copy_envs_", &meta_copy_envs);
   m.impl("ix_step_tail_", &meta_ix_step_tail);

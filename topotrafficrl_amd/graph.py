@@ -60,7 +60,7 @@ class StepGraph:
 
     def _body(self):
         if self.policy is not None:
-            a = self.policy.act(self.obs, epsilon=self.epsilon, step=self.step)
+            a = self.policy.act(self.obs, epsilon=self.epsilon, step=self.step, dtype=torch.int32)
             self.actions.copy_(a)
         obs, reward, terminated, truncated, _ = self.env.step(self.actions)
         self.obs.copy_(obs)

@@ -179,13 +179,15 @@ def _device_only(state: BatchState) -> None:
 
 
 def ix_reset(state: BatchState, network: RoadNetwork, params: _abi.Params, cfg: _abi.IxCfg,
-             entropy: torch.Tensor, mask: torch.Tensor | None = None) -> None:
-    """IntersectionEnv.reset on the device: env e replays ``default_rng(list(entropy[e]))``."""
+             entropy: torch.Tensor, mask: torch.Tensor | None = None, order: torch.Tensor | None = None) -> None:
+    """IntersectionEnv.reset on the device: env e replays ``default_rng(list(entropy[e]))``.
+    ``order``: the masked envs packed first, then -1 (the warm-up launch's dispatch order;
+    ix_step_tail_'s spare_order) -- the same scenes, in fewer warm-up workgroups."""
     if entropy.dim() != 2 or entropy.shape[0] != state.n_envs or entropy.dtype != torch.int32:
         raise ValueError("entropy must be an int32 [n_envs, n_words] tensor of uint32 words")
     _device_only(state)
     ops.T.ix_reset_(state.tensors(), ops.st(network.table), ops.st(params), ops.st(cfg),
-                    entropy.to(state.device), mask)
+                    entropy.to(state.device), mask, order)
 
 
 def ix_clear_spawn(state: BatchState, network: RoadNetwork, params: _abi.Params, cfg: _abi.IxCfg,
@@ -318,11 +320,18 @@ class VecIntersectionEnv:
         # a latency chain of about one step) go to the two side streams in turn, so the chains of
         # consecutive steps overlap instead of queueing behind each other.
         self._spare = None
+        # optional int64 device scalar: each overlapped step's tail adds the vehicles present after
+        # it (the next step's live vehicles) -- a live vehicle-step count with no launch of its own
+        self.live_counter: torch.Tensor | None = None
         if c["auto_reset"] and c["overlap_resets"]:
             E = self.num_envs
             self._spare = BatchState(2 * E, int(c["vehicle_slots"]), device=self.device, dtype=c["dtype"])
             self._spare_slot = (self._spare.rows(0, E), self._spare.rows(E, E))
             self._spare_par = torch.zeros(E, dtype=torch.uint8, device=self.device)
+            # the step launch's dispatch order (ix_step_tail_ rewrites it after every step: workgroups
+            # heaviest first, see ix_order_kernel) and its scratch; any permutation is valid
+            self._order = torch.cat([torch.arange(E, dtype=torch.int32, device=self.device),
+                                     torch.zeros(E, dtype=torch.int32, device=self.device)])
             self._sides = tuple(torch.cuda.Stream(self.device) for _ in range(max(1, int(c["reset_streams"]))))
             self._side_i = 0
             self._spare_ready = self._spare_prev = torch.cuda.Event()
@@ -391,7 +400,7 @@ class VecIntersectionEnv:
         for side in self._sides:
             main.wait_stream(side)
 
-    def _prepare_spares(self, mask: torch.Tensor | None) -> None:
+    def _prepare_spares(self, mask: torch.Tensor | None, order: torch.Tensor | None = None) -> None:
         """Reset the spare scenes of ``mask`` ([2E]; all: None) on the next side stream, after the
         main stream's work so far (the swap that consumed them).  The side stream reads the seed
         words and episode counters of the masked rows only; the main stream writes a row's counter
@@ -402,11 +411,12 @@ class VecIntersectionEnv:
         self._side_i = (self._side_i + 1) % len(self._sides)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            ix_reset(self._spare, self.network, self.params, self.ix, self._spare_ent, mask)
+            ix_reset(self._spare, self.network, self.params, self.ix, self._spare_ent, mask, order)
             ev = torch.cuda.Event()
             ev.record(side)
-        if mask is not None:
-            mask.record_stream(side)
+        for t in (mask, order):
+            if t is not None:
+                t.record_stream(side)
         self._spare_prev, self._spare_ready = self._spare_ready, ev
 
     def step(self, action):
@@ -444,7 +454,7 @@ class VecIntersectionEnv:
         self.steps += frames
         obs, ids, *outs = self.road.env_step(codes, frames, 1 / self.config["simulation_frequency"],
                                              ot.fused_cfg() if kin else None, self.reward_cfg, self.time,
-                                             1 / self.config["policy_frequency"])
+                                             1 / self.config["policy_frequency"], self._order)
         reward, terminated, truncated = _keep_tail(self, outs)
         if not kin:
             obs = ot.observe()
@@ -456,12 +466,13 @@ class VecIntersectionEnv:
         # (vehicle_slots > 64) take the masked observation launch instead, which draws the same
         # shuffles from the same generators (test_overlapped_resets_equal_in_place_resets[96])
         fused_obs = kin and self.state.n_veh <= 64
+        sorder = torch.empty(2 * self.num_envs, dtype=torch.int32, device=self.device)  # fresh: read on a side stream
         done, smask, obs2, ids2 = ops.T.ix_step_tail_(
             self.state.tensors(), ops.st(self.network.table), ops.st(self.params), ops.st(self.ix),
             self._spare.tensors(), terminated, truncated, self._spare_par, self._entropy, self._spare_ent, self.time,
             ops.kin_cfg_tensor(ot.fused_cfg()) if fused_obs else None, obs if fused_obs else None,
-            ids if fused_obs else None)
-        self._prepare_spares(smask)
+            ids if fused_obs else None, self.live_counter, self._order, sorder)
+        self._prepare_spares(smask, sorder)
         info["final_observation"], info["final_mask"] = obs, done
         if fused_obs:
             ot.fused_result(obs2, ids2)
@@ -546,6 +557,7 @@ class VecIntersectionEnv:
             new._spare_slot = (new._spare.rows(0, self.num_envs), new._spare.rows(self.num_envs, self.num_envs))
             new._spare_ent = self._spare_ent.clone()
             new._spare_par = self._spare_par.clone()
+            new._order = self._order.clone()
             new._sides = tuple(torch.cuda.Stream(self.device) for _ in self._sides)
             new._side_i = 0
             new._spare_ready = torch.cuda.Event()
