@@ -1831,9 +1831,13 @@ struct StepOut {
   float* comp;
   void* ego_speed;
   uint8_t* ego_crashed;
-  // road networks: workgroup slot -> env (a permutation of the envs, EPW consecutive entries per
-  // workgroup; null: slot order).  A dispatch order only: every env's result is independent of it.
+  // workgroup slot -> env (a permutation of the envs, EPW consecutive entries per workgroup; -1
+  // entries: none; null: slot order).  A dispatch order only: every env's result is independent
+  // of it.
   const int32_t* order;
+  // optional [n_envs]: each env's wall-clock ticks (100 MHz) in this launch, lane 0 of the env
+  // (order_by_cost_kernel turns them into the next launch's order)
+  uint32_t* cost;
 };
 
 // The env of workgroup slot q: order[q] under a dispatch order, else q.  Slots past the batch (the
@@ -1893,7 +1897,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
   const int le = tid / NS, i = tid % NS;
   const int N = st.n_veh, nl = R.n_lanes;
   // road networks take their envs in so.order (heaviest workgroups first, see ix_order_kernel)
-  const int32_t* ord = GR ? so.order : nullptr;
+  const int32_t* ord = so.order;
+  const unsigned long long t_cost0 = so.cost ? wall_clock64() : 0ull;
   const int env = env_at(ord, blockIdx.x * EPW + le, st.n_envs);
   const bool env_on = env < st.n_envs && (!env_mask || env_mask[env]);  // masked-out envs: untouched
   if (env_mask) {  // a workgroup with no active env leaves at once (uniform: before any barrier)
@@ -2904,6 +2909,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
       }
     }
   }
+  if (so.cost && i == 0 && env_on) so.cost[env] = (uint32_t)(wall_clock64() - t_cost0);
   }
   PH_FLUSH
 }
@@ -4455,41 +4461,13 @@ __device__ __forceinline__ void ix_count_live(const ttrl_state_t& st, const IxTa
   }
 }
 
-// The next step's dispatch orders (one workgroup, after the tail).
-// order (optional): the simulate launch's groups of G consecutive envs (its workgroups), heaviest
-// first by the group's live vehicles (a counting sort on 0..kmax; ties in any order).  The hardware
-// dispatches workgroups in slot order, so the long-running groups start first and the cheap ones
-// fill in behind them -- and behind the warm-up waves of the spare resets a step launch finds
-// resident (the slots they hold push the last-dispatched groups into a second round).  [0, E)
-// out, [E, 2E) the tail's live counts.
-// spare_order (optional): the spare rows to reset (spare_mask != 0) first, in any order, then -1:
-// the warm-up launch of those resets packs them G to a workgroup instead of spreading them over
-// ~one workgroup each, halving the warm-up waves that share the chip with the next step launch.
-// Results do not depend on either order (test_dispatch_order_leaves_results_unchanged,
-// test_overlapped_resets_equal_in_place_resets).
-__global__ void __launch_bounds__(1024) ix_order_kernel(int32_t* __restrict__ order, int E, int G, int kmax,
-                                                        const uint8_t* __restrict__ spare_mask,
-                                                        int32_t* __restrict__ spare_order, int n_spare) {
-  constexpr int NB = 320;  // buckets (kmax <= 256), 5 per lane of the scanning wave
-  __shared__ int h[NB];
-  __shared__ int n_on;
-  const int tid = threadIdx.x, P = E / G;
-  if (spare_order) {
-    if (tid == 0) n_on = 0;
-    __syncthreads();
-    for (int r = tid; r < n_spare; r += blockDim.x)
-      if (spare_mask[r]) spare_order[atomicAdd(&n_on, 1)] = r;
-    __syncthreads();
-    for (int r = n_on + tid; r < n_spare; r += blockDim.x) spare_order[r] = -1;
-  }
-  if (!order) return;
-  const int32_t* live = order + E;
-  auto key_of = [&](int p) {
-    int k = 0;
-    for (int q = 0; q < G; ++q) k += live[p * G + q];
-    return kmax - min(max(k, 0), kmax);  // descending
-  };
-  for (int b = tid; b < NB; b += blockDim.x) h[b] = 0;
+// Counting sort of the P groups of G consecutive envs by key_of(p) in [0, NB) ascending (ties in
+// any order), into order[0, P * G): one workgroup.  h: NB ints of LDS.
+constexpr int ORDER_BUCKETS = 320;  // 5 per lane of the scanning wave
+template <typename KeyFn>
+__device__ void sort_groups(int32_t* __restrict__ order, int P, int G, int* h, KeyFn key_of) {
+  const int tid = threadIdx.x;
+  for (int b = tid; b < ORDER_BUCKETS; b += blockDim.x) h[b] = 0;
   __syncthreads();
   for (int p = tid; p < P; p += blockDim.x) atomicAdd(&h[key_of(p)], 1);
   __syncthreads();
@@ -4509,6 +4487,66 @@ __global__ void __launch_bounds__(1024) ix_order_kernel(int32_t* __restrict__ or
     const int pos = atomicAdd(&h[key_of(p)], 1);
     for (int q = 0; q < G; ++q) order[pos * G + q] = p * G + q;
   }
+}
+
+// The next step's dispatch orders (one workgroup, after the tail).
+// order (optional): the simulate launch's groups of G consecutive envs (its workgroups), heaviest
+// first by the group's live vehicles (kmax <= 256).  The hardware dispatches workgroups in slot
+// order, so the long-running groups start first and the cheap ones fill in behind them -- and
+// behind the warm-up waves of the spare resets a step launch finds resident (the slots they hold
+// push the last-dispatched groups into a second round).  [0, E) out, [E, 2E) the tail's live
+// counts.
+// spare_order (optional): the spare rows to reset (spare_mask != 0) first, in any order, then -1:
+// the warm-up launch of those resets packs them G to a workgroup instead of spreading them over
+// ~one workgroup each, halving the warm-up waves that share the chip with the next step launch.
+// Results do not depend on either order (test_dispatch_order_leaves_results_unchanged,
+// test_overlapped_resets_equal_in_place_resets).
+__global__ void __launch_bounds__(1024) ix_order_kernel(int32_t* __restrict__ order, int E, int G, int kmax,
+                                                        const uint8_t* __restrict__ spare_mask,
+                                                        int32_t* __restrict__ spare_order, int n_spare) {
+  __shared__ int h[ORDER_BUCKETS];
+  __shared__ int n_on;
+  const int tid = threadIdx.x;
+  if (spare_order) {
+    if (tid == 0) n_on = 0;
+    __syncthreads();
+    for (int r = tid; r < n_spare; r += blockDim.x)
+      if (spare_mask[r]) spare_order[atomicAdd(&n_on, 1)] = r;
+    __syncthreads();
+    for (int r = n_on + tid; r < n_spare; r += blockDim.x) spare_order[r] = -1;
+  }
+  if (!order) return;
+  const int32_t* live = order + E;
+  sort_groups(order, E / G, G, h, [&](int p) {
+    int k = 0;
+    for (int q = 0; q < G; ++q) k += live[p * G + q];
+    return kmax - min(max(k, 0), kmax);  // descending
+  });
+}
+
+// The next launch's dispatch order from this launch's measured cost (ttrl_env_step with cost):
+// the groups of G envs (the simulate workgroups) by their wall-clock ticks, longest first, in
+// ORDER_BUCKETS buckets of the largest.  A pile-up env stays slow from one step to the next, so the
+// long waves start first and -- where a launch needs more than one round of the chip's wave slots
+// -- the short ones fill in behind them.
+__global__ void __launch_bounds__(1024) order_by_cost_kernel(const uint32_t* __restrict__ cost, int E, int G,
+                                                             int32_t* __restrict__ order) {
+  __shared__ int h[ORDER_BUCKETS];
+  __shared__ unsigned s_max;
+  const int tid = threadIdx.x, P = E / G;
+  if (tid == 0) s_max = 1u;
+  __syncthreads();
+  unsigned m = 0;
+  for (int e = tid; e < E; e += blockDim.x) m = max(m, cost[e]);
+  atomicMax(&s_max, m);
+  __syncthreads();
+  const unsigned long long top = s_max;
+  sort_groups(order, P, G, h, [&](int p) {
+    unsigned c = 0;
+    for (int q = 0; q < G; ++q) c = max(c, cost[p * G + q]);
+    const int k = (int)((unsigned long long)c * (ORDER_BUCKETS - 1) / top);
+    return ORDER_BUCKETS - 1 - min(k, ORDER_BUCKETS - 1);  // descending
+  });
 }
 
 template <typename T>
@@ -4778,12 +4816,13 @@ int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
                   int32_t frames, double dt, const ttrl_kin_cfg_t* obs_cfg, float* obs, int32_t* obs_ids,
                   const ttrl_reward_cfg_t* reward_cfg, double* time, double time_inc, float* reward,
                   uint8_t* terminated, uint8_t* truncated, float* components, void* ego_speed, uint8_t* ego_crashed,
-                  const int32_t* order, void* stream) {
+                  int32_t* order, uint32_t* cost, void* stream) {
   int rc = check_state(s, road);
   if (rc) return rc < 0 ? rc : TTRL_OK;
   if ((!obs_cfg) != (!obs) || (obs_cfg && check_kin_cfg(s, obs_cfg))) return TTRL_E_ARG;
   if (reward_cfg && (!time || !reward || !terminated || !truncated || (!ego_speed) != (!ego_crashed)))
     return TTRL_E_ARG;
+  if (cost && !order) return TTRL_E_ARG;
   StepOut so{};
   if (obs_cfg) { so.kcfg = *obs_cfg; so.obs = obs; so.ids = obs_ids; }
   if (reward_cfg) {
@@ -4791,7 +4830,13 @@ int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
     so.trunc = truncated; so.comp = components; so.ego_speed = ego_speed; so.ego_crashed = ego_crashed;
   }
   so.order = order;
-  return run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream, 0, nullptr, &so);
+  so.cost = cost;
+  if ((rc = run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream, 0, nullptr, &so)))
+    return rc;
+  const int G = slots_for(s->n_veh) == 32 ? 2 : 1;  // the simulate instance's envs per workgroup
+  if (cost && s->n_envs % G == 0)  // the next launch's order, from this one's measured cost
+    hipLaunchKernelGGL(order_by_cost_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, cost, s->n_envs, G, order);
+  return launch_status();
 }
 
 /* Diagnostic only (not in include/): the simulate kernel's LDS view bytes per workgroup. */
