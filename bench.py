@@ -262,8 +262,6 @@ def main():
                     help="highway envs restart on termination inside env.step (the RL rollout mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--dispatch-order", action="store_true",
-                    help="highway configs: dispatch the step launch's envs longest-first by the previous step's cost")
     ap.add_argument("--graph", action="store_true",
                     help="replay each step as one captured HIP graph (policy + env.step for config 5)")
     args = ap.parse_args()
@@ -318,8 +316,7 @@ def main():
                                   "dtype": args.dtype, "env_id_offset": offset, "auto_reset": True})
     else:
         env = VecHighwayEnv({"num_envs": E, "vehicles_count": N, "observation": C["obs"], "device": str(dev),
-                             "dtype": args.dtype, "env_id_offset": offset, "auto_reset": bool(args.auto_reset),
-                             "dispatch_order": bool(args.dispatch_order)})
+                             "dtype": args.dtype, "env_id_offset": offset, "auto_reset": bool(args.auto_reset)})
     policy = None
     if args.config == 5:
         from topotrafficrl_amd.agent import EgoAttentionPolicy
@@ -460,8 +457,7 @@ def main():
         "config": {"workload": C["name"], "envs_per_gpu": E, "global_envs": global_envs, "vehicles_per_env": N,
                    "frames_per_step": 15,
                    "observation": C["obs"]["type"], "parallelism": f"env-sharded x{world}, no collective on the step",
-                   "hip_graph": bool(args.graph), "auto_reset": bool(args.auto_reset or ix),
-                   "dispatch_order": "live vehicles" if ix else ("measured cost" if args.dispatch_order else "slot")},
+                   "hip_graph": bool(args.graph), "auto_reset": bool(args.auto_reset or ix)},
         # the HBM roofline of the fused launch: algorithmic bytes (state read + written once, the
         # observation written once) over the launch time measured here with HIP events
         "roofline": dict(bound="hbm", **hbm, kernel=kernel, kernel_ms=kern_ms, alg_bytes_per_launch=alg_bytes,

@@ -287,17 +287,15 @@ int ttrl_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road,
  * calls, on every road (the intersection's network with routes included, where an
  * order_shuffled == 2 observation draws from state.rng as ttrl_observe_kinematics does).
  * order (optional, device [n_envs] int32): a permutation of the envs, the order in which the
- * launch's workgroups take them (heaviest first: as ttrl_ix_step_tail writes it from the live
- * vehicles, or as this call writes it with cost); a dispatch order only -- every output is the
- * same with or without it.  cost (optional, device [n_envs] uint32, needs order): the launch
- * measures each env's wall-clock ticks there and then rewrites order for the next call, longest
- * first. */
+ * launch's workgroups take them on a road network (as ttrl_ix_step_tail writes it: heaviest
+ * first); a dispatch order only -- every output is the same with or without it; other roads
+ * ignore it. */
 int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                   const int32_t* actions, int32_t frames, double dt,
                   const ttrl_kin_cfg_t* obs_cfg, float* obs, int32_t* obs_ids,
                   const ttrl_reward_cfg_t* reward_cfg, double* time, double time_inc,
                   float* reward, uint8_t* terminated, uint8_t* truncated, float* components,
-                  void* ego_speed, uint8_t* ego_crashed, int32_t* order, uint32_t* cost, void* stream);
+                  void* ego_speed, uint8_t* ego_crashed, const int32_t* order, void* stream);
 /* Road.neighbour_vehicles(v, lane) for every vehicle; query_lane [E*N] int32
  * (-1 = the vehicle's own lane).  front/rear [E*N] int32 vehicle index or -1. */
 int ttrl_neighbours(const ttrl_state_t* s, const ttrl_lane_table_t* road,
@@ -379,13 +377,10 @@ int ttrl_ego_attention_act(const float* obs, int32_t batch, int32_t n_entities, 
  * default_rng(SeedSequence(entropy[e][0..n_words-1])) into state.rng, then _make_vehicles:
  * initial spawns, warmup_frames of Road.act/step (RegulatedRoad), the challenger, the ego
  * MDPVehicle (appended after the traffic) and the removal of vehicles near it.  Requires the
- * network fields and state.rng.  Vehicles beyond n_veh slots are dropped (draws still made).
- * order (optional, device [n_envs] int32): the warm-up launch's dispatch order -- every masked
- * env once, in any order, then -1 padding (ttrl_ix_step_tail's spare_order), so the masked envs
- * share workgroups; results are the same without it. */
+ * network fields and state.rng.  Vehicles beyond n_veh slots are dropped (draws still made). */
 int ttrl_ix_reset(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                   const ttrl_ix_cfg_t* cfg, const uint32_t* entropy, int32_t n_words, const uint8_t* mask,
-                  const int32_t* order, void* stream);
+                  void* stream);
 /* Copy every row of the envs with mask[e] != 0 (all fields, per-env route / regulation / rng
  * words included) from src to dst, which have the same shape and dtype: swapping in scenes reset
  * ahead of time (the intersection's double-buffered auto-reset). */
@@ -409,16 +404,13 @@ int ttrl_ix_clear_spawn(const ttrl_state_t* s, const ttrl_lane_table_t* road, co
  * first n_envs initialised to any permutation of the envs): receives in [0, n_envs) the next
  * ttrl_env_step's dispatch order -- the envs grouped as that launch's workgroups hold them,
  * groups sorted by their live vehicles, heaviest first; [n_envs, 2 n_envs) is its scratch.
- * spare_order (optional, device [2 n_envs] int32): receives the spare rows flagged in spare_mask,
- * in any order, then -1 padding -- ttrl_ix_reset's order for resetting exactly those rows.
  * Reference: intersection_env.py:135-139, :350-362, :320-348; abstract.py:188-214. */
 int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                       const ttrl_ix_cfg_t* cfg, const ttrl_state_t* spare, const uint8_t* terminated,
                       const uint8_t* truncated, uint8_t* spare_parity, uint32_t* entropy, uint32_t* spare_entropy,
                       int32_t n_words, double* time, uint8_t* done, uint8_t* spare_mask,
                       const ttrl_kin_cfg_t* obs_cfg, const float* obs_in, float* obs_out, const int32_t* obs_ids_in,
-                      int32_t* obs_ids_out, int64_t* live_count, int32_t* order, int32_t* spare_order,
-                      void* stream);
+                      int32_t* obs_ids_out, int64_t* live_count, int32_t* order, void* stream);
 /* Per-env reward [E] float32, terminated/truncated [E] uint8, given time [E] float64, for the
  * env's controlled vehicle (its first TTRL_MDP slot). */
 int ttrl_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* road,

@@ -74,8 +74,7 @@ def test_argument_errors_need_no_device():
     net = intersection_network()
     cfg = ix_cfg(net, VecIntersectionEnv.default_config(), p)
     words = (C.c_uint32 * 4)(1, 2, 3, 4)
-    assert lib.ttrl_ix_reset(C.byref(s), C.byref(net.table), C.byref(p), C.byref(cfg), words, 1, None, None,
-                             None) == -1
+    assert lib.ttrl_ix_reset(C.byref(s), C.byref(net.table), C.byref(p), C.byref(cfg), words, 1, None, None) == -1
     assert lib.ttrl_ix_clear_spawn(C.byref(s), C.byref(net.table), C.byref(p), C.byref(cfg), None, None) == -1
     kin = _abi.kin_cfg(order="shuffled", shuffle_rng="np_random")
     assert lib.ttrl_observe_kinematics_masked(C.byref(s), C.byref(lanes), C.byref(p), C.byref(kin), None, None,

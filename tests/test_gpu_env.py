@@ -55,31 +55,6 @@ def test_env_step_matches_oracle(road, hip_device):
             assert np.allclose(info["rewards"][name].cpu().numpy(), ref_c[:, i], atol=1e-6), name
 
 
-@pytest.mark.parametrize("N,dtype", [(64, "f64"), (32, "f64"), (40, "f32")])
-def test_dispatch_order_by_cost_leaves_the_rollout_unchanged(N, dtype, hip_device):
-    """dispatch_order: each step launch measures its envs' cost and writes the next launch's order
-    (longest first, EPW-env groups kept together); the rollout is bit-identical to slot order."""
-    a, b = make(64, N, dtype=dtype, dispatch_order=True), make(64, N, dtype=dtype)
-    oa, _ = a.reset(seed=3)
-    ob, _ = b.reset(seed=3)
-    g = torch.Generator(device=hip_device).manual_seed(5)
-    for t in range(4):
-        act = torch.randint(0, 5, (64,), device=hip_device, generator=g)
-        ra, rb = a.step(act), b.step(act)
-        for x, y in zip(ra[:4], rb[:4]):
-            assert torch.equal(x, y), t
-    for k in a.state.t:
-        assert torch.equal(a.state[k], b.state[k]), k
-    order = a._order.cpu()
-    assert torch.equal(order.sort().values, torch.arange(64, dtype=torch.int32))
-    G = 2 if N <= 32 else 1
-    assert torch.equal(order.view(-1, G), order.view(-1, G)[:, :1] + torch.arange(G, dtype=torch.int32))
-    cost = a._cost.cpu()[order.long()].view(-1, G).max(1).values
-    assert bool((cost > 0).all())
-    # buckets of 1/319 of the largest: the order is non-increasing up to that quantisation
-    assert bool((cost[1:] <= cost[:-1] + cost.max() // 319 + 1).all())
-
-
 def test_truncation_and_auto_reset(hip_device):
     env = make(8, 20, duration=3, auto_reset=True)
     env.reset(seed=1)

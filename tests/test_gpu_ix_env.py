@@ -289,19 +289,6 @@ def test_dispatch_order_leaves_results_unchanged(E, hip_device):
         for k in st.t:
             assert torch.equal(st[k], runs[0][1][k]), k
         assert torch.equal(t, runs[0][2])
-    # the masked reset's warm-up launch with the masked envs packed first (ix_step_tail_'s spare_order)
-    mask = (torch.rand(E, generator=torch.Generator().manual_seed(2)) < 0.3).to(torch.uint8).to(hip_device)
-    on = torch.nonzero(mask).flatten().to(torch.int32)
-    packed = torch.full((E,), -1, dtype=torch.int32, device=hip_device)
-    packed[:on.numel()] = on.flip(0)
-    ent = torch.randint(0, 2 ** 31 - 1, (E, 2), dtype=torch.int32, generator=torch.Generator().manual_seed(3))
-    outs = []
-    for order in (None, packed):
-        env.state.copy_(snap)
-        ix_reset(env.state, env.network, env.params, env.ix, ent.to(hip_device), mask, order)
-        outs.append(env.state.clone())
-    for k in outs[0].t:
-        assert torch.equal(outs[0][k], outs[1][k]), k
 
 
 def test_deepcopy_forks_an_independent_env(hip_device):

@@ -24,7 +24,7 @@ _SIGS = {
     "ttrl_road_step": ([_P, _P, _P, C.c_double, _P], C.c_int),
     "ttrl_simulate": ([_P, _P, _P, _P, C.c_int32, C.c_double, _P], C.c_int),
     "ttrl_env_step": ([_P, _P, _P, _P, C.c_int32, C.c_double, _P, _P, _P, _P, _P, C.c_double, _P, _P, _P, _P, _P,
-                       _P, _P, _P, _P], C.c_int),
+                       _P, _P, _P], C.c_int),
     "ttrl_neighbours": ([_P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_observe_kinematics": ([_P, _P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_observe_kinematics_masked": ([_P, _P, _P, _P, _P, _P, _P, _P], C.c_int),
@@ -38,10 +38,10 @@ _SIGS = {
     "ttrl_rewards": ([_P, _P, _P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_rewards_ex": ([_P, _P, _P, _P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_rewards_step": ([_P, _P, _P, _P, C.c_double, _P, _P, _P, _P, _P, _P, _P], C.c_int),
-    "ttrl_ix_reset": ([_P, _P, _P, _P, _P, C.c_int32, _P, _P, _P], C.c_int),
+    "ttrl_ix_reset": ([_P, _P, _P, _P, _P, C.c_int32, _P, _P], C.c_int),
     "ttrl_ix_clear_spawn": ([_P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_ix_step_tail": ([_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, C.c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                           _P, _P],
+                           _P],
                           C.c_int),
     "ttrl_copy_envs": ([_P, _P, _P, _P], C.c_int),
     "ttrl_ego_attention_sizes": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P], C.c_int64),

@@ -1835,18 +1835,12 @@ struct StepOut {
   // entries: none; null: slot order).  A dispatch order only: every env's result is independent
   // of it.
   const int32_t* order;
-  // optional [n_envs]: each env's wall-clock ticks (100 MHz) in this launch, lane 0 of the env
-  // (order_by_cost_kernel turns them into the next launch's order)
-  uint32_t* cost;
 };
 
-// The env of workgroup slot q: order[q] under a dispatch order, else q.  Slots past the batch (the
-// last workgroup of an odd batch) and -1 entries (a compacted masked launch's padding) map out of
-// range: no env.
+// The env of workgroup slot q: order[q] under a dispatch order, else q (slots past the batch stay
+// out of range: the last workgroup of an odd batch).
 __device__ __forceinline__ int env_at(const int32_t* order, int q, int n_envs) {
-  if (!order || q >= n_envs) return q;
-  const int e = order[q];
-  return e < 0 ? n_envs : e;
+  return order && q < n_envs ? order[q] : q;
 }
 
 // A per-vehicle value only its own thread reads: a register, or (L) its slot in an LDS view array.
@@ -1897,8 +1891,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
   const int le = tid / NS, i = tid % NS;
   const int N = st.n_veh, nl = R.n_lanes;
   // road networks take their envs in so.order (heaviest workgroups first, see ix_order_kernel)
-  const int32_t* ord = so.order;
-  const unsigned long long t_cost0 = so.cost ? wall_clock64() : 0ull;
+  const int32_t* ord = GR ? so.order : nullptr;
   const int env = env_at(ord, blockIdx.x * EPW + le, st.n_envs);
   const bool env_on = env < st.n_envs && (!env_mask || env_mask[env]);  // masked-out envs: untouched
   if (env_mask) {  // a workgroup with no active env leaves at once (uniform: before any barrier)
@@ -2909,7 +2902,6 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
       }
     }
   }
-  if (so.cost && i == 0 && env_on) so.cost[env] = (uint32_t)(wall_clock64() - t_cost0);
   }
   PH_FLUSH
 }
@@ -4489,63 +4481,20 @@ __device__ void sort_groups(int32_t* __restrict__ order, int P, int G, int* h, K
   }
 }
 
-// The next step's dispatch orders (one workgroup, after the tail).
-// order (optional): the simulate launch's groups of G consecutive envs (its workgroups), heaviest
-// first by the group's live vehicles (kmax <= 256).  The hardware dispatches workgroups in slot
-// order, so the long-running groups start first and the cheap ones fill in behind them -- and
-// behind the warm-up waves of the spare resets a step launch finds resident (the slots they hold
-// push the last-dispatched groups into a second round).  [0, E) out, [E, 2E) the tail's live
-// counts.
-// spare_order (optional): the spare rows to reset (spare_mask != 0) first, in any order, then -1:
-// the warm-up launch of those resets packs them G to a workgroup instead of spreading them over
-// ~one workgroup each, halving the warm-up waves that share the chip with the next step launch.
-// Results do not depend on either order (test_dispatch_order_leaves_results_unchanged,
-// test_overlapped_resets_equal_in_place_resets).
-__global__ void __launch_bounds__(1024) ix_order_kernel(int32_t* __restrict__ order, int E, int G, int kmax,
-                                                        const uint8_t* __restrict__ spare_mask,
-                                                        int32_t* __restrict__ spare_order, int n_spare) {
+// The next step's dispatch order (one workgroup, after the tail): the simulate launch's groups of G
+// consecutive envs (its workgroups), heaviest first by the group's live vehicles (kmax <= 256).
+// The hardware dispatches workgroups in slot order, so the long-running groups start first and the
+// cheap ones fill in behind them -- and behind the warm-up waves of the spare resets a step launch
+// finds resident (the slots they hold push the last-dispatched groups into a second round).  The
+// step's results do not depend on the order (test_dispatch_order_leaves_results_unchanged,
+// test_overlapped_resets_equal_in_place_resets).  order: [0, E) out, [E, 2E) the tail's live counts.
+__global__ void __launch_bounds__(1024) ix_order_kernel(int32_t* __restrict__ order, int E, int G, int kmax) {
   __shared__ int h[ORDER_BUCKETS];
-  __shared__ int n_on;
-  const int tid = threadIdx.x;
-  if (spare_order) {
-    if (tid == 0) n_on = 0;
-    __syncthreads();
-    for (int r = tid; r < n_spare; r += blockDim.x)
-      if (spare_mask[r]) spare_order[atomicAdd(&n_on, 1)] = r;
-    __syncthreads();
-    for (int r = n_on + tid; r < n_spare; r += blockDim.x) spare_order[r] = -1;
-  }
-  if (!order) return;
   const int32_t* live = order + E;
   sort_groups(order, E / G, G, h, [&](int p) {
     int k = 0;
     for (int q = 0; q < G; ++q) k += live[p * G + q];
     return kmax - min(max(k, 0), kmax);  // descending
-  });
-}
-
-// The next launch's dispatch order from this launch's measured cost (ttrl_env_step with cost):
-// the groups of G envs (the simulate workgroups) by their wall-clock ticks, longest first, in
-// ORDER_BUCKETS buckets of the largest.  A pile-up env stays slow from one step to the next, so the
-// long waves start first and -- where a launch needs more than one round of the chip's wave slots
-// -- the short ones fill in behind them.
-__global__ void __launch_bounds__(1024) order_by_cost_kernel(const uint32_t* __restrict__ cost, int E, int G,
-                                                             int32_t* __restrict__ order) {
-  __shared__ int h[ORDER_BUCKETS];
-  __shared__ unsigned s_max;
-  const int tid = threadIdx.x, P = E / G;
-  if (tid == 0) s_max = 1u;
-  __syncthreads();
-  unsigned m = 0;
-  for (int e = tid; e < E; e += blockDim.x) m = max(m, cost[e]);
-  atomicMax(&s_max, m);
-  __syncthreads();
-  const unsigned long long top = s_max;
-  sort_groups(order, P, G, h, [&](int p) {
-    unsigned c = 0;
-    for (int q = 0; q < G; ++q) c = max(c, cost[p * G + q]);
-    const int k = (int)((unsigned long long)c * (ORDER_BUCKETS - 1) / top);
-    return ORDER_BUCKETS - 1 - min(k, ORDER_BUCKETS - 1);  // descending
   });
 }
 
@@ -4816,13 +4765,12 @@ int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
                   int32_t frames, double dt, const ttrl_kin_cfg_t* obs_cfg, float* obs, int32_t* obs_ids,
                   const ttrl_reward_cfg_t* reward_cfg, double* time, double time_inc, float* reward,
                   uint8_t* terminated, uint8_t* truncated, float* components, void* ego_speed, uint8_t* ego_crashed,
-                  int32_t* order, uint32_t* cost, void* stream) {
+                  const int32_t* order, void* stream) {
   int rc = check_state(s, road);
   if (rc) return rc < 0 ? rc : TTRL_OK;
   if ((!obs_cfg) != (!obs) || (obs_cfg && check_kin_cfg(s, obs_cfg))) return TTRL_E_ARG;
   if (reward_cfg && (!time || !reward || !terminated || !truncated || (!ego_speed) != (!ego_crashed)))
     return TTRL_E_ARG;
-  if (cost && !order) return TTRL_E_ARG;
   StepOut so{};
   if (obs_cfg) { so.kcfg = *obs_cfg; so.obs = obs; so.ids = obs_ids; }
   if (reward_cfg) {
@@ -4830,13 +4778,7 @@ int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
     so.trunc = truncated; so.comp = components; so.ego_speed = ego_speed; so.ego_crashed = ego_crashed;
   }
   so.order = order;
-  so.cost = cost;
-  if ((rc = run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream, 0, nullptr, &so)))
-    return rc;
-  const int G = slots_for(s->n_veh) == 32 ? 2 : 1;  // the simulate instance's envs per workgroup
-  if (cost && s->n_envs % G == 0)  // the next launch's order, from this one's measured cost
-    hipLaunchKernelGGL(order_by_cost_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, cost, s->n_envs, G, order);
-  return launch_status();
+  return run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream, 0, nullptr, &so);
 }
 
 /* Diagnostic only (not in include/): the simulate kernel's LDS view bytes per workgroup. */
@@ -5052,7 +4994,7 @@ static int check_ix(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttr
 
 int ttrl_ix_reset(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                   const ttrl_ix_cfg_t* cfg, const uint32_t* entropy, int32_t n_words, const uint8_t* mask,
-                  const int32_t* order, void* stream) {
+                  void* stream) {
   int rc = check_ix(s, road, p, cfg);
   if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!entropy || n_words < 1 || n_words > 64) return TTRL_E_ARG;
@@ -5067,10 +5009,7 @@ int ttrl_ix_reset(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
                        (const unsigned*)entropy, (int)n_words, mask);
   if ((rc = launch_status())) return rc;
   // _make_vehicles' warm-up: 3 s of Road.act / Road.step with no controlled vehicle yet
-  StepOut wo{};
-  wo.order = order;  // the masked rows packed to the front (ix_order_kernel's spare_order)
-  if ((rc = run_sim(s, road, p, nullptr, cfg->warmup_frames, cfg->warmup_dt, MODE_ACT | MODE_STEP, stream, 0, mask,
-                    &wo)))
+  if ((rc = run_sim(s, road, p, nullptr, cfg->warmup_frames, cfg->warmup_dt, MODE_ACT | MODE_STEP, stream, 0, mask)))
     return rc;
   if (s->dtype == TTRL_F64)
     hipLaunchKernelGGL(ix_finish_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg, mask);
@@ -5124,8 +5063,7 @@ int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
                       const uint8_t* truncated, uint8_t* spare_parity, uint32_t* entropy, uint32_t* spare_entropy,
                       int32_t n_words, double* time, uint8_t* done, uint8_t* spare_mask,
                       const ttrl_kin_cfg_t* obs_cfg, const float* obs_in, float* obs_out, const int32_t* obs_ids_in,
-                      int32_t* obs_ids_out, int64_t* live_count, int32_t* order, int32_t* spare_order,
-                      void* stream) {
+                      int32_t* obs_ids_out, int64_t* live_count, int32_t* order, void* stream) {
   int rc = check_ix(s, road, p, cfg);
   if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!spare || !terminated || !truncated || !spare_parity || !entropy || !spare_entropy || n_words < 1 ||
@@ -5161,9 +5099,8 @@ int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
     hipLaunchKernelGGL(ix_step_tail_kernel<double>, dim3(s->n_envs), dim3(64), 0, st, *s, *road, *p, *cfg, t);
   else
     hipLaunchKernelGGL(ix_step_tail_kernel<float>, dim3(s->n_envs), dim3(64), 0, st, *s, *road, *p, *cfg, t);
-  if (ordered || spare_order)
-    hipLaunchKernelGGL(ix_order_kernel, dim3(1), dim3(1024), 0, st, ordered ? order : nullptr, s->n_envs, G,
-                       G * s->n_veh, spare_mask, spare_order, 2 * s->n_envs);
+  if (ordered)
+    hipLaunchKernelGGL(ix_order_kernel, dim3(1), dim3(1024), 0, st, order, s->n_envs, G, G * s->n_veh);
   return launch_status();
 }
 

@@ -155,8 +155,7 @@ env_step_outputs(const at::Tensor& x, const ttrl_kin_cfg_t* kc) {
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> env_step_(
     at::TensorList state, const at::Tensor& lanes, const at::Tensor& params, const c10::optional<at::Tensor>& actions,
     int64_t frames, double dt, const c10::optional<at::Tensor>& kin_cfg, const at::Tensor& reward_cfg,
-    const at::Tensor& time, double time_inc, const c10::optional<at::Tensor>& order,
-    const c10::optional<at::Tensor>& cost) {
+    const at::Tensor& time, double time_inc, const c10::optional<at::Tensor>& order) {
   check_hip(state[0]);
   ttrl_state_t s = state_of(state);
   const ttrl_kin_cfg_t* kc = kin_cfg && kin_cfg->defined() ? as_struct<ttrl_kin_cfg_t>(*kin_cfg, "kin_cfg") : nullptr;
@@ -169,11 +168,6 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
     TORCH_CHECK(order->device() == state[0].device() && order->scalar_type() == at::kInt && order->is_contiguous() &&
                     order->numel() >= s.n_envs,
                 "ttrl: order must be a contiguous int32 tensor of at least n_envs entries on the state's device");
-  const bool cd = cost && cost->defined();
-  if (cd)  // the measured ticks, from which the launch rewrites order for the next call
-    TORCH_CHECK(od && cost->device() == state[0].device() && cost->scalar_type() == at::kInt &&
-                    cost->is_contiguous() && cost->numel() == s.n_envs,
-                "ttrl: cost must be a contiguous int32 [n_envs] tensor on the state's device, with an order");
   auto out = env_step_outputs(state[0], kc);
   auto& [obs, ids, rew, term, trunc, comp, speed, crashed] = out;
   ok(ttrl_env_step(&s, as_struct<ttrl_lane_table_t>(lanes, "lanes"), as_struct<ttrl_params_t>(params, "params"),
@@ -183,7 +177,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
                    rew.data_ptr<float>(), static_cast<uint8_t*>(term.data_ptr()),
                    static_cast<uint8_t*>(trunc.data_ptr()), comp.data_ptr<float>(), speed.data_ptr(),
                    static_cast<uint8_t*>(crashed.data_ptr()), od ? order->data_ptr<int32_t>() : nullptr,
-                   cd ? reinterpret_cast<uint32_t*>(cost->data_ptr<int32_t>()) : nullptr, stream_of(state[0])),
+                   stream_of(state[0])),
      "ttrl_env_step");
   return out;
 }
@@ -348,21 +342,14 @@ at::Tensor auto_reset_highway_(at::TensorList state, const at::Tensor& lanes, co
 }
 
 void ix_reset_(at::TensorList state, const at::Tensor& lanes, const at::Tensor& params, const at::Tensor& cfg,
-               const at::Tensor& entropy, const c10::optional<at::Tensor>& mask,
-               const c10::optional<at::Tensor>& order) {
+               const at::Tensor& entropy, const c10::optional<at::Tensor>& mask) {
   check_hip(state[0]);
   ttrl_state_t s = state_of(state);
   at::Tensor w = entropy_words(entropy, s, state[0]);
   at::Tensor m = dev_u8(mask, s.n_envs, state[0], "mask");
-  const bool od = order && order->defined();
-  if (od)  // every masked env once, then -1 (ix_step_tail_'s spare_order)
-    TORCH_CHECK(m.defined() && order->device() == state[0].device() && order->scalar_type() == at::kInt &&
-                    order->is_contiguous() && order->numel() == s.n_envs,
-                "ttrl: order must be a contiguous int32 [n_envs] tensor on the state's device, with a mask");
   ok(ttrl_ix_reset(&s, as_struct<ttrl_lane_table_t>(lanes, "lanes"), as_struct<ttrl_params_t>(params, "params"),
                    as_struct<ttrl_ix_cfg_t>(cfg, "cfg"), reinterpret_cast<const uint32_t*>(w.data_ptr()),
-                   static_cast<int32_t>(w.size(1)), static_cast<const uint8_t*>(ptr(m)),
-                   od ? order->data_ptr<int32_t>() : nullptr, stream_of(state[0])),
+                   static_cast<int32_t>(w.size(1)), static_cast<const uint8_t*>(ptr(m)), stream_of(state[0])),
      "ttrl_ix_reset");
 }
 
@@ -387,7 +374,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ix_step_tail_(
     const at::Tensor& entropy, const at::Tensor& spare_entropy, const at::Tensor& time,
     const c10::optional<at::Tensor>& kin_cfg, const c10::optional<at::Tensor>& obs,
     const c10::optional<at::Tensor>& ids, const c10::optional<at::Tensor>& live_count,
-    const c10::optional<at::Tensor>& order, const c10::optional<at::Tensor>& spare_order) {
+    const c10::optional<at::Tensor>& order) {
   check_hip(state[0]);
   ttrl_state_t s = state_of(state), sp = state_of(spare);
   const auto& x = state[0];
@@ -434,11 +421,6 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ix_step_tail_(
     TORCH_CHECK(order->device() == x.device() && order->scalar_type() == at::kInt && order->is_contiguous() &&
                     order->numel() == 2 * int64_t(s.n_envs),
                 "ttrl: order must be a contiguous int32 [2 * n_envs] tensor on the state's device");
-  const bool so = spare_order && spare_order->defined();
-  if (so)
-    TORCH_CHECK(spare_order->device() == x.device() && spare_order->scalar_type() == at::kInt &&
-                    spare_order->is_contiguous() && spare_order->numel() == 2 * int64_t(s.n_envs),
-                "ttrl: spare_order must be a contiguous int32 [2 * n_envs] tensor on the state's device");
   at::Tensor done = at::empty({s.n_envs}, opts(x, at::kBool));
   at::Tensor smask = at::empty({2 * s.n_envs}, opts(x, at::kByte));
   ok(ttrl_ix_step_tail(&s, as_struct<ttrl_lane_table_t>(lanes, "lanes"), as_struct<ttrl_params_t>(params, "params"),
@@ -450,8 +432,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ix_step_tail_(
                        static_cast<uint8_t*>(smask.data_ptr()), kc, kc ? oin.data_ptr<float>() : nullptr,
                        kc ? obs_out.data_ptr<float>() : nullptr, kc ? iin.data_ptr<int32_t>() : nullptr,
                        kc ? ids_out.data_ptr<int32_t>() : nullptr, lc ? live_count->data_ptr<int64_t>() : nullptr,
-                       od ? order->data_ptr<int32_t>() : nullptr, so ? spare_order->data_ptr<int32_t>() : nullptr,
-                       stream_of(x)),
+                       od ? order->data_ptr<int32_t>() : nullptr, stream_of(x)),
      "ttrl_ix_step_tail");
   return {done, smask, obs_out, ids_out};
 }
@@ -594,7 +575,7 @@ void meta_none_meta(at::TensorList, const at::Tensor&, const at::Tensor&, const 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor>
 meta_env_step(at::TensorList state, const at::Tensor&, const at::Tensor&, const c10::optional<at::Tensor>&, int64_t,
               double, const c10::optional<at::Tensor>& kin_cfg, const at::Tensor&, const at::Tensor&, double,
-              const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&) {
+              const c10::optional<at::Tensor>&) {
   const ttrl_kin_cfg_t* kc = kin_cfg && kin_cfg->defined() ? as_struct<ttrl_kin_cfg_t>(*kin_cfg, "kin_cfg") : nullptr;
   return env_step_outputs(meta_x(state), kc);
 }
@@ -632,8 +613,6 @@ at::Tensor meta_lidar(at::TensorList state, const at::Tensor&, const at::Tensor&
 void meta_reset(at::TensorList, const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&) {}
 void meta_reset_seeded(at::TensorList, const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&,
                        const c10::optional<at::Tensor>&) {}
-void meta_ix_reset(at::TensorList, const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&,
-                   const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&) {}
 void meta_clear_spawn(at::TensorList, const at::Tensor&, const at::Tensor&, const at::Tensor&,
                       const c10::optional<at::Tensor>&) {}
 void meta_copy_envs(at::TensorList, at::TensorList, const at::Tensor&) {}
@@ -641,7 +620,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> meta_ix_step_tail(
     at::TensorList state, const at::Tensor&, const at::Tensor&, const at::Tensor&, at::TensorList, const at::Tensor&,
     const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&,
     const c10::optional<at::Tensor>& kin_cfg, const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&,
-    const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&) {
+    const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&) {
   const auto& x = meta_x(state);
   const int64_t E = x.size(0);
   at::Tensor o = at::empty({0}, opts(x, at::kFloat)), i = at::empty({0}, opts(x, at::kInt));
@@ -695,8 +674,8 @@ TORCH_LIBRARY(ttrl, m) {
   m.def("road_step_(Tensor(a!)[] state, Tensor lanes, Tensor params, float dt) -> ()");
   m.def("meta_action_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor actions) -> ()");
   m.def("env_step_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor? actions, int frames, float dt, "
-        "Tensor? kin_cfg, Tensor reward_cfg, Tensor(b!) time, float time_inc, Tensor(c!)? order=None, "
-        "Tensor(d!)? cost=None) -> (Tensor obs, Tensor ids, "
+        "Tensor? kin_cfg, Tensor reward_cfg, Tensor(b!) time, float time_inc, Tensor? order=None) -> (Tensor obs, "
+        "Tensor ids, "
         "Tensor reward, Tensor terminated, Tensor truncated, Tensor components, Tensor ego_speed, Tensor ego_crashed)");
   m.def("neighbours(Tensor[] state, Tensor lanes, Tensor? query_lane) -> (Tensor front, Tensor rear)");
   // the np_random-shuffled observation (order_shuffled 2) advances state.rng: the state is mutated
@@ -711,15 +690,13 @@ TORCH_LIBRARY(ttrl, m) {
         "Tensor? mask) -> ()");
   m.def("auto_reset_highway_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor(b!) entropy, "
         "int episode_word, Tensor terminated, Tensor truncated, Tensor(c!) time) -> Tensor done");
-  m.def("ix_reset_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor entropy, Tensor? mask, "
-        "Tensor? order=None) -> ()");
+  m.def("ix_reset_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor entropy, Tensor? mask) -> ()");
   m.def("ix_clear_spawn_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor? mask) -> ()");
   m.def("copy_envs_(Tensor(a!)[] dst, Tensor[] src, Tensor mask) -> ()");
   m.def("ix_step_tail_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor[] spare, "
         "Tensor terminated, Tensor truncated, Tensor(b!) spare_parity, Tensor(c!) entropy, Tensor(d!) spare_entropy, "
         "Tensor(e!) time, Tensor? kin_cfg, Tensor? obs, Tensor? ids, Tensor(f!)? live_count=None, "
-        "Tensor(g!)? order=None, Tensor(h!)? spare_order=None) -> (Tensor done, Tensor spare_mask, Tensor obs, "
-        "Tensor ids)");
+        "Tensor(g!)? order=None) -> (Tensor done, Tensor spare_mask, Tensor obs, Tensor ids)");
   m.def("rewards(Tensor[] state, Tensor lanes, Tensor cfg, Tensor time) -> (Tensor reward, Tensor terminated, "
         "Tensor truncated)");
   m.def("rewards_ex(Tensor[] state, Tensor lanes, Tensor cfg, Tensor time) -> (Tensor reward, Tensor terminated, "
@@ -772,7 +749,7 @@ TORCH_LIBRARY_IMPL(ttrl, Meta, m) {
   m.impl("reset_highway_", &meta_reset);
   m.impl("reset_highway_seeded_", &meta_reset_seeded);
   m.impl("auto_reset_highway_", &meta_auto_reset);
-  m.impl("ix_reset_", &meta_ix_reset);
+  m.impl("ix_reset_", &meta_reset_seeded);
   m.impl("ix_clear_spawn_", &meta_clear_spawn);
   m.impl("copy_envs_", &meta_copy_envs);
   m.impl("ix_step_tail_", &meta_ix_step_tail);

@@ -136,9 +136,6 @@ class VecHighwayEnv:
             "device": "cuda",
             "dtype": "f64",
             "auto_reset": False,
-            # the step launch takes its envs longest-first, by the previous step's measured cost
-            # (ttrl_env_step's order / cost; the results are the same either way)
-            "dispatch_order": False,
         }
 
     def configure(self, config: dict | None) -> None:
@@ -183,10 +180,6 @@ class VecHighwayEnv:
         # auto-reset entropy per env: [seed lo word, seed hi word, episode]; episode k >= 1 of an env
         # reset with seed s replays np.random.default_rng([s & 0xffffffff, s >> 32, k])
         self._entropy = torch.zeros(self.num_envs, 3, dtype=torch.int32, device=self.device)
-        self._order = self._cost = None
-        if c["dispatch_order"]:
-            self._order = torch.arange(self.num_envs, dtype=torch.int32, device=self.device)
-            self._cost = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
         self.define_spaces()
 
     @property
@@ -271,7 +264,7 @@ class VecHighwayEnv:
         kin = isinstance(self.observation_type, BatchedKinematicObservation)
         kc = self.observation_type.fused_cfg() if kin else None
         obs, ids, *outs = self.road.env_step(codes, frames, dt, kc, self.reward_cfg, self.time,
-                                             1 / self.config["policy_frequency"], self._order, self._cost)
+                                             1 / self.config["policy_frequency"])
         if kin:
             self.observation_type.fused_result(obs, ids)
         return (obs if kin else None), _keep_tail(self, outs)
@@ -325,8 +318,6 @@ class VecHighwayEnv:
         new.time = self.time.clone()
         if self._entropy is not None:  # the fork's auto-resets must not advance our episode counters
             new._entropy = self._entropy.clone()
-        if self._order is not None:  # its own dispatch order and cost scratch
-            new._order, new._cost = self._order.clone(), self._cost.clone()
         new.define_spaces()
         return new
 

@@ -179,15 +179,13 @@ def _device_only(state: BatchState) -> None:
 
 
 def ix_reset(state: BatchState, network: RoadNetwork, params: _abi.Params, cfg: _abi.IxCfg,
-             entropy: torch.Tensor, mask: torch.Tensor | None = None, order: torch.Tensor | None = None) -> None:
-    """IntersectionEnv.reset on the device: env e replays ``default_rng(list(entropy[e]))``.
-    ``order``: the masked envs packed first, then -1 (the warm-up launch's dispatch order;
-    ix_step_tail_'s spare_order) -- the same scenes, in fewer warm-up workgroups."""
+             entropy: torch.Tensor, mask: torch.Tensor | None = None) -> None:
+    """IntersectionEnv.reset on the device: env e replays ``default_rng(list(entropy[e]))``."""
     if entropy.dim() != 2 or entropy.shape[0] != state.n_envs or entropy.dtype != torch.int32:
         raise ValueError("entropy must be an int32 [n_envs, n_words] tensor of uint32 words")
     _device_only(state)
     ops.T.ix_reset_(state.tensors(), ops.st(network.table), ops.st(params), ops.st(cfg),
-                    entropy.to(state.device), mask, order)
+                    entropy.to(state.device), mask)
 
 
 def ix_clear_spawn(state: BatchState, network: RoadNetwork, params: _abi.Params, cfg: _abi.IxCfg,
@@ -400,7 +398,7 @@ class VecIntersectionEnv:
         for side in self._sides:
             main.wait_stream(side)
 
-    def _prepare_spares(self, mask: torch.Tensor | None, order: torch.Tensor | None = None) -> None:
+    def _prepare_spares(self, mask: torch.Tensor | None) -> None:
         """Reset the spare scenes of ``mask`` ([2E]; all: None) on the next side stream, after the
         main stream's work so far (the swap that consumed them).  The side stream reads the seed
         words and episode counters of the masked rows only; the main stream writes a row's counter
@@ -411,12 +409,11 @@ class VecIntersectionEnv:
         self._side_i = (self._side_i + 1) % len(self._sides)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            ix_reset(self._spare, self.network, self.params, self.ix, self._spare_ent, mask, order)
+            ix_reset(self._spare, self.network, self.params, self.ix, self._spare_ent, mask)
             ev = torch.cuda.Event()
             ev.record(side)
-        for t in (mask, order):
-            if t is not None:
-                t.record_stream(side)
+        if mask is not None:
+            mask.record_stream(side)
         self._spare_prev, self._spare_ready = self._spare_ready, ev
 
     def step(self, action):
@@ -466,13 +463,12 @@ class VecIntersectionEnv:
         # (vehicle_slots > 64) take the masked observation launch instead, which draws the same
         # shuffles from the same generators (test_overlapped_resets_equal_in_place_resets[96])
         fused_obs = kin and self.state.n_veh <= 64
-        sorder = torch.empty(2 * self.num_envs, dtype=torch.int32, device=self.device)  # fresh: read on a side stream
         done, smask, obs2, ids2 = ops.T.ix_step_tail_(
             self.state.tensors(), ops.st(self.network.table), ops.st(self.params), ops.st(self.ix),
             self._spare.tensors(), terminated, truncated, self._spare_par, self._entropy, self._spare_ent, self.time,
             ops.kin_cfg_tensor(ot.fused_cfg()) if fused_obs else None, obs if fused_obs else None,
-            ids if fused_obs else None, self.live_counter, self._order, sorder)
-        self._prepare_spares(smask, sorder)
+            ids if fused_obs else None, self.live_counter, self._order)
+        self._prepare_spares(smask)
         info["final_observation"], info["final_mask"] = obs, done
         if fused_obs:
             ot.fused_result(obs2, ids2)
