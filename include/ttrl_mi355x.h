@@ -381,6 +381,16 @@ int ttrl_ego_attention_act(const float* obs, int32_t batch, int32_t n_entities, 
 int ttrl_ix_reset(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                   const ttrl_ix_cfg_t* cfg, const uint32_t* entropy, int32_t n_words, const uint8_t* mask,
                   void* stream);
+/* ttrl_ix_reset in parts, each over its own env mask (NULL: all): TTRL_IX_BEGIN (seeding and the
+ * initial spawns, from entropy), TTRL_IX_WARMUP (warm_frames of the warm-up frames -- consecutive
+ * calls continue the same warm-up), TTRL_IX_FINISH (the challenger, the ego and the removals).
+ * ttrl_ix_reset == all three over one mask with warm_frames = cfg->warmup_frames.  Lets a caller
+ * spread a reset's warm-up over several steps, the chunks of different resets in one launch. */
+enum { TTRL_IX_BEGIN = 1, TTRL_IX_WARMUP = 2, TTRL_IX_FINISH = 4 };
+int ttrl_ix_reset_parts(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                        const ttrl_ix_cfg_t* cfg, int32_t parts, const uint32_t* entropy, int32_t n_words,
+                        const uint8_t* begin_mask, const uint8_t* warm_mask, int32_t warm_frames,
+                        const uint8_t* finish_mask, void* stream);
 /* Copy every row of the envs with mask[e] != 0 (all fields, per-env route / regulation / rng
  * words included) from src to dst, which have the same shape and dtype: swapping in scenes reset
  * ahead of time (the intersection's double-buffered auto-reset). */
@@ -390,14 +400,15 @@ int ttrl_copy_envs(const ttrl_state_t* dst, const ttrl_state_t* src, const uint8
 int ttrl_ix_clear_spawn(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                         const ttrl_ix_cfg_t* cfg, const uint8_t* mask, void* stream);
 /* VecIntersectionEnv.step after ttrl_env_step (fused frames, observation, rewards), with the
- * auto-reset from scenes reset ahead of time, in one launch.  spare: 2E rows (slot q of env e is
- * row q * E + e), reset by ttrl_ix_reset from spare_entropy.  An env with terminated | truncated
- * == 0 runs the IntersectionEnv.step tail (as ttrl_ix_clear_spawn) and copies its observation row
- * obs_in -> obs_out; a finished env instead takes the spare row of slot spare_parity[e] (every
- * field, rng and regulation words included), flips spare_parity[e], adds 1 to its episode word
- * entropy[e][n_words - 1] and 2 to spare_entropy[row][n_words - 1], zeroes time[e] and writes its
- * first observation into obs_out / obs_ids_out (obs_cfg: Kinematics, n_veh <= 64).  done[E] =
- * terminated | truncated; spare_mask[2E] flags the consumed spare rows (to be reset again).
+ * auto-reset from scenes reset ahead of time, in one launch.  spare: K * E rows, K in [2, 8] (slot
+ * q of env e is row q * E + e), reset by ttrl_ix_reset from spare_entropy.  An env with
+ * terminated | truncated == 0 runs the IntersectionEnv.step tail (as ttrl_ix_clear_spawn) and
+ * copies its observation row obs_in -> obs_out; a finished env instead takes the spare row of slot
+ * spare_parity[e] (every field, rng and regulation words included), moves spare_parity[e] to the
+ * next slot (mod K), adds 1 to its episode word entropy[e][n_words - 1] and K to
+ * spare_entropy[row][n_words - 1], zeroes time[e] and writes its first observation into obs_out /
+ * obs_ids_out (obs_cfg: Kinematics, n_veh <= 64).  done[E] = terminated | truncated;
+ * spare_mask[K * E] flags the consumed spare rows (to be reset again).
  * live_count (optional, one int64 on the device): += the vehicles present in the E envs after
  * the tail -- the next step's live vehicles, counted without a launch of its own (the
  * intersection bench's live vehicle-steps).  order (optional, device [2 * n_envs] int32, the

@@ -15,7 +15,7 @@ LANES = ops.struct_tensor(_abi.straight_lane_table(4))
 PARAMS = ops.struct_tensor(_abi.default_params())
 MUTATES = {"simulate_", "road_act_", "road_step_", "meta_action_", "env_step_", "kinematics_obs",
            "kinematics_obs_masked_", "reset_highway_", "reset_highway_seeded_", "auto_reset_highway_", "ix_reset_",
-           "ix_clear_spawn_", "ix_step_tail_", "copy_envs_"}
+           "ix_reset_parts_", "ix_clear_spawn_", "ix_step_tail_", "copy_envs_"}
 
 
 def test_every_device_entry_point_is_an_operator():
@@ -27,6 +27,7 @@ def test_every_device_entry_point_is_an_operator():
                           "observe_lidar": "observe_lidar", "reset_highway_": "reset_highway",
                           "reset_highway_seeded_": "reset_highway_seeded",
                           "auto_reset_highway_": "auto_reset_highway", "ix_reset_": "ix_reset",
+                          "ix_reset_parts_": "ix_reset_parts",
                           "ix_clear_spawn_": "ix_clear_spawn", "ix_step_tail_": "ix_step_tail",
                           "copy_envs_": "copy_envs", "rewards": "rewards",
                           "rewards_ex": "rewards_ex", "rewards_step_": "rewards_step",
@@ -320,6 +321,17 @@ def test_intersection_ops_equal_the_c_abi(hip_device):
     torch.ops.ttrl.copy_envs_(d.tensors(), b.tensors(), mask)
     torch.cuda.synchronize()
     _equal(c, d)
+    # the reset in parts: begin, the 45 warm-up frames as 15 + 30, finish, through the C ABI and the
+    # operator, equals the whole reset of the same envs (masked: the others keep their rows)
+    e, f = a.clone(), a.clone()
+    w2 = words + 100
+    assert lib.ttrl_ix_reset(_c(e), R, P, IX, w2.data_ptr(), 1, mask.data_ptr(), _stream()) == 0
+    assert lib.ttrl_ix_reset_parts(_c(f), R, P, IX, 3, w2.data_ptr(), 1, mask.data_ptr(), mask.data_ptr(), 15, None,
+                                   _stream()) == 0
+    torch.ops.ttrl.ix_reset_parts_(f.tensors(), lanes, params, cfg, 6, None, None, mask, 30, mask)
+    torch.cuda.synchronize()
+    _equal(e, f)
+    assert lib.ttrl_ix_reset_parts(_c(f), R, P, IX, 8, None, 0, None, None, 0, None, _stream()) == -1
 
 
 @pytest.mark.gpu

@@ -39,6 +39,7 @@ _SIGS = {
     "ttrl_rewards_ex": ([_P, _P, _P, _P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_rewards_step": ([_P, _P, _P, _P, C.c_double, _P, _P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_ix_reset": ([_P, _P, _P, _P, _P, C.c_int32, _P, _P], C.c_int),
+    "ttrl_ix_reset_parts": ([_P, _P, _P, _P, C.c_int32, _P, C.c_int32, _P, _P, C.c_int32, _P, _P], C.c_int),
     "ttrl_ix_clear_spawn": ([_P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_ix_step_tail": ([_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, C.c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                            _P],

@@ -4418,12 +4418,13 @@ __device__ __forceinline__ void copy_env_rows(const ttrl_state_t& dst, const ttr
 //   spare_mask for the side stream's reset, the parity flips, time is zeroed, and the first
 //   observation of the new scene is written to obs_out / ids_out (kin_observe, one slot per lane).
 struct IxTail {
-  ttrl_state_t spare;  // 2E rows: slot p of env e is row p * E + e
+  ttrl_state_t spare;  // K * E rows: slot p of env e is row p * E + e
+  int K;               // spare slots per env, taken in rotation
   const uint8_t* term;
   const uint8_t* trunc;
   uint8_t* par;        // [E] the next slot each env takes
   uint32_t* ent;       // [E][nw] entropy words, the episode counter last
-  uint32_t* spare_ent; // [2E][nw]
+  uint32_t* spare_ent; // [K * E][nw]
   int nw;
   double* time;
   uint8_t* done;       // [E] out
@@ -4510,7 +4511,10 @@ __global__ void __launch_bounds__(64) ix_step_tail_kernel(ttrl_state_t st, ttrl_
   const bool d = t.term[env] || t.trunc[env];
   const int V = t.kcfg.vehicles_count, F = t.kcfg.n_features;
   if (!d) {
-    if (lane == 0) { t.done[env] = 0; t.spare_mask[env] = 0; t.spare_mask[E + env] = 0; }
+    if (lane == 0) {
+      t.done[env] = 0;
+      for (int q = 0; q < t.K; ++q) t.spare_mask[q * E + env] = 0;
+    }
     if (t.obs) {  // the row observed by the fused launch stays this step's observation
       for (int q = lane; q < V * F; q += 64) t.obs_out[(size_t)env * V * F + q] = t.obs_in[(size_t)env * V * F + q];
       if (t.ids_out)
@@ -4526,10 +4530,9 @@ __global__ void __launch_bounds__(64) ix_step_tail_kernel(ttrl_state_t st, ttrl_
   if (lane == 0) {
     t.done[env] = 1;
     t.ent[(size_t)env * t.nw + t.nw - 1] += 1u;
-    t.spare_ent[(size_t)row * t.nw + t.nw - 1] += 2u;
-    t.spare_mask[row] = 1;
-    t.spare_mask[(1 - p) * E + env] = 0;
-    t.par[env] = (uint8_t)(p ^ 1);
+    t.spare_ent[(size_t)row * t.nw + t.nw - 1] += (unsigned)t.K;  // this slot's next episode
+    for (int q = 0; q < t.K; ++q) t.spare_mask[q * E + env] = q == p;
+    t.par[env] = (uint8_t)(p + 1 == t.K ? 0 : p + 1);
     t.time[env] = 0.0;
   }
   if (t.live || t.live_env) ix_count_live<T>(st, t, env, lane);
@@ -4992,30 +4995,46 @@ static int check_ix(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttr
   return TTRL_OK;
 }
 
-int ttrl_ix_reset(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
-                  const ttrl_ix_cfg_t* cfg, const uint32_t* entropy, int32_t n_words, const uint8_t* mask,
-                  void* stream) {
+int ttrl_ix_reset_parts(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                        const ttrl_ix_cfg_t* cfg, int32_t parts, const uint32_t* entropy, int32_t n_words,
+                        const uint8_t* begin_mask, const uint8_t* warm_mask, int32_t warm_frames,
+                        const uint8_t* finish_mask, void* stream) {
   int rc = check_ix(s, road, p, cfg);
   if (rc) return rc < 0 ? rc : TTRL_OK;
-  if (!entropy || n_words < 1 || n_words > 64) return TTRL_E_ARG;
+  if (parts < 0 || parts > 7 || warm_frames < 0) return TTRL_E_ARG;
+  if ((parts & TTRL_IX_BEGIN) && (!entropy || n_words < 1 || n_words > 64)) return TTRL_E_ARG;
   if (s->n_envs == 0) return TTRL_OK;
   hipStream_t st = (hipStream_t)stream;
   const int blocks = s->n_envs;  // one wavefront per env
-  if (s->dtype == TTRL_F64)
-    hipLaunchKernelGGL(ix_begin_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg,
-                       (const unsigned*)entropy, (int)n_words, mask);
-  else
-    hipLaunchKernelGGL(ix_begin_kernel<float>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg,
-                       (const unsigned*)entropy, (int)n_words, mask);
-  if ((rc = launch_status())) return rc;
-  // _make_vehicles' warm-up: 3 s of Road.act / Road.step with no controlled vehicle yet
-  if ((rc = run_sim(s, road, p, nullptr, cfg->warmup_frames, cfg->warmup_dt, MODE_ACT | MODE_STEP, stream, 0, mask)))
+  if (parts & TTRL_IX_BEGIN) {
+    if (s->dtype == TTRL_F64)
+      hipLaunchKernelGGL(ix_begin_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg,
+                         (const unsigned*)entropy, (int)n_words, begin_mask);
+    else
+      hipLaunchKernelGGL(ix_begin_kernel<float>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg,
+                         (const unsigned*)entropy, (int)n_words, begin_mask);
+    if ((rc = launch_status())) return rc;
+  }
+  // _make_vehicles' warm-up: 3 s of Road.act / Road.step with no controlled vehicle yet; frames
+  // [f, f + n) then [f + n, ...) equal [f, ...) in one launch (the state round-trips HBM exactly)
+  if ((parts & TTRL_IX_WARMUP) && warm_frames > 0 &&
+      (rc = run_sim(s, road, p, nullptr, warm_frames, cfg->warmup_dt, MODE_ACT | MODE_STEP, stream, 0, warm_mask)))
     return rc;
-  if (s->dtype == TTRL_F64)
-    hipLaunchKernelGGL(ix_finish_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg, mask);
-  else
-    hipLaunchKernelGGL(ix_finish_kernel<float>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg, mask);
+  if (parts & TTRL_IX_FINISH) {
+    if (s->dtype == TTRL_F64)
+      hipLaunchKernelGGL(ix_finish_kernel<double>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg, finish_mask);
+    else
+      hipLaunchKernelGGL(ix_finish_kernel<float>, dim3(blocks), dim3(64), 0, st, *s, *road, *p, *cfg, finish_mask);
+  }
   return launch_status();
+}
+
+int ttrl_ix_reset(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                  const ttrl_ix_cfg_t* cfg, const uint32_t* entropy, int32_t n_words, const uint8_t* mask,
+                  void* stream) {
+  if (!cfg) return TTRL_E_ARG;
+  return ttrl_ix_reset_parts(s, road, p, cfg, TTRL_IX_BEGIN | TTRL_IX_WARMUP | TTRL_IX_FINISH, entropy, n_words,
+                             mask, mask, cfg->warmup_frames, mask, stream);
 }
 
 int ttrl_copy_envs(const ttrl_state_t* dst, const ttrl_state_t* src, const uint8_t* mask, void* stream) {
@@ -5069,7 +5088,8 @@ int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
   if (!spare || !terminated || !truncated || !spare_parity || !entropy || !spare_entropy || n_words < 1 ||
       n_words > 65 || !time || !done || !spare_mask)
     return TTRL_E_ARG;
-  if (spare->n_envs != 2 * s->n_envs || spare->n_veh != s->n_veh || spare->dtype != s->dtype || !spare->rng ||
+  const int K = s->n_envs > 0 ? spare->n_envs / s->n_envs : 0;
+  if (K < 2 || K > 8 || spare->n_envs != K * s->n_envs || spare->n_veh != s->n_veh || spare->dtype != s->dtype || !spare->rng ||
       !spare->reg_steps || !spare->route_road || !spare->route_lane || !spare->route_n || !spare->yielding)
     return TTRL_E_ARG;
   const void* sp[] = {spare->x, spare->y, spare->heading, spare->speed, spare->target_speed, spare->timer,
@@ -5083,7 +5103,7 @@ int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
       return obs_cfg && s->n_veh > 64 ? TTRL_E_UNSUPPORTED : TTRL_E_ARG;
   }
   IxTail t{};
-  t.spare = *spare; t.term = terminated; t.trunc = truncated; t.par = spare_parity; t.ent = entropy;
+  t.spare = *spare; t.K = K; t.term = terminated; t.trunc = truncated; t.par = spare_parity; t.ent = entropy;
   t.spare_ent = spare_entropy; t.nw = n_words; t.time = time; t.done = done; t.spare_mask = spare_mask;
   t.live = reinterpret_cast<unsigned long long*>(live_count);
   // the dispatch order groups the envs of one simulate workgroup (EPW: 2 on 32 slots, else 1)

@@ -353,6 +353,31 @@ void ix_reset_(at::TensorList state, const at::Tensor& lanes, const at::Tensor& 
      "ttrl_ix_reset");
 }
 
+// ttrl_ix_reset in parts (bits 1 begin, 2 warm-up frames, 4 finish), each over its own mask.
+void ix_reset_parts_(at::TensorList state, const at::Tensor& lanes, const at::Tensor& params, const at::Tensor& cfg,
+                     int64_t parts, const c10::optional<at::Tensor>& entropy,
+                     const c10::optional<at::Tensor>& begin_mask, const c10::optional<at::Tensor>& warm_mask,
+                     int64_t warm_frames, const c10::optional<at::Tensor>& finish_mask) {
+  check_hip(state[0]);
+  ttrl_state_t s = state_of(state);
+  TORCH_CHECK(parts >= 0 && parts <= 7 && warm_frames >= 0, "ttrl: parts must be a mask of 1 | 2 | 4");
+  at::Tensor w;
+  if (parts & TTRL_IX_BEGIN) {
+    TORCH_CHECK(entropy && entropy->defined(), "ttrl: the begin part needs the entropy words");
+    w = entropy_words(*entropy, s, state[0]);
+  }
+  at::Tensor bm = dev_u8(begin_mask, s.n_envs, state[0], "begin_mask");
+  at::Tensor wm = dev_u8(warm_mask, s.n_envs, state[0], "warm_mask");
+  at::Tensor fm = dev_u8(finish_mask, s.n_envs, state[0], "finish_mask");
+  ok(ttrl_ix_reset_parts(&s, as_struct<ttrl_lane_table_t>(lanes, "lanes"), as_struct<ttrl_params_t>(params, "params"),
+                         as_struct<ttrl_ix_cfg_t>(cfg, "cfg"), static_cast<int32_t>(parts),
+                         w.defined() ? reinterpret_cast<const uint32_t*>(w.data_ptr()) : nullptr,
+                         w.defined() ? static_cast<int32_t>(w.size(1)) : 0, static_cast<const uint8_t*>(ptr(bm)),
+                         static_cast<const uint8_t*>(ptr(wm)), static_cast<int32_t>(warm_frames),
+                         static_cast<const uint8_t*>(ptr(fm)), stream_of(state[0])),
+     "ttrl_ix_reset_parts");
+}
+
 void ix_clear_spawn_(at::TensorList state, const at::Tensor& lanes, const at::Tensor& params, const at::Tensor& cfg,
                      const c10::optional<at::Tensor>& mask) {
   check_hip(state[0]);
@@ -378,9 +403,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ix_step_tail_(
   check_hip(state[0]);
   ttrl_state_t s = state_of(state), sp = state_of(spare);
   const auto& x = state[0];
-  TORCH_CHECK(spare[0].device() == x.device() && sp.n_envs == 2 * s.n_envs && sp.n_veh == s.n_veh &&
+  const int64_t K = s.n_envs > 0 ? sp.n_envs / s.n_envs : 0;  // spare slots per env
+  TORCH_CHECK(spare[0].device() == x.device() && K >= 2 && K <= 8 && sp.n_envs == K * s.n_envs &&
+                  sp.n_veh == s.n_veh &&
                   sp.dtype == s.dtype,
-              "ttrl: spare must be a state of 2 * n_envs rows of the same width and dtype on the state's device");
+              "ttrl: spare must be a state of K * n_envs rows (K in [2, 8]) of the same width and dtype on the "
+              "state's device");
   for (const at::Tensor* t : {&terminated, &truncated})
     TORCH_CHECK(t->device() == x.device() && t->numel() == s.n_envs && t->is_contiguous() &&
                     (t->scalar_type() == at::kBool || t->scalar_type() == at::kByte),
@@ -391,10 +419,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ix_step_tail_(
   TORCH_CHECK(entropy.dim() == 2 && entropy.size(0) == s.n_envs && entropy.scalar_type() == at::kInt &&
                   entropy.is_contiguous() && entropy.device() == x.device(),
               "ttrl: entropy must be a contiguous int32 [n_envs, n_words] tensor on the state's device");
-  TORCH_CHECK(spare_entropy.dim() == 2 && spare_entropy.size(0) == 2 * s.n_envs &&
+  TORCH_CHECK(spare_entropy.dim() == 2 && spare_entropy.size(0) == sp.n_envs &&
                   spare_entropy.size(1) == entropy.size(1) && spare_entropy.scalar_type() == at::kInt &&
                   spare_entropy.is_contiguous() && spare_entropy.device() == x.device(),
-              "ttrl: spare_entropy must be a contiguous int32 [2 * n_envs, n_words] tensor on the state's device");
+              "ttrl: spare_entropy must be a contiguous int32 [K * n_envs, n_words] tensor on the state's device");
   check_time(time, s, x);
   const ttrl_kin_cfg_t* kc = kin_cfg && kin_cfg->defined() ? as_struct<ttrl_kin_cfg_t>(*kin_cfg, "kin_cfg") : nullptr;
   at::Tensor obs_out, ids_out, oin, iin;
@@ -422,7 +450,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ix_step_tail_(
                     order->numel() == 2 * int64_t(s.n_envs),
                 "ttrl: order must be a contiguous int32 [2 * n_envs] tensor on the state's device");
   at::Tensor done = at::empty({s.n_envs}, opts(x, at::kBool));
-  at::Tensor smask = at::empty({2 * s.n_envs}, opts(x, at::kByte));
+  at::Tensor smask = at::empty({sp.n_envs}, opts(x, at::kByte));
   ok(ttrl_ix_step_tail(&s, as_struct<ttrl_lane_table_t>(lanes, "lanes"), as_struct<ttrl_params_t>(params, "params"),
                        as_struct<ttrl_ix_cfg_t>(cfg, "cfg"), &sp, static_cast<const uint8_t*>(terminated.data_ptr()),
                        static_cast<const uint8_t*>(truncated.data_ptr()),
@@ -613,6 +641,9 @@ at::Tensor meta_lidar(at::TensorList state, const at::Tensor&, const at::Tensor&
 void meta_reset(at::TensorList, const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&) {}
 void meta_reset_seeded(at::TensorList, const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&,
                        const c10::optional<at::Tensor>&) {}
+void meta_ix_reset_parts(at::TensorList, const at::Tensor&, const at::Tensor&, const at::Tensor&, int64_t,
+                         const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&,
+                         const c10::optional<at::Tensor>&, int64_t, const c10::optional<at::Tensor>&) {}
 void meta_clear_spawn(at::TensorList, const at::Tensor&, const at::Tensor&, const at::Tensor&,
                       const c10::optional<at::Tensor>&) {}
 void meta_copy_envs(at::TensorList, at::TensorList, const at::Tensor&) {}
@@ -691,6 +722,8 @@ TORCH_LIBRARY(ttrl, m) {
   m.def("auto_reset_highway_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor(b!) entropy, "
         "int episode_word, Tensor terminated, Tensor truncated, Tensor(c!) time) -> Tensor done");
   m.def("ix_reset_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor entropy, Tensor? mask) -> ()");
+  m.def("ix_reset_parts_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, int parts, Tensor? entropy, "
+        "Tensor? begin_mask, Tensor? warm_mask, int warm_frames, Tensor? finish_mask) -> ()");
   m.def("ix_clear_spawn_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor? mask) -> ()");
   m.def("copy_envs_(Tensor(a!)[] dst, Tensor[] src, Tensor mask) -> ()");
   m.def("ix_step_tail_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor[] spare, "
@@ -724,6 +757,7 @@ TORCH_LIBRARY_IMPL(ttrl, CUDA, m) {  // the HIP device of ROCm PyTorch
   m.impl("reset_highway_seeded_", &reset_highway_seeded_);
   m.impl("auto_reset_highway_", &auto_reset_highway_);
   m.impl("ix_reset_", &ix_reset_);
+  m.impl("ix_reset_parts_", &ix_reset_parts_);
   m.impl("ix_clear_spawn_", &ix_clear_spawn_);
   m.impl("copy_envs_", &copy_envs_);
   m.impl("ix_step_tail_", &ix_step_tail_);
@@ -750,6 +784,7 @@ TORCH_LIBRARY_IMPL(ttrl, Meta, m) {
   m.impl("reset_highway_seeded_", &meta_reset_seeded);
   m.impl("auto_reset_highway_", &meta_auto_reset);
   m.impl("ix_reset_", &meta_reset_seeded);
+  m.impl("ix_reset_parts_", &meta_ix_reset_parts);
   m.impl("ix_clear_spawn_", &meta_clear_spawn);
   m.impl("copy_envs_", &meta_copy_envs);
   m.impl("ix_step_tail_", &meta_ix_step_tail);

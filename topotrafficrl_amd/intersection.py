@@ -279,7 +279,11 @@ class VecIntersectionEnv:
             # finished env swaps in its next episode's scene, whose 45 warm-up frames ran
             # overlapped with earlier steps, and the following one is prepared in the background
             "overlap_resets": True,
-            "reset_streams": 2,  # side streams the overlapped resets rotate over
+            # the spare resets' 45 warm-up frames in chunks of this many frames, one chunk per step
+            # (every step's chunks of the resets in flight in one launch on one side stream); 0: the
+            # whole warm-up at once, on side streams in rotation
+            "reset_chunk_frames": 15,
+            "reset_streams": 2,  # side streams the whole-warm-up resets rotate over (chunks: one)
         }
 
     def configure(self, config: dict | None) -> None:
@@ -317,24 +321,40 @@ class VecIntersectionEnv:
         # back (_spare_prev).  A step's spare resets (45 warm-up frames for a few hundred envs:
         # a latency chain of about one step) go to the two side streams in turn, so the chains of
         # consecutive steps overlap instead of queueing behind each other.
+        #
+        # reset_chunk_frames (default): a reset's warm-up instead runs 15 frames per step, so its
+        # waves last ~a third as long and mostly finish inside the step launch they start behind
+        # (a warm-up wave resident when a step launch starts holds one of the workgroup slots the
+        # launch needs, pushing a workgroup into a second round).  A scene consumed at step t is
+        # begun and warmed 15 frames after step t's tail, warmed 15 more after t+1's, and finished
+        # after t+2's; every step's side work is one launch over all resets in flight (begin,
+        # the union's chunk, finish) on one side stream.  Each env then owns C + 1 = 4 spare
+        # scenes (C chunks), so a slot is taken again 4 finishes later and the step still waits
+        # only for the side work of two steps back.
         self._spare = None
         # optional int64 device scalar: each overlapped step's tail adds the vehicles present after
         # it (the next step's live vehicles) -- a live vehicle-step count with no launch of its own
         self.live_counter: torch.Tensor | None = None
         if c["auto_reset"] and c["overlap_resets"]:
             E = self.num_envs
-            self._spare = BatchState(2 * E, int(c["vehicle_slots"]), device=self.device, dtype=c["dtype"])
-            self._spare_slot = (self._spare.rows(0, E), self._spare.rows(E, E))
+            chunk, wf = int(c["reset_chunk_frames"]), int(self.ix.warmup_frames)
+            # chunks must divide the warm-up, and the tail kernel rotates over at most 8 slots
+            self._chunk = chunk if 0 < chunk < wf and wf % chunk == 0 and wf // chunk + 1 <= 8 else 0
+            self._n_chunks = wf // self._chunk if self._chunk else 1
+            self._slots = self._n_chunks + 1 if self._chunk else 2  # spare scenes per env
+            self._cohorts = []  # the consumed-row masks of the resets still warming up, oldest first
+            self._spare = BatchState(self._slots * E, int(c["vehicle_slots"]), device=self.device, dtype=c["dtype"])
             self._spare_par = torch.zeros(E, dtype=torch.uint8, device=self.device)
             # the step launch's dispatch order (ix_step_tail_ rewrites it after every step: workgroups
             # heaviest first, see ix_order_kernel) and its scratch; any permutation is valid
             self._order = torch.cat([torch.arange(E, dtype=torch.int32, device=self.device),
                                      torch.zeros(E, dtype=torch.int32, device=self.device)])
-            self._sides = tuple(torch.cuda.Stream(self.device) for _ in range(max(1, int(c["reset_streams"]))))
+            n_sides = 1 if self._chunk else max(1, int(c["reset_streams"]))
+            self._sides = tuple(torch.cuda.Stream(self.device) for _ in range(n_sides))
             self._side_i = 0
             self._spare_ready = self._spare_prev = torch.cuda.Event()
-            # [2E, words + 1]: each spare scene's seed words and episode counter (the last word);
-            # ix_step_tail_ advances the counter of a consumed row by two
+            # [slots * E, words + 1]: each spare scene's seed words and episode counter (the last
+            # word); ix_step_tail_ advances the counter of a consumed row by the number of slots
             self._spare_ent = None
         self.define_spaces()
 
@@ -380,11 +400,12 @@ class VecIntersectionEnv:
         self.steps = 0
         self.done = False
         ix_reset(self.state, self.network, self.params, self.ix, self._entropy[:, :-1])
-        if self._spare is not None:  # every env's second and third episodes, in the background
-            ent = self._entropy
-            self._spare_ent = torch.cat([torch.cat([ent[:, :-1], ent[:, :-1]]),
-                                         torch.cat([ent[:, -1:] + 1, ent[:, -1:] + 2])], 1).contiguous()
+        if self._spare is not None:  # every env's next episodes (one per spare slot), in the background
+            ent, K = self._entropy, self._slots
+            self._spare_ent = torch.cat([ent[:, :-1].repeat(K, 1),
+                                         torch.cat([ent[:, -1:] + 1 + q for q in range(K)])], 1).contiguous()
             self._spare_par.zero_()
+            self._cohorts = []
             self._prepare_spares(None)
             self._spare_prev = self._spare_ready
         obs = self.observation_type.observe()
@@ -409,7 +430,19 @@ class VecIntersectionEnv:
         self._side_i = (self._side_i + 1) % len(self._sides)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            ix_reset(self._spare, self.network, self.params, self.ix, self._spare_ent, mask)
+            if mask is None or not self._chunk:  # the whole reset at once
+                ix_reset(self._spare, self.network, self.params, self.ix, self._spare_ent, mask)
+            else:  # begin this step's resets, warm every reset in flight one chunk, finish the oldest
+                self._cohorts.append(mask)
+                warm = self._cohorts[0]
+                for m in self._cohorts[1:]:
+                    warm = warm | m
+                last = len(self._cohorts) == self._n_chunks
+                ops.T.ix_reset_parts_(self._spare.tensors(), ops.st(self.network.table), ops.st(self.params),
+                                      ops.st(self.ix), 7 if last else 3, self._spare_ent, mask, warm, self._chunk,
+                                      self._cohorts[0] if last else None)
+                if last:
+                    self._cohorts.pop(0)
             ev = torch.cuda.Event()
             ev.record(side)
         if mask is not None:
@@ -550,7 +583,7 @@ class VecIntersectionEnv:
         if self._spare is not None:  # its own spare scenes, side streams and events
             self._join_sides()  # every in-flight spare reset (not only the latest) lands before the clone
             new._spare = self._spare.clone()
-            new._spare_slot = (new._spare.rows(0, self.num_envs), new._spare.rows(self.num_envs, self.num_envs))
+            new._cohorts = [m.clone() for m in self._cohorts]
             new._spare_ent = self._spare_ent.clone()
             new._spare_par = self._spare_par.clone()
             new._order = self._order.clone()
