@@ -400,7 +400,7 @@ int ttrl_copy_envs(const ttrl_state_t* dst, const ttrl_state_t* src, const uint8
 int ttrl_ix_clear_spawn(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                         const ttrl_ix_cfg_t* cfg, const uint8_t* mask, void* stream);
 /* VecIntersectionEnv.step after ttrl_env_step (fused frames, observation, rewards), with the
- * auto-reset from scenes reset ahead of time, in one launch.  spare: K * E rows, K in [2, 8] (slot
+ * auto-reset from scenes reset ahead of time, in one launch.  spare: K * E rows, K in [2, 16] (slot
  * q of env e is row q * E + e), reset by ttrl_ix_reset from spare_entropy.  An env with
  * terminated | truncated == 0 runs the IntersectionEnv.step tail (as ttrl_ix_clear_spawn) and
  * copies its observation row obs_in -> obs_out; a finished env instead takes the spare row of slot

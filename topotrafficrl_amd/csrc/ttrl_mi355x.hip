@@ -5089,7 +5089,7 @@ int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
       n_words > 65 || !time || !done || !spare_mask)
     return TTRL_E_ARG;
   const int K = s->n_envs > 0 ? spare->n_envs / s->n_envs : 0;
-  if (K < 2 || K > 8 || spare->n_envs != K * s->n_envs || spare->n_veh != s->n_veh || spare->dtype != s->dtype || !spare->rng ||
+  if (K < 2 || K > 16 || spare->n_envs != K * s->n_envs || spare->n_veh != s->n_veh || spare->dtype != s->dtype || !spare->rng ||
       !spare->reg_steps || !spare->route_road || !spare->route_lane || !spare->route_n || !spare->yielding)
     return TTRL_E_ARG;
   const void* sp[] = {spare->x, spare->y, spare->heading, spare->speed, spare->target_speed, spare->timer,

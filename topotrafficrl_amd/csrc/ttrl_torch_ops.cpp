@@ -404,10 +404,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ix_step_tail_(
   ttrl_state_t s = state_of(state), sp = state_of(spare);
   const auto& x = state[0];
   const int64_t K = s.n_envs > 0 ? sp.n_envs / s.n_envs : 0;  // spare slots per env
-  TORCH_CHECK(spare[0].device() == x.device() && K >= 2 && K <= 8 && sp.n_envs == K * s.n_envs &&
+  TORCH_CHECK(spare[0].device() == x.device() && K >= 2 && K <= 16 && sp.n_envs == K * s.n_envs &&
                   sp.n_veh == s.n_veh &&
                   sp.dtype == s.dtype,
-              "ttrl: spare must be a state of K * n_envs rows (K in [2, 8]) of the same width and dtype on the "
+              "ttrl: spare must be a state of K * n_envs rows (K in [2, 16]) of the same width and dtype on the "
               "state's device");
   for (const at::Tensor* t : {&terminated, &truncated})
     TORCH_CHECK(t->device() == x.device() && t->numel() == s.n_envs && t->is_contiguous() &&

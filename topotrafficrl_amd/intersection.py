@@ -338,8 +338,8 @@ class VecIntersectionEnv:
         if c["auto_reset"] and c["overlap_resets"]:
             E = self.num_envs
             chunk, wf = int(c["reset_chunk_frames"]), int(self.ix.warmup_frames)
-            # chunks must divide the warm-up, and the tail kernel rotates over at most 8 slots
-            self._chunk = chunk if 0 < chunk < wf and wf % chunk == 0 and wf // chunk + 1 <= 8 else 0
+            # chunks must divide the warm-up, and the tail kernel rotates over at most 16 slots
+            self._chunk = chunk if 0 < chunk < wf and wf % chunk == 0 and wf // chunk + 1 <= 16 else 0
             self._n_chunks = wf // self._chunk if self._chunk else 1
             self._slots = self._n_chunks + 1 if self._chunk else 2  # spare scenes per env
             self._cohorts = []  # the consumed-row masks of the resets still warming up, oldest first
@@ -445,8 +445,9 @@ class VecIntersectionEnv:
                     self._cohorts.pop(0)
             ev = torch.cuda.Event()
             ev.record(side)
-        if mask is not None:
-            mask.record_stream(side)
+        # the masks are read on the side stream (a fork's cloned cohorts were made on the main one)
+        for m in ([mask] if mask is not None else []) + self._cohorts:
+            m.record_stream(side)
         self._spare_prev, self._spare_ready = self._spare_ready, ev
 
     def step(self, action):
