@@ -289,13 +289,17 @@ int ttrl_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road,
  * order (optional, device [n_envs] int32): a permutation of the envs, the order in which the
  * launch's workgroups take them on a road network (as ttrl_ix_step_tail writes it: heaviest
  * first); a dispatch order only -- every output is the same with or without it; other roads
- * ignore it. */
+ * ignore it.  action_lut (host, n_action_lut <= 8 meta-action codes; n_action_lut 0: none): actions
+ * are action indices, mapped to their codes in the launch (DiscreteMetaAction's index -> action
+ * name -> code), so a non-identity action set needs no lookup launch; an index outside the table
+ * is no meta-action. */
 int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                   const int32_t* actions, int32_t frames, double dt,
                   const ttrl_kin_cfg_t* obs_cfg, float* obs, int32_t* obs_ids,
                   const ttrl_reward_cfg_t* reward_cfg, double* time, double time_inc,
                   float* reward, uint8_t* terminated, uint8_t* truncated, float* components,
-                  void* ego_speed, uint8_t* ego_crashed, const int32_t* order, void* stream);
+                  void* ego_speed, uint8_t* ego_crashed, const int32_t* order, const int32_t* action_lut,
+                  int32_t n_action_lut, void* stream);
 /* Road.neighbour_vehicles(v, lane) for every vehicle; query_lane [E*N] int32
  * (-1 = the vehicle's own lane).  front/rear [E*N] int32 vehicle index or -1. */
 int ttrl_neighbours(const ttrl_state_t* s, const ttrl_lane_table_t* road,

@@ -24,7 +24,7 @@ _SIGS = {
     "ttrl_road_step": ([_P, _P, _P, C.c_double, _P], C.c_int),
     "ttrl_simulate": ([_P, _P, _P, _P, C.c_int32, C.c_double, _P], C.c_int),
     "ttrl_env_step": ([_P, _P, _P, _P, C.c_int32, C.c_double, _P, _P, _P, _P, _P, C.c_double, _P, _P, _P, _P, _P,
-                       _P, _P, _P], C.c_int),
+                       _P, _P, _P, C.c_int32, _P], C.c_int),
     "ttrl_neighbours": ([_P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_observe_kinematics": ([_P, _P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_observe_kinematics_masked": ([_P, _P, _P, _P, _P, _P, _P, _P], C.c_int),

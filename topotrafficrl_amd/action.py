@@ -32,17 +32,26 @@ class BatchedDiscreteMetaAction:
             raise ValueError("At least longitudinal or lateral actions must be included")
         self.actions_indexes = {v: k for k, v in self.actions.items()}
         self._lut = None
+        self._tab = None  # the index -> code table (_indices)
 
     def space(self) -> Discrete:
         return Discrete(len(self.actions))
 
-    def _codes(self, actions) -> torch.Tensor:
-        dev = self.env.road.state.device
-        if self._lut is None or self._lut.device != dev:
-            self._lut = torch.tensor([self._CODE[self.actions[i]] for i in range(len(self.actions))],
-                                     dtype=torch.int32, device=dev)
-            # the default action set maps index i to code i: no lookup launch then
-            self._identity = bool(torch.equal(self._lut.cpu(), torch.arange(len(self.actions), dtype=torch.int32)))
+    def _table(self) -> list[int]:
+        """The meta-action code of each action index (ttrl_meta_action's codes)."""
+        return [self._CODE[self.actions[i]] for i in range(len(self.actions))]
+
+    def _indices(self, actions) -> tuple[torch.Tensor, list[int] | None]:
+        """(int32 device action indices, the index -> code table, or None when index i is code i):
+        ttrl_env_step maps the indices in its own launch, so the step needs no lookup launch."""
+        if self._tab is None:
+            self._tab = self._table()
+        table = self._tab
+        a = self._checked(actions)
+        a = a.to(device=self.env.road.state.device, dtype=torch.int32).reshape(-1)
+        return a, (None if table == list(range(len(table))) else table)
+
+    def _checked(self, actions) -> torch.Tensor:
         a = torch.as_tensor(actions)
         if a.device.type == "cpu":
             an = a.numpy()
@@ -51,9 +60,17 @@ class BatchedDiscreteMetaAction:
         elif self.check_device_actions and a.numel():
             lo, hi = torch.aminmax(a)
             torch._assert_async((lo >= 0) & (hi < len(self.actions)), "action out of range")
+        return a
+
+    def _codes(self, actions) -> torch.Tensor:
+        dev = self.env.road.state.device
+        if self._lut is None or self._lut.device != dev:
+            self._lut = torch.tensor(self._table(), dtype=torch.int32, device=dev)
+            # the default action set maps index i to code i: no lookup launch then
+            self._identity = bool(torch.equal(self._lut.cpu(), torch.arange(len(self.actions), dtype=torch.int32)))
+        a = self._checked(actions)
         if self._identity:
             return a.to(device=dev, dtype=torch.int32).reshape(-1)
-        # int32 / int64 indices index the table directly (one gather launch, no cast launch first)
         a = a.to(dev).reshape(-1)
         return self._lut[a if a.dtype in (torch.int32, torch.int64) else a.long()]
 

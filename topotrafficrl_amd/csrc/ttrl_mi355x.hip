@@ -1835,6 +1835,10 @@ struct StepOut {
   // entries: none; null: slot order).  A dispatch order only: every env's result is independent
   // of it.
   const int32_t* order;
+  // n_lut > 0: actions[] are action indices, mapped to meta-action codes by lut (an index outside
+  // the table: no meta-action)
+  int8_t lut[8];
+  int32_t n_lut;
 };
 
 // The env of workgroup slot q: order[q] under a dispatch order, else q (slots past the batch stay
@@ -1988,7 +1992,14 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
   for (int frame = 0; frame < frames; ++frame) {
     // ---------------- ego meta-action (DiscreteMetaAction.act, action.py:259-260) ----
     if ((mode & MODE_META) && frame == 0 && actions && present && kind == TTRL_MDP) {
-      const int act = actions[env];
+      int act = actions[env];
+      if (so.n_lut > 0) {  // the env's action index -> its meta-action code (a select chain)
+        int c = -1;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (q < so.n_lut && act == q) c = so.lut[q];
+        act = c;
+      }
       const T x = V.x[me], y = V.y[me], h = V.h[me], v = V.v[me];
       T ts = V.ts[me];
       int tgt = V.tgt[me];
@@ -4768,13 +4779,19 @@ int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
                   int32_t frames, double dt, const ttrl_kin_cfg_t* obs_cfg, float* obs, int32_t* obs_ids,
                   const ttrl_reward_cfg_t* reward_cfg, double* time, double time_inc, float* reward,
                   uint8_t* terminated, uint8_t* truncated, float* components, void* ego_speed, uint8_t* ego_crashed,
-                  const int32_t* order, void* stream) {
+                  const int32_t* order, const int32_t* action_lut, int32_t n_action_lut, void* stream) {
   int rc = check_state(s, road);
   if (rc) return rc < 0 ? rc : TTRL_OK;
   if ((!obs_cfg) != (!obs) || (obs_cfg && check_kin_cfg(s, obs_cfg))) return TTRL_E_ARG;
   if (reward_cfg && (!time || !reward || !terminated || !truncated || (!ego_speed) != (!ego_crashed)))
     return TTRL_E_ARG;
+  if (n_action_lut < 0 || n_action_lut > 8 || (n_action_lut > 0 && !action_lut)) return TTRL_E_ARG;
   StepOut so{};
+  for (int q = 0; q < n_action_lut; ++q) {
+    if (action_lut[q] < TTRL_LANE_LEFT || action_lut[q] > TTRL_SLOWER) return TTRL_E_ARG;
+    so.lut[q] = (int8_t)action_lut[q];
+  }
+  so.n_lut = n_action_lut;
   if (obs_cfg) { so.kcfg = *obs_cfg; so.obs = obs; so.ids = obs_ids; }
   if (reward_cfg) {
     so.rcfg = *reward_cfg; so.time = time; so.time_inc = time_inc; so.reward = reward; so.term = terminated;

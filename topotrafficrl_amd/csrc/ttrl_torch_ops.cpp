@@ -155,7 +155,8 @@ env_step_outputs(const at::Tensor& x, const ttrl_kin_cfg_t* kc) {
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> env_step_(
     at::TensorList state, const at::Tensor& lanes, const at::Tensor& params, const c10::optional<at::Tensor>& actions,
     int64_t frames, double dt, const c10::optional<at::Tensor>& kin_cfg, const at::Tensor& reward_cfg,
-    const at::Tensor& time, double time_inc, const c10::optional<at::Tensor>& order) {
+    const at::Tensor& time, double time_inc, const c10::optional<at::Tensor>& order,
+    at::OptionalIntArrayRef action_lut) {
   check_hip(state[0]);
   ttrl_state_t s = state_of(state);
   const ttrl_kin_cfg_t* kc = kin_cfg && kin_cfg->defined() ? as_struct<ttrl_kin_cfg_t>(*kin_cfg, "kin_cfg") : nullptr;
@@ -168,6 +169,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
     TORCH_CHECK(order->device() == state[0].device() && order->scalar_type() == at::kInt && order->is_contiguous() &&
                     order->numel() >= s.n_envs,
                 "ttrl: order must be a contiguous int32 tensor of at least n_envs entries on the state's device");
+  std::vector<int32_t> lut;  // the action index -> meta-action code table (host; ttrl_env_step copies it)
+  if (action_lut.has_value())
+    for (int64_t c : *action_lut) lut.push_back(static_cast<int32_t>(c));
   auto out = env_step_outputs(state[0], kc);
   auto& [obs, ids, rew, term, trunc, comp, speed, crashed] = out;
   ok(ttrl_env_step(&s, as_struct<ttrl_lane_table_t>(lanes, "lanes"), as_struct<ttrl_params_t>(params, "params"),
@@ -177,7 +181,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
                    rew.data_ptr<float>(), static_cast<uint8_t*>(term.data_ptr()),
                    static_cast<uint8_t*>(trunc.data_ptr()), comp.data_ptr<float>(), speed.data_ptr(),
                    static_cast<uint8_t*>(crashed.data_ptr()), od ? order->data_ptr<int32_t>() : nullptr,
-                   stream_of(state[0])),
+                   lut.empty() ? nullptr : lut.data(), static_cast<int32_t>(lut.size()), stream_of(state[0])),
      "ttrl_env_step");
   return out;
 }
@@ -603,7 +607,7 @@ void meta_none_meta(at::TensorList, const at::Tensor&, const at::Tensor&, const 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor>
 meta_env_step(at::TensorList state, const at::Tensor&, const at::Tensor&, const c10::optional<at::Tensor>&, int64_t,
               double, const c10::optional<at::Tensor>& kin_cfg, const at::Tensor&, const at::Tensor&, double,
-              const c10::optional<at::Tensor>&) {
+              const c10::optional<at::Tensor>&, at::OptionalIntArrayRef) {
   const ttrl_kin_cfg_t* kc = kin_cfg && kin_cfg->defined() ? as_struct<ttrl_kin_cfg_t>(*kin_cfg, "kin_cfg") : nullptr;
   return env_step_outputs(meta_x(state), kc);
 }
@@ -705,8 +709,8 @@ TORCH_LIBRARY(ttrl, m) {
   m.def("road_step_(Tensor(a!)[] state, Tensor lanes, Tensor params, float dt) -> ()");
   m.def("meta_action_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor actions) -> ()");
   m.def("env_step_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor? actions, int frames, float dt, "
-        "Tensor? kin_cfg, Tensor reward_cfg, Tensor(b!) time, float time_inc, Tensor? order=None) -> (Tensor obs, "
-        "Tensor ids, "
+        "Tensor? kin_cfg, Tensor reward_cfg, Tensor(b!) time, float time_inc, Tensor? order=None, "
+        "int[]? action_lut=None) -> (Tensor obs, Tensor ids, "
         "Tensor reward, Tensor terminated, Tensor truncated, Tensor components, Tensor ego_speed, Tensor ego_crashed)");
   m.def("neighbours(Tensor[] state, Tensor lanes, Tensor? query_lane) -> (Tensor front, Tensor rear)");
   // the np_random-shuffled observation (order_shuffled 2) advances state.rng: the state is mutated

@@ -254,17 +254,17 @@ class VecHighwayEnv:
         truncated))."""
         frames = int(self.config["simulation_frequency"] // self.config["policy_frequency"])
         dt = 1 / self.config["simulation_frequency"]
-        codes = None
-        if action is not None and not self.config["manual_control"]:
-            codes = self.action_type._codes(action)
+        act = action is not None and not self.config["manual_control"]
         self.steps += frames
         if not tail:
-            self.road.simulate(codes, frames, dt)
+            self.road.simulate(self.action_type._codes(action) if act else None, frames, dt)
             return None
+        # action indices: the launch maps them to meta-action codes (no lookup launch)
+        idx, lut = self.action_type._indices(action) if act else (None, None)
         kin = isinstance(self.observation_type, BatchedKinematicObservation)
         kc = self.observation_type.fused_cfg() if kin else None
-        obs, ids, *outs = self.road.env_step(codes, frames, dt, kc, self.reward_cfg, self.time,
-                                             1 / self.config["policy_frequency"])
+        obs, ids, *outs = self.road.env_step(idx, frames, dt, kc, self.reward_cfg, self.time,
+                                             1 / self.config["policy_frequency"], None, lut)
         if kin:
             self.observation_type.fused_result(obs, ids)
         return (obs if kin else None), _keep_tail(self, outs)

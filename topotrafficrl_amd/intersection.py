@@ -479,20 +479,21 @@ class VecIntersectionEnv:
         ot = self.observation_type
         kin = isinstance(ot, BatchedKinematicObservation)
         frames = int(self.config["simulation_frequency"] // self.config["policy_frequency"])
-        codes = None
+        idx, lut = None, None
         if action is not None and not self.config["manual_control"]:
-            codes = self.action_type._codes(action)
+            idx, lut = self.action_type._indices(action)  # the launch maps them to meta-action codes
         self.steps += frames
-        obs, ids, *outs = self.road.env_step(codes, frames, 1 / self.config["simulation_frequency"],
+        # the slots this step's tail takes were prepared two steps back at the latest: the wait is
+        # enqueued ahead of the launch, so it has long resolved when the tail follows the launch
+        torch.cuda.current_stream(self.device).wait_event(self._spare_prev)
+        obs, ids, *outs = self.road.env_step(idx, frames, 1 / self.config["simulation_frequency"],
                                              ot.fused_cfg() if kin else None, self.reward_cfg, self.time,
-                                             1 / self.config["policy_frequency"], self._order)
+                                             1 / self.config["policy_frequency"], self._order, lut)
         reward, terminated, truncated = _keep_tail(self, outs)
         if not kin:
             obs = ot.observe()
         info = self._info(obs, action)
         _device_only(self.state)
-        # the slots this step takes were prepared two steps back at the latest
-        torch.cuda.current_stream(self.device).wait_event(self._spare_prev)
         # the tail launch re-observes a new scene with one slot per lane of a wavefront: wider rows
         # (vehicle_slots > 64) take the masked observation launch instead, which draws the same
         # shuffles from the same generators (test_overlapped_resets_equal_in_place_resets[96])
