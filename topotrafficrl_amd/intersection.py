@@ -406,6 +406,7 @@ class VecIntersectionEnv:
                                          torch.cat([ent[:, -1:] + 1 + q for q in range(K)])], 1).contiguous()
             self._spare_par.zero_()
             self._cohorts = []
+            self._pinned = []  # the side streams the current spare buffers are recorded on
             self._prepare_spares(None)
             self._spare_prev = self._spare_ready
         obs = self.observation_type.observe()
@@ -420,20 +421,28 @@ class VecIntersectionEnv:
             main.wait_stream(side)
 
     def _prepare_spares(self, mask: torch.Tensor | None) -> None:
-        """Reset the spare scenes of ``mask`` ([2E]; all: None) on the next side stream, after the
-        main stream's work so far (the swap that consumed them).  The side stream reads the seed
-        words and episode counters of the masked rows only; the main stream writes a row's counter
-        when it consumes that row again, two steps later at the earliest, after waiting for this
-        reset (_spare_prev), so the rows in flight are never written under it."""
+        """Reset the spare scenes of ``mask`` ([slots * E]; all: None) on the next side stream,
+        after the main stream's work so far (the swap that consumed them) -- whole, or chunked (the
+        class comment in _build).  The side stream reads the seed words and episode counters of the
+        masked rows only; the main stream writes a row's counter when it consumes that row again,
+        after waiting for the side work that finished it (_spare_prev), so the rows in flight are
+        never written under it.  The spare buffers are made on the main stream and used on the side
+        ones: they are recorded there, so freeing them (a reset, a dropped env) waits for that work."""
         main = torch.cuda.current_stream(self.device)
         side = self._sides[self._side_i]
         self._side_i = (self._side_i + 1) % len(self._sides)
         side.wait_stream(main)
+        if side not in self._pinned:  # once per side stream and buffer set
+            for t in self._spare.tensors() + [self._spare_ent]:
+                t.record_stream(side)
+            self._pinned.append(side)
         with torch.cuda.stream(side):
             if mask is None or not self._chunk:  # the whole reset at once
                 ix_reset(self._spare, self.network, self.params, self.ix, self._spare_ent, mask)
             else:  # begin this step's resets, warm every reset in flight one chunk, finish the oldest
                 self._cohorts.append(mask)
+                for m in self._cohorts:  # read on the side stream (a fork's cohorts were cloned on the
+                    m.record_stream(side)  # main one), before the oldest is dropped below
                 warm = self._cohorts[0]
                 for m in self._cohorts[1:]:
                     warm = warm | m
@@ -445,9 +454,8 @@ class VecIntersectionEnv:
                     self._cohorts.pop(0)
             ev = torch.cuda.Event()
             ev.record(side)
-        # the masks are read on the side stream (a fork's cloned cohorts were made on the main one)
-        for m in ([mask] if mask is not None else []) + self._cohorts:
-            m.record_stream(side)
+        if mask is not None:
+            mask.record_stream(side)
         self._spare_prev, self._spare_ready = self._spare_ready, ev
 
     def step(self, action):
@@ -483,9 +491,6 @@ class VecIntersectionEnv:
         if action is not None and not self.config["manual_control"]:
             idx, lut = self.action_type._indices(action)  # the launch maps them to meta-action codes
         self.steps += frames
-        # the slots this step's tail takes were prepared two steps back at the latest: the wait is
-        # enqueued ahead of the launch, so it has long resolved when the tail follows the launch
-        torch.cuda.current_stream(self.device).wait_event(self._spare_prev)
         obs, ids, *outs = self.road.env_step(idx, frames, 1 / self.config["simulation_frequency"],
                                              ot.fused_cfg() if kin else None, self.reward_cfg, self.time,
                                              1 / self.config["policy_frequency"], self._order, lut)
@@ -494,6 +499,9 @@ class VecIntersectionEnv:
             obs = ot.observe()
         info = self._info(obs, action)
         _device_only(self.state)
+        # the slots this step's tail takes were prepared two steps back at the latest (waited for
+        # here, after the step launch is queued: the side work gets the launch's time as slack)
+        torch.cuda.current_stream(self.device).wait_event(self._spare_prev)
         # the tail launch re-observes a new scene with one slot per lane of a wavefront: wider rows
         # (vehicle_slots > 64) take the masked observation launch instead, which draws the same
         # shuffles from the same generators (test_overlapped_resets_equal_in_place_resets[96])
@@ -586,6 +594,7 @@ class VecIntersectionEnv:
             self._join_sides()  # every in-flight spare reset (not only the latest) lands before the clone
             new._spare = self._spare.clone()
             new._cohorts = [m.clone() for m in self._cohorts]
+            new._pinned = []
             new._spare_ent = self._spare_ent.clone()
             new._spare_par = self._spare_par.clone()
             new._order = self._order.clone()
