@@ -326,11 +326,12 @@ class VecIntersectionEnv:
         # waves last ~a third as long and mostly finish inside the step launch they start behind
         # (a warm-up wave resident when a step launch starts holds one of the workgroup slots the
         # launch needs, pushing a workgroup into a second round).  A scene consumed at step t is
-        # begun and warmed 15 frames after step t's tail, warmed 15 more after t+1's, and finished
-        # after t+2's; every step's side work is one launch over all resets in flight (begin,
-        # the union's chunk, finish) on one side stream.  Each env then owns C + 1 = 4 spare
-        # scenes (C chunks), so a slot is taken again 4 finishes later and the step still waits
-        # only for the side work of two steps back.
+        # begun and warmed 15 frames after step t's tail, warmed 15 more after t+1's and t+2's
+        # (side stream A: one call per step, begin + the chunk of every reset in flight), and
+        # finished after t+3's tail on side stream B -- at the start of a step, so that B's
+        # latency-bound finish has ended before the next tail instead of running beside it.  Each
+        # env then owns C + 1 = 4 spare scenes (C chunks), so a slot is taken again 4 finishes
+        # later; the tail waits for the previous step's finishes (_wait_ev).
         self._spare = None
         # optional int64 device scalar: each overlapped step's tail adds the vehicles present after
         # it (the next step's live vehicles) -- a live vehicle-step count with no launch of its own
@@ -349,10 +350,11 @@ class VecIntersectionEnv:
             # heaviest first, see ix_order_kernel) and its scratch; any permutation is valid
             self._order = torch.cat([torch.arange(E, dtype=torch.int32, device=self.device),
                                      torch.zeros(E, dtype=torch.int32, device=self.device)])
-            n_sides = 1 if self._chunk else max(1, int(c["reset_streams"]))
+            n_sides = 2 if self._chunk else max(1, int(c["reset_streams"]))  # chunks: A (begin, warm), B (finish)
             self._sides = tuple(torch.cuda.Stream(self.device) for _ in range(n_sides))
             self._side_i = 0
-            self._spare_ready = self._spare_prev = torch.cuda.Event()
+            self._spare_ready = self._spare_prev = self._wait_ev = self._warm_ev = torch.cuda.Event()
+            self._to_finish = None  # chunked: the cohort whose last chunk ran in the previous step
             # [slots * E, words + 1]: each spare scene's seed words and episode counter (the last
             # word); ix_step_tail_ advances the counter of a consumed row by the number of slots
             self._spare_ent = None
@@ -405,10 +407,10 @@ class VecIntersectionEnv:
             self._spare_ent = torch.cat([ent[:, :-1].repeat(K, 1),
                                          torch.cat([ent[:, -1:] + 1 + q for q in range(K)])], 1).contiguous()
             self._spare_par.zero_()
-            self._cohorts = []
+            self._cohorts, self._to_finish = [], None
             self._pinned = []  # the side streams the current spare buffers are recorded on
             self._prepare_spares(None)
-            self._spare_prev = self._spare_ready
+            self._spare_prev = self._wait_ev = self._warm_ev = self._spare_ready
         obs = self.observation_type.observe()
         self._rewards_and_dones()  # abstract.py:211 reset's _info evaluates _rewards too
         return obs, self._info(obs, None)
@@ -429,34 +431,51 @@ class VecIntersectionEnv:
         never written under it.  The spare buffers are made on the main stream and used on the side
         ones: they are recorded there, so freeing them (a reset, a dropped env) waits for that work."""
         main = torch.cuda.current_stream(self.device)
-        side = self._sides[self._side_i]
-        self._side_i = (self._side_i + 1) % len(self._sides)
-        side.wait_stream(main)
-        if side not in self._pinned:  # once per side stream and buffer set
-            for t in self._spare.tensors() + [self._spare_ent]:
-                t.record_stream(side)
-            self._pinned.append(side)
-        with torch.cuda.stream(side):
-            if mask is None or not self._chunk:  # the whole reset at once
-                ix_reset(self._spare, self.network, self.params, self.ix, self._spare_ent, mask)
-            else:  # begin this step's resets, warm every reset in flight one chunk, finish the oldest
-                self._cohorts.append(mask)
-                for m in self._cohorts:  # read on the side stream (a fork's cohorts were cloned on the
-                    m.record_stream(side)  # main one), before the oldest is dropped below
+        for side in self._sides:
+            if side not in self._pinned:  # once per side stream and buffer set
+                for t in self._spare.tensors() + [self._spare_ent]:
+                    t.record_stream(side)
+                self._pinned.append(side)
+        args = (ops.st(self.network.table), ops.st(self.params), ops.st(self.ix))
+        if mask is not None and self._chunk:
+            A, B = self._sides
+            if self._to_finish is not None:  # B: finish the resets whose last chunk ran in the previous step
+                B.wait_stream(main)
+                B.wait_event(self._warm_ev)
+                fin = self._to_finish
+                fin.record_stream(B)
+                with torch.cuda.stream(B):
+                    ops.T.ix_reset_parts_(self._spare.tensors(), *args, 4, None, None, None, 0, fin)
+                    self._wait_ev = torch.cuda.Event()
+                    self._wait_ev.record(B)
+                self._to_finish = None
+            A.wait_stream(main)  # A: begin this step's resets, warm every reset in flight one chunk
+            self._cohorts.append(mask)
+            for m in self._cohorts:  # read on A (a fork's cohorts were cloned on the main stream)
+                m.record_stream(A)
+            with torch.cuda.stream(A):
                 warm = self._cohorts[0]
                 for m in self._cohorts[1:]:
                     warm = warm | m
-                last = len(self._cohorts) == self._n_chunks
-                ops.T.ix_reset_parts_(self._spare.tensors(), ops.st(self.network.table), ops.st(self.params),
-                                      ops.st(self.ix), 7 if last else 3, self._spare_ent, mask, warm, self._chunk,
-                                      self._cohorts[0] if last else None)
-                if last:
-                    self._cohorts.pop(0)
+                ops.T.ix_reset_parts_(self._spare.tensors(), *args, 3, self._spare_ent, mask, warm, self._chunk, None)
+                self._warm_ev = torch.cuda.Event()
+                self._warm_ev.record(A)
+            if len(self._cohorts) == self._n_chunks:
+                self._to_finish = self._cohorts.pop(0)
+            self._spare_prev, self._spare_ready = self._spare_ready, self._warm_ev
+            return
+        side = self._sides[0] if self._chunk else self._sides[self._side_i]  # the whole reset at once
+        self._side_i = (self._side_i + 1) % len(self._sides)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            ix_reset(self._spare, self.network, self.params, self.ix, self._spare_ent, mask)
             ev = torch.cuda.Event()
             ev.record(side)
         if mask is not None:
             mask.record_stream(side)
         self._spare_prev, self._spare_ready = self._spare_ready, ev
+        if not self._chunk:
+            self._wait_ev = self._spare_prev  # the tail waits for the resets of two steps back
 
     def step(self, action):
         """IntersectionEnv.step (intersection_env.py:135-139) over AbstractEnv.step (abstract.py:224-250)."""
@@ -501,7 +520,7 @@ class VecIntersectionEnv:
         _device_only(self.state)
         # the slots this step's tail takes were prepared two steps back at the latest (waited for
         # here, after the step launch is queued: the side work gets the launch's time as slack)
-        torch.cuda.current_stream(self.device).wait_event(self._spare_prev)
+        torch.cuda.current_stream(self.device).wait_event(self._wait_ev)
         # the tail launch re-observes a new scene with one slot per lane of a wavefront: wider rows
         # (vehicle_slots > 64) take the masked observation launch instead, which draws the same
         # shuffles from the same generators (test_overlapped_resets_equal_in_place_resets[96])
@@ -594,6 +613,7 @@ class VecIntersectionEnv:
             self._join_sides()  # every in-flight spare reset (not only the latest) lands before the clone
             new._spare = self._spare.clone()
             new._cohorts = [m.clone() for m in self._cohorts]
+            new._to_finish = None if self._to_finish is None else self._to_finish.clone()
             new._pinned = []
             new._spare_ent = self._spare_ent.clone()
             new._spare_par = self._spare_par.clone()
@@ -602,6 +622,6 @@ class VecIntersectionEnv:
             new._side_i = 0
             new._spare_ready = torch.cuda.Event()
             new._spare_ready.record(torch.cuda.current_stream(self.device))
-            new._spare_prev = new._spare_ready
+            new._spare_prev = new._wait_ev = new._warm_ev = new._spare_ready
         new.define_spaces()
         return new
