@@ -206,9 +206,15 @@ def launch_ranks(n: int, argv: list) -> int:
         print(f"bench.py: expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr)
         return 1
     out = json.loads(lines[0])
-    if out.get("n_gpus") != n:
+    if out.get("ranks", out.get("n_gpus")) != n:
+        print(f"bench.py: --gpus {n} but the job reports {out.get('ranks')} ranks", file=sys.stderr)
+        return 3
+    if out.get("n_gpus") != n and not out.get("shared_gpu"):
         print(f"bench.py: --gpus {n} but the ranks report n_gpus = {out.get('n_gpus')}", file=sys.stderr)
         return 3
+    if out.get("shared_gpu"):  # a rehearsal of the N-rank logic, never an N-GPU measurement
+        print(f"bench.py: {n} ranks shared one GPU (TTRL_BENCH_SHARED_GPU=1): n_gpus = 1, not a scaling point",
+              file=sys.stderr)
     out["launcher"] = {"ranks": n, "cmd": "python -m torch.distributed.run --nnodes=1 --nproc-per-node "
                        f"{n} --master-addr 127.0.0.1 bench.py ...", "parent_imported_torch": "torch" in sys.modules}
     print(json.dumps(out), flush=True)
@@ -229,7 +235,7 @@ def dry_run(args, rank: int, world: int) -> None:
         dist.all_gather_object(shards, (offset, count))
     elapsed = sharding.max_over_ranks(0.001 * (rank + 1))
     if rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": world, "scaling": "strong" if args.strong else "weak",
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": world, "scaling": "strong" if args.strong else "weak",
                           "global_envs": g, "shards": shards, "max_elapsed": elapsed}), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -320,7 +326,7 @@ def main():
     policy = None
     if args.config == 5:
         from topotrafficrl_amd.agent import EgoAttentionPolicy
-        policy = EgoAttentionPolicy(device=dev, seed=0)
+        policy = EgoAttentionPolicy(device=dev, seed=0, env_id_offset=offset)  # draws keyed on global env ids
     obs, _ = env.reset(seed=12345)
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
@@ -445,7 +451,11 @@ def main():
         "metric": "vehicle-steps/sec at 4096 envs×64 vehicles; 1/2/4/8 GPUs; HBM GB/s achieved",
         "value": value,
         "unit": "vehicle-steps/s",
-        "n_gpus": world,
+        # the physical devices: a shared-GPU rehearsal (TTRL_BENCH_SHARED_GPU=1) runs every rank on
+        # cuda:0, so it is one GPU however many ranks it has (``ranks``, ``shared_gpu``)
+        "n_gpus": 1 if shared else world,
+        "ranks": world,
+        "shared_gpu": shared,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define TTRL_ABI_VERSION 5
+#define TTRL_ABI_VERSION 6
 #define TTRL_MAX_LANES 32
 #define TTRL_MAX_ROADS 32
 #define TTRL_MAX_NODES 32
@@ -289,7 +289,8 @@ int ttrl_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road,
  * order (optional, device [n_envs] int32): a permutation of the envs, the order in which the
  * launch's workgroups take them on a road network (as ttrl_ix_step_tail writes it: heaviest
  * first); a dispatch order only -- every output is the same with or without it; other roads
- * ignore it.  action_lut (host, n_action_lut <= 8 meta-action codes; n_action_lut 0: none): actions
+ * ignore it.  It must name every env at most once (a repeated env would be written by two
+ * workgroups; not checked, that would need a host sync); a negative entry is an idle slot.  action_lut (host, n_action_lut <= 8 meta-action codes; n_action_lut 0: none): actions
  * are action indices, mapped to their codes in the launch (DiscreteMetaAction's index -> action
  * name -> code), so a non-identity action set needs no lookup launch; an index outside the table
  * is no meta-action. */
@@ -369,14 +370,16 @@ int ttrl_ego_attention_q(const float* obs, int32_t batch, int32_t n_entities, in
  * batch, in the same launch as the forward above: q [batch][n_actions] (as ttrl_ego_attention_q)
  * and actions [batch] int64 = np.argmax(q[e]) (first maximum), replaced with probability epsilon by
  * a uniform action -- the reference's action distribution.  The draws are Philox4x32-10 keyed on
- * seed, counter (env, step): reproducible per (seed, env, step) whatever the batch.  epsilon_dev /
+ * seed, counter (env_offset + e, step), env_offset the global id of row 0 (a rank's shard offset):
+ * reproducible per (seed, global env, step) whatever the batch split, and distinct across the
+ * data-parallel shards of one seed.  epsilon_dev /
  * step_dev (device scalars, optional) override epsilon / step, for captured graphs.  epsilon must
  * lie in [0, 1].  actions / actions32: the same actions as int64 and as int32 (the env's action
  * index type, ttrl_simulate's `actions`); either may be NULL, not both. */
 int ttrl_ego_attention_act(const float* obs, int32_t batch, int32_t n_entities, int32_t n_features,
                            int32_t heads, const float* weights, int32_t n_actions, float epsilon,
                            const float* epsilon_dev, uint64_t seed, int64_t step, const int64_t* step_dev,
-                           float* q, int64_t* actions, int32_t* actions32, void* stream);
+                           int64_t env_offset, float* q, int64_t* actions, int32_t* actions32, void* stream);
 /* IntersectionEnv._reset for the envs with mask[e] != 0 (mask NULL: all): np_random =
  * default_rng(SeedSequence(entropy[e][0..n_words-1])) into state.rng, then _make_vehicles:
  * initial spawns, warmup_frames of Road.act/step (RegulatedRoad), the challenger, the ego

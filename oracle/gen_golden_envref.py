@@ -233,6 +233,7 @@ def episode(env: IntersectionEnv, seed: int, actions: np.ndarray):
     assert np.array_equal(obs0, mine_obs0) and obs0.dtype == mine_obs0.dtype, (seed, "reset obs")
     assert_same_snapshot(X.snapshot(env), X.snapshot(mine), f"s{seed} reset state")
     assert rng_words(env.np_random).tolist() == rng_words(mine.np_random).tolist(), (seed, "reset rng")
+    rng_reset = rng_words(env.np_random)  # np_random after reset: the state step 0 starts from
     # AbstractEnv.reset's _info is evaluated on the reset scene (its sampled action is unused)
     assert_same_info(info0, mine.info(), f"s{seed} reset info")
     rec = {"pre": [], "frames": [], "post": [], "obs": [], "reward": [], "terminated": [], "truncated": [],
@@ -271,10 +272,10 @@ def episode(env: IntersectionEnv, seed: int, actions: np.ndarray):
         rec["info"].append(info_row(info))
         rec["rng"].append(rng_words(env.np_random))
     rec["obs0"], rec["info0"] = obs0, info_row(info0)
-    return rec, mine.spawns
+    return rec, mine.spawns, rng_reset
 
 
-def save(seed: int, actions: np.ndarray, rec: dict, rng0: np.ndarray, spawns: dict):
+def save(seed: int, actions: np.ndarray, rec: dict, rng0: np.ndarray, spawns: dict, rng_reset: np.ndarray):
     allsnaps = rec["pre"] + rec["post"] + [s for f in rec["frames"] for s in f]
     nmax = max(len(s["x"]) for s in allsnaps)
     d = {}
@@ -292,6 +293,7 @@ def save(seed: int, actions: np.ndarray, rec: dict, rng0: np.ndarray, spawns: di
     d["truncated"] = np.array(rec["truncated"], dtype=np.uint8)
     d["info"] = np.stack(rec["info"])
     d["rng"] = np.stack(rec["rng"])
+    d["rng_reset"] = rng_reset  # rng[p - 1] is the state step p starts from; rng_reset that of step 0
     d["meta"] = np.array([seed, len(actions), nmax], dtype=np.int64)
     # the episode's _spawn_vehicle outcomes (reset and steps): placed, rejected by the 15 m test
     # after its draws, not drawn (the spawn-probability uniform alone)
@@ -310,8 +312,8 @@ def main():
         else:
             actions = np.full(STEPS, 2, dtype=np.int32)
         rng0 = rng_words(np.random.default_rng(seed))
-        rec, spawns = episode(env, seed, actions)
-        d = save(seed, actions, rec, rng0, spawns)
+        rec, spawns, rng_reset = episode(env, seed, actions)
+        d = save(seed, actions, rec, rng0, spawns, rng_reset)
         crashed = int(d["info"][:, 1].max())
         arrived = int((d["info"][:, 4] > 0).any())
         for k, v in spawns.items():

@@ -37,6 +37,26 @@ def load_golden(path):
         return {k: d[k] for k in d.files}
 
 
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    """The worst parity errors the checks observed (tests/parity_log.py), and TTRL_PARITY_LOG."""
+    import parity_log
+    rows = parity_log.rows()
+    if not rows:
+        return
+    tr = terminalreporter
+    tr.write_sep("-", "worst observed parity errors (check, field: worst [where] samples)")
+    for r in rows:
+        if "worst" in r:
+            tr.write_line(f"{r['check']:48s} {r['field']:16s} {r['worst']:.3e}  [{r['where']}]  n={r['samples']}")
+        else:
+            tr.write_line(f"{r['check']:48s} {r['count']:16s} {r['n']}")
+    path = os.environ.get("TTRL_PARITY_LOG")
+    if path:
+        import json
+        with open(path, "w") as f:
+            json.dump(rows, f, indent=1)
+
+
 @pytest.fixture(scope="session")
 def hip_device():
     import torch

@@ -1,16 +1,23 @@
 """The intersection scenario on the MI355X (simulate kernel, NET_GRAPH instance) against the
 golden episodes of the reference (oracle/gen_golden_ix.py) and the float64 oracle.
 
-Tolerances as tests/test_gpu_parity.py: one frame f64 <= 1e-9 * (1 + |x|), 15-frame fused
-steps f64 <= 1e-6 * (1 + |x|); every discrete field exact, including routes (popped in place
-by follow_road), RegulatedRoad yields and the regulation frame counter."""
+Against the reference's goldens, continuous fields relative to 1 + |x| within about 10x the worst
+values seen on the MI355X (round 5, profiles/r05/r05a_parity.json): one frame IX_FRAME_TOL, a
+15-frame fused step IX_STEP_TOL.  The steering command is the loosest field: a vehicle at
+0.15 m/s (ix_s3 step 5) carries the difference between numpy's float64 transcendentals and the
+device's (or glibc's: the oracle lands on the same value) through the steering law's 1 / v^2
+gain, 4.5e-10 in one frame and 8.1e-9 after fifteen; its pose then moves by 2.7e-11.  Against
+the float64 oracle itself (the crowded-lane cases) the highway's F64_TOL.  Every discrete field
+exact, including routes (popped in place by follow_road), RegulatedRoad yields and the
+regulation frame counter."""
 import numpy as np
 import pytest
 import torch
 
+import parity_log
 from conftest import golden_files, load_golden
 from oracle.oracle import HostState
-from test_gpu_parity import to_dev
+from test_gpu_parity import F64_TOL, to_dev
 from test_ix_oracle import LONGI, P_IX, ix_lanes
 from topotrafficrl_amd.road import BatchedRoad, RoadNetwork
 
@@ -20,17 +27,24 @@ CONT = ["x", "y", "heading", "speed", "target_speed", "timer", "steer", "acc"]
 DISC = ["lane", "target_lane", "crashed", "has_impact", "speed_index", "kind", "yielding", "route_n",
         "route_road", "route_lane"]
 IDS = lambda p: p.split("/")[-1][:-4]  # noqa: E731
+IX_FRAME_TOL = {"x": 1e-13, "y": 1e-13, "heading": 1e-13, "speed": 1e-13, "steer": 5e-9, "acc": 1e-12,
+                "target_speed": 0.0, "timer": 0.0, "impact_x": 1e-13, "impact_y": 1e-13}
+IX_STEP_TOL = {"x": 1e-10, "y": 1e-10, "heading": 1e-10, "speed": 1e-12, "steer": 1e-7, "acc": 1e-11,
+               "target_speed": 0.0, "timer": 0.0, "impact_x": 1e-13, "impact_y": 1e-13}
 
 
 def compare(dev, g: HostState, tol: float, n: int):
     d = dev.to_numpy()
+    check, where = parity_log.current_check(), parity_log.current_case()
     for k in CONT:
         a, b = d[k][:, :n].astype(np.float64), g[k][:, :n]
-        err = np.max(np.abs(a - b) / (1 + np.abs(b)))
-        assert err <= tol, (k, err)
+        err = parity_log.note(check, k, parity_log.rel_err(a, b), where)
+        t = tol[k] if isinstance(tol, dict) else tol
+        assert err <= t, (k, err, t)
     imp = g["has_impact"][:, :n].astype(bool)
     for k in ("impact_x", "impact_y"):
-        assert np.max(np.abs(d[k][:, :n][imp] - g[k][:, :n][imp]), initial=0.0) <= tol, k
+        err = parity_log.note(check, k, np.abs(d[k][:, :n][imp] - g[k][:, :n][imp]), where)
+        assert err <= (tol[k] if isinstance(tol, dict) else tol), k
     for k in DISC:
         assert np.array_equal(d[k][:, :n], g[k][:, :n]), (k, d[k][:, :n], g[k][:, :n])
     assert np.array_equal(d["reg_steps"], g["reg_steps"])
@@ -50,9 +64,9 @@ def test_ix_frames_vs_golden(path, pad, hip_device):
             if f > 0:
                 dev.load_numpy(to_dev(HostState.from_ix(d, "frame", (p, f - 1)), hip_device, pad_to=pad).to_numpy())
             road.act()
-            compare(dev, HostState.from_ix(d, "act", (p, f)), 1e-9, n)
+            compare(dev, HostState.from_ix(d, "act", (p, f)), IX_FRAME_TOL, n)
             road.step(1 / 15)
-            compare(dev, HostState.from_ix(d, "frame", (p, f)), 1e-9, n)
+            compare(dev, HostState.from_ix(d, "frame", (p, f)), IX_FRAME_TOL, n)
 
 
 @pytest.mark.parametrize("path", golden_files("ix_*"), ids=IDS)
@@ -63,7 +77,7 @@ def test_ix_fused_steps_vs_golden(path, hip_device):
         dev = to_dev(HostState.from_ix(d, "pre", p), hip_device, pad_to=32)
         road = BatchedRoad(RoadNetwork(ix_lanes(d)), dev, P_IX)
         road.simulate(torch.tensor([LONGI[int(d["actions"][p])]]), 15, 1 / 15)
-        compare(dev, HostState.from_ix(d, "frame", (p, 14)), 1e-6, n)
+        compare(dev, HostState.from_ix(d, "frame", (p, 14)), IX_STEP_TOL, n)
 
 
 def test_ix_batch_of_episodes(hip_device):
@@ -131,13 +145,13 @@ def test_crowded_lane_beyond_list_capacity(hip_device):
     for f in range(4):  # frame by frame
         road.act()
         o.road_act(g)
-        compare(dev, g, 1e-9, n)
+        compare(dev, g, F64_TOL, n)
         road.step(1 / 15)
         o.road_step(g, 1 / 15)
-        compare(dev, g, 1e-9, n)
+        compare(dev, g, F64_TOL, n)
     road.simulate(torch.tensor([LONGI[1]]), 15, 1 / 15)  # and a fused step
     o.simulate(g, [LONGI[1]], 15, 1 / 15)
-    compare(dev, g, 1e-6, n)
+    compare(dev, g, F64_TOL, n)
 
 
 def test_crowded_lane_mobil_on_a_regulated_road(hip_device):
@@ -171,10 +185,10 @@ def test_crowded_lane_mobil_on_a_regulated_road(hip_device):
     for f in range(6):
         road.act()
         o.road_act(g)
-        compare(dev, g, 1e-9, n)
+        compare(dev, g, F64_TOL, n)
         road.step(1 / 15)
         o.road_step(g, 1 / 15)
-        compare(dev, g, 1e-9, n)
+        compare(dev, g, F64_TOL, n)
     road.simulate(torch.tensor([LONGI[1]]), 15, 1 / 15)
     o.simulate(g, [LONGI[1]], 15, 1 / 15)
-    compare(dev, g, 1e-6, n)
+    compare(dev, g, F64_TOL, n)

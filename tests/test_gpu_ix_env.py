@@ -8,7 +8,8 @@ import torch
 
 from conftest import golden_files, load_golden
 from oracle.oracle import HostState, Oracle
-from test_ix_env_oracle import EPISODE_TOL, KIN, obs_tol, same_state
+import parity_log
+from test_ix_env_oracle import EPISODE_TOL, KIN, check_obs, ref_step_input, reward_tol, same_state
 from test_host_logic import _reward_from_terms
 from test_ix_oracle import P_IX
 from topotrafficrl_amd import _abi
@@ -44,11 +45,12 @@ def test_device_episodes_match_reference(hip_device):
         obs, rew, term, trunc, info = env.step(torch.from_numpy(acts[p]).to(hip_device))
         st = env.state.to_numpy()
         for e, d in enumerate(GOLD):
-            tol = obs_tol(HostState.from_ix(d, "frame", (p, 14), pad_to=32), EPISODE_TOL)
-            assert np.max(np.abs(obs[e].cpu().numpy() - d["obs"][p])) <= tol, (e, p)
-            assert abs(float(rew[e]) - d["reward"][p]) <= tol, (e, p)
+            end = HostState.from_ix(d, "frame", (p, 14), pad_to=32)
+            check_obs(obs[e].cpu().numpy(), d["obs"][p], end, EPISODE_TOL, f"env {e} step {p}", "device ix episodes from seed")
+            assert abs(float(rew[e]) - d["reward"][p]) <= reward_tol(end, EPISODE_TOL), (e, p)
             assert bool(term[e]) == bool(d["terminated"][p]) and bool(trunc[e]) == bool(d["truncated"][p]), (e, p)
-            same_state(env_view(st, e), HostState.from_ix(d, "post", p, pad_to=32), EPISODE_TOL, f"env {e} step {p}")
+            same_state(env_view(st, e), HostState.from_ix(d, "post", p, pad_to=32), EPISODE_TOL, f"env {e} step {p}",
+                       "device ix episodes from seed")
         # IntersectionEnv._info (intersection_env.py:120-128): the terms rebuild the reward
         terms = np.stack([info["rewards"][n].cpu().numpy() for n in env.REWARD_TERMS], 1)
         for e in range(len(GOLD)):
@@ -435,8 +437,10 @@ def test_device_episodes_match_the_reference_env(hip_device):
         speed, crashed = info["speed"].cpu().numpy(), info["crashed"].cpu().numpy()
         ar, at = info["agents_rewards"][0].cpu().numpy(), info["agents_terminated"][0].cpu().numpy()
         for e, d in enumerate(refs):
-            tol = obs_tol(HostState.from_ix(d, "end", p, pad_to=32), EPISODE_TOL)
-            assert np.max(np.abs(obs[e].cpu().numpy() - d["obs"][p])) <= tol, (e, p)
+            end = HostState.from_ix(d, "end", p, pad_to=32)
+            check_obs(obs[e].cpu().numpy(), d["obs"][p], end, EPISODE_TOL, f"env {e} step {p}",
+                      "device envref episodes from seed")
+            tol = reward_tol(end, EPISODE_TOL)  # the reward and the info terms follow the ego alone
             assert abs(float(rew[e]) - d["reward"][p]) <= tol, (e, p)
             assert bool(term[e]) == bool(d["terminated"][p]) and bool(trunc[e]) == bool(d["truncated"][p]), (e, p)
             want = d["info"][p]
@@ -444,5 +448,78 @@ def test_device_episodes_match_the_reference_env(hip_device):
             assert terms[e, 0] == want[2] and terms[e, 2] == want[4] and terms[e, 3] == want[5], (e, p)
             assert abs(terms[e, 1] - want[3]) <= tol and abs(float(ar[e]) - want[6]) <= tol, (e, p)
             assert bool(at[e]) == bool(want[7]), (e, p)
-            same_state(env_view(st, e), HostState.from_ix(d, "post", p, pad_to=32), EPISODE_TOL, f"env {e} step {p}")
+            same_state(env_view(st, e), HostState.from_ix(d, "post", p, pad_to=32), EPISODE_TOL, f"env {e} step {p}",
+                       "device envref episodes from seed")
             assert np.array_equal(st["rng"][e], d["rng"][p]), (e, p, "np_random state")
+
+
+# one step (15 frames) from the reference's own state on the device, float64 against the reference:
+# about 10x the worst values seen on the MI355X (round 5, profiles/r05/r05a_parity.json: steering
+# 8.1e-9 on a 0.15 m/s vehicle -- numpy's float64 transcendentals against the device's through the
+# steering law's 1 / v^2 gain, the oracle lands on the same value -- pose 2.7e-11, speed 2.1e-14,
+# acceleration 4.6e-13, observations 2.2e-16, the reward the float32 rounding of the reference's);
+# discrete fields, np_random and the flags exact
+DEV_STEP_TOL = {"x": 1e-10, "y": 1e-10, "heading": 1e-10, "speed": 1e-12, "target_speed": 0.0, "timer": 0.0,
+                "steer": 1e-7, "acc": 1e-11, "delta": 0.0}
+DEV_STEP_OBS_TOL = 1e-14
+
+
+def test_device_steps_from_reference_state(hip_device):
+    """Every step of the 18 reference IntersectionEnv episodes (234 steps, the 12 episodes whose
+    ego drives to its exit included), each started on the device from the reference's own state
+    and np_random (``pre``; tests/test_ix_env_oracle.py::ref_step_input), all in one batch: the
+    fused frames give the reference's ``end`` state; env.step gives its shuffled observation,
+    reward, flags and info; clear / spawn its ``post`` state; and np_random's words after the step
+    are the reference's.  No standstill allowance: one step holds every vehicle to DEV_STEP_TOL."""
+    from test_ix_env_oracle import ENVREF, INFO_TERMS
+    from test_ix_oracle import LONGI
+    from topotrafficrl_amd.road import BatchedRoad
+    from topotrafficrl_amd.state import BatchState
+    chk = "device envref one step from reference state"
+    refs = [load_golden(p) for p in ENVREF]
+    cases = [(i, p) for i, d in enumerate(refs) for p in range(int(d["meta"][1]))]
+    E = len(cases)
+    big = HostState(E, 32)
+    for e, (i, p) in enumerate(cases):
+        h = ref_step_input(refs[i], p)
+        for k in big.a:
+            big.a[k][e] = h.a[k][0]
+    acts = np.array([int(refs[i]["actions"][p]) for i, p in cases])
+    env = VecIntersectionEnv({**ENV_JSON, "num_envs": E, "device": hip_device})
+    env.reset(seed=0)
+    # the frames alone: the state entering the observation
+    frames = BatchState(E, 32, device=hip_device).load_numpy(big.a)
+    BatchedRoad(env.network, frames, env.params).simulate(torch.tensor([LONGI[int(a)] for a in acts]), 15, 1 / 15)
+    fr = frames.to_numpy()
+    for e, (i, p) in enumerate(cases):
+        same_state(env_view(fr, e), HostState.from_ix(refs[i], "end", p, pad_to=32), DEV_STEP_TOL,
+                   f"envref_ix_s{int(refs[i]['meta'][0])} step {p}", chk, standstill=False)
+    # the whole env.step from the same state
+    env.state.load_numpy(big.a)
+    env.time.copy_(torch.tensor([float(p) for _, p in cases], dtype=torch.float64))
+    obs, rew, term, trunc, info = env.step(torch.from_numpy(acts).to(hip_device))
+    st = env.state.to_numpy()
+    obs = obs.cpu().numpy()
+    terms = np.stack([info["rewards"][n].cpu().numpy() for n in INFO_TERMS], 1)
+    speed, crashed = info["speed"].cpu().numpy(), info["crashed"].cpu().numpy()
+    at = info["agents_terminated"][0].cpu().numpy()
+    for e, (i, p) in enumerate(cases):
+        d = refs[i]
+        what = f"envref_ix_s{int(d['meta'][0])} step {p}"
+        err = np.abs(obs[e].astype(np.float64) - d["obs"][p])
+        parity_log.note(chk, "obs", err, what)
+        assert err.max() <= DEV_STEP_OBS_TOL, (what, "obs", err.max())
+        parity_log.note(chk, "reward", abs(float(rew[e]) - d["reward"][p]), what)
+        assert rew[e].item() == float(np.float32(d["reward"][p])), (what, "reward: float32 of the reference's")
+        assert bool(term[e]) == bool(d["terminated"][p]) and bool(trunc[e]) == bool(d["truncated"][p]), what
+        want = d["info"][p]
+        assert abs(float(speed[e]) - want[0]) <= DEV_STEP_TOL["speed"] * (1 + abs(want[0])), (what, "info speed")
+        parity_log.note(chk, "info high_speed_reward", abs(terms[e, 1] - want[3]), what)
+        assert bool(crashed[e]) == bool(want[1]) and bool(at[e]) == bool(want[7]), what
+        assert terms[e, 0] == want[2] and terms[e, 2] == want[4] and terms[e, 3] == want[5], what
+        assert terms[e, 1] == np.float32(want[3]), (what, "high_speed_reward: float32 of the reference's")
+        same_state(env_view(st, e), HostState.from_ix(d, "post", p, pad_to=32), DEV_STEP_TOL, what, chk + " (post)",
+                   standstill=False)
+        assert np.array_equal(st["rng"][e], d["rng"][p]), (what, "np_random state")
+    parity_log.count(chk, "steps", E)
+    parity_log.count(chk, "arrived steps", int(sum(refs[i]["info"][p][4] > 0 for i, p in cases)))

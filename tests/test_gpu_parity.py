@@ -1,9 +1,12 @@
 """HIP path vs the float64 oracle and the reference golden vectors (run on an MI355X).
 
 Tolerances (stated per SURVEY.md §8(d)):
-  * f64 kernels, one frame from a golden state: |d| <= 1e-9 * (1 + |x|); discrete fields exact.
-  * f64 kernels, multi-frame rollouts: discrete fields exact, continuous <= 1e-6 * (1 + |x|)
-    (only libm ulp differences between the device and numpy can accumulate).
+  * f64 kernels, one frame from a golden state and multi-frame rollouts (fused 15-frame steps
+    against the goldens and the oracle, every BASELINE batch size): discrete fields exact,
+    continuous fields within F64_TOL relative to 1 + |x|.  The bounds are about 10x the worst
+    values seen on the MI355X (round 5, profiles/r05/r05a_parity.json: pose, speed and steering
+    <= 7.5e-15, acceleration and impacts <= 6.3e-14, timers and target speeds exact), far inside
+    SURVEY.md's 1e-9 for the fp64 parity mode.
   * f32 kernels, one frame, against the float64 oracle on the same float32-rounded inputs:
     |d| <= 1e-4 * (1 + |x|) on every continuous field; discrete fields exact except flips at a
     float64 decision margin below 1e-5 (oracle_frame_links; check_f32_flips) -- the vehicle's
@@ -18,6 +21,7 @@ import numpy as np
 import pytest
 import torch
 
+import parity_log
 from conftest import golden_files, load_golden, scene_files
 from oracle.oracle import HostState, Oracle
 from topotrafficrl_amd import _abi
@@ -36,6 +40,8 @@ G7 = _abi.grid_cfg(features=["presence", "x", "y", "vx", "vy", "cos_h", "sin_h"]
                    grid_size=[[-32, 32], [-32, 32]], grid_step=[2, 2])
 GR = _abi.grid_cfg()
 CONT = ["x", "y", "heading", "speed", "timer", "target_speed", "steer", "acc"]
+F64_TOL = {"x": 1e-13, "y": 1e-13, "heading": 1e-13, "speed": 1e-13, "steer": 1e-13, "acc": 1e-12,
+           "timer": 0.0, "target_speed": 0.0, "impact_x": 1e-12, "impact_y": 1e-12}
 DISC = ["lane", "target_lane", "crashed", "has_impact", "speed_index"]
 
 
@@ -55,22 +61,30 @@ def to_dev(h: HostState, device, dtype="f64", pad_to=None):
     return b.load_numpy(arr)
 
 
-def compare(dev: BatchState, h: HostState, tol, disc_exact=True, n=None):
+def compare(dev: BatchState, h: HostState, tol, disc_exact=True, n=None, where: str = ""):
+    """Device state vs the oracle / golden: discrete fields exact (``disc_exact``), every continuous
+    field within ``tol`` (a float, or a per-field dict) relative to 1 + |x|; each field's worst
+    error goes to parity_log under the calling test's name."""
     d = dev.to_numpy()
     n = n or h.N
     worst = 0.0
+    check, where = parity_log.current_check(), where or parity_log.current_case()
     for k in CONT:
         a, b = d[k][:, :n].astype(np.float64), h[k][:, :n]
-        err = np.max(np.abs(a - b) / (1 + np.abs(b))) if a.size else 0.0
-        worst = max(worst, float(err))
+        err = parity_log.note(check, k, parity_log.rel_err(a, b), where)
+        t = tol[k] if isinstance(tol, dict) else tol
+        assert err <= t, (k, err, t)
+        worst = max(worst, err)
     imp = h["has_impact"][:, :n].astype(bool)
     if imp.any():
         for k in ("impact_x", "impact_y"):
-            worst = max(worst, float(np.max(np.abs(d[k][:, :n][imp] - h[k][:, :n][imp]))))
+            err = parity_log.note(check, k, np.abs(d[k][:, :n][imp] - h[k][:, :n][imp]), where)
+            t = tol[k] if isinstance(tol, dict) else tol
+            assert err <= t, (k, err, t)
+            worst = max(worst, err)
     mism = {k: int(np.sum(d[k][:, :n] != h[k][:, :n])) for k in DISC}
     if disc_exact:
         assert sum(mism.values()) == 0, mism
-    assert worst <= tol, (worst, tol)
     return worst, mism
 
 
@@ -93,9 +107,9 @@ def test_single_frames_f64_vs_golden(path, hip_device):
             road.meta_action(torch.tensor([int(d["actions"][f // 15])]))
         road.act()
         torch.cuda.synchronize()
-        compare(dev, HostState.from_golden(d, f, prefix="act_"), 1e-9)
+        compare(dev, HostState.from_golden(d, f, prefix="act_"), F64_TOL)
         road.step(1 / 15)
-        compare(dev, HostState.from_golden(d, f + 1), 1e-9)
+        compare(dev, HostState.from_golden(d, f + 1), F64_TOL)
 
 
 @pytest.mark.parametrize("path", golden_files(), ids=lambda p: p.split("/")[-1][:-4])
@@ -104,7 +118,7 @@ def test_fused_rollout_f64_vs_golden(path, hip_device):
     o, road, h, dev = roads(d, hip_device)
     for p in range(int(d["meta"][2])):
         road.simulate(torch.tensor([int(d["actions"][p])]), 15, 1 / 15)
-        compare(dev, HostState.from_golden(d, 15 * (p + 1)), 1e-6)
+        compare(dev, HostState.from_golden(d, 15 * (p + 1)), F64_TOL)
 
 
 @pytest.mark.parametrize("path", golden_files("highway_*"), ids=lambda p: p.split("/")[-1][:-4])
@@ -117,7 +131,7 @@ def test_padded_slots_are_invisible(path, hip_device):
         pytest.skip("no larger slot class than 128 in the suite")
     o, road, h, dev = roads(d, hip_device, pad_to=pad)
     road.simulate(torch.tensor([int(d["actions"][0])]), 15, 1 / 15)
-    compare(dev, HostState.from_golden(d, 15), 1e-6, n=n)
+    compare(dev, HostState.from_golden(d, 15), F64_TOL, n=n)
 
 
 def f32_inputs(h: HostState) -> HostState:
@@ -310,7 +324,7 @@ def test_random_batch_rollout_vs_oracle(n, hip_device):
         acts = rng.integers(0, 5, size=E).astype(np.int32)
         o.simulate(h, acts, 15, 1 / 15)
         road.simulate(torch.from_numpy(acts), 15, 1 / 15)
-        compare(dev, h, 1e-6)
+        compare(dev, h, F64_TOL)
 
 
 @pytest.mark.parametrize("n", [24, 64, 100, 128])
@@ -334,12 +348,12 @@ def test_tied_positions_vs_oracle(n, hip_device):
     acts = rng.integers(0, 5, size=E).astype(np.int32)
     o.simulate(h, acts, 1, 1 / 15)
     road.simulate(torch.from_numpy(acts), 1, 1 / 15)
-    compare(dev, h, 1e-9)
+    compare(dev, h, F64_TOL)
     for _ in range(2):
         acts = rng.integers(0, 5, size=E).astype(np.int32)
         o.simulate(h, acts, 15, 1 / 15)
         road.simulate(torch.from_numpy(acts), 15, 1 / 15)
-        compare(dev, h, 1e-6)
+        compare(dev, h, F64_TOL)
 
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
@@ -512,4 +526,4 @@ def test_empty_batch_and_largest_slot_class(hip_device):
     acts = np.array([0, 1, 3, 4], dtype=np.int32)
     o.simulate(h, acts, 15, 1 / 15)
     road.simulate(torch.from_numpy(acts), 15, 1 / 15)
-    compare(dev, h, 1e-6)
+    compare(dev, h, F64_TOL)

@@ -13,6 +13,7 @@ info dict and np_random's state included.  CPU only."""
 import numpy as np
 import pytest
 
+import parity_log
 from conftest import golden_files, load_golden
 from oracle.oracle import HostState, Oracle
 from test_ix_oracle import CONT, DISC, LONGI, P_IX, ix_lanes
@@ -32,34 +33,91 @@ CFG = VecIntersectionEnv.default_config()
 # function itself (seen: 0.026 rad on ix_s2 step 11, v = 0.0033 m/s) and are not compared there.
 # Below STANDSTILL the pose itself inherits that chaos over the following frames: the device
 # (ocml) and numpy (libm) roundings part by up to ~3e-3 m / rad on such a vehicle (seen on the
-# MI355X: ix_s4 step 11, v = 0.004 m/s, steering flipped between its clip bounds), so its pose
-# and the observation of its env are held to STANDSTILL_TOL.
+# MI355X: ix_s4 step 11, v = 0.004 m/s, steering flipped between its clip bounds).  The allowance
+# is per vehicle: only that vehicle's own state fields and its own observation row are held to
+# STANDSTILL_TOL (row_vehicles maps the reference's observation rows to vehicles), and the ego's
+# reward only while the ego itself is that slow; everything else in the env keeps EPISODE_TOL.
 EPISODE_TOL = 1e-4
 STANDSTILL = 0.1
 STANDSTILL_TOL = 1e-2
 REW = _abi.reward_cfg(-5, 1, [7.0, 9.0], False, False, 13, arrived_reward=1)
+# one step (15 frames) from the reference's own state: the float64 oracle against the reference
+# (the largest differences seen: pose 2.7e-11, steer 8.1e-9 relative on a 0.15 m/s vehicle in
+# envref_ix_s3 step 5, everything else <= 1.2e-12; observations and np_random exact)
+STEP_TOL = {"x": 1e-9, "y": 1e-9, "heading": 1e-9, "speed": 1e-9, "target_speed": 0.0, "timer": 1e-12,
+            "steer": 1e-7, "acc": 1e-9, "delta": 0.0}
 
 
-def same_state(h: HostState, g: HostState, tol: float, what: str):
+def same_state(h: HostState, g: HostState, tol, what: str, check: str | None = None, standstill: bool = True):
+    """Every live vehicle of env 0: discrete fields exact, continuous ones within ``tol`` (a float,
+    or a per-field dict) relative; with ``standstill``, a vehicle slower than STANDSTILL is allowed
+    STANDSTILL_TOL more on its pose and its steering / acceleration commands are not compared
+    (multi-step episodes; one step from the reference's state holds every vehicle alike).
+    ``check`` names the parity_log entry the worst errors go to."""
     n = int((g["kind"] > 0).sum())
     assert int((h["kind"] > 0).sum()) == n, (what, "vehicle count", int((h["kind"] > 0).sum()), n)
-    moving = np.abs(g["speed"][:, :n]) >= STANDSTILL
+    moving = np.abs(g["speed"][:, :n]) >= (STANDSTILL if standstill else 0.0)
+    if check:
+        parity_log.count(check, "slow vehicles", int((~moving).sum()))
     for k in CONT + ["delta"]:
         err = np.abs(h[k][:, :n] - g[k][:, :n]) / (1 + np.abs(g[k][:, :n]))
+        t = tol[k] if isinstance(tol, dict) else tol
         if k in ("steer", "acc"):
             err = err[moving]
         else:
+            if check:
+                parity_log.note(check + " (slow vehicles)", k, err[~moving], what)
             err = np.where(moving, err, np.maximum(err - STANDSTILL_TOL, 0.0))
-        assert np.max(err, initial=0.0) <= tol, (what, k, np.max(err, initial=0.0))
+        if check:
+            parity_log.note(check, k, err, what)
+        assert np.max(err, initial=0.0) <= t, (what, k, np.max(err, initial=0.0))
     for k in DISC:
         assert np.array_equal(h[k][:, :n], g[k][:, :n]), (what, k, h[k][:, :n], g[k][:, :n])
     assert np.array_equal(h["reg_steps"], g["reg_steps"]), what
 
 
-def obs_tol(g: HostState, tol: float) -> float:
-    """Observation tolerance of an env: STANDSTILL_TOL while one of its vehicles is stopped."""
+def row_vehicles(ref_obs: np.ndarray, g: HostState) -> np.ndarray:
+    """The vehicle slot (env 0 of ``g``) behind each row of the reference's absolute Kinematics
+    observation ``ref_obs`` [V, 7] (presence, x, y, vx, vy, cos_h, sin_h; KIN's ranges): row 0 is
+    the ego, a present row is the live vehicle whose own normalised, clipped feature row is nearest
+    to it (the rows are shuffled), an empty row -1."""
     n = int((g["kind"] > 0).sum())
-    return tol if np.all(np.abs(g["speed"][:, :n]) >= STANDSTILL) else max(tol, STANDSTILL_TOL)
+    x, y, v, h = (g[k][0, :n] for k in ("x", "y", "speed", "heading"))
+    feats = np.stack([np.ones(n), np.clip(x / 100, -1, 1), np.clip(y / 100, -1, 1),
+                      np.clip(v * np.cos(h) / 20, -1, 1), np.clip(v * np.sin(h) / 20, -1, 1),
+                      np.cos(h), np.sin(h)], 1)
+    out = np.full(len(ref_obs), -1, dtype=np.int64)
+    out[0] = int(np.argmax(g["kind"][0, :n] == _abi.MDP))
+    for r in range(1, len(ref_obs)):
+        if ref_obs[r, 0] > 0:
+            out[r] = int(np.argmin(np.abs(feats - ref_obs[r].astype(np.float64)).max(1)))
+    return out
+
+
+def obs_row_tols(ref_obs: np.ndarray, g: HostState, tol: float, check: str | None = None) -> np.ndarray:
+    """Per-row tolerance of an observation [V] against the reference's ``ref_obs``: STANDSTILL_TOL
+    for the row of a vehicle slower than STANDSTILL (its own pose may carry the standstill chaos),
+    ``tol`` for every other row."""
+    ids = row_vehicles(ref_obs, g)
+    slow = np.array([i >= 0 and abs(g["speed"][0, i]) < STANDSTILL for i in ids])
+    if check:
+        parity_log.count(check, "excused obs rows", int(slow.sum()))
+    return np.where(slow, max(tol, STANDSTILL_TOL), tol)
+
+
+def check_obs(got: np.ndarray, ref_obs: np.ndarray, g: HostState, tol: float, what: str, check: str):
+    """An env's observation [V, F] against the reference's, row by row (obs_row_tols)."""
+    tols = obs_row_tols(ref_obs, g, tol, check)
+    err = np.abs(got.astype(np.float64) - ref_obs).max(1)
+    parity_log.note(check, "obs (moving rows)", err[tols <= tol], what)
+    parity_log.note(check, "obs (excused rows)", err[tols > tol], what)
+    assert np.all(err <= tols), (what, err, tols)
+
+
+def reward_tol(g: HostState, tol: float) -> float:
+    """The ego's reward tolerance: ``tol``, or STANDSTILL_TOL while the ego itself is that slow."""
+    ego = int(np.argmax(g["kind"][0] == _abi.MDP))
+    return tol if abs(g["speed"][0, ego]) >= STANDSTILL else max(tol, STANDSTILL_TOL)
 
 
 def test_product_network_is_the_reference_network():
@@ -101,14 +159,14 @@ def test_ix_episode_from_seed(path):
     assert np.max(np.abs(obs[0] - d["obs0"])) <= 1e-6
     for p in range(steps):
         o.simulate(h, [LONGI[int(d["actions"][p])]], 15, 1 / 15)
-        same_state(h, HostState.from_ix(d, "frame", (p, 14), pad_to=32), EPISODE_TOL, f"frames {p}")
+        end = HostState.from_ix(d, "frame", (p, 14), pad_to=32)
+        same_state(h, end, EPISODE_TOL, f"frames {p}", "oracle ix episode from seed")
         obs, _ = o.observe_kinematics(h, KIN)
-        post = HostState.from_ix(d, "frame", (p, 14), pad_to=32)
-        assert np.max(np.abs(obs[0] - d["obs"][p])) <= obs_tol(post, EPISODE_TOL), p
+        check_obs(obs[0], d["obs"][p], end, EPISODE_TOL, f"step {p}", "oracle ix episode from seed")
         rew, term, trunc = o.rewards(h, REW, float(p + 1))
-        assert abs(rew[0] - d["reward"][p]) <= obs_tol(post, EPISODE_TOL) and term[0] == d["terminated"][p] and trunc[0] == d["truncated"][p]
+        assert abs(rew[0] - d["reward"][p]) <= reward_tol(end, EPISODE_TOL) and term[0] == d["terminated"][p] and trunc[0] == d["truncated"][p]
         o.ix_clear_spawn(h, cfg)
-        same_state(h, HostState.from_ix(d, "post", p, pad_to=32), EPISODE_TOL, f"post {p}")
+        same_state(h, HostState.from_ix(d, "post", p, pad_to=32), EPISODE_TOL, f"post {p}", "oracle ix episode from seed")
 
 
 def test_ix_batch_and_mask():
@@ -237,10 +295,10 @@ def test_reference_env_episode_from_seed(path):
     for p in range(steps):
         o.simulate(h, [LONGI[int(d["actions"][p])]], 15, 1 / 15)
         end = HostState.from_ix(d, "end", p, pad_to=32)
-        same_state(h, end, EPISODE_TOL, f"frames {p}")
+        same_state(h, end, EPISODE_TOL, f"frames {p}", "oracle envref episode from seed")
         obs, _ = o.observe_kinematics(h, KIN)
-        tol = obs_tol(end, EPISODE_TOL)
-        assert np.max(np.abs(obs[0] - d["obs"][p])) <= tol, p
+        check_obs(obs[0], d["obs"][p], end, EPISODE_TOL, f"step {p}", "oracle envref episode from seed")
+        tol = reward_tol(end, EPISODE_TOL)  # the reward and the info terms follow the ego alone
         rew, term, trunc, comp = o.rewards(h, REW, float(p + 1), components=True)
         assert abs(rew[0] - d["reward"][p]) <= tol and term[0] == d["terminated"][p] and trunc[0] == d["truncated"][p], p
         got, want = _info_of(h, comp), d["info"][p]
@@ -249,5 +307,44 @@ def test_reference_env_episode_from_seed(path):
         assert got[1] == want[1] and got[7] == want[7] and got[4] == want[4] and got[5] == want[5], (p, got, want)
         assert abs(got[3] - want[3]) <= tol and got[2] == want[2] and abs(got[6] - want[6]) <= tol, (p, got, want)
         o.ix_clear_spawn(h, cfg)
-        same_state(h, HostState.from_ix(d, "post", p, pad_to=32), EPISODE_TOL, f"post {p}")
+        same_state(h, HostState.from_ix(d, "post", p, pad_to=32), EPISODE_TOL, f"post {p}",
+                   "oracle envref episode from seed")
         assert np.array_equal(h["rng"][0], d["rng"][p]), (p, "np_random state")
+
+
+def ref_step_input(d: dict, p: int, pad_to: int = 32) -> HostState:
+    """The reference env's own state entering step p (``pre``), with np_random as it stood then:
+    after reset (``rng_reset``) for step 0, after step p - 1 otherwise."""
+    h = HostState.from_ix(d, "pre", p, pad_to=pad_to)
+    h["rng"][0] = d["rng_reset"] if p == 0 else d["rng"][p - 1]
+    return h
+
+
+def test_reference_env_steps_from_reference_state():
+    """Every step of the 18 reference episodes (234 steps, the 12 whose ego reaches its exit
+    included), each started from the reference's own state and np_random (no drift carried over
+    from earlier steps): the float64 oracle's frames equal the reference's state entering the
+    observation (``end``) within STEP_TOL, discrete fields exact; the shuffled observation, the
+    reward, the flags and the info terms equal the reference's; clear / spawn gives its ``post``
+    state, and np_random's words after the step are the reference's."""
+    net = intersection_network()
+    o = Oracle(net.table, P_IX)
+    cfg = ix_cfg(net, CFG, P_IX)
+    chk = "oracle envref one step from reference state"
+    for path in ENVREF:
+        d = load_golden(path)
+        for p in range(int(d["meta"][1])):
+            what = f"{IDS(path)} step {p}"
+            h = ref_step_input(d, p)
+            o.simulate(h, [LONGI[int(d["actions"][p])]], 15, 1 / 15)
+            same_state(h, HostState.from_ix(d, "end", p, pad_to=32), STEP_TOL, what, chk, standstill=False)
+            obs, _ = o.observe_kinematics(h, KIN)
+            assert np.array_equal(obs[0], d["obs"][p]), what
+            rew, term, trunc, comp = o.rewards(h, REW, float(p + 1), components=True)
+            assert rew[0] == np.float32(d["reward"][p]) and term[0] == d["terminated"][p] and trunc[0] == d["truncated"][p], what
+            got, want = _info_of(h, comp), d["info"][p]
+            assert got[0] == want[0] and got[1] == want[1] and got[7] == want[7], (what, got, want)
+            assert np.array_equal(np.float32(got[2:6]), np.float32(want[2:6])), (what, got, want)
+            o.ix_clear_spawn(h, cfg)
+            same_state(h, HostState.from_ix(d, "post", p, pad_to=32), STEP_TOL, what, chk + " (post)", standstill=False)
+            assert np.array_equal(h["rng"][0], d["rng"][p]), (what, "np_random state")

@@ -354,10 +354,12 @@ def test_ego_attention_op_equals_the_c_abi(hip_device):
     act1 = torch.empty(100, dtype=torch.int64, device=hip_device)
     act32 = torch.empty(100, dtype=torch.int32, device=hip_device)
     q3 = torch.empty((100, 5), device=hip_device)
-    assert lib.ttrl_ego_attention_act(x.data_ptr(), 100, 15, 7, 2, w.data_ptr(), 5, 0.3, None, 77, 5, None,
+    assert lib.ttrl_ego_attention_act(x.data_ptr(), 100, 15, 7, 2, w.data_ptr(), 5, 0.3, None, 77, 5, None, 0,
                                       q3.data_ptr(), act1.data_ptr(), act32.data_ptr(), _stream()) == 0
-    assert lib.ttrl_ego_attention_act(x.data_ptr(), 100, 15, 7, 2, w.data_ptr(), 5, 0.3, None, 77, 5, None,
+    assert lib.ttrl_ego_attention_act(x.data_ptr(), 100, 15, 7, 2, w.data_ptr(), 5, 0.3, None, 77, 5, None, 0,
                                       q3.data_ptr(), None, None, _stream()) != 0  # no action output
+    assert lib.ttrl_ego_attention_act(x.data_ptr(), 100, 15, 7, 2, w.data_ptr(), 5, 0.3, None, 77, 5, None, -1,
+                                      q3.data_ptr(), act1.data_ptr(), None, _stream()) != 0  # negative offset
     act2, q4 = torch.ops.ttrl.ego_attention_act(x, w, 2, 5, 0.3, 77, 5)
     act3, _ = torch.ops.ttrl.ego_attention_act(x, w, 2, 5, 0.3, 77, 5, int32_actions=True)
     torch.cuda.synchronize()

@@ -136,9 +136,16 @@ def test_fused_epsilon_greedy(hip_device):
     r2, _ = ops.T.ego_attention_act(big, w, 2, A, 0.5, 11, 7)
     r3, _ = ops.T.ego_attention_act(big, w, 2, A, 0.5, 11, 8)
     assert torch.equal(r1, r2) and not torch.equal(r1, r3)
-    # env e's draw does not depend on the batch it is in
+    # env e's draw does not depend on the batch it is in: a prefix, and any other slice given its
+    # global offset (a data-parallel rank's shard), draws the rows of the whole batch
     r4, _ = ops.T.ego_attention_act(big[:1000], w, 2, A, 0.5, 11, 7)
     assert torch.equal(r4, r1[:1000])
+    r6, _ = ops.T.ego_attention_act(big[3000:5500], w, 2, A, 0.5, 11, 7, env_offset=3000)
+    assert torch.equal(r6, r1[3000:5500])
+    # the same rows at offset 0 (what every rank drew before the offset): other draws
+    r7, _ = ops.T.ego_attention_act(big[3000:5500], w, 2, A, 1.0, 11, 7)
+    r8, _ = ops.T.ego_attention_act(big[3000:5500], w, 2, A, 1.0, 11, 7, env_offset=3000)
+    assert (r7 != r8).float().mean() > 0.5
     # device scalars override epsilon / step (the captured-graph path)
     eps = torch.tensor(0.5, device=hip_device)
     stp = torch.tensor(7, dtype=torch.int64, device=hip_device)

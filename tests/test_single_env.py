@@ -73,7 +73,7 @@ def test_single_ids_resolve():
 
 @pytest.mark.gpu
 def test_single_intersection_replays_the_reference(hip_device):
-    from test_ix_env_oracle import EPISODE_TOL, obs_tol
+    from test_ix_env_oracle import EPISODE_TOL, check_obs, reward_tol
     from oracle.oracle import HostState
     from topotrafficrl_amd.intersection import VecIntersectionEnv
     # scripts/configs/IntersectionEnv/env.json: the default Kinematics observation, order "shuffled"
@@ -85,8 +85,9 @@ def test_single_intersection_replays_the_reference(hip_device):
         assert isinstance(obs, np.ndarray) and np.max(np.abs(obs - d["obs0"])) <= 1e-6
         for p, a in enumerate(d["actions"]):
             obs, r, term, trunc, info = env.step(int(a))
-            tol = obs_tol(HostState.from_ix(d, "frame", (p, 14), pad_to=32), EPISODE_TOL)
-            assert np.max(np.abs(obs - d["obs"][p])) <= tol and abs(r - d["reward"][p]) <= tol, p
+            end = HostState.from_ix(d, "frame", (p, 14), pad_to=32)
+            check_obs(obs, d["obs"][p], end, EPISODE_TOL, f"step {p}", "single ix env from seed")
+            assert abs(r - d["reward"][p]) <= reward_tol(end, EPISODE_TOL), p
             assert term == bool(d["terminated"][p]) and trunc == bool(d["truncated"][p])
             assert info["agents_rewards"] == (r,) and isinstance(info["rewards"]["collision_reward"], bool)
 

@@ -90,3 +90,18 @@ def test_ego_attention_masks_absent_rows():
     y = x.clone()
     y[:, 5:, 1:] = torch.rand(2, 10, 6, generator=g) * 9
     assert torch.allclose(net(x), net(y), atol=1e-6)
+
+
+def test_evaluation_keys_exploration_on_the_env_shard():
+    """BatchedEvaluation hands the env's global id offset (a data-parallel rank's shard,
+    env_id_offset) to the agent's policy, whose fused epsilon-greedy draws are keyed on global env
+    ids: shards of one seed explore independently (ttrl_ego_attention_act's env_offset)."""
+    from topotrafficrl_amd.trainer import BatchedDQNAgent
+
+    class ShardEnv:
+        config = {"env_id_offset": 8192}
+
+    agent = BatchedDQNAgent("cpu", n_actions=3)
+    assert agent.policy.env_id_offset == 0
+    BatchedEvaluation(ShardEnv(), agent, num_episodes=1, sim_seed=0)
+    assert agent.policy.env_id_offset == 8192

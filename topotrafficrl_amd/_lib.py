@@ -48,7 +48,7 @@ _SIGS = {
     "ttrl_ego_attention_sizes": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P], C.c_int64),
     "ttrl_ego_attention_q": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, C.c_int32, _P, _P, _P], C.c_int),
     "ttrl_ego_attention_act": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, C.c_int32, C.c_float, _P,
-                                C.c_uint64, C.c_int64, _P, _P, _P, _P, _P], C.c_int),
+                                C.c_uint64, C.c_int64, _P, C.c_int64, _P, _P, _P, _P], C.c_int),
 }
 EXPORTS = [k for k in _SIGS]
 
@@ -78,7 +78,7 @@ def load(path: str | None = None) -> C.CDLL:
             continue  # an older build loaded for comparison (tools/variants.py)
         fn.argtypes = args
         fn.restype = res
-    if lib.ttrl_abi_version() != 5:
+    if lib.ttrl_abi_version() != 6:  # include/ttrl_mi355x.h TTRL_ABI_VERSION
         raise ImportError("ABI version mismatch with include/ttrl_mi355x.h")
     if path is None:
         _lib = lib

@@ -143,8 +143,12 @@ class EgoAttentionPolicy:
     """Batched DQN acting: Q = value_net(obs[E, V, F]); epsilon-greedy on the device."""
 
     def __init__(self, device, n_actions: int = 5, seed: int = 0, tau: float = 15000.0, temperature: float = 1.0,
-                 final_temperature: float = 0.05, fused: bool = True):
+                 final_temperature: float = 0.05, fused: bool = True, env_id_offset: int = 0):
         self.device = torch.device(device)
+        # the global env id of obs row 0 (a data-parallel rank's shard offset, sharding.shard): the
+        # fused draws are keyed on the global env, so every shard of one seed explores independently
+        # and any split of the global batch draws the same action for the same env
+        self.env_id_offset = int(env_id_offset)
         self.fused = fused  # acting through the fused HIP forward on a GPU (training uses the torch graph)
         g = torch.Generator(device="cpu")
         g.manual_seed(seed)
@@ -183,7 +187,7 @@ class EgoAttentionPolicy:
         env.step takes without a cast launch).
 
         On a GPU the forward, argmax and draw are ONE launch (ttrl::ego_attention_act, Philox
-        keyed on (seed, env, step)); elsewhere the torch forward with torch's generator."""
+        keyed on (seed, env_id_offset + row, step)); elsewhere the torch forward with torch's generator."""
         t = self.time if t is None else int(t)
         self.time = t + 1
         self.last_epsilon = self.epsilon(self.time) if epsilon is None else epsilon
@@ -193,7 +197,8 @@ class EgoAttentionPolicy:
             act, _ = ops.T.ego_attention_act(obs.float(), net.packed_weights(), net.attention_layer.h,
                                              net.output_layer.predict.out_features,
                                              self.last_epsilon if epsilon is None else 0.0, self.seed, self.time,
-                                             epsilon, step, int32_actions=dtype == torch.int32)
+                                             epsilon, step, int32_actions=dtype == torch.int32,
+                                             env_offset=self.env_id_offset)
             return act if act.dtype == dtype else act.to(dtype)
         epsilon = self.last_epsilon
         q = self.value_net(obs)

@@ -24,28 +24,7 @@ namespace {
 // log/exp) are register-hungry; inlined at every call site they force spills of the
 // resident vehicle state.  Out of line, the fused kernel fits its register budget with no
 // scratch; the call overhead is paid ~10 times per vehicle-frame.
-#ifdef TTRL_INLINE_TRANSC
-#define TTRL_TRANSC __forceinline__
-#else
 #define TTRL_TRANSC __noinline__
-#endif
-#ifdef TTRL_FAKE_TRANSC
-// Diagnostic timing build only (tools/variants.py): float32 hardware approximations stand in
-// for the float64 transcendentals, so the results are NOT the reference's.
-__device__ __forceinline__ double t_sin(double x) { return __sinf((float)x); }
-__device__ __forceinline__ double t_cos(double x) { return __cosf((float)x); }
-__device__ __forceinline__ double t_tan(double x) { return __tanf((float)x); }
-__device__ __forceinline__ double t_atan(double x) { return atanf((float)x); }
-__device__ __forceinline__ double t_asin(double x) { return asinf((float)x); }
-__device__ __forceinline__ double t_pow(double x, double y) { return __expf((float)y * __logf((float)x)); }
-template <typename T> struct SinCos { T s, c; };
-__device__ __forceinline__ SinCos<double> t_sincos(double x) {
-  SinCos<double> r;
-  r.s = __sinf((float)x);
-  r.c = __cosf((float)x);
-  return r;
-}
-#else
 __device__ TTRL_TRANSC double t_sin(double x) { return ::sin(x); }
 __device__ TTRL_TRANSC double t_cos(double x) { return ::cos(x); }
 __device__ TTRL_TRANSC double t_tan(double x) { return ::tan(x); }
@@ -53,11 +32,7 @@ __device__ TTRL_TRANSC double t_atan(double x) { return ::atan(x); }
 __device__ TTRL_TRANSC double t_asin(double x) { return ::asin(x); }
 // pow(x, y) for x >= 0, y > 0 (IDM's (v / v0)^DELTA): exp(y log x) is within ~|y log x| ulp of
 // the correctly rounded power (far inside the stated tolerances) at half of ocml pow's cost.
-#ifdef TTRL_POW_LIBM
-__device__ TTRL_TRANSC double t_pow(double x, double y) { return ::pow(x, y); }
-#else
 __device__ TTRL_TRANSC double t_pow(double x, double y) { return ::exp(y * ::log(x)); }
-#endif
 template <typename T> struct SinCos { T s, c; };
 // one shared argument reduction; ocml's sincos returns the same values as sin and cos
 __device__ TTRL_TRANSC SinCos<double> t_sincos(double x) {
@@ -65,12 +40,7 @@ __device__ TTRL_TRANSC SinCos<double> t_sincos(double x) {
   ::sincos(x, &r.s, &r.c);
   return r;
 }
-#endif
-#ifdef TTRL_F32_TRANSC_NOINLINE
-#define TTRL_TRANSC32 __noinline__
-#else
 #define TTRL_TRANSC32 __forceinline__
-#endif
 __device__ TTRL_TRANSC32 float t_sin(float x) { return ::sinf(x); }
 __device__ TTRL_TRANSC32 float t_cos(float x) { return ::cosf(x); }
 __device__ TTRL_TRANSC32 float t_tan(float x) { return ::tanf(x); }
@@ -85,12 +55,6 @@ __device__ TTRL_TRANSC32 SinCos<float> t_sincos(float x) {
 
 // Elementary functions of the simulate kernel's vehicle model (steering, bicycle model, IDM):
 // float64 through the short inline fdlibm restatements of ttrl_math.h, float32 through ocml.
-#ifdef TTRL_FAKE_TRANSC
-__device__ __forceinline__ SinCos<double> k_sincos(double x) { return t_sincos(x); }
-__device__ __forceinline__ double k_atan(double x) { return t_atan(x); }
-__device__ __forceinline__ double k_asin(double x) { return t_asin(x); }
-__device__ __forceinline__ double k_pow(double x, double y) { return t_pow(x, y); }
-#else
 __device__ __forceinline__ SinCos<double> k_sincos(double x) {
   SinCos<double> r;
   ttrl_math::sincos_d(x, r.s, r.c);
@@ -99,7 +63,6 @@ __device__ __forceinline__ SinCos<double> k_sincos(double x) {
 __device__ __forceinline__ double k_atan(double x) { return ttrl_math::atan_d(x); }
 __device__ __forceinline__ double k_asin(double x) { return ttrl_math::asin_d(x); }
 __device__ __forceinline__ double k_pow(double x, double y) { return ttrl_math::pow_d(x, y); }
-#endif
 __device__ __forceinline__ SinCos<float> k_sincos(float x) { return t_sincos(x); }
 __device__ __forceinline__ float k_atan(float x) { return t_atan(x); }
 __device__ __forceinline__ float k_asin(float x) { return t_asin(x); }
@@ -152,10 +115,8 @@ template <typename T> __device__ __forceinline__ T pymod(T a, T b) {
   // moves into the divisor's sign with one rounded a + b.
   if (b > T(0)) {
     if (a >= T(0) && a < b) return a;
-#ifndef TTRL_NO_PYMOD_FAST
     if (a >= b && a < T(2) * b) return a - b;
     if (a < T(0) && a > -b) return a + b;
-#endif
   }
   T m = fmod(a, b);
   if (m != T(0)) { if ((b < T(0)) != (m < T(0))) m += b; }
@@ -219,11 +180,7 @@ template <> inline ParamsF params_for<float>(const ttrl_params_t& p) { return pa
 template <typename T> struct Pair { T a, b; };
 // Inlined: the curved-lane geometry runs only in the NET_CURVED / NET_GRAPH instances, where
 // the call overhead cost more than the registers (intersection f64 launch 1.84 -> 1.60 ms).
-#ifdef TTRL_CURVED_NOINLINE
-#define TTRL_CURVED_ATTR __noinline__
-#else
 #define TTRL_CURVED_ATTR __forceinline__
-#endif
 template <typename T>
 __device__ TTRL_CURVED_ATTR Pair<T> curved_local(int type, T px, T py, T sx, T sy, T ux, T uy, T amp, T puls, T ph,
                                              T cx, T cy, T rad, T sph, T dirn) {
@@ -326,12 +283,22 @@ __device__ inline float4 lane_box(const LaneT<T>& L) {
   } else if (L.type == TTRL_LANE_CIRCULAR) {
     const T a0 = L.sph, a1 = a0 + L.dirn * L.len / L.rad;
     const T lo = fmin(a0, a1), hi = fmax(a0, a1);
+    // a degenerate arc (radius 0, a non-finite angle) gets no box; one sweeping a full turn or more
+    // the whole circle -- so the cardinal-point walk below takes at most four steps
+    if (!(isfinite(lo) && isfinite(hi) && isfinite(L.rad))) return make_float4(-INFINITY, -INFINITY, INFINITY, INFINITY);
+    if (hi - lo >= T(6.283185307179586)) {
+      const T r = fabs(L.rad);
+      x0 = L.cx - r; x1 = L.cx + r; y0 = L.cy - r; y1 = L.cy + r;
+      const float m = 1e-3f + 1e-6f * (float)(fabs(x0) + fabs(x1) + fabs(y0) + fabs(y1));
+      return make_float4((float)x0 - m, (float)y0 - m, (float)x1 + m, (float)y1 + m);
+    }
     x0 = x1 = L.cx + L.rad * cos(a0);
     y0 = y1 = L.cy + L.rad * sin(a0);
     const T ex = L.cx + L.rad * cos(a1), ey = L.cy + L.rad * sin(a1);
     x0 = fmin(x0, ex); x1 = fmax(x1, ex); y0 = fmin(y0, ey); y1 = fmax(y1, ey);
     const T q = T(1.5707963267948966);
-    for (T a = ceil(lo / q) * q; a <= hi; a += q) {  // cardinal points within the arc
+    T a = ceil(lo / q) * q;
+    for (int k = 0; k < 5 && a <= hi; ++k, a += q) {  // cardinal points within the arc (< 2 pi: at most 4)
       const T px = L.cx + L.rad * cos(a), py = L.cy + L.rad * sin(a);
       x0 = fmin(x0, px); x1 = fmax(x1, px); y0 = fmin(y0, py); y1 = fmax(y1, py);
     }
@@ -379,11 +346,7 @@ __device__ __forceinline__ int speed_to_index(const PP& P, T v) {
 #ifndef TTRL_SIM_WAVES
 #define TTRL_SIM_WAVES 0   // min waves/SIMD for the fused kernel; 0 = tuned default (f64: 2, f32: 4)
 #endif
-#ifdef TTRL_SAT_NOINLINE
-#define TTRL_SAT_ATTR __noinline__
-#else
 #define TTRL_SAT_ATTR
-#endif
 
 // utils.are_polygons_intersecting utils.py:194-239 on the closed 5-point rectangles of
 // RoadObject.polygon objects.py:168-180.  a = lower-index vehicle (the reference's self).
@@ -861,11 +824,7 @@ __device__ __forceinline__ int project_all(const View<T>& V, const PP& P, int nl
       const LaneT<T> L = V.lanes[l];
       T s, r;
       bool full = true;  // s computed (always, on a straight lane)
-#ifndef TTRL_NO_RING
       if constexpr (CV) {
-#else
-      if constexpr (false) {
-#endif
         if (L.type == TTRL_LANE_CIRCULAR) {
           // CircularLane.local_coordinates (lane.py:327-334) lateral part first: the atan2 of s is
           // needed only inside the on_lane band, or below the closest distance so far -- every term
@@ -1170,9 +1129,6 @@ __device__ __forceinline__ void slot_nbrs(const View<T>& V, int le, int self, in
   }
 }
 
-#ifdef TTRL_CHECK_ITEMS
-__device__ int g_dbg_count = 0;
-#endif
 // project_all for the road-network instance (one wavefront per workgroup), over (vehicle, lane)
 // items: a scene holds ~8 live vehicles in its 32 slots, so one vehicle per SIMD lane left 3/4 of
 // the lanes idle through the frame's longest phase (every vehicle on all 20 lanes, atan2 on the
@@ -1184,18 +1140,10 @@ __device__ int g_dbg_count = 0;
 // (Round 2 noted non-finite states / hangs here for the float32 road-network instance at a 4-wave
 // (128-VGPR) budget.  Not reproducible from any committed source: the commit that wrote the note,
 // rebuilt at 4 waves, passes its intersection GPU tests and 40 finite steps, and so does this
-// source at 4 waves with TTRL_CHECK_ITEMS silent (profiles/r03/netgraph_4wave/).  The
+// source at 4 waves with round 3's item bounds checks silent (profiles/r03/netgraph_4wave/).  The
 // 2-wave budget of the road networks is a tuning choice, not a correctness one.)
-#ifndef TTRL_ITEMS_NOINLINE
 #define TTRL_ITEMS_ATTR __forceinline__
-#else
-#define TTRL_ITEMS_ATTR __noinline__
-#endif
-#ifndef TTRL_NO_PROJ_PRUNE
 constexpr bool PROJ_PRUNE = true;
-#else
-constexpr bool PROJ_PRUNE = false;
-#endif
 template <typename T, int NS, int EPW, int LC, typename PP>
 __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int nl, int tid, int le, int i,
                              bool present, bool want_closest, float4 my_box, float onb) {
@@ -1343,12 +1291,6 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int 
     const T h = V.h[v];
     for (int kk = g; kk < nl; kk += G) {
       int l = V.lperm[kk];
-#ifdef TTRL_CHECK_ITEMS
-      if (l < 0 || l >= nl) {
-        if (atomicAdd(&g_dbg_count, 1) < 20) printf("items: blk %d tid %d lperm[%d] = %d\n", (int)blockIdx.x, tid, kk, l);
-        l = kk;
-      }
-#endif
       const LaneT<T> L = V.lanes[l];
       T s, r;
       lane_local<true>(L, x, y, s, r);
@@ -1411,47 +1353,6 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int 
     V.cnt[e * (LMAX + 1) + l] = c;
     atomicMax(&V.cnt[e * (LMAX + 1) + LMAX], c);
   }
-#ifdef TTRL_CHECK_ITEMS
-  __syncthreads();
-  if (present) {  // the per-vehicle projection, compared
-    const int sh = le * NS;
-    const unsigned long long seg = NS == 64 ? ~0ull : ((1ull << NS) - 1);
-    const T x = V.x[tid], y = V.y[tid], h = V.h[tid];
-    T bd2 = T(0), ang2 = T(0);
-    int best2 = 0;
-    for (int l = 0; l < nl; ++l) {
-      const LaneT<T> L = V.lanes[l];
-      T s, r;
-      lane_local<true>(L, x, y, s, r);
-      const bool on = fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl;
-      const unsigned long long m = (V.onm[l] >> sh) & seg;
-      const bool on1 = (m >> i) & 1ull;
-      const int pos = __popcll(m & ((1ull << i) - 1));
-      const size_t base = ((size_t)l * EPW + le) * NSP;
-      if (on != on1 || (on && pos < LC && (V.key[base + pos] != s || V.idx[base + pos] != i)))
-        if (atomicAdd(&g_dbg_count, 1) < 20)
-          printf("items: blk %d tid %d lane %d on %d/%d pos %d key %g/%g idx %d total %d\n", (int)blockIdx.x, tid,
-                 l, (int)on, (int)on1, pos, (double)V.key[base + pos], (double)s, (int)V.idx[base + pos], total);
-      if (want_closest) {
-        const T hdl = heading_at<true>(L, s);
-        ang2 = fabs(wrap_to_pi(h - hdl));
-        T a = s - L.len; if (!(a > T(0))) a = T(0);
-        T b = T(0) - s; if (!(b > T(0))) b = T(0);
-        const T d = fabs(r) + a + b + T(1) * ang2;
-        if (l == 0 || d < bd2) { bd2 = d; best2 = l; }
-      }
-    }
-    if (want_closest && best2 != cl && atomicAdd(&g_dbg_count, 1) < 20)
-      printf("items: blk %d tid %d closest %d/%d total %d G %d\n", (int)blockIdx.x, tid, cl, best2, total, G);
-  }
-  if (tid == 0)
-    for (int a = 0; a < nl; ++a) {
-      bool found = false;
-      for (int b = 0; b < nl; ++b) found |= V.lperm[b] == a;
-      if (!found && atomicAdd(&g_dbg_count, 1) < 20) printf("items: blk %d lperm lacks %d\n", (int)blockIdx.x, a);
-    }
-  __syncthreads();
-#endif
   return cl;
 }
 
@@ -1512,11 +1413,7 @@ __device__ int next_given(const LaneT<T>* lanes, const RoadTab& R, int cur_road,
 template <typename T>
 // Inlined into the NET_GRAPH instance, the only one that calls them (measured: intersection
 // launch f64 1.115 -> 1.072 ms, f32 0.579 -> 0.529 ms against out-of-line calls).
-#ifdef TTRL_NET_NOINLINE
-#define TTRL_NET_ATTR __noinline__
-#else
 #define TTRL_NET_ATTR __forceinline__
-#endif
 __device__ TTRL_NET_ATTR int follow_road(const LaneT<T>* lanes, const RoadTab& R, T vl, int tgt, T x, T y, int8_t* rr,
                                         int8_t* rl, int8_t* rn, T s) {  // s: the position along lanes[tgt]
   const LaneT<T>& L = lanes[tgt];
@@ -1831,9 +1728,9 @@ struct StepOut {
   float* comp;
   void* ego_speed;
   uint8_t* ego_crashed;
-  // workgroup slot -> env (a permutation of the envs, EPW consecutive entries per workgroup; -1
-  // entries: none; null: slot order).  A dispatch order only: every env's result is independent
-  // of it.
+  // workgroup slot -> env (a permutation of the envs, EPW consecutive entries per workgroup; a
+  // negative entry: an idle slot; null: slot order).  A dispatch order only: every env's result is
+  // independent of it.  It must not name an env twice (two workgroups would write one env).
   const int32_t* order;
   // n_lut > 0: actions[] are action indices, mapped to meta-action codes by lut (an index outside
   // the table: no meta-action)
@@ -1897,12 +1794,12 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
   // road networks take their envs in so.order (heaviest workgroups first, see ix_order_kernel)
   const int32_t* ord = GR ? so.order : nullptr;
   const int env = env_at(ord, blockIdx.x * EPW + le, st.n_envs);
-  const bool env_on = env < st.n_envs && (!env_mask || env_mask[env]);  // masked-out envs: untouched
+  const bool env_on = (unsigned)env < (unsigned)st.n_envs && (!env_mask || env_mask[env]);  // masked-out envs: untouched
   if (env_mask) {  // a workgroup with no active env leaves at once (uniform: before any barrier)
     bool any = false;
     for (int q = 0; q < EPW; ++q) {
       const int e = env_at(ord, blockIdx.x * EPW + q, st.n_envs);
-      any |= e < st.n_envs && env_mask[e];
+      any |= (unsigned)e < (unsigned)st.n_envs && env_mask[e];
     }
     if (!any) return;
   }
@@ -2578,11 +2475,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
       }
       PH(6);
       int cl;
-#ifndef TTRL_NO_ITEMS
       if constexpr (GR && NS * EPW == 64)
-#else
-      if constexpr (false)
-#endif
         cl = project_items<T, NS, EPW, LC>(V, P, nl, tid, le, i, present, !(ablate & A_NO_LANE), my_box, onb_all);
       else {
         int ob = 0;
@@ -2815,13 +2708,8 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
             if (lo ? sat_separated(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt)
                    : sat_separated(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt))
               continue;
-#ifdef TTRL_SAT_OOL  // round 2's out-of-line call (A/B only: see DESIGN.md "the NET_GRAPH 4-wave fault")
-            if (lo) sat_pair_ool(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt, inter, will, tx, ty);
-            else sat_pair_ool(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt, inter, will, tx, ty);
-#else
             if (lo) sat_pair(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt, inter, will, tx, ty);
             else sat_pair(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt, inter, will, tx, ty);
-#endif
             if (will) {
               if (lo) { best_gt = j; gx = tx / T(2); gy = ty / T(2); }
               else { best_lt = j; lx = -tx / T(2); ly = -ty / T(2); }
@@ -2847,7 +2735,7 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
   asm volatile("" : "+v"(tid_r));
   const int le = tid_r / NS, i = tid_r % NS;
   const int env = env_at(ord, blockIdx.x * EPW + le, st.n_envs);
-  const bool env_on = env < st.n_envs && (!env_mask || env_mask[env]);
+  const bool env_on = (unsigned)env < (unsigned)st.n_envs && (!env_mask || env_mask[env]);
   const bool slot = env_on && i < N;
   const size_t k = (size_t)env * N + i;
   const int me = le * NS + i;

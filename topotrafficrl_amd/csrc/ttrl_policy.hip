@@ -146,6 +146,7 @@ struct Explore {
   long long step;
   const int64_t* step_dev; // overrides step when set
   unsigned seed_lo, seed_hi;
+  long long env_offset;    // global env id of row 0: the draws are keyed on (env_offset + row, step)
 };
 
 __device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 key) {
@@ -441,7 +442,7 @@ __global__ void __launch_bounds__(64, 2) ego_attention_kernel(const float* __res
       }
       const float eps = ex.eps_dev ? *ex.eps_dev : ex.eps;
       const unsigned long long step = ex.step_dev ? (unsigned long long)*ex.step_dev : (unsigned long long)ex.step;
-      const unsigned long long env = (unsigned long long)(b0 + k);
+      const unsigned long long env = (unsigned long long)ex.env_offset + (unsigned long long)(b0 + k);
       const uint4 r = philox4x32(make_uint4((unsigned)env, (unsigned)(env >> 32), (unsigned)step, (unsigned)(step >> 32)),
                                  make_uint2(ex.seed_lo, ex.seed_hi));
       const float uni = (float)(r.x >> 8) * 0x1p-24f;                       // U[0, 1)
@@ -512,10 +513,11 @@ int ttrl_ego_attention_q(const float* obs, int32_t batch, int32_t n_entities, in
 
 int ttrl_ego_attention_act(const float* obs, int32_t batch, int32_t n_entities, int32_t n_features, int32_t heads,
                            const float* weights, int32_t n_actions, float epsilon, const float* epsilon_dev,
-                           uint64_t seed, int64_t step, const int64_t* step_dev, float* q, int64_t* actions,
-                           int32_t* actions32, void* stream) {
-  if ((!actions && !actions32) || !(epsilon >= 0.0f && epsilon <= 1.0f)) return TTRL_E_ARG;
+                           uint64_t seed, int64_t step, const int64_t* step_dev, int64_t env_offset, float* q,
+                           int64_t* actions, int32_t* actions32, void* stream) {
+  if ((!actions && !actions32) || !(epsilon >= 0.0f && epsilon <= 1.0f) || env_offset < 0) return TTRL_E_ARG;
   Explore ex{};
+  ex.env_offset = env_offset;
   ex.act = actions; ex.act32 = actions32;
   ex.eps = epsilon; ex.eps_dev = epsilon_dev; ex.step = step; ex.step_dev = step_dev;
   ex.seed_lo = (unsigned)seed; ex.seed_hi = (unsigned)(seed >> 32);

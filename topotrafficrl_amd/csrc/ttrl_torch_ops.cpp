@@ -559,12 +559,13 @@ std::tuple<at::Tensor, at::Tensor> ego_attention_act(const at::Tensor& obs, cons
                                                      int64_t n_actions, double epsilon, int64_t seed, int64_t step,
                                                      const c10::optional<at::Tensor>& epsilon_dev,
                                                      const c10::optional<at::Tensor>& step_dev,
-                                                     bool int32_actions) {
+                                                     bool int32_actions, int64_t env_offset) {
   check_hip(obs);
   TORCH_CHECK(obs.dim() == 3 && obs.scalar_type() == at::kFloat, "ttrl: obs must be float32 [B, entities, features]");
   TORCH_CHECK(weights.device() == obs.device() && weights.scalar_type() == at::kFloat && weights.is_contiguous(),
               "ttrl: weights must be a contiguous float32 tensor on the obs device (packed layout)");
   TORCH_CHECK(epsilon >= 0.0 && epsilon <= 1.0, "ttrl: epsilon must lie in [0, 1]");
+  TORCH_CHECK(env_offset >= 0, "ttrl: env_offset must be non-negative");
   const bool ed = epsilon_dev && epsilon_dev->defined(), sd = step_dev && step_dev->defined();
   if (ed)
     TORCH_CHECK(epsilon_dev->device() == obs.device() && epsilon_dev->scalar_type() == at::kFloat &&
@@ -583,7 +584,7 @@ std::tuple<at::Tensor, at::Tensor> ego_attention_act(const at::Tensor& obs, cons
   ok(ttrl_ego_attention_act(x.data_ptr<float>(), B, NE, F, static_cast<int32_t>(heads), weights.data_ptr<float>(),
                             static_cast<int32_t>(n_actions), static_cast<float>(epsilon),
                             ed ? epsilon_dev->data_ptr<float>() : nullptr, static_cast<uint64_t>(seed), step,
-                            sd ? step_dev->data_ptr<int64_t>() : nullptr, q.data_ptr<float>(),
+                            sd ? step_dev->data_ptr<int64_t>() : nullptr, env_offset, q.data_ptr<float>(),
                             int32_actions ? nullptr : act.data_ptr<int64_t>(),
                             int32_actions ? act.data_ptr<int32_t>() : nullptr, stream_of(x)),
      "ttrl_ego_attention_act");
@@ -696,7 +697,8 @@ at::Tensor meta_ego_attention(const at::Tensor& obs, const at::Tensor&, int64_t,
 std::tuple<at::Tensor, at::Tensor> meta_ego_attention_act(const at::Tensor& obs, const at::Tensor&, int64_t,
                                                           int64_t n_actions, double, int64_t, int64_t,
                                                           const c10::optional<at::Tensor>&,
-                                                          const c10::optional<at::Tensor>&, bool int32_actions) {
+                                                          const c10::optional<at::Tensor>&, bool int32_actions,
+                                                          int64_t) {
   return {at::empty({obs.size(0)}, opts(obs, int32_actions ? at::kInt : at::kLong)),
           at::empty({obs.size(0), n_actions}, opts(obs, at::kFloat))};
 }
@@ -742,7 +744,7 @@ TORCH_LIBRARY(ttrl, m) {
         "Tensor terminated, Tensor truncated, Tensor components, Tensor ego_speed, Tensor ego_crashed)");
   m.def("ego_attention_q(Tensor obs, Tensor weights, int heads, int n_actions) -> Tensor");
   m.def("ego_attention_act(Tensor obs, Tensor weights, int heads, int n_actions, float epsilon, int seed, int step, "
-        "Tensor? epsilon_dev=None, Tensor? step_dev=None, bool int32_actions=False) -> (Tensor, Tensor)");
+        "Tensor? epsilon_dev=None, Tensor? step_dev=None, bool int32_actions=False, int env_offset=0) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(ttrl, CUDA, m) {  // the HIP device of ROCm PyTorch

@@ -107,7 +107,9 @@ class BatchedRoad:
         Kinematics observation of the final state (``kin_cfg``; else obs / ids are empty) and the step
         tail (time += time_inc, reward, terminated, truncated, components, the info's ego speed /
         crashed).  Returns those 8 tensors.  ``order``: an optional dispatch order of the envs (int32
-        permutation, ix_step_tail_ writes it; road networks only, results unchanged).
+        permutation, ix_step_tail_ writes it; road networks only, results unchanged).  It must be a
+        permutation: an env named twice would be written by two workgroups (not checked on the
+        device: that would need a host sync); a negative entry is an idle slot.
         ``action_lut``: ``actions`` are action indices and this maps them to meta-action codes inside
         the launch (DiscreteMetaAction._indices)."""
         a = None if actions is None else self._actions(actions)

@@ -30,8 +30,8 @@ class BatchedDQNAgent:
     the EgoAttention-2h value net and epsilon-greedy exploration, learning with the batched
     replay memory / double-DQN residual / Adam / target sync of ``dqn.DQNLearner``."""
 
-    def __init__(self, device, n_actions: int = 5, seed: int = 0, config: dict | None = None):
-        self.policy = EgoAttentionPolicy(device, n_actions=n_actions, seed=seed)
+    def __init__(self, device, n_actions: int = 5, seed: int = 0, config: dict | None = None, env_id_offset: int = 0):
+        self.policy = EgoAttentionPolicy(device, n_actions=n_actions, seed=seed, env_id_offset=env_id_offset)
         self.config = {**DEFAULT_CONFIG, **(config or {})}
         self.seed_value = seed
         self.learner = None  # built on the first record (the observation shape is known then)
@@ -109,6 +109,9 @@ class BatchedEvaluation:
         self.observation = None
         if hasattr(agent, "set_writer"):
             agent.set_writer(writer)
+        if isinstance(getattr(agent, "policy", None), EgoAttentionPolicy) and hasattr(env, "config"):
+            # the env's global ids (a data-parallel rank's shard): exploration keyed on them
+            agent.policy.env_id_offset = int(env.config.get("env_id_offset", 0))
         agent.evaluation = self
 
     # evaluation.py:115-121
