@@ -105,6 +105,26 @@ def cpu_baseline(vehicles: int, obs_cfg: dict, seconds_target: float = 10.0, env
                       f"of the reference loop order (oracle/ttrl_oracle.c), OpenMP over envs, {el:.1f} s"}
 
 
+def reference_equiv(vehicles: int, seconds_target: float = 10.0, processes: int | None = None) -> dict:
+    """the reference's own loop structure on the host cores -- oracle/objsim.py,
+    the per-vehicle-object NumPy restatement (it reproduces the goldens, tests/test_objsim.py), one
+    process per core as the reference's Pool design (evaluation.py:234-235), each on its own scenes
+    of the synthetic highway for about ``seconds_target``.  Calibrated in the build container
+    against the reference's Road.act / Road.step on the same scenes and one core
+    (oracle/time_reference.py): ``reference_estimate`` = value / ratio is the reference itself."""
+    from oracle import objsim
+    processes = processes or host_threads()
+    r = objsim.throughput(n=vehicles, seconds=seconds_target, processes=processes)
+    ratio = objsim.REFERENCE_RATIO
+    return {"value": r["value"], "unit": "vehicle-steps/s", "cores": processes, "kind": "reference-equivalent",
+            "per_core": r["per_core"], "calibration_ratio": ratio,
+            "reference_estimate": r["value"] / ratio if ratio else None,
+            "calibration": "oracle/time_reference.py, profiles/r05/reference_equiv_calibration.txt",
+            "sample": f"{processes} processes x 5 env.steps (15 frames) per {vehicles}-vehicle highway scene, "
+                      f"Road.act + Road.step over per-vehicle numpy objects (oracle/objsim.py; the observation "
+                      f"is not timed: ~2 % of the reference's step), {r['wall_s']:.1f} s wall"}
+
+
 def cpu_baseline_ix(seconds_target: float = 10.0) -> dict:
     """The intersection episodes on the float64 C restatement (oracle/), OpenMP over envs: env.step
     = fused frames + shuffled Kinematics + rewards + clear/spawn, with resets (and their 45
@@ -511,6 +531,10 @@ def main():
         out["cpu_baseline"] = (cpu_baseline_ix(args.cpu_seconds) if ix else
                                cpu_baseline(N, C["obs"] if C["obs"]["type"] == "Kinematics" else GRID7,
                                             args.cpu_seconds, envs=E, threads=1 if E == 1 else None))
+        # beside the C port: the reference's own per-object loop structure (straight highways only;
+        # the intersection's network lanes are not in oracle/objsim.py)
+        out["cpu_baseline"]["reference_equiv"] = (
+            None if ix else reference_equiv(N, args.cpu_seconds, processes=1 if E == 1 else None))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -1,0 +1,535 @@
+"""A NumPy per-vehicle-object restatement of the reference's frame loop -- TEST INFRASTRUCTURE ONLY
+(bench.py's cpu_baseline leg and tests/; never the product).
+
+SURVEY.md §8(d)(i): the CPU baseline "mirrors the reference's loop structure", one Python object
+per vehicle holding numpy 2-vectors, a per-frame ``Road.act`` / ``Road.step`` over the vehicle list,
+neighbour scans over every vehicle through each lane's local coordinates, and the pairwise
+collision pass with its separating-axis test -- so its speed per core stands in for the reference's
+own Python, which cannot run on the GPU box (/root/reference is absent there).  It is a fresh
+restatement of the algorithm (the same one oracle/ttrl_oracle.c restates in C), on straight lanes
+(the synthetic highway of the bench), and it reproduces the reference goldens
+(tests/test_objsim.py).  Its speed against the reference's own loop is calibrated in the build
+container by oracle/time_reference.py (REFERENCE_RATIO below).
+
+Reference call sites restated here:
+  Road.act / Road.step road.py:461-478; Road.neighbour_vehicles road.py:480-513
+  StraightLane lane.py:159-213 (local_coordinates, heading_at, position), AbstractLane.on_lane
+    :80-102, is_reachable_from :104-118, after_end :120-125, distance_with_heading :132-147
+  RoadNetwork.get_closest_lane_index road.py:55-71, side_lanes :200-211
+  IDMVehicle.act behavior.py:93-137, step :139-148, acceleration :150-190, desired_gap :192-217,
+    change_lane_policy :219-263, mobil :265-324; utils.do_every / not_zero / wrap_to_pi utils.py
+  ControlledVehicle.act controller.py:89-133, follow_road :135-143, steering_control :145-187,
+    speed_control :189-198; MDPVehicle.act :295-315, speed_to_index :326-344
+  Vehicle.step kinematics.py:130-153, clip_actions :155-168, on_state_update :170-177
+  RoadObject.handle_collisions objects.py:91-119, _is_colliding :121-137, polygon :168-180,
+    lane_distance_to :182-197; utils.are_polygons_intersecting utils.py:175-239
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from topotrafficrl_amd import _abi
+
+# objsim vehicle-frames/s over the reference's own, same scenes, one core of the build container
+# (oracle/time_reference.py; profiles/r05/reference_equiv_calibration.txt): a bench figure divided
+# by this ratio is the reference loop's speed.
+REFERENCE_RATIO = 1.040  # run 2 (80 s); run 1 (40 s) gave 1.098: within the ±20 % SURVEY.md §8(d) asks for
+
+ACTIONS = {0: "LANE_LEFT", 1: "IDLE", 2: "LANE_RIGHT", 3: "FASTER", 4: "SLOWER"}
+
+
+def not_zero(x: float, eps: float = 1e-2) -> float:
+    if abs(x) > eps:
+        return x
+    elif x >= 0:
+        return eps
+    else:
+        return -eps
+
+
+def wrap_to_pi(x: float) -> float:
+    return ((x + np.pi) % (2 * np.pi)) - np.pi
+
+
+class StraightLane:
+    VEHICLE_LENGTH = 5.0
+
+    def __init__(self, start, end, width: float, speed_limit: float, forbidden: bool = False):
+        self.start = np.array(start, dtype=np.float64)
+        self.end = np.array(end, dtype=np.float64)
+        self.width = width
+        self.speed_limit = speed_limit
+        self.forbidden = forbidden
+        self.heading = np.arctan2(self.end[1] - self.start[1], self.end[0] - self.start[0])
+        self.length = np.linalg.norm(self.end - self.start)
+        self.direction = (self.end - self.start) / self.length
+        self.direction_lateral = np.array([-self.direction[1], self.direction[0]])
+
+    def position(self, s: float, r: float) -> np.ndarray:
+        return self.start + s * self.direction + r * self.direction_lateral
+
+    def heading_at(self, s: float) -> float:
+        return self.heading
+
+    def width_at(self, s: float) -> float:
+        return self.width
+
+    def local_coordinates(self, position: np.ndarray):
+        delta = position - self.start
+        return float(np.dot(delta, self.direction)), float(np.dot(delta, self.direction_lateral))
+
+    # the generic lane methods below go through width_at / local_angle and numpy scalar
+    # operations as the reference's AbstractLane does, so that their cost per call is the same
+    def on_lane(self, position, s=None, r=None, margin: float = 0.0) -> bool:
+        if s is None or r is None:
+            s, r = self.local_coordinates(position)
+        return bool(np.abs(r) <= self.width_at(s) / 2 + margin
+                    and -self.VEHICLE_LENGTH <= s < self.length + self.VEHICLE_LENGTH)
+
+    def is_reachable_from(self, position) -> bool:
+        if self.forbidden:
+            return False
+        s, r = self.local_coordinates(position)
+        return bool(np.abs(r) <= 2 * self.width_at(s) and 0 <= s < self.length + self.VEHICLE_LENGTH)
+
+    def after_end(self, position, s=None) -> bool:
+        if not s:
+            s, _ = self.local_coordinates(position)
+        return s > self.length - self.VEHICLE_LENGTH / 2
+
+    def local_angle(self, heading: float, s: float) -> float:
+        return wrap_to_pi(heading - self.heading_at(s))
+
+    def distance_with_heading(self, position, heading: float, heading_weight: float = 1.0) -> float:
+        if heading is None:
+            s, r = self.local_coordinates(position)
+            return abs(r) + max(s - self.length, 0) + max(0 - s, 0)
+        s, r = self.local_coordinates(position)
+        angle = np.abs(self.local_angle(heading, s))
+        return abs(r) + max(s - self.length, 0) + max(0 - s, 0) + heading_weight * angle
+
+
+class Network:
+    """One road ("0" -> "1") of parallel straight lanes: graph {from: {to: [lanes]}}."""
+
+    def __init__(self, lanes: list):
+        self.graph = {"0": {"1": lanes}}
+
+    def get_lane(self, index) -> StraightLane:
+        return self.graph[index[0]][index[1]][index[2]]
+
+    def get_closest_lane_index(self, position, heading):
+        distances, indexes = [], []
+        for fr, tos in self.graph.items():
+            for to, lanes in tos.items():
+                for i, lane in enumerate(lanes):
+                    distances.append(lane.distance_with_heading(position, heading))
+                    indexes.append((fr, to, i))
+        return indexes[int(np.argmin(distances))]
+
+    def side_lanes(self, index):
+        fr, to, i = index
+        out = []
+        if i > 0:
+            out.append((fr, to, i - 1))
+        if i < len(self.graph[fr][to]) - 1:
+            out.append((fr, to, i + 1))
+        return out
+
+    def next_lane(self, index):
+        return index  # the single road: no road leaves "1" (the reference's KeyError branch)
+
+
+class Vehicle:
+    """Kinematics + ControlledVehicle (+ IDMVehicle / MDPVehicle behaviour below)."""
+
+    def __init__(self, road, position, heading, speed, p: _abi.Params):
+        self.road, self.p = road, p
+        self.position = np.array(position, dtype=np.float64)
+        self.heading, self.speed = float(heading), float(speed)
+        self.lane_index = road.network.get_closest_lane_index(self.position, self.heading)
+        self.lane = road.network.get_lane(self.lane_index)
+        self.target_lane_index = self.lane_index
+        self.target_speed = self.speed
+        self.action = {"steering": 0.0, "acceleration": 0.0}
+        self.crashed = False
+        self.impact = None
+        self.diagonal = np.sqrt(p.length ** 2 + p.width ** 2)
+
+    @property
+    def direction(self) -> np.ndarray:
+        return np.array([np.cos(self.heading), np.sin(self.heading)])
+
+    @property
+    def velocity(self) -> np.ndarray:
+        return self.speed * self.direction
+
+    def lane_distance_to(self, other) -> float:
+        if other is None:
+            return np.nan
+        return self.lane.local_coordinates(other.position)[0] - self.lane.local_coordinates(self.position)[0]
+
+    def follow_road(self):
+        if self.road.network.get_lane(self.target_lane_index).after_end(self.position):
+            self.target_lane_index = self.road.network.next_lane(self.target_lane_index)
+
+    def steering_control(self, target_lane_index) -> float:
+        p = self.p
+        target_lane = self.road.network.get_lane(target_lane_index)
+        s, r = target_lane.local_coordinates(self.position)
+        lane_future_heading = target_lane.heading_at(s + self.speed * p.tau_pursuit)
+        lateral_speed_command = -p.kp_lateral * r
+        heading_command = np.arcsin(np.clip(lateral_speed_command / not_zero(self.speed), -1, 1))
+        heading_ref = lane_future_heading + np.clip(heading_command, -np.pi / 4, np.pi / 4)
+        heading_rate_command = p.kp_heading * wrap_to_pi(heading_ref - self.heading)
+        slip_angle = np.arcsin(np.clip(p.length / 2 / not_zero(self.speed) * heading_rate_command, -1, 1))
+        steering_angle = np.arctan(2 * np.tan(slip_angle))
+        return float(np.clip(steering_angle, -p.max_steering, p.max_steering))
+
+    def controlled_act(self, action: str | None = None):
+        """ControlledVehicle.act: lateral meta-actions, then the two controllers."""
+        self.follow_road()
+        if action in ("LANE_RIGHT", "LANE_LEFT"):
+            fr, to, i = self.target_lane_index
+            n = len(self.road.network.graph[fr][to])
+            idx = (fr, to, int(np.clip(i + (1 if action == "LANE_RIGHT" else -1), 0, n - 1)))
+            if self.road.network.get_lane(idx).is_reachable_from(self.position):
+                self.target_lane_index = idx
+        self.action = {"steering": self.steering_control(self.target_lane_index),
+                       "acceleration": self.p.kp_a * (self.target_speed - self.speed)}
+        self.action["steering"] = float(np.clip(self.action["steering"], -self.p.max_steering, self.p.max_steering))
+
+    def clip_actions(self):
+        p = self.p
+        if self.crashed:
+            self.action["steering"] = 0
+            self.action["acceleration"] = -1.0 * self.speed
+        self.action["steering"] = float(self.action["steering"])
+        self.action["acceleration"] = float(self.action["acceleration"])
+        if self.speed > p.max_speed:
+            self.action["acceleration"] = min(self.action["acceleration"], 1.0 * (p.max_speed - self.speed))
+        elif self.speed < p.min_speed:
+            self.action["acceleration"] = max(self.action["acceleration"], 1.0 * (p.min_speed - self.speed))
+
+    def step(self, dt: float):
+        self.clip_actions()
+        beta = np.arctan(1 / 2 * np.tan(self.action["steering"]))
+        v = self.speed * np.array([np.cos(self.heading + beta), np.sin(self.heading + beta)])
+        self.position = self.position + v * dt
+        if self.impact is not None:
+            self.position = self.position + self.impact
+            self.crashed = True
+            self.impact = None
+        self.heading += self.speed * np.sin(beta) / (self.p.length / 2) * dt
+        self.speed += self.action["acceleration"] * dt
+        self.lane_index = self.road.network.get_closest_lane_index(self.position, self.heading)
+        self.lane = self.road.network.get_lane(self.lane_index)
+
+    def polygon(self) -> np.ndarray:
+        L, W = self.p.length, self.p.width
+        pts = np.array([[-L / 2, -W / 2], [-L / 2, +W / 2], [+L / 2, +W / 2], [+L / 2, -W / 2]]).T
+        c, s = np.cos(self.heading), np.sin(self.heading)
+        rot = np.array([[c, -s], [s, c]])
+        pts = (rot @ pts).T + np.tile(self.position, (4, 1))
+        return np.vstack([pts, pts[0:1]])
+
+    def handle_collisions(self, other, dt: float):
+        if other is self:
+            return
+        if np.linalg.norm(other.position - self.position) > (self.diagonal + other.diagonal) / 2 + self.speed * dt:
+            return
+        inter, will, transition = separating_axes(self.polygon(), other.polygon(), self.velocity * dt,
+                                                  other.velocity * dt)
+        if will:
+            self.impact = transition / 2
+            other.impact = -transition / 2
+        if inter:
+            self.crashed = other.crashed = True
+
+
+class IDMVehicle(Vehicle):
+    def __init__(self, road, position, heading, speed, p, delta: float, timer: float):
+        super().__init__(road, position, heading, speed, p)
+        self.DELTA, self.timer = float(delta), float(timer)
+
+    def act(self, action=None):
+        if self.crashed:
+            return
+        act = {}
+        self.follow_road()
+        self.change_lane_policy()
+        act["steering"] = self.steering_control(self.target_lane_index)
+        act["steering"] = float(np.clip(act["steering"], -self.p.max_steering, self.p.max_steering))
+        front, rear = self.road.neighbour_vehicles(self, self.lane_index)
+        act["acceleration"] = self.acceleration(self, front, rear)
+        if self.lane_index != self.target_lane_index:
+            front, rear = self.road.neighbour_vehicles(self, self.target_lane_index)
+            act["acceleration"] = min(act["acceleration"], self.acceleration(self, front, rear))
+        act["acceleration"] = float(np.clip(act["acceleration"], -self.p.acc_max, self.p.acc_max))
+        self.action = act
+
+    def step(self, dt: float):
+        self.timer += dt
+        super().step(dt)
+
+    def acceleration(self, ego, front=None, rear=None) -> float:
+        if ego is None:
+            return 0.0
+        p = self.p
+        target_speed = float(np.clip(ego.target_speed, 0, ego.lane.speed_limit))
+        acc = p.comfort_acc_max * (1 - np.power(max(ego.speed, 0) / abs(not_zero(target_speed)), self.DELTA))
+        if front is not None:
+            d = ego.lane_distance_to(front)
+            acc -= p.comfort_acc_max * np.power(self.desired_gap(ego, front) / not_zero(d), 2)
+        return float(acc)
+
+    def desired_gap(self, ego, front) -> float:
+        p = self.p
+        ab = -p.comfort_acc_max * p.comfort_acc_min
+        dv = np.dot(ego.velocity - front.velocity, ego.direction)
+        return p.distance_wanted + ego.speed * p.time_wanted + ego.speed * dv / (2 * np.sqrt(ab))
+
+    def change_lane_policy(self):
+        if self.lane_index != self.target_lane_index:
+            if self.lane_index[:2] == self.target_lane_index[:2]:
+                for v in self.road.vehicles:
+                    if (v is not self and v.lane_index != self.target_lane_index
+                            and v.target_lane_index == self.target_lane_index):
+                        d = self.lane_distance_to(v)
+                        d_star = self.desired_gap(self, v)
+                        if 0 < d < d_star:
+                            self.target_lane_index = self.lane_index
+                            break
+            return
+        if not self.p.lane_change_delay < self.timer:  # utils.do_every
+            return
+        self.timer = 0
+        for lane_index in self.road.network.side_lanes(self.lane_index):
+            if not self.road.network.get_lane(lane_index).is_reachable_from(self.position):
+                continue
+            if np.abs(self.speed) < 1:
+                continue
+            if self.mobil(lane_index):
+                self.target_lane_index = lane_index
+
+    def mobil(self, lane_index) -> bool:
+        p = self.p
+        new_pre, new_fol = self.road.neighbour_vehicles(self, lane_index)
+        new_fol_a = self.acceleration(new_fol, new_pre)
+        new_fol_pred_a = self.acceleration(new_fol, self)
+        if new_fol_pred_a < -p.lane_change_max_braking:
+            return False
+        old_pre, old_fol = self.road.neighbour_vehicles(self)
+        self_pred_a = self.acceleration(self, new_pre)
+        self_a = self.acceleration(self, old_pre)
+        old_fol_a = self.acceleration(old_fol, self)
+        old_fol_pred_a = self.acceleration(old_fol, old_pre)
+        jerk = self_pred_a - self_a + p.politeness * (new_fol_pred_a - new_fol_a + old_fol_pred_a - old_fol_a)
+        return not jerk < p.lane_change_min_acc_gain
+
+
+class MDPVehicle(Vehicle):
+    def __init__(self, road, position, heading, speed, p):
+        super().__init__(road, position, heading, speed, p)
+        self.target_speeds = np.array(p.target_speeds[:p.n_target_speeds], dtype=np.float64)
+        self.speed_index = self.speed_to_index(self.target_speed)
+        self.target_speed = float(self.target_speeds[self.speed_index])
+
+    def speed_to_index(self, speed: float) -> int:
+        ts = self.target_speeds
+        x = (speed - ts[0]) / (ts[-1] - ts[0])
+        return int(np.clip(np.round(x * (ts.size - 1)), 0, ts.size - 1))
+
+    def act(self, action: str | None = None):
+        if action in ("FASTER", "SLOWER"):
+            self.speed_index = self.speed_to_index(self.speed) + (1 if action == "FASTER" else -1)
+            self.speed_index = int(np.clip(self.speed_index, 0, self.target_speeds.size - 1))
+            self.target_speed = float(self.target_speeds[self.speed_index])
+            self.controlled_act()
+            return
+        self.controlled_act(action)
+
+
+def separating_axes(a: np.ndarray, b: np.ndarray, disp_a: np.ndarray, disp_b: np.ndarray):
+    """(intersecting, will_intersect, translation) of two closed polygons moving by disp_a / disp_b."""
+    intersecting = will_intersect = True
+    min_distance = np.inf
+    translation = translation_axis = None
+    for polygon in (a, b):
+        for p1, p2 in zip(polygon, polygon[1:]):
+            normal = np.array([-p2[1] + p1[1], p2[0] - p1[0]])
+            normal /= np.linalg.norm(normal)
+            min_a, max_a = _project(a, normal)
+            min_b, max_b = _project(b, normal)
+            if _interval_distance(min_a, max_a, min_b, max_b) > 0:
+                intersecting = False
+            vp = normal.dot(disp_a - disp_b)
+            if vp < 0:
+                min_a += vp
+            else:
+                max_a += vp
+            distance = _interval_distance(min_a, max_a, min_b, max_b)
+            if distance > 0:
+                will_intersect = False
+            if not intersecting and not will_intersect:
+                break
+            if abs(distance) < min_distance:
+                min_distance = abs(distance)
+                d = a[:-1].mean(axis=0) - b[:-1].mean(axis=0)
+                translation_axis = normal if d.dot(normal) > 0 else -normal
+    if will_intersect:
+        translation = min_distance * translation_axis
+    return intersecting, will_intersect, translation
+
+
+def _project(polygon, axis):
+    lo = hi = None
+    for pt in polygon:
+        q = pt.dot(axis)
+        if lo is None or q < lo:
+            lo = q
+        if hi is None or q > hi:
+            hi = q
+    return lo, hi
+
+
+def _interval_distance(min_a, max_a, min_b, max_b):
+    return min_b - max_a if min_a < min_b else min_a - max_b
+
+
+class Landmark:
+    """A road object the neighbour scan skips (none on the highway)."""
+
+
+class Road:
+    def __init__(self, network: Network, vehicles: list):
+        self.network, self.vehicles = network, vehicles
+        self.objects: list = []  # obstacles / landmarks: none on the synthetic highway
+
+    def act(self):
+        for v in self.vehicles:
+            v.act()
+
+    def step(self, dt: float):
+        for v in self.vehicles:
+            v.step(dt)
+        for i, v in enumerate(self.vehicles):
+            for other in self.vehicles[i + 1:]:
+                v.handle_collisions(other, dt)
+            for other in self.objects:
+                v.handle_collisions(other, dt)
+
+    def neighbour_vehicles(self, vehicle, lane_index=None):
+        lane_index = lane_index or vehicle.lane_index
+        lane = self.network.get_lane(lane_index)
+        s = lane.local_coordinates(vehicle.position)[0]
+        s_front = s_rear = None
+        v_front = v_rear = None
+        for v in self.vehicles + self.objects:
+            if v is not vehicle and not isinstance(v, Landmark):
+                s_v, lat_v = lane.local_coordinates(v.position)
+                if not lane.on_lane(v.position, s_v, lat_v, margin=1):
+                    continue
+                if s <= s_v and (s_front is None or s_v <= s_front):
+                    s_front, v_front = s_v, v
+                if s_v < s and (s_rear is None or s_v > s_rear):
+                    s_rear, v_rear = s_v, v
+        return v_front, v_rear
+
+    def simulate(self, action: int | None, frames: int, dt: float):
+        """AbstractEnv._simulate: the ego's meta-action on the first frame, then act + step."""
+        for f in range(frames):
+            if f == 0 and action is not None:
+                self.vehicles[0].act(ACTIONS[int(action)])
+            self.act()
+            self.step(dt)
+
+
+def straight_network(table: _abi.LaneTable) -> Network:
+    lanes = [StraightLane([table.start_x[l], table.start_y[l]],
+                          [table.start_x[l] + table.length[l] * table.dir_x[l],
+                           table.start_y[l] + table.length[l] * table.dir_y[l]],
+                          table.width[l], table.speed_limit[l], bool(table.forbidden[l]))
+             for l in range(table.n_lanes)]
+    return Network(lanes)
+
+
+def road_from_state(h, e: int, table: _abi.LaneTable, p: _abi.Params) -> Road:
+    """Env e of an oracle HostState (highway: slot 0 the MDP ego, then IDM vehicles) as objects."""
+    net = straight_network(table)
+    road = Road(net, [])
+    for i in range(h.N):
+        kind = int(h["kind"][e, i])
+        if kind == _abi.ABSENT:
+            continue
+        pos = [h["x"][e, i], h["y"][e, i]]
+        if kind == _abi.MDP:
+            v = MDPVehicle(road, pos, h["heading"][e, i], h["speed"][e, i], p)
+            v.speed_index = int(h["speed_index"][e, i])
+        else:
+            v = IDMVehicle(road, pos, h["heading"][e, i], h["speed"][e, i], p, h["delta"][e, i], h["timer"][e, i])
+        v.target_speed = float(h["target_speed"][e, i])
+        v.lane_index = ("0", "1", int(h["lane"][e, i]))
+        v.lane = net.get_lane(v.lane_index)
+        v.target_lane_index = ("0", "1", int(h["target_lane"][e, i]))
+        v.crashed = bool(h["crashed"][e, i])
+        v.impact = np.array([h["impact_x"][e, i], h["impact_y"][e, i]]) if h["has_impact"][e, i] else None
+        v.action = {"steering": float(h["steer"][e, i]), "acceleration": float(h["acc"][e, i])}
+        road.vehicles.append(v)
+    return road
+
+
+def state_of(road: Road) -> dict:
+    """The objects' state as arrays in list order (fields of ttrl_state_t)."""
+    vs = road.vehicles
+    return {"x": np.array([v.position[0] for v in vs]), "y": np.array([v.position[1] for v in vs]),
+            "heading": np.array([v.heading for v in vs]), "speed": np.array([v.speed for v in vs]),
+            "target_speed": np.array([v.target_speed for v in vs]),
+            "timer": np.array([getattr(v, "timer", 0.0) for v in vs]),
+            "steer": np.array([v.action["steering"] for v in vs]),
+            "acc": np.array([v.action["acceleration"] for v in vs]),
+            "lane": np.array([v.lane_index[2] for v in vs]), "target_lane": np.array([v.target_lane_index[2] for v in vs]),
+            "crashed": np.array([v.crashed for v in vs]), "has_impact": np.array([v.impact is not None for v in vs]),
+            "impact_x": np.array([v.impact[0] if v.impact is not None else 0.0 for v in vs]),
+            "impact_y": np.array([v.impact[1] if v.impact is not None else 0.0 for v in vs])}
+
+
+def _worker(args):
+    """One process: env scenes of the synthetic highway for ``seconds``; vehicle-frames, seconds."""
+    import time
+    from oracle.oracle import HostState, Oracle
+    n, seconds, seed0 = args
+    table = _abi.straight_lane_table(4)
+    p = _abi.default_params()
+    o = Oracle(table, p)
+    frames = scenes = 0
+    el = 0.0
+    while el < seconds:
+        h = HostState(1, n)
+        o.reset_highway(h, _abi.reset_cfg(n, table), [seed0 + scenes])  # scene building not timed
+        road = road_from_state(h, 0, table, p)
+        scenes += 1
+        t0 = time.perf_counter()
+        for step in range(5):  # 5 env steps of 15 frames per scene, as oracle/time_reference.py
+            road.simulate(1, 15, 1 / 15)
+            frames += 15
+        el += time.perf_counter() - t0
+    return frames * n, el
+
+
+def throughput(n: int = 64, seconds: float = 10.0, processes: int = 1) -> dict:
+    """Vehicle-frames/s of ``processes`` worker processes, one per core (the reference's Pool
+    design, evaluation.py:234-235), each for about ``seconds``."""
+    import multiprocessing as mp
+    import time
+    t0 = time.perf_counter()
+    if processes == 1:
+        res = [_worker((n, seconds, 1000))]
+    else:
+        with mp.get_context("spawn").Pool(processes) as pool:
+            res = pool.map(_worker, [(n, seconds, 1000 + 7919 * k) for k in range(processes)])
+    wall = time.perf_counter() - t0
+    veh_frames = sum(r[0] for r in res)
+    per_proc = [r[0] / r[1] for r in res]
+    return {"value": float(sum(per_proc)), "per_core": float(np.mean(per_proc)), "veh_frames": int(veh_frames),
+            "processes": processes, "wall_s": wall}

@@ -4,7 +4,10 @@ Imports the unmodified reference simulation core exactly as oracle/gen_golden.py
 package __init__s that need gymnasium are bypassed) and times Road.act + Road.step(1/15) on the
 synthetic 64-vehicle straight highway of SURVEY.md §3.C, single-threaded, next to the float64 C
 oracle (oracle/ttrl_oracle.c) on the same scenes and one core.  /root/reference does not exist
-on the GPU box, so bench.py's cpu_baseline is the C port; this records the reference itself.
+on the GPU box, so bench.py's cpu_baseline is the C port plus oracle/objsim.py, the per-vehicle-
+object NumPy restatement: this also times objsim on the same scenes (the oracle's reset of the same
+seeds is the reference's scene bit for bit) in alternating rounds and prints its speed ratio to the
+reference loop -- the calibration of bench.py's ``reference_equiv`` (objsim.REFERENCE_RATIO).
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python oracle/time_reference.py [seconds]
 """
@@ -20,21 +23,34 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ.setdefault("OMP_NUM_THREADS", "1")
 
 
-def main(seconds: float = 20.0, n: int = 64) -> None:
+def reference_rate(n: int, seconds: float, seed0: int = 1000) -> tuple:
+    """The reference's Road.act + Road.step: vehicle-frames, seconds (scene building not timed)."""
     from oracle import gen_golden as G
-    from oracle.oracle import HostState, Oracle
-    from topotrafficrl_amd import _abi
     frames, el, scenes = 0, 0.0, 0
     while el < seconds:
-        road = G.make_highway(n, 1000 + scenes)
+        road = G.make_highway(n, seed0 + scenes)
         scenes += 1
         s = time.perf_counter()
-        for _ in range(15 * 5):  # 5 env steps of 15 frames per scene (scene building not timed)
+        for _ in range(15 * 5):  # 5 env steps of 15 frames per scene
             road.act()
             road.step(1 / 15)
             frames += 1
         el += time.perf_counter() - s
-    ref = frames * n / el
+    return frames * n, el, scenes
+
+
+def main(seconds: float = 20.0, n: int = 64) -> None:
+    from oracle import objsim
+    from oracle.oracle import HostState, Oracle
+    from topotrafficrl_amd import _abi
+    rf = re = of = oe = 0.0
+    for _ in range(4):  # alternating rounds: the same machine state for both
+        a, b, _ = reference_rate(n, seconds / 4)
+        rf, re = rf + a, re + b
+        a, b = objsim._worker((n, seconds / 4, 1000))
+        of, oe = of + a, oe + b
+    ref, obj = rf / re, of / oe
+    frames, scenes = int(rf / n), -1
     lanes = _abi.straight_lane_table(4)
     o = Oracle(lanes, _abi.default_params())
     E = 64
@@ -46,7 +62,9 @@ def main(seconds: float = 20.0, n: int = 64) -> None:
         steps += 1
     port = steps * 15 * E * n / (time.perf_counter() - t1)
     print(f"reference Python (Road.act + Road.step, {n} vehicles, 1 core): {ref:.4g} vehicle-frames/s "
-          f"({frames} frames over {scenes} scenes, {el:.1f} s)")
+          f"({frames} frames, {re:.1f} s)")
+    print(f"oracle/objsim.py (per-vehicle-object NumPy restatement, same scenes, 1 core): {obj:.4g} "
+          f"vehicle-frames/s ({of / n:.0f} frames, {oe:.1f} s); ratio objsim / reference = {obj / ref:.3f}")
     print(f"float64 C oracle, same workload shape, 1 core (OMP_NUM_THREADS=1): {port:.4g} vehicle-frames/s "
           f"({port / ref:.0f}x the reference)")
 
