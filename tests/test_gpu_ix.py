@@ -192,3 +192,51 @@ def test_crowded_lane_mobil_on_a_regulated_road(hip_device):
     road.simulate(torch.tensor([LONGI[1]]), 15, 1 / 15)
     o.simulate(g, [LONGI[1]], 15, 1 / 15)
     compare(dev, g, F64_TOL, n)
+
+
+def test_full_turn_arc_keeps_the_projection_bounded(hip_device):
+    """A road network whose second lane is a CircularLane sweeping three full turns: its bounding
+    box for the projection's pruning is the whole circle (lane_box walks at most four cardinal
+    points; an unbounded walk over the arc would hang the launch).  Frames and a fused step with
+    vehicles on both lanes equal the oracle."""
+    from oracle.oracle import Oracle
+    from topotrafficrl_amd import _abi
+    from topotrafficrl_amd.intersection import network_from_graph
+    straight = [_abi.LANE_STRAIGHT, 0.0, 0.0, 300.0, 0.0, 4.0, 15.0, 0, 0, 0, 0, 0, 0, 0, 0, 0]
+    arc = [_abi.LANE_CIRCULAR, 0, 0, 0, 0, 4.0, 15.0, 0, 0, 0, 150.0, 40.0, 30.0, np.pi / 2, np.pi / 2 - 6 * np.pi, 0.0]
+    net = network_from_graph({"a": {"b": [(straight, 1), (arc, 1)]}}, regulation_frequency=2)
+    t = net.table
+    assert t.n_lanes == 2 and t.length[1] > 6 * np.pi * 30 - 1
+    h = HostState(1, 32)
+    xs = [20.0, 45.0, 70.0, 95.0, 130.0, 160.0, 190.0]
+    for q, x in enumerate(xs):
+        h["kind"][0, q] = _abi.MDP if q == 0 else _abi.IDM
+        h["x"][0, q], h["y"][0, q] = x, 0.3 * (q % 2)
+        h["speed"][0, q] = h["target_speed"][0, q] = 8.0 + q
+        h["lane"][0, q] = h["target_lane"][0, q] = 0
+        h["timer"][0, q] = 0.95
+        h["lane_change"][0, q] = 0 if q == 0 else 1
+    for q, a in enumerate([0.3, 1.9, 3.5]):  # three vehicles on the (counter-clockwise) arc, heading along it
+        r = len(xs) + q
+        h["kind"][0, r] = _abi.IDM
+        h["x"][0, r], h["y"][0, r] = 150.0 + 30.0 * np.cos(a), 40.0 + 30.0 * np.sin(a)
+        h["heading"][0, r] = a - np.pi / 2
+        h["speed"][0, r] = h["target_speed"][0, r] = 6.0
+        h["lane"][0, r] = h["target_lane"][0, r] = 1
+        h["lane_change"][0, r] = 1
+    h["speed_index"][0, 0] = 1
+    n = len(xs) + 3
+    o = Oracle(t, P_IX)
+    dev = to_dev(h, hip_device)
+    road = BatchedRoad(RoadNetwork(t), dev, P_IX)
+    g = h.copy()
+    for f in range(3):
+        road.act()
+        o.road_act(g)
+        compare(dev, g, F64_TOL, n)
+        road.step(1 / 15)
+        o.road_step(g, 1 / 15)
+        compare(dev, g, F64_TOL, n)
+    road.simulate(torch.tensor([LONGI[1]]), 15, 1 / 15)
+    o.simulate(g, [LONGI[1]], 15, 1 / 15)
+    compare(dev, g, F64_TOL, n)

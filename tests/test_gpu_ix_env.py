@@ -225,10 +225,12 @@ def test_dqn_training_on_the_intersection(hip_device):
     assert len(L.memory) == 512 and L.steps == 8 and torch.isfinite(L.last_loss)
 
 
-@pytest.mark.parametrize("duration,dtype,streams,slots,chunk", [
-    (1, "f64", 2, 32, 15), (3, "f64", 2, 32, 15), (3, "f32", 2, 32, 15), (2, "f64", 1, 32, 15), (2, "f64", 2, 96, 15),
-    (1, "f64", 2, 32, 9), (2, "f64", 2, 32, 5), (1, "f64", 2, 32, 0), (3, "f64", 2, 32, 0), (2, "f64", 1, 32, 0), (1, "f64", 3, 32, 0)])
-def test_overlapped_resets_equal_in_place_resets(duration, dtype, streams, slots, chunk, hip_device):
+@pytest.mark.parametrize("duration,dtype,streams,slots,chunk,init", [
+    (1, "f64", 2, 32, 15, 10), (3, "f64", 2, 32, 15, 10), (3, "f32", 2, 32, 15, 10), (2, "f64", 1, 32, 15, 10),
+    (2, "f64", 2, 96, 15, 10), (1, "f64", 2, 32, 9, 10), (2, "f64", 2, 32, 5, 10), (1, "f64", 2, 32, 0, 10),
+    (3, "f64", 2, 32, 0, 10), (2, "f64", 1, 32, 0, 10), (1, "f64", 3, 32, 0, 10), (4, "f64", 2, 32, 15, 16),
+    (4, "f32", 2, 32, 15, 16)])
+def test_overlapped_resets_equal_in_place_resets(duration, dtype, streams, slots, chunk, init, hip_device):
     """overlap_resets (each env's next two episodes prepared on side streams, swapped in from
     alternating spare slots by ix_step_tail when an env finishes, the new episode observed in the
     same launch) gives the same trajectories, bit for bit, as the in-place composition of separate
@@ -236,11 +238,14 @@ def test_overlapped_resets_equal_in_place_resets(duration, dtype, streams, slots
     finishes every env at every step (every spare slot in turn).  chunk: the warm-up frames per
     step of a spare reset (15: three chunks, four spare slots; 9: five chunks, six slots; 5: nine
     chunks, ten slots; 0: the whole warm-up at once on `streams` side streams, two slots).  96 slots: the new scenes are observed by the masked observation launch
-    instead of the tail launch (one slot per lane there).  The
+    instead of the tail launch (one slot per lane there).  32 slots: the step launch runs the mixed
+    dispatch (envs holding <= 16 vehicles four to a wave on 16 slots); init 16 initial vehicles
+    (plus the challenger and the ego) puts envs above 16, so both parts of the launch run.  The
     tail's live-vehicle counter (the config-6 bench's count) equals the vehicles present after
     every step."""
     cfg = {**ENV_JSON, "num_envs": 48, "device": hip_device, "auto_reset": True, "duration": duration,
-           "dtype": dtype, "reset_streams": streams, "vehicle_slots": slots, "reset_chunk_frames": chunk}
+           "dtype": dtype, "reset_streams": streams, "vehicle_slots": slots, "reset_chunk_frames": chunk,
+           "initial_vehicle_count": init}
     a = VecIntersectionEnv({**cfg, "overlap_resets": True})
     b = VecIntersectionEnv({**cfg, "overlap_resets": False})
     a.live_counter = torch.zeros((), dtype=torch.int64, device=hip_device)
@@ -259,13 +264,17 @@ def test_overlapped_resets_equal_in_place_resets(duration, dtype, streams, slots
     for k in a.state.t:
         assert torch.equal(a.state[k], b.state[k]), k
     assert int(a.live_counter) == present
-    # the next step's dispatch order: the envs in workgroup groups, heaviest group first
+    # the next step's dispatch order: the envs in workgroup groups, heaviest group first (32 slots:
+    # the mixed order -- every env by its live vehicles, and n_wide the count of those above 16)
     order = a._order[:48].cpu()
     assert torch.equal(order.sort().values, torch.arange(48, dtype=torch.int32))
-    G = 2 if slots <= 32 else 1
-    assert torch.equal(order.view(-1, G), order.view(-1, G)[:, :1] + torch.arange(G, dtype=torch.int32))
-    w = (a.state["kind"] != 0).sum(1).cpu()[order.long()].view(-1, G).sum(1)
+    live = (a.state["kind"] != 0).sum(1).cpu()
+    w = live[order.long()]
     assert bool((w[:-1] >= w[1:]).all()), w
+    if slots == 32:
+        assert int(a._n_wide) == int((live > 16).sum())
+        if init == 16:
+            parity_log.count("overlapped resets (mixed dispatch)", "envs on 32 slots", int(a._n_wide))
 
 
 @pytest.mark.parametrize("E", [64, 63])
@@ -523,3 +532,25 @@ def test_device_steps_from_reference_state(hip_device):
         assert np.array_equal(st["rng"][e], d["rng"][p]), (what, "np_random state")
     parity_log.count(chk, "steps", E)
     parity_log.count(chk, "arrived steps", int(sum(refs[i]["info"][p][4] > 0 for i, p in cases)))
+
+
+def test_negative_dispatch_order_entry_is_an_idle_slot(hip_device):
+    """A negative entry of the dispatch order is an idle workgroup slot (not row -1): the env it
+    replaces is left untouched by the launch, every other env steps as under slot order."""
+    E = 16
+    env = VecIntersectionEnv({**ENV_JSON, "num_envs": E, "device": hip_device})
+    env.reset(seed=8)
+    snap, t0 = env.state.clone(), env.time.clone()
+    codes = env.action_type._codes(torch.ones(E, dtype=torch.int64, device=hip_device))
+    kc = env.observation_type.fused_cfg()
+    env.road.env_step(codes, 15, 1 / 15, kc, env.reward_cfg, env.time, 1.0, None)
+    full = env.state.clone()
+    env.state.copy_(snap)
+    env.time.copy_(t0)
+    order = torch.arange(E, dtype=torch.int32, device=hip_device)
+    order[5] = -1
+    env.road.env_step(codes, 15, 1 / 15, kc, env.reward_cfg, env.time, 1.0, order)
+    keep = torch.arange(E, device=hip_device) != 5
+    for k in env.state.t:
+        assert torch.equal(env.state[k][keep], full[k][keep]), k
+        assert torch.equal(env.state[k][5], snap[k][5]), k
