@@ -96,8 +96,11 @@ def _rollout(E, N, obs_cfg, seed, steps, actions_fn=None):
     return env, h, crashed
 
 
-@pytest.mark.parametrize("E,N,seed", [(4096, 32, 101), (4096, 64, 202)], ids=["config2_4096x32", "config4_4096x64"])
+@pytest.mark.parametrize("E,N,seed", [(4096, 32, 101), (4096, 64, 202), (8192, 32, 505)],
+                         ids=["config2_4096x32", "config4_4096x64", "8192x32_4wave"])
 def test_full_size_kinematics_vs_oracle(E, N, seed, hip_device):
+    """4096 x 32 runs the two-env-per-wave instance's 2-wave twin (2048 waves, all resident at 2 per
+    SIMD); 8192 x 32 (4096 waves) its 4-wave original."""
     env, h, crashed = _rollout(E, N, KIN15, seed, steps=3)
     assert crashed > 0  # the batch is big enough to hold crashes, impacts and their SAT pairs
     assert (h["lane"] != h["target_lane"]).any() or (h["lane"][:, 1:] != 0).any()

@@ -39,3 +39,9 @@ def test_objsim_reproduces_the_goldens(path):
 def test_objsim_throughput_reports_per_core():
     r = objsim.throughput(n=16, seconds=0.3)
     assert r["processes"] == 1 and r["value"] > 0 and r["veh_frames"] % (16 * 15) == 0
+
+
+def test_objsim_pool_runs_one_process_per_core():
+    """bench.py's reference_equiv: one spawn-context worker per core, each on its own scenes."""
+    r = objsim.throughput(n=16, seconds=0.3, processes=2)
+    assert r["processes"] == 2 and r["value"] > r["per_core"] > 0

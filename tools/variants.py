@@ -12,7 +12,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "_variants")
 VARIANTS = {"head": [], "cur": []}  # committed kernel vs working tree, tuned defaults
-TIMING = {"timing": ["-DTTRL_PHASE_TIMING"], "wtrace": ["-DTTRL_WAVE_TRACE"]}  # built, not timed: tools/phases.py
+# built, not timed: tools/phases.py (timing, wtrace); tools/ablate.py, insts.py, evolve.py (ablate: the
+# phase-ablation bits of ttrl_diag_simulate exist only in -DTTRL_DIAG_ABLATE builds)
+TIMING = {"timing": ["-DTTRL_PHASE_TIMING"], "wtrace": ["-DTTRL_WAVE_TRACE"], "ablate": ["-DTTRL_DIAG_ABLATE"]}
 if os.environ.get("WAVE_VARIANTS"):
     VARIANTS.update({f"w{w}": [f"-DTTRL_SIM_WAVES={w}"] for w in (2, 3, 4, 5, 6)})
 for arg in os.environ.get("EXTRA_VARIANTS", "").split(";"):

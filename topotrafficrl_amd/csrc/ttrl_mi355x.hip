@@ -2585,6 +2585,23 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
         }
         const T xi = V.x[me], yi = V.y[me], vi = V.v[me];
         const T thr = thr0 + vi * dt;
+        // objects.py:123-133 exact, first for every window candidate (a few cheap rounds): norm >
+        // thr drops the pair (far pairs skip it; inside thr - 1 no sqrt needed).  The 1-D window
+        // also holds the vehicles of the other lanes at a similar x; dropping them here keeps the
+        // expensive rounds below (one separating-axis proof per lane per round, the wave running
+        // as many rounds as its busiest lane) to the pairs within the threshold.
+        {
+          unsigned long long mn = 0;
+          for (unsigned long long mm = m; mm; mm &= mm - 1) {
+            const int j = __ffsll((long long)mm) - 1;
+            const T dx = V.x[eb + j] - xi, dy = V.y[eb + j] - yi;
+            const T d2 = dx * dx + dy * dy;
+            if (!(d2 > (thr + T(1)) * (thr + T(1))) &&
+                !(!(thr > T(1) && d2 < (thr - T(1)) * (thr - T(1))) && sqrt(d2) > thr))
+              mn |= 1ull << j;
+          }
+          m = mn;
+        }
         const unsigned long long seg = NS == 64 ? ~0ull : ((1ull << NS) - 1) << ((tid & 63) / NS * NS);
         const unsigned long long below = (1ull << (tid & 63)) - 1;
         int base = 0;  // pairs of this env queued so far
@@ -2594,13 +2611,8 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
           if (m) {
             j = __ffsll((long long)m) - 1;
             m &= m - 1;
-            const T dx = V.x[eb + j] - xi, dy = V.y[eb + j] - yi;
-            const T d2 = dx * dx + dy * dy;
-            // objects.py:123-133 exact: norm > thr (far pairs skip it; inside thr - 1 no sqrt needed),
-            // then pairs the SAT provably separates contribute nothing
-            push = !(d2 > (thr + T(1)) * (thr + T(1))) &&
-                   !(!(thr > T(1) && d2 < (thr - T(1)) * (thr - T(1))) && sqrt(d2) > thr) &&
-                   !sat_separated(P, xi, yi, V.ch[me], V.sh[me], vi, V.x[eb + j], V.y[eb + j], V.ch[eb + j],
+            // pairs the SAT provably separates contribute nothing
+            push = !sat_separated(P, xi, yi, V.ch[me], V.sh[me], vi, V.x[eb + j], V.y[eb + j], V.ch[eb + j],
                                   V.sh[eb + j], V.v[eb + j], dt);
           }
           const unsigned long long bal = __ballot(push) & seg;
@@ -2631,17 +2643,41 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
         };
         if (SO && V.stie[le] == 0) {
           // the 128-slot sorted view: walk out from this vehicle's sorted position while inside the
-          // window (the queue's order is free: pass 3 folds each vehicle's pairs by their indices)
+          // window (the queue's order is free: pass 3 folds each vehicle's pairs by their indices),
+          // keeping the partners within the exact norm threshold (cheap); the separating-axis
+          // proofs then run over those only, so the wave's rounds follow its busiest lane's close
+          // pairs rather than every vehicle of the other lanes at a similar x
           if (!(ablate & A_NO_PREF)) {
+            constexpr int MW = (NS + 63) / 64;  // mask words (the sorted view: NS = 128)
+            unsigned long long mk[MW];
+#pragma unroll
+            for (int w = 0; w < MW; ++w) mk[w] = 0ull;
+            auto near = [&](int j) {
+              const T dx = V.x[eb + j] - xi, dy = V.y[eb + j] - yi;
+              const T d2 = dx * dx + dy * dy;
+              if (d2 > (thr + T(1)) * (thr + T(1))) return;
+              if (!(thr > T(1) && d2 < (thr - T(1)) * (thr - T(1))) && sqrt(d2) > thr) return;
+              mk[j >> 6] |= 1ull << (j & 63);
+            };
             const int p = V.spos[me];
             for (int q = p + 1; q < NS && !(V.sxf[eb + q] - xfi > Rwf); ++q) {
               const int j = V.sord[eb + q];
-              if (j > i) test_push(j);
+              if (j > i) near(j);
             }
             for (int q = p - 1; q >= 0 && !(xfi - V.sxf[eb + q] > Rwf); --q) {
               const int j = V.sord[eb + q];
-              if (j > i) test_push(j);
+              if (j > i) near(j);
             }
+#pragma unroll
+            for (int w = 0; w < MW; ++w)
+              for (unsigned long long mm = mk[w]; mm; mm &= mm - 1) {
+                const int j = w * 64 + __ffsll((long long)mm) - 1;
+                if (sat_separated(P, xi, yi, V.ch[me], V.sh[me], vi, V.x[eb + j], V.y[eb + j], V.ch[eb + j],
+                                  V.sh[eb + j], V.v[eb + j], dt))
+                  continue;  // provably (false, false): contributes nothing
+                const int q = atomicAdd(&V.pq_n[le], 1);
+                if (q < NS) V.pq_ij[le * NS + q] = pair_pack(i, j, 0);
+              }
           }
         } else {
 #pragma unroll
