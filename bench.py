@@ -66,6 +66,25 @@ def state_bytes(dtype: str) -> tuple[int, int]:
     return 11 * r + 3 * 4 + 4, 10 * r + 3 * 4 + 2
 
 
+def launch_bytes(E: int, N: int, dtype: str, obs_cfg: dict | None, graph: bool) -> int:
+    """Algorithmic HBM bytes of one env.step launch (ttrl_env_step): every slot's state read and
+    written once (state_bytes); on a road network also its route rows (road, lane: 4 + 4 int8),
+    route length and yield flag, read and written; per env the step tail (time read + written,
+    reward, terminated, truncated, the 4 reward terms, the info's ego speed / crashed), the action
+    read, and on a road network the regulation counter and np_random's 5 words (the shuffled
+    observation draws from it), read and written, and the dispatch order read; the Kinematics
+    observation and its ids written once."""
+    rd, wr = state_bytes(dtype)
+    r = 8 if dtype == "f64" else 4
+    per_slot = rd + wr + (2 * (4 + 4 + 1 + 1) if graph else 0)
+    per_env = 2 * 8 + 4 + 1 + 1 + 4 * 4 + r + 1 + 4 + ((2 * 4 + 2 * 40 + 4) if graph else 0)
+    if obs_cfg is not None and obs_cfg["type"] == "Kinematics":
+        V = obs_cfg.get("vehicles_count", 5)
+        F = len(obs_cfg.get("features", ["presence", "x", "y", "vx", "vy"]))
+        per_env += V * F * 4 + (V - 1) * 4
+    return E * (N * per_slot + per_env)
+
+
 def host_threads() -> int:
     """The host cores the CPU baseline uses: the granted CPU share when the job is given one
     (OMP_NUM_THREADS: 16 on the GPU box, whose os.cpu_count() reports the whole machine), else
@@ -456,13 +475,11 @@ def main():
         veh_steps = int(sharding.sum_over_ranks(float(live_steps), device=None if shared else dev)) * 15
     value = veh_steps / elapsed
     rd, wr = state_bytes(args.dtype)
-    alg_bytes = E * N * (rd + wr)  # per fused simulate launch
-    kernel = "simulate_kernel (fused 15-frame Road.act+Road.step)"
-    if C["obs"]["type"] == "Kinematics" and not ix:  # the launch also writes the observation (ttrl_env_step)
-        V = C["obs"].get("vehicles_count", 5)
-        F = len(C["obs"].get("features", ["presence", "x", "y", "vx", "vy"]))
-        alg_bytes += E * (V * F * 4 + (V - 1) * 4)
-        kernel = "simulate_kernel (fused 15-frame Road.act+Road.step + Kinematics observation)"
+    # per env.step launch: the state, the step tail and (Kinematics) the observation (launch_bytes)
+    alg_bytes = launch_bytes(E, N, args.dtype, C["obs"], graph=ix)
+    kernel = "simulate_kernel (fused 15-frame Road.act+Road.step + step tail)"
+    if C["obs"]["type"] == "Kinematics":  # the launch also writes the observation (ttrl_env_step)
+        kernel = "simulate_kernel (fused 15-frame Road.act+Road.step + Kinematics observation + step tail)"
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     pmc, pmc_source = read_pmc(args.dtype, args.config)
     hbm = {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define TTRL_ABI_VERSION 7
+#define TTRL_ABI_VERSION 6
 #define TTRL_MAX_LANES 32
 #define TTRL_MAX_ROADS 32
 #define TTRL_MAX_NODES 32
@@ -291,10 +291,7 @@ int ttrl_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road,
  * first); a dispatch order only -- every output is the same with or without it; other roads
  * ignore it.  It must name every env at most once (a repeated env would be written by two
  * workgroups; not checked, that would need a host sync); a negative entry is an idle slot.
- * n_wide (optional, device int32, with order, a road network of 17..32 slots): the first *n_wide
- * envs of the order hold more than 16 vehicles, every other env holds its vehicles in its first 16
- * slots -- as ttrl_ix_step_tail's mixed order leaves them; the launch then runs those envs four to a
- * wavefront on 16 slots (the same outputs).  action_lut (host, n_action_lut <= 8 meta-action codes; n_action_lut 0: none): actions
+ * action_lut (host, n_action_lut <= 8 meta-action codes; n_action_lut 0: none): actions
  * are action indices, mapped to their codes in the launch (DiscreteMetaAction's index -> action
  * name -> code), so a non-identity action set needs no lookup launch; an index outside the table
  * is no meta-action. */
@@ -303,8 +300,8 @@ int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
                   const ttrl_kin_cfg_t* obs_cfg, float* obs, int32_t* obs_ids,
                   const ttrl_reward_cfg_t* reward_cfg, double* time, double time_inc,
                   float* reward, uint8_t* terminated, uint8_t* truncated, float* components,
-                  void* ego_speed, uint8_t* ego_crashed, const int32_t* order, const int32_t* n_wide,
-                  const int32_t* action_lut, int32_t n_action_lut, void* stream);
+                  void* ego_speed, uint8_t* ego_crashed, const int32_t* order, const int32_t* action_lut,
+                  int32_t n_action_lut, void* stream);
 /* Road.neighbour_vehicles(v, lane) for every vehicle; query_lane [E*N] int32
  * (-1 = the vehicle's own lane).  front/rear [E*N] int32 vehicle index or -1. */
 int ttrl_neighbours(const ttrl_state_t* s, const ttrl_lane_table_t* road,
@@ -426,16 +423,13 @@ int ttrl_ix_clear_spawn(const ttrl_state_t* s, const ttrl_lane_table_t* road, co
  * first n_envs initialised to any permutation of the envs): receives in [0, n_envs) the next
  * ttrl_env_step's dispatch order -- the envs grouped as that launch's workgroups hold them,
  * groups sorted by their live vehicles, heaviest first; [n_envs, 2 n_envs) is its scratch.
- * n_wide (optional, device int32, with order, 17..32 slots): the mixed order instead -- every env
- * sorted by its live vehicles, heaviest first, and *n_wide = the number with more than 16 (the
- * order and n_wide of the next ttrl_env_step).
  * Reference: intersection_env.py:135-139, :350-362, :320-348; abstract.py:188-214. */
 int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                       const ttrl_ix_cfg_t* cfg, const ttrl_state_t* spare, const uint8_t* terminated,
                       const uint8_t* truncated, uint8_t* spare_parity, uint32_t* entropy, uint32_t* spare_entropy,
                       int32_t n_words, double* time, uint8_t* done, uint8_t* spare_mask,
                       const ttrl_kin_cfg_t* obs_cfg, const float* obs_in, float* obs_out, const int32_t* obs_ids_in,
-                      int32_t* obs_ids_out, int64_t* live_count, int32_t* order, int32_t* n_wide, void* stream);
+                      int32_t* obs_ids_out, int64_t* live_count, int32_t* order, void* stream);
 /* Per-env reward [E] float32, terminated/truncated [E] uint8, given time [E] float64, for the
  * env's controlled vehicle (its first TTRL_MDP slot). */
 int ttrl_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* road,

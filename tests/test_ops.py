@@ -191,7 +191,7 @@ def test_env_step_and_rewards_ops_equal_the_c_abi(hip_device):
     sp = torch.empty(E, dtype=torch.float64, device=hip_device)
     assert lib.ttrl_env_step(_c(st), R, P, a.data_ptr(), 15, 1 / 15, C.byref(kin), obs.data_ptr(), ids.data_ptr(), RC,
                              t1.data_ptr(), 1.0, rew.data_ptr(), te.data_ptr(), tr.data_ptr(), comp.data_ptr(),
-                             sp.data_ptr(), cr.data_ptr(), None, None, None, 0, _stream()) == 0
+                             sp.data_ptr(), cr.data_ptr(), None, None, 0, _stream()) == 0
     outs = torch.ops.ttrl.env_step_(other.tensors(), lanes, params, a, 15, 1 / 15, ops.struct_tensor(kin), rc, t2, 1.0)
     torch.cuda.synchronize()
     _equal(st, other)

@@ -1,7 +1,10 @@
 # round 5: the mixed intersection dispatch measured, the GPU suite, the bench lines of configs 2, 6
 # and 4, then diagnostics (head vs working-tree A/B, the headline's phases and instruction mix)
 export TMPDIR=/tmp
-timeout -k 10 200 python tools/ix_ns16.py > gpurun_out/r05e_ns16.txt 2>&1 || exit $?
+timeout -k 10 200 python tools/ix_ns16.py > gpurun_out/r05e_ns16.txt 2>&1
+rc=$?
+echo "ns16 rc=$rc"
+[ $rc -le 1 ] || exit $rc
 TTRL_PARITY_LOG=gpurun_out/r05e_parity.json timeout -k 10 600 python -u -m pytest tests -m gpu -q -rs --timeout 300 --timeout-method thread > gpurun_out/r05e_gpu_tests.txt 2>&1
 rc=$?
 echo "tests rc=$rc"

@@ -1732,10 +1732,6 @@ struct StepOut {
   // negative entry: an idle slot; null: slot order).  A dispatch order only: every env's result is
   // independent of it.  It must not name an env twice (two workgroups would write one env).
   const int32_t* order;
-  // with order, on a road network of 17..32 slots (simulate_mixed_kernel): *n_wide is the number
-  // of leading order entries whose envs hold more than 16 vehicles; the others hold theirs in
-  // their first 16 slots (compacted at the front, as the intersection keeps them)
-  const int32_t* n_wide;
   // n_lut > 0: actions[] are action indices, mapped to meta-action codes by lut (an index outside
   // the table: no meta-action)
   int8_t lut[8];
@@ -1743,7 +1739,7 @@ struct StepOut {
 };
 
 // The env of workgroup slot q: order[q] under a dispatch order, else q; -1 (no env) for slots at or
-// past qend (the last workgroup of an odd batch, a mixed launch's part boundary).
+// past qend (the last workgroup of an odd batch).
 __device__ __forceinline__ int env_at(const int32_t* order, int q, int qend) {
   return q < qend ? (order ? order[q] : q) : -1;
 }
@@ -1768,7 +1764,7 @@ template <bool L, typename T> struct Own {
 // and written once); each phase loads the few fields it needs into registers, so no state is
 // live across phases and the kernel runs at high occupancy without spilling.  The workgroup
 // takes the envs of slots [q0, q0 + EPW) (below qend) of the dispatch order (simulate_kernel:
-// q0 = blockIdx.x * EPW; simulate_mixed_kernel: its part's slots).
+// q0 = blockIdx.x * EPW, qend = n_envs).
 template <typename T, int NS, int EPW, int NET>
 __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state_t& st, const ttrl_lane_table_t& R,
                                               const ParamsT<T>& P, const int32_t* __restrict__ actions,
@@ -1791,31 +1787,6 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
                 const uint8_t* __restrict__ env_mask, int frames, double dt_d, int mode, int ablate_arg, StepOut so) {
   simulate_body<T, NS, EPW, NET>((int)blockIdx.x * EPW, st.n_envs, st, R, P, actions, env_mask, frames, dt_d, mode,
                                  ablate_arg, so);
-}
-
-// A road network's 17..32-slot rows as one launch in two parts (VecIntersectionEnv's mixed dispatch
-// order, ix_order_kernel): the first *so.n_wide envs of the order hold more than 16 vehicles and run
-// two per workgroup on the 32-slot body; every other env has its vehicles in its first 16 slots
-// and runs four per workgroup on the 16-slot body, so the per-vehicle phases keep ~half the lanes
-// of a wave busy instead of a quarter (~8 live vehicles per intersection scene) and the launch
-// issues about half the waves.  Grid ceil(E / 2): the workgroups past the 16-slot part leave at
-// once.  Same results as simulate_kernel<T, 32, 2, NET_GRAPH> bit for bit (the per-vehicle
-// arithmetic and every list order are the same; test_overlapped_resets_equal_in_place_resets).
-template <typename T>
-__global__ void __launch_bounds__(64, 2)
-simulate_mixed_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_t* __restrict__ actions,
-                      const uint8_t* __restrict__ env_mask, int frames, double dt_d, int mode, int ablate_arg,
-                      StepOut so) {
-  const int K = min(max(*so.n_wide, 0), st.n_envs);
-  const int nA = (K + 1) / 2, b = (int)blockIdx.x;
-  if (b < nA) {
-    simulate_body<T, 32, 2, NET_GRAPH>(2 * b, K, st, R, P, actions, env_mask, frames, dt_d, mode, ablate_arg, so);
-  } else {
-    const int q0 = K + 4 * (b - nA);
-    if (q0 < st.n_envs)
-      simulate_body<T, 16, 4, NET_GRAPH>(q0, st.n_envs, st, R, P, actions, env_mask, frames, dt_d, mode, ablate_arg,
-                                         so);
-  }
 }
 
 template <typename T, int NS, int EPW, int NET>
@@ -4473,27 +4444,14 @@ __device__ void sort_groups(int32_t* __restrict__ order, int P, int G, int* h, K
 // finds resident (the slots they hold push the last-dispatched groups into a second round).  The
 // step's results do not depend on the order (test_dispatch_order_leaves_results_unchanged,
 // test_overlapped_resets_equal_in_place_resets).  order: [0, E) out, [E, 2E) the tail's live counts.
-__global__ void __launch_bounds__(1024) ix_order_kernel(int32_t* __restrict__ order, int E, int G, int kmax,
-                                                        int32_t* __restrict__ n_wide, int narrow) {
+__global__ void __launch_bounds__(1024) ix_order_kernel(int32_t* __restrict__ order, int E, int G, int kmax) {
   __shared__ int h[ORDER_BUCKETS];
-  __shared__ int wide;
   const int32_t* live = order + E;
-  if (n_wide) {  // the mixed order (G = 1): how many envs need more than `narrow` slots (they sort first)
-    if (threadIdx.x == 0) wide = 0;
-    __syncthreads();
-    int c = 0;
-    for (int e = threadIdx.x; e < E; e += blockDim.x) c += live[e] > narrow;
-    if (c) atomicAdd(&wide, c);
-  }
   sort_groups(order, E / G, G, h, [&](int p) {
     int k = 0;
     for (int q = 0; q < G; ++q) k += live[p * G + q];
     return kmax - min(max(k, 0), kmax);  // descending
   });
-  if (n_wide) {
-    __syncthreads();
-    if (threadIdx.x == 0) *n_wide = wide;
-  }
 }
 
 template <typename T>
@@ -4597,9 +4555,6 @@ int check_state(const ttrl_state_t* s, const ttrl_lane_table_t* R) {
 }
 
 int slots_for(int n) { return n <= 32 ? 32 : n <= 64 ? 64 : n <= 128 ? 128 : 256; }
-// Envs per simulate workgroup: a road network of <= 16 slots runs four 16-slot envs per wave
-// (its scenes hold ~8 live vehicles: the per-vehicle phases then keep most of the lanes busy).
-int sim_epw(int n_veh, bool graph) { return graph && n_veh <= 16 ? 4 : slots_for(n_veh) == 32 ? 2 : 1; }
 
 // The reset instance for a road: CV = false when every lane is straight along +x (the highway).
 template <typename T>
@@ -4618,6 +4573,15 @@ void launch_reset(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_
 }
 
 int launch_status() { return hipGetLastError() == hipSuccess ? TTRL_OK : TTRL_E_LAUNCH; }
+
+// ttrl_env_step's tail scratch (the observation's keys, rows and counts; simulate_body's epilogue)
+// fits the act phase's block it overlays (dead after the last frame).
+template <typename T>
+bool tail_fits(const ViewLayout& o, int EPW, int NS) {
+  const size_t M = (size_t)EPW * NS;
+  const size_t need = ((sizeof(T) * M + 15) & ~(size_t)15) + 2 * sizeof(int) * 64 * EPW + 2 * sizeof(int) * EPW;
+  return o.afree + need <= o.item + sizeof(short) * 2 * M;
+}
 
 // SIMDs of the current device (4 per CU on CDNA), cached per device id.
 int simds_of_current_device() {
@@ -4646,26 +4610,12 @@ int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_par
   const size_t lds = host_view_bytes(sizeof(T) == 8 ? TTRL_F64 : TTRL_F32, EPW, NS,
                                      graph || curved ? R.n_lanes : STRAIGHT_LANE_CAP, graph,
                                      !graph && !curved && sorted_view(NS, EPW, NET_STRAIGHT));
-  if (ob.obs || ob.reward) {  // the tail's scratch must fit the act phase's block it overlays (it does for every NS)
+  if (ob.obs || ob.reward) {  // the tail's scratch must fit the dead block it overlays (it does for every NS)
     const ViewLayout o = view_layout<T>(EPW, NS, graph || curved ? R.n_lanes : STRAIGHT_LANE_CAP, graph,
                                         !graph && !curved && sorted_view(NS, EPW, NET_STRAIGHT));
-    const size_t M = (size_t)EPW * NS;
-    const size_t need = ((sizeof(T) * M + 15) & ~(size_t)15) + 2 * sizeof(int) * 64 * EPW + 2 * sizeof(int) * EPW;
-    if (o.afree + need > o.item + sizeof(short) * 2 * M) return TTRL_E_UNSUPPORTED;
+    if (!tail_fits<T>(o, EPW, NS)) return TTRL_E_UNSUPPORTED;
   }
   const ParamsT<T> PT = params_for<T>(P);
-  if constexpr (NS == 32 && EPW == 2) {
-    // a road network's mixed dispatch order: the 32-slot envs first, the others four to a wave
-    const ViewLayout o16 = view_layout<T>(4, 16, R.n_lanes, true, false);
-    const size_t need16 = ((sizeof(T) * 64 + 15) & ~(size_t)15) + 2 * sizeof(int) * 64 * 4 + 2 * sizeof(int) * 4;
-    const bool tail16 = !(ob.obs || ob.reward) || o16.afree + need16 <= o16.item + sizeof(short) * 2 * 64;
-    if (graph && ob.order && ob.n_wide && s.n_veh > 16 && tail16) {
-      const size_t lds16 = o16.total;
-      hipLaunchKernelGGL(simulate_mixed_kernel<T>, dim3((s.n_envs + 1) / 2), dim3(64), lds > lds16 ? lds : lds16,
-                         stream, s, R, PT, actions, mask, frames, dt, mode, ablate, ob);
-      return launch_status();
-    }
-  }
   if constexpr (NS == 32 && EPW == 2) {
     // every wave resident at 2 per SIMD: the 2-wave register budget (no spills) costs no occupancy
     if (!graph && !curved && blocks <= 2 * simds_of_current_device()) {
@@ -4674,12 +4624,9 @@ int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_par
       return launch_status();
     }
   }
-  if (graph) {
+  if (graph)
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_GRAPH>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R, PT,
                        actions, mask, frames, dt, mode, ablate, ob);
-    return launch_status();
-  }
-  if constexpr (NS < 32) return TTRL_E_UNSUPPORTED;  // the 16-slot class: road networks only (sim_epw)
   else if (curved)
     hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_CURVED>), dim3(blocks), dim3(NS * EPW), lds, stream, s, R,
                        PT, actions, mask, frames, dt, mode, ablate, ob);
@@ -4693,8 +4640,6 @@ template <typename T>
 int dispatch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const int32_t* actions,
                  const uint8_t* mask, int frames, double dt, int mode, int ablate, hipStream_t stream,
                  const StepOut& ob) {
-  if (sim_epw(s.n_veh, is_graph(R)) == 4)
-    return launch_sim<T, 16, 4>(s, R, P, actions, mask, frames, dt, mode, ablate, stream, ob);
   switch (slots_for(s.n_veh)) {
     case 32: return launch_sim<T, 32, 2>(s, R, P, actions, mask, frames, dt, mode, ablate, stream, ob);
     case 64: return launch_sim<T, 64, 1>(s, R, P, actions, mask, frames, dt, mode, ablate, stream, ob);
@@ -4805,8 +4750,7 @@ int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
                   int32_t frames, double dt, const ttrl_kin_cfg_t* obs_cfg, float* obs, int32_t* obs_ids,
                   const ttrl_reward_cfg_t* reward_cfg, double* time, double time_inc, float* reward,
                   uint8_t* terminated, uint8_t* truncated, float* components, void* ego_speed, uint8_t* ego_crashed,
-                  const int32_t* order, const int32_t* n_wide, const int32_t* action_lut, int32_t n_action_lut,
-                  void* stream) {
+                  const int32_t* order, const int32_t* action_lut, int32_t n_action_lut, void* stream) {
   int rc = check_state(s, road);
   if (rc) return rc < 0 ? rc : TTRL_OK;
   if ((!obs_cfg) != (!obs) || (obs_cfg && check_kin_cfg(s, obs_cfg))) return TTRL_E_ARG;
@@ -4825,7 +4769,6 @@ int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
     so.trunc = truncated; so.comp = components; so.ego_speed = ego_speed; so.ego_crashed = ego_crashed;
   }
   so.order = order;
-  so.n_wide = order ? n_wide : nullptr;
   return run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream, 0, nullptr, &so);
 }
 
@@ -5127,7 +5070,7 @@ int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
                       const uint8_t* truncated, uint8_t* spare_parity, uint32_t* entropy, uint32_t* spare_entropy,
                       int32_t n_words, double* time, uint8_t* done, uint8_t* spare_mask,
                       const ttrl_kin_cfg_t* obs_cfg, const float* obs_in, float* obs_out, const int32_t* obs_ids_in,
-                      int32_t* obs_ids_out, int64_t* live_count, int32_t* order, int32_t* n_wide, void* stream) {
+                      int32_t* obs_ids_out, int64_t* live_count, int32_t* order, void* stream) {
   int rc = check_ix(s, road, p, cfg);
   if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!spare || !terminated || !truncated || !spare_parity || !entropy || !spare_entropy || n_words < 1 ||
@@ -5152,9 +5095,7 @@ int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
   t.spare_ent = spare_entropy; t.nw = n_words; t.time = time; t.done = done; t.spare_mask = spare_mask;
   t.live = reinterpret_cast<unsigned long long*>(live_count);
   // the dispatch order groups the envs of one simulate workgroup (EPW: 2 on 32 slots, else 1)
-  // mixed (n_wide): one env per group, the 32-slot envs counted into *n_wide (simulate_mixed_kernel)
-  const bool mixed = n_wide && order && is_graph(*road) && s->n_veh > 16 && s->n_veh <= 32;
-  const int G = mixed ? 1 : sim_epw(s->n_veh, is_graph(*road));
+  const int G = slots_for(s->n_veh) == 32 ? 2 : 1;
   const bool ordered = order && s->n_envs % G == 0;
   if (ordered) t.live_env = order + s->n_envs;
   if (obs_cfg) {
@@ -5167,8 +5108,7 @@ int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
   else
     hipLaunchKernelGGL(ix_step_tail_kernel<float>, dim3(s->n_envs), dim3(64), 0, st, *s, *road, *p, *cfg, t);
   if (ordered)
-    hipLaunchKernelGGL(ix_order_kernel, dim3(1), dim3(1024), 0, st, order, s->n_envs, G, G * s->n_veh,
-                       mixed ? n_wide : nullptr, 16);
+    hipLaunchKernelGGL(ix_order_kernel, dim3(1), dim3(1024), 0, st, order, s->n_envs, G, G * s->n_veh);
   return launch_status();
 }
 

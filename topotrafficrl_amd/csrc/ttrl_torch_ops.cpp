@@ -156,7 +156,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
     at::TensorList state, const at::Tensor& lanes, const at::Tensor& params, const c10::optional<at::Tensor>& actions,
     int64_t frames, double dt, const c10::optional<at::Tensor>& kin_cfg, const at::Tensor& reward_cfg,
     const at::Tensor& time, double time_inc, const c10::optional<at::Tensor>& order,
-    at::OptionalIntArrayRef action_lut, const c10::optional<at::Tensor>& n_wide) {
+    at::OptionalIntArrayRef action_lut) {
   check_hip(state[0]);
   ttrl_state_t s = state_of(state);
   const ttrl_kin_cfg_t* kc = kin_cfg && kin_cfg->defined() ? as_struct<ttrl_kin_cfg_t>(*kin_cfg, "kin_cfg") : nullptr;
@@ -169,10 +169,6 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
     TORCH_CHECK(order->device() == state[0].device() && order->scalar_type() == at::kInt && order->is_contiguous() &&
                     order->numel() >= s.n_envs,
                 "ttrl: order must be a contiguous int32 tensor of at least n_envs entries on the state's device");
-  const bool wd = od && n_wide && n_wide->defined();  // the mixed order (ix_step_tail_'s, with its n_wide)
-  if (wd)
-    TORCH_CHECK(n_wide->device() == state[0].device() && n_wide->scalar_type() == at::kInt && n_wide->numel() == 1,
-                "ttrl: n_wide must be an int32 scalar on the state's device");
   std::vector<int32_t> lut;  // the action index -> meta-action code table (host; ttrl_env_step copies it)
   if (action_lut.has_value())
     for (int64_t c : *action_lut) lut.push_back(static_cast<int32_t>(c));
@@ -185,8 +181,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
                    rew.data_ptr<float>(), static_cast<uint8_t*>(term.data_ptr()),
                    static_cast<uint8_t*>(trunc.data_ptr()), comp.data_ptr<float>(), speed.data_ptr(),
                    static_cast<uint8_t*>(crashed.data_ptr()), od ? order->data_ptr<int32_t>() : nullptr,
-                   wd ? n_wide->data_ptr<int32_t>() : nullptr, lut.empty() ? nullptr : lut.data(),
-                   static_cast<int32_t>(lut.size()), stream_of(state[0])),
+                   lut.empty() ? nullptr : lut.data(), static_cast<int32_t>(lut.size()), stream_of(state[0])),
      "ttrl_env_step");
   return out;
 }
@@ -408,7 +403,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ix_step_tail_(
     const at::Tensor& entropy, const at::Tensor& spare_entropy, const at::Tensor& time,
     const c10::optional<at::Tensor>& kin_cfg, const c10::optional<at::Tensor>& obs,
     const c10::optional<at::Tensor>& ids, const c10::optional<at::Tensor>& live_count,
-    const c10::optional<at::Tensor>& order, const c10::optional<at::Tensor>& n_wide) {
+    const c10::optional<at::Tensor>& order) {
   check_hip(state[0]);
   ttrl_state_t s = state_of(state), sp = state_of(spare);
   const auto& x = state[0];
@@ -458,10 +453,6 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ix_step_tail_(
     TORCH_CHECK(order->device() == x.device() && order->scalar_type() == at::kInt && order->is_contiguous() &&
                     order->numel() == 2 * int64_t(s.n_envs),
                 "ttrl: order must be a contiguous int32 [2 * n_envs] tensor on the state's device");
-  const bool wd = od && n_wide && n_wide->defined();
-  if (wd)
-    TORCH_CHECK(n_wide->device() == x.device() && n_wide->scalar_type() == at::kInt && n_wide->numel() == 1,
-                "ttrl: n_wide must be an int32 scalar on the state's device");
   at::Tensor done = at::empty({s.n_envs}, opts(x, at::kBool));
   at::Tensor smask = at::empty({sp.n_envs}, opts(x, at::kByte));
   ok(ttrl_ix_step_tail(&s, as_struct<ttrl_lane_table_t>(lanes, "lanes"), as_struct<ttrl_params_t>(params, "params"),
@@ -473,8 +464,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ix_step_tail_(
                        static_cast<uint8_t*>(smask.data_ptr()), kc, kc ? oin.data_ptr<float>() : nullptr,
                        kc ? obs_out.data_ptr<float>() : nullptr, kc ? iin.data_ptr<int32_t>() : nullptr,
                        kc ? ids_out.data_ptr<int32_t>() : nullptr, lc ? live_count->data_ptr<int64_t>() : nullptr,
-                       od ? order->data_ptr<int32_t>() : nullptr, wd ? n_wide->data_ptr<int32_t>() : nullptr,
-                       stream_of(x)),
+                       od ? order->data_ptr<int32_t>() : nullptr, stream_of(x)),
      "ttrl_ix_step_tail");
   return {done, smask, obs_out, ids_out};
 }
@@ -618,7 +608,7 @@ void meta_none_meta(at::TensorList, const at::Tensor&, const at::Tensor&, const 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor>
 meta_env_step(at::TensorList state, const at::Tensor&, const at::Tensor&, const c10::optional<at::Tensor>&, int64_t,
               double, const c10::optional<at::Tensor>& kin_cfg, const at::Tensor&, const at::Tensor&, double,
-              const c10::optional<at::Tensor>&, at::OptionalIntArrayRef, const c10::optional<at::Tensor>&) {
+              const c10::optional<at::Tensor>&, at::OptionalIntArrayRef) {
   const ttrl_kin_cfg_t* kc = kin_cfg && kin_cfg->defined() ? as_struct<ttrl_kin_cfg_t>(*kin_cfg, "kin_cfg") : nullptr;
   return env_step_outputs(meta_x(state), kc);
 }
@@ -666,7 +656,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> meta_ix_step_tail(
     at::TensorList state, const at::Tensor&, const at::Tensor&, const at::Tensor&, at::TensorList, const at::Tensor&,
     const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&,
     const c10::optional<at::Tensor>& kin_cfg, const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&,
-    const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&) {
+    const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&) {
   const auto& x = meta_x(state);
   const int64_t E = x.size(0);
   at::Tensor o = at::empty({0}, opts(x, at::kFloat)), i = at::empty({0}, opts(x, at::kInt));
@@ -722,7 +712,7 @@ TORCH_LIBRARY(ttrl, m) {
   m.def("meta_action_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor actions) -> ()");
   m.def("env_step_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor? actions, int frames, float dt, "
         "Tensor? kin_cfg, Tensor reward_cfg, Tensor(b!) time, float time_inc, Tensor? order=None, "
-        "int[]? action_lut=None, Tensor? n_wide=None) -> (Tensor obs, Tensor ids, "
+        "int[]? action_lut=None) -> (Tensor obs, Tensor ids, "
         "Tensor reward, Tensor terminated, Tensor truncated, Tensor components, Tensor ego_speed, Tensor ego_crashed)");
   m.def("neighbours(Tensor[] state, Tensor lanes, Tensor? query_lane) -> (Tensor front, Tensor rear)");
   // the np_random-shuffled observation (order_shuffled 2) advances state.rng: the state is mutated
@@ -745,7 +735,7 @@ TORCH_LIBRARY(ttrl, m) {
   m.def("ix_step_tail_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor[] spare, "
         "Tensor terminated, Tensor truncated, Tensor(b!) spare_parity, Tensor(c!) entropy, Tensor(d!) spare_entropy, "
         "Tensor(e!) time, Tensor? kin_cfg, Tensor? obs, Tensor? ids, Tensor(f!)? live_count=None, "
-        "Tensor(g!)? order=None, Tensor(h!)? n_wide=None) -> (Tensor done, Tensor spare_mask, Tensor obs, Tensor ids)");
+        "Tensor(g!)? order=None) -> (Tensor done, Tensor spare_mask, Tensor obs, Tensor ids)");
   m.def("rewards(Tensor[] state, Tensor lanes, Tensor cfg, Tensor time) -> (Tensor reward, Tensor terminated, "
         "Tensor truncated)");
   m.def("rewards_ex(Tensor[] state, Tensor lanes, Tensor cfg, Tensor time) -> (Tensor reward, Tensor terminated, "

@@ -284,10 +284,6 @@ class VecIntersectionEnv:
             # whole warm-up at once, on side streams in rotation
             "reset_chunk_frames": 15,
             "reset_streams": 2,  # side streams the whole-warm-up resets rotate over (chunks: one)
-            # the step launch's mixed dispatch (17..32 slots, overlapped resets): the envs holding
-            # <= 16 vehicles run four to a wavefront on their first 16 slots, the rest two to a
-            # wavefront on 32 (ix_step_tail_ sorts the envs and counts the wide ones; same results)
-            "narrow_rows": True,
         }
 
     def configure(self, config: dict | None) -> None:
@@ -354,10 +350,6 @@ class VecIntersectionEnv:
             # heaviest first, see ix_order_kernel) and its scratch; any permutation is valid
             self._order = torch.cat([torch.arange(E, dtype=torch.int32, device=self.device),
                                      torch.zeros(E, dtype=torch.int32, device=self.device)])
-            # the mixed dispatch's count of 32-slot envs (the first _n_wide[0] of the order): all
-            # of them until the first tail has counted
-            self._n_wide = (torch.full((1,), E, dtype=torch.int32, device=self.device)
-                            if c["narrow_rows"] and 16 < int(c["vehicle_slots"]) <= 32 else None)
             n_sides = 2 if self._chunk else max(1, int(c["reset_streams"]))  # chunks: A (begin, warm), B (finish)
             self._sides = tuple(torch.cuda.Stream(self.device) for _ in range(n_sides))
             self._side_i = 0
@@ -415,8 +407,6 @@ class VecIntersectionEnv:
             self._spare_ent = torch.cat([ent[:, :-1].repeat(K, 1),
                                          torch.cat([ent[:, -1:] + 1 + q for q in range(K)])], 1).contiguous()
             self._spare_par.zero_()
-            if self._n_wide is not None:  # the new scenes are not counted yet: every env 32-slot
-                self._n_wide.fill_(self.num_envs)
             self._cohorts, self._to_finish = [], None
             self._pinned = []  # the side streams the current spare buffers are recorded on
             self._prepare_spares(None)
@@ -522,7 +512,7 @@ class VecIntersectionEnv:
         self.steps += frames
         obs, ids, *outs = self.road.env_step(idx, frames, 1 / self.config["simulation_frequency"],
                                              ot.fused_cfg() if kin else None, self.reward_cfg, self.time,
-                                             1 / self.config["policy_frequency"], self._order, lut, self._n_wide)
+                                             1 / self.config["policy_frequency"], self._order, lut)
         reward, terminated, truncated = _keep_tail(self, outs)
         if not kin:
             obs = ot.observe()
@@ -539,7 +529,7 @@ class VecIntersectionEnv:
             self.state.tensors(), ops.st(self.network.table), ops.st(self.params), ops.st(self.ix),
             self._spare.tensors(), terminated, truncated, self._spare_par, self._entropy, self._spare_ent, self.time,
             ops.kin_cfg_tensor(ot.fused_cfg()) if fused_obs else None, obs if fused_obs else None,
-            ids if fused_obs else None, self.live_counter, self._order, self._n_wide)
+            ids if fused_obs else None, self.live_counter, self._order)
         self._prepare_spares(smask)
         info["final_observation"], info["final_mask"] = obs, done
         if fused_obs:
@@ -628,7 +618,6 @@ class VecIntersectionEnv:
             new._spare_ent = self._spare_ent.clone()
             new._spare_par = self._spare_par.clone()
             new._order = self._order.clone()
-            new._n_wide = None if self._n_wide is None else self._n_wide.clone()
             new._sides = tuple(torch.cuda.Stream(self.device) for _ in self._sides)
             new._side_i = 0
             new._spare_ready = torch.cuda.Event()

@@ -102,7 +102,7 @@ class BatchedRoad:
 
     def env_step(self, actions: torch.Tensor | None, frames: int, dt: float, kin_cfg: _abi.KinCfg | None,
                  reward_cfg: _abi.RewardCfg, time: torch.Tensor, time_inc: float, order: torch.Tensor | None = None,
-                 action_lut: list[int] | None = None, n_wide: torch.Tensor | None = None):
+                 action_lut: list[int] | None = None):
         """AbstractEnv.step (abstract.py:224-250) in one launch (ttrl_env_step): the fused frames, the
         Kinematics observation of the final state (``kin_cfg``; else obs / ids are empty) and the step
         tail (time += time_inc, reward, terminated, truncated, components, the info's ego speed /
@@ -111,13 +111,11 @@ class BatchedRoad:
         permutation: an env named twice would be written by two workgroups (not checked on the
         device: that would need a host sync); a negative entry is an idle slot.
         ``action_lut``: ``actions`` are action indices and this maps them to meta-action codes inside
-        the launch (DiscreteMetaAction._indices).  ``n_wide`` (with ``order``, a road network of
-        17..32 slots: ix_step_tail_'s mixed order): the first ``n_wide`` envs of the order need 32
-        slots, the others run four to a wavefront on their first 16 (same results)."""
+        the launch (DiscreteMetaAction._indices)."""
         a = None if actions is None else self._actions(actions)
         kc = None if kin_cfg is None else ops.kin_cfg_tensor(kin_cfg)
         return ops.T.env_step_(*self._args(), a, int(frames), float(dt), kc, ops.st(reward_cfg), time,
-                               float(time_inc), order, action_lut, n_wide)
+                               float(time_inc), order, action_lut)
 
     def neighbour_vehicles(self, query_lane: torch.Tensor | None = None):
         """Road.neighbour_vehicles (road.py:480-513) for every vehicle: (front, rear) slot ids, -1 = None."""
