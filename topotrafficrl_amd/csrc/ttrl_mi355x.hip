@@ -2534,8 +2534,34 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
           const float xfi = V.xf[me];
           const float Rwf = (float)Rw * 1.0001f + 1e-5f * fabsf(xfi) + 1e-3f;
           const int p = V.spos[me];
-          for (int q = p + 1; q < NS && !(V.sxf[eb + q] - xfi > Rwf); ++q) m |= 1ull << V.sord[eb + q];
-          for (int q = p - 1; q >= 0 && !(xfi - V.sxf[eb + q] > Rwf); --q) m |= 1ull << V.sord[eb + q];
+          // WW positions each way per round, their LDS loads independent of each other (one LDS
+          // latency per round instead of one per position; a window rarely spans more than WW)
+          constexpr int WW = 3;
+          int qu = p + 1, qd = p - 1;
+          bool up = qu < NS, dn = qd >= 0;
+          while (up || dn) {
+            float xu[WW], xd[WW];
+            int su[WW], sd[WW];
+#pragma unroll
+            for (int u = 0; u < WW; ++u) {
+              const int a = min(qu + u, NS - 1), b = max(qd - u, 0);
+              xu[u] = V.sxf[eb + a]; su[u] = V.sord[eb + a];
+              xd[u] = V.sxf[eb + b]; sd[u] = V.sord[eb + b];
+            }
+#pragma unroll
+            for (int u = 0; u < WW; ++u) {
+              if (up) {
+                if (qu + u < NS && !(xu[u] - xfi > Rwf)) m |= 1ull << su[u];
+                else up = false;
+              }
+              if (dn) {
+                if (qd - u >= 0 && !(xfi - xd[u] > Rwf)) m |= 1ull << sd[u];
+                else dn = false;
+              }
+            }
+            qu += WW;
+            qd -= WW;
+          }
           m &= ~((2ull << i) - 1);  // keep j > i
           if (ablate & A_NO_PREF) m = 0;
         } else if (present && do_coll) {
@@ -2631,13 +2657,37 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
               mk[j >> 6] |= 1ull << (j & 63);
             };
             const int p = V.spos[me];
-            for (int q = p + 1; q < NS && !(V.sxf[eb + q] - xfi > Rwf); ++q) {
-              const int j = V.sord[eb + q];
-              if (j > i) near(j);
-            }
-            for (int q = p - 1; q >= 0 && !(xfi - V.sxf[eb + q] > Rwf); --q) {
-              const int j = V.sord[eb + q];
-              if (j > i) near(j);
+            constexpr int WW = 3;  // positions each way per round, loaded independently (as NS <= 64)
+            int qu = p + 1, qd = p - 1;
+            bool up = qu < NS, dn = qd >= 0;
+            while (up || dn) {
+              float xu[WW], xd[WW];
+              int su[WW], sd[WW];
+#pragma unroll
+              for (int u = 0; u < WW; ++u) {
+                const int a = min(qu + u, NS - 1), b = max(qd - u, 0);
+                xu[u] = V.sxf[eb + a]; su[u] = V.sord[eb + a];
+                xd[u] = V.sxf[eb + b]; sd[u] = V.sord[eb + b];
+              }
+#pragma unroll
+              for (int u = 0; u < WW; ++u) {
+                if (up) {
+                  if (qu + u < NS && !(xu[u] - xfi > Rwf)) {
+                    if (su[u] > i) near(su[u]);
+                  } else {
+                    up = false;
+                  }
+                }
+                if (dn) {
+                  if (qd - u >= 0 && !(xfi - xd[u] > Rwf)) {
+                    if (sd[u] > i) near(sd[u]);
+                  } else {
+                    dn = false;
+                  }
+                }
+              }
+              qu += WW;
+              qd -= WW;
             }
 #pragma unroll
             for (int w = 0; w < MW; ++w)
