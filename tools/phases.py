@@ -1,5 +1,6 @@
 """Per-phase cycle breakdown of the fused simulate kernel (diagnostic build with
--DTTRL_PHASE_TIMING, see tools/variants.py 'timing'): mid-episode 4096x64 state."""
+-DTTRL_PHASE_TIMING, see tools/variants.py 'timing'): mid-episode 4096x64 state; with --ix the
+intersection's in-loop scenes (each launch times the frames of one real env.step on a copy of its state)."""
 import ctypes as C
 import os
 import sys
@@ -33,22 +34,34 @@ def main(dtype="f64", steps=30, frames=15, ix=False, E=4096):
     rd = lib.ttrl_diag_phase_read
     rd.argtypes = [C.c_void_p]
     stream = torch.cuda.current_stream(dev).cuda_stream
-    buf = np.zeros(20, dtype=np.uint64)
-    tot = np.zeros(20)
+    buf = np.zeros(25, dtype=np.uint64)  # 20 phases, then project_items' 5 steps (road-network instance)
+    tot = np.zeros(25)
+    work = env.state.clone() if ix else env.state
     for t in range(steps):
-        a = env.action_type._codes(torch.randint(0, n_act, (E,), device=dev, generator=g))
+        a_idx = torch.randint(0, n_act, (E,), device=dev, generator=g)
+        a = env.action_type._codes(a_idx)
+        if ix:
+            # the scenes of a real episode: the product's env.step (clears, spawns, resets) advances the
+            # batch, and the timing build runs the same step's frames on a copy of its start state
+            work.copy_(env.state)
+            env.step(a_idx)
+            torch.cuda.synchronize()
         rd(buf.ctypes.data)
-        sim(C.byref(env.state.struct()), C.byref(env.network.table), C.byref(env.params), a.data_ptr(), frames, 1 / 15,
+        sim(C.byref(work.struct()), C.byref(env.network.table), C.byref(env.params), a.data_ptr(), frames, 1 / 15,
             stream)
         torch.cuda.synchronize()
         rd(buf.ctypes.data)
         if t >= 10:
             tot += buf.astype(np.float64)
     waves = (E if not ix else 2048) * (steps - 10)  # ix: two envs per 64-lane workgroup
-    per = tot / waves
+    per, pp = tot[:20] / waves, tot[20:] / waves
     print(f"[{dtype}] E={E} cycles per wave per {frames}-frame launch (mean over {steps - 10} launches), total {per.sum():.0f}")
     for n, c in zip(NAMES, per):
         print(f"  {n:16s} {c:10.0f}  {100 * c / per.sum():5.1f}%  ({c / frames:8.0f} per frame)")
+    if pp.any():
+        print("  project_items steps, cycles per wave per frame: " + ", ".join(
+            f"{n} {c / frames:.0f}" for n, c in zip(["A boxes", "B projections", "C minimum", "D lists",
+                                                    "counts"], pp)))
     # the last launch, wave by wave: start / end spread and the per-SIMD finish (load balance)
     nw = E if not ix else 2048
     tr = np.zeros((nw, 3), dtype=np.uint64)

@@ -17,6 +17,16 @@ VARIANTS = {"head": [], "cur": []}  # committed kernel vs working tree, tuned de
 TIMING = {"timing": ["-DTTRL_PHASE_TIMING"], "wtrace": ["-DTTRL_WAVE_TRACE"], "ablate": ["-DTTRL_DIAG_ABLATE"]}
 if os.environ.get("WAVE_VARIANTS"):
     VARIANTS.update({f"w{w}": [f"-DTTRL_SIM_WAVES={w}"] for w in (2, 3, 4, 5, 6)})
+# variants built from an edited copy of the working-tree source (measured experiments that need no
+# flag in the product source): name -> [(old, new)], each old text present exactly once
+SOURCE_EDITS = {
+    # 32-slot straight envs one per wave (32 lanes of 64 live, 4096 waves at config 2) on the sorted view
+    "ns32x1": [("case 32: return launch_sim<T, 32, 2>", "case 32: return launch_sim<T, 32, 1>"),
+               ("(NS * EPW == 64 || (NS == 128 && EPW == 1))", "(NS * EPW == 64 || NS == 32 || (NS == 128 && EPW == 1))")],
+}
+for name in os.environ.get("EDIT_VARIANTS", "").split(","):
+    if name.strip():
+        VARIANTS[name.strip()] = []
 for arg in os.environ.get("EXTRA_VARIANTS", "").split(";"):
     if arg.strip():
         name, flags = arg.split("=", 1)
@@ -31,10 +41,22 @@ def build():
     with open(head, "w") as f:
         f.write(subprocess.run(["git", "-C", ROOT, "show", "HEAD:topotrafficrl_amd/csrc/ttrl_mi355x.hip"],
                                check=True, capture_output=True, text=True).stdout)
+    for name in VARIANTS:
+        if name in SOURCE_EDITS:
+            text = open(src).read()
+            for old, new in SOURCE_EDITS[name]:
+                assert text.count(old) == 1, (name, old)
+                text = text.replace(old, new)
+            with open(os.path.join(OUT, f"{name}.hip"), "w") as f:
+                f.write(text)
+    only = os.environ.get("ONLY")  # build just these (comma-separated)
     for name, flags in {**VARIANTS, **TIMING}.items():
+        if only and name not in only.split(","):
+            continue
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
                "-shared", "-mllvm", "-disable-machine-licm", "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "topotrafficrl_amd", "csrc"), *flags, "-o", os.path.join(OUT, f"lib_{name}.so"),
-               head if name.startswith("head") else src]
+               head if name.startswith("head") else
+               os.path.join(OUT, f"{name}.hip") if name in SOURCE_EDITS else src]
         procs.append(subprocess.Popen(cmd))
     for p in procs:
         assert p.wait() == 0

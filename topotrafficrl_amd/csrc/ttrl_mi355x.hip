@@ -188,7 +188,7 @@ __device__ TTRL_CURVED_ATTR Pair<T> curved_local(int type, T px, T py, T sx, T s
   if (type == TTRL_LANE_SINE) {  // SineLane.local_coordinates lane.py:275-279
     const T dx = px - sx, dy = py - sy;
     o.a = dx * ux + dy * uy;
-    o.b = dx * (-uy) + dy * ux - amp * t_sin(puls * o.a + ph);
+    o.b = dx * (-uy) + dy * ux - amp * k_sincos(puls * o.a + ph).s;
   } else {  // CircularLane.local_coordinates lane.py:327-334
     const T dx = px - cx, dy = py - cy;
     T phi = atan2(dy, dx);
@@ -225,7 +225,7 @@ __device__ __forceinline__ void lane_local(const LaneT<T>& L, T px, T py, T& s, 
 template <typename T>
 __device__ TTRL_CURVED_ATTR T curved_heading(int type, T s, T hd, T amp, T puls, T ph, T rad, T sph, T dirn) {
   if (type == TTRL_LANE_SINE)  // SineLane.heading_at lane.py:269-273
-    return hd + t_atan(amp * puls * t_cos(puls * s + ph));
+    return hd + k_atan(amp * puls * k_sincos(puls * s + ph).c);
   const T phi = dirn * s / rad + sph;  // CircularLane.heading_at lane.py:318-321
   return phi + Tpi<T>() / T(2) * dirn;
 }
@@ -241,11 +241,12 @@ __device__ __forceinline__ void lane_position(const LaneT<T>& L, T s, T r, T& x,
   if (L.type == TTRL_LANE_CIRCULAR) {
     const T phi = L.dirn * s / L.rad + L.sph;
     const T k = L.rad - r * L.dirn;
-    x = L.cx + k * t_cos(phi);
-    y = L.cy + k * t_sin(phi);
+    const SinCos<T> sc = k_sincos(phi);
+    x = L.cx + k * sc.c;
+    y = L.cy + k * sc.s;
     return;
   }
-  if (L.type == TTRL_LANE_SINE) r = r + L.amp * t_sin(L.puls * s + L.ph);
+  if (L.type == TTRL_LANE_SINE) r = r + L.amp * k_sincos(L.puls * s + L.ph).s;
   x = L.sx + s * L.dx + r * (-L.dy);
   y = L.sy + s * L.dy + r * L.dx;
 }
@@ -274,7 +275,7 @@ __host__ __device__ inline LaneT<T> make_lane(const ttrl_lane_table_t& R, int l)
 // cardinal points the arc passes; a sine lane gets no box (+-inf: never pruned).  A lower bound of
 // distance_with_heading for project_items' pruning.
 template <typename T>
-__device__ inline float4 lane_box(const LaneT<T>& L) {
+__device__ __forceinline__ float4 lane_box(const LaneT<T>& L) {
   T x0, y0, x1, y1;
   if (L.type == TTRL_LANE_STRAIGHT) {
     const T ex = L.sx + L.len * L.dx, ey = L.sy + L.len * L.dy;
@@ -497,11 +498,17 @@ __device__ __forceinline__ void sat_axis(const PP& P, int k, T ax, T ay, T ac, T
   if (dx * nx + dy * ny > T(0)) { axx = nx; axy = ny; } else { axx = -nx; axy = -ny; }
 }
 
-// Out-of-line copy for the rare overflow sweep (keeps the hot path's register budget).
+// sat_pair for the rare overflow sweep, its results returned by value: the compiler keeps this
+// call out of line in the register-heavy road-network instance, and out-parameters of a call
+// would live in scratch.  flags: bit 0 intersecting, bit 1 will_intersect.
+template <typename T> struct SatRes { T tx, ty; int flags; };
 template <typename T, typename PP>
-__device__ __noinline__ void sat_pair_ool(const PP& P, T ax, T ay, T ac, T as, T av, T bx, T by, T bc,
-                                          T bs, T bv, T dt, bool& inter, bool& will, T& tx, T& ty) {
-  sat_pair(P, ax, ay, ac, as, av, bx, by, bc, bs, bv, dt, inter, will, tx, ty);
+__device__ SatRes<T> sat_pair_v(const PP& P, T ax, T ay, T ac, T as, T av, T bx, T by, T bc, T bs, T bv, T dt) {
+  bool inter, will;
+  SatRes<T> o;
+  sat_pair(P, ax, ay, ac, as, av, bx, by, bc, bs, bv, dt, inter, will, o.tx, o.ty);
+  o.flags = (inter ? 1 : 0) | (will ? 2 : 0);
+  return o;
 }
 
 // ---------------------------------------------------------------------------------
@@ -1142,12 +1149,28 @@ __device__ __forceinline__ void slot_nbrs(const View<T>& V, int le, int self, in
 // rebuilt at 4 waves, passes its intersection GPU tests and 40 finite steps, and so does this
 // source at 4 waves with round 3's item bounds checks silent (profiles/r03/netgraph_4wave/).  The
 // 2-wave budget of the road networks is a tuning choice, not a correctness one.)
+#ifdef TTRL_PHASE_TIMING
+// the phase accumulators of PH (below): 20 phases + project_items' 5 steps (PJ), one row per wave,
+// in LDS (namespace scope, so project_items reaches them)
+__shared__ unsigned ph_acc[4][25];
+#define PJ_INIT unsigned long long pj_t = __builtin_readcyclecounter();
+#define PJ(k)                                                                                     \
+  do {                                                                                            \
+    const unsigned long long pj_n = __builtin_readcyclecounter();                                 \
+    if ((threadIdx.x & 63) == 0) ph_acc[threadIdx.x >> 6][20 + (k)] += (unsigned)(pj_n - pj_t);   \
+    pj_t = pj_n;                                                                                  \
+  } while (0)
+#else
+#define PJ_INIT
+#define PJ(k)
+#endif
 #define TTRL_ITEMS_ATTR __forceinline__
 constexpr bool PROJ_PRUNE = true;
 template <typename T, int NS, int EPW, int LC, typename PP>
 __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int nl, int tid, int le, int i,
                              bool present, bool want_closest, float4 my_box, float onb) {
   static_assert(NS * EPW == 64, "one wavefront per workgroup");
+  PJ_INIT
   constexpr int NSP = LC + 1;
   constexpr unsigned long long SEG = NS == 64 ? ~0ull : ((1ull << NS) - 1);
   const T vl = T(P.lane_vehicle_length);
@@ -1226,16 +1249,25 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int 
       if (keep && pos < cap) psv[pos] = (short)(vv << 5 | kk);
       nsv += __popcll(bal);
     }
+    PJ(0);
     if (nsv <= cap) {
       pruned = true;
       if (tid == 0) pstart[total] = (short)nsv;
       __syncthreads();
-      // (B) the survivors' projections
-      for (int k = tid; k < nsv; k += 64) {
+      // (B) the survivors' projections.  The lane that projects survivor k also writes its list entry
+      // in (D): the s of its first SREG survivors stays in registers (a turn's s costs an atan2)
+      constexpr int SREG = 2;
+      T sreg[SREG];
+#pragma unroll
+      for (int u = 0; u < SREG; ++u) sreg[u] = T(0);
+      for (int k = tid, u = 0; k < nsv; k += 64, ++u) {
         const int vv = psv[k] >> 5, l = V.lperm[psv[k] & 31];
         const LaneT<T> L = V.lanes[l];
         T s, r;
         lane_local<true>(L, V.x[vv], V.y[vv], s, r);
+#pragma unroll
+        for (int w = 0; w < SREG; ++w)
+          if (u == w) sreg[w] = s;
         if (fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl)  // AbstractLane.on_lane margin 1
           atomicOr(&V.onm[l], 1ull << vv);
         if (want_closest) {  // distance_with_heading lane.py:132-147
@@ -1246,20 +1278,31 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int 
         }
       }
       __syncthreads();
+      PJ(1);
       // (C) the first minimum of each vehicle over its run (lperm order, ties to the lower lane)
       if (want_closest && present) {
         const int q = __popcll(live & below);
         T cd = T(0);
         cl = -1;
-        for (int k = pstart[q], k1 = pstart[q + 1]; k < k1; ++k) {
-          const int lu = pl_[k];
-          const T du = pd_[k];
-          if (cl < 0 || du < cd || (du == cd && lu < cl)) { cd = du; cl = lu; }
+        const int k1 = pstart[q + 1];
+        for (int k = pstart[q]; k < k1; k += 4) {  // four entries' loads at a time
+          int lu[4];
+          T du[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int kk = min(k + u, k1 - 1);
+            lu[u] = pl_[kk];
+            du[u] = pd_[kk];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (k + u < k1 && (cl < 0 || du[u] < cd || (du[u] == cd && lu[u] < cl))) { cd = du[u]; cl = lu[u]; }
         }
       }
       __syncthreads();  // (C)'s reads of the key rows before (D) writes them
+      PJ(2);
       // (D) each on-lane survivor's list position (slot order = list order), key and slot
-      for (int k = tid; k < nsv; k += 64) {
+      for (int k = tid, u = 0; k < nsv; k += 64, ++u) {
         const int vv = psv[k] >> 5, l = V.lperm[psv[k] & 31];
         const unsigned long long m = V.onm[l];
         if (!((m >> vv) & 1ull)) continue;
@@ -1267,8 +1310,14 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int 
         const int pos = __popcll((m >> (e * NS)) & SEG & ((1ull << sl) - 1));
         V.mypos[(size_t)l * EPW * NS + vv] = (short)pos;
         if (pos < LC) {
-          T sq, rq;
-          lane_local<true>(V.lanes[l], V.x[vv], V.y[vv], sq, rq);
+          T sq = T(0), rq;
+          if (u < SREG) {
+#pragma unroll
+            for (int w = 0; w < SREG; ++w)
+              if (u == w) sq = sreg[w];
+          } else {
+            lane_local<true>(V.lanes[l], V.x[vv], V.y[vv], sq, rq);
+          }
           const size_t base = ((size_t)l * EPW + e) * NSP;
           V.key[base + pos] = sq;
           V.idx[base + pos] = (uint8_t)sl;
@@ -1346,6 +1395,7 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int 
     }
   }
   }  // !pruned
+  PJ(3);
   // the list lengths, one thread per (lane, env)
   if (tid < nl * EPW) {
     const int l = tid / EPW, e = tid - l * EPW;
@@ -1353,6 +1403,7 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int 
     V.cnt[e * (LMAX + 1) + l] = c;
     atomicMax(&V.cnt[e * (LMAX + 1) + LMAX], c);
   }
+  PJ(4);
   return cl;
 }
 
@@ -1655,7 +1706,7 @@ enum { FL_CRASHED = 1, FL_IMPACT = 2, FL_LC = 4, FL_YIELD = 8 };
 // wave's (start, end) shader clock with its HW_ID / XCC_ID, no LDS (tools/phases.py --waves).
 // The production kernel carries neither.
 #if defined(TTRL_PHASE_TIMING) || defined(TTRL_WAVE_TRACE)
-__device__ unsigned long long g_phase[20];
+__device__ unsigned long long g_phase[25];  // 20 phases + project_items' 5 steps
 constexpr int WTRACE_MAX = 16384;
 __device__ unsigned long long g_wtrace[WTRACE_MAX][3];
 __device__ unsigned g_wphase[WTRACE_MAX][20];  // PHASE_TIMING: each wave's phase cycles of the last launch
@@ -1673,8 +1724,7 @@ __device__ unsigned g_wphase[WTRACE_MAX][20];  // PHASE_TIMING: each wave's phas
 #ifdef TTRL_PHASE_TIMING
 #define PH_INIT                                                        \
   WT_INIT                                                              \
-  __shared__ unsigned ph_acc[4][20];                                   \
-  if ((threadIdx.x & 63) < 20) ph_acc[threadIdx.x >> 6][threadIdx.x & 63] = 0; \
+  if ((threadIdx.x & 63) < 25) ph_acc[threadIdx.x >> 6][threadIdx.x & 63] = 0; \
   unsigned long long ph_t = ph_t0;
 #define PH(k)                                                          \
   do {                                                                 \
@@ -1683,10 +1733,10 @@ __device__ unsigned g_wphase[WTRACE_MAX][20];  // PHASE_TIMING: each wave's phas
     ph_t = ph_n;                                                       \
   } while (0)
 #define PH_FLUSH                                                       \
-  if ((threadIdx.x & 63) < 20) {                                       \
+  if ((threadIdx.x & 63) < 25) {                                       \
     atomicAdd(&g_phase[threadIdx.x & 63], (unsigned long long)ph_acc[threadIdx.x >> 6][threadIdx.x & 63]); \
     const unsigned ph_w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); \
-    if (ph_w < WTRACE_MAX) g_wphase[ph_w][threadIdx.x & 63] = ph_acc[threadIdx.x >> 6][threadIdx.x & 63]; \
+    if (ph_w < WTRACE_MAX && (threadIdx.x & 63) < 20) g_wphase[ph_w][threadIdx.x & 63] = ph_acc[threadIdx.x >> 6][threadIdx.x & 63]; \
   }                                                                    \
   WT_FLUSH
 #elif defined(TTRL_WAVE_TRACE)
@@ -2808,19 +2858,17 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
             const T d2 = dx * dx + dy * dy;
             if (d2 > (thr + T(1)) * (thr + T(1))) continue;
             if (sqrt(d2) > thr) continue;
-            bool inter, will;
-            T tx, ty;
             const T ci = V.ch[me], si = V.sh[me], cj = V.ch[eb + j], sj = V.sh[eb + j];
-            if (lo ? sat_separated(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt)
-                   : sat_separated(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt))
-              continue;
-            if (lo) sat_pair(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt, inter, will, tx, ty);
-            else sat_pair(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt, inter, will, tx, ty);
-            if (will) {
-              if (lo) { best_gt = j; gx = tx / T(2); gy = ty / T(2); }
-              else { best_lt = j; lx = -tx / T(2); ly = -ty / T(2); }
+            // the pair as the reference orders it: a = the lower index
+            const T ax = lo ? xi : xj, ay = lo ? yi : yj, ac = lo ? ci : cj, as = lo ? si : sj, av = lo ? vi : vj;
+            const T bx = lo ? xj : xi, by = lo ? yj : yi, bc = lo ? cj : ci, bs = lo ? sj : si, bv = lo ? vj : vi;
+            if (sat_separated(P, ax, ay, ac, as, av, bx, by, bc, bs, bv, dt)) continue;
+            const SatRes<T> sr = sat_pair_v(P, ax, ay, ac, as, av, bx, by, bc, bs, bv, dt);
+            if (sr.flags & 2) {
+              if (lo) { best_gt = j; gx = sr.tx / T(2); gy = sr.ty / T(2); }
+              else { best_lt = j; lx = -sr.tx / T(2); ly = -sr.ty / T(2); }
             }
-            if (inter) crash = true;
+            if (sr.flags & 1) crash = true;
           }
         }
         int fl = V.flags[me];
@@ -4844,10 +4892,10 @@ int ttrl_diag_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road, con
 }
 
 #if defined(TTRL_PHASE_TIMING) || defined(TTRL_WAVE_TRACE)
-// Diagnostic build only: read and clear the per-phase cycle sums (20 u64).
+// Diagnostic build only: read and clear the per-phase cycle sums (25 u64: 20 phases, project_items' 5 steps).
 int ttrl_diag_phase_read(unsigned long long* out) {
-  unsigned long long z[20] = {};
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 20) != hipSuccess) return TTRL_E_LAUNCH;
+  unsigned long long z[25] = {};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(z)) != hipSuccess) return TTRL_E_LAUNCH;
   return hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) == hipSuccess ? TTRL_OK : TTRL_E_LAUNCH;
 }
 // ... each wave's phase cycles of the last launch (PHASE_TIMING builds): n x 20 u32
