@@ -34,8 +34,8 @@ def main(dtype="f64", steps=30, frames=15, ix=False, E=4096):
     rd = lib.ttrl_diag_phase_read
     rd.argtypes = [C.c_void_p]
     stream = torch.cuda.current_stream(dev).cuda_stream
-    buf = np.zeros(25, dtype=np.uint64)  # 20 phases, then project_items' 5 steps (road-network instance)
-    tot = np.zeros(25)
+    buf = np.zeros(32, dtype=np.uint64)  # 20 phases, project_items' 5 steps, the regulation's 5 steps, 2 counts
+    tot = np.zeros(32)
     work = env.state.clone() if ix else env.state
     for t in range(steps):
         a_idx = torch.randint(0, n_act, (E,), device=dev, generator=g)
@@ -54,7 +54,7 @@ def main(dtype="f64", steps=30, frames=15, ix=False, E=4096):
         if t >= 10:
             tot += buf.astype(np.float64)
     waves = (E if not ix else 2048) * (steps - 10)  # ix: two envs per 64-lane workgroup
-    per, pp = tot[:20] / waves, tot[20:] / waves
+    per, pp, rg = tot[:20] / waves, tot[20:25] / waves, tot[25:30] / waves
     print(f"[{dtype}] E={E} cycles per wave per {frames}-frame launch (mean over {steps - 10} launches), total {per.sum():.0f}")
     for n, c in zip(NAMES, per):
         print(f"  {n:16s} {c:10.0f}  {100 * c / per.sum():5.1f}%  ({c / frames:8.0f} per frame)")
@@ -62,6 +62,12 @@ def main(dtype="f64", steps=30, frames=15, ix=False, E=4096):
         print("  project_items steps, cycles per wave per frame: " + ", ".join(
             f"{n} {c / frames:.0f}" for n, c in zip(["A boxes", "B projections", "C minimum", "D lists",
                                                     "counts"], pp)))
+    if rg.any():
+        print("  regulation steps, cycles per wave per frame: " + ", ".join(
+            f"{n} {c / frames:.0f}" for n, c in zip(["P reach+pairs", "A items", "B exact", "C priorities",
+                                                    "serial fallback"], rg)))
+        print(f"  regulation fallbacks per wave per launch: more pairs than RQ_PAIRS {tot[30] / waves:.3f}, "
+              f"more items than the queue {tot[31] / waves:.3f}")
     # the last launch, wave by wave: start / end spread and the per-SIMD finish (load balance)
     nw = E if not ix else 2048
     tr = np.zeros((nw, 3), dtype=np.uint64)
@@ -90,16 +96,20 @@ def main(dtype="f64", steps=30, frames=15, ix=False, E=4096):
     st = t0 - lo[inv]
     print(f"wave start offset within its SIMD: mean {st.mean():.0f} max {st.max()}")
     if os.environ.get("TIMING_LIB", "lib_timing.so").endswith("lib_timing.so"):  # per-wave phase cycles
-        wp = np.zeros((nw, 20), dtype=np.uint32)
+        wp = np.zeros((nw, 32), dtype=np.uint32)
         lib.ttrl_diag_wave_phases.argtypes = [C.c_void_p, C.c_int]
         lib.ttrl_diag_wave_phases(wp.ctypes.data, nw)
-        tot = wp.sum(1).astype(np.float64)
+        tot = wp[:, :20].sum(1).astype(np.float64)
         slow = tot >= np.percentile(tot, 95)
         mid = (tot >= np.percentile(tot, 40)) & (tot <= np.percentile(tot, 60))
         print(f"the slowest 5% of waves (phase sum {tot[slow].mean():.0f}) vs the median ones ({tot[mid].mean():.0f}), "
               f"cycles per launch:")
-        for k in np.argsort(-(wp[slow].mean(0) - wp[mid].mean(0)))[:10]:
-            print(f"  {NAMES[k]:16s} slow {wp[slow, k].mean():9.0f}  median {wp[mid, k].mean():9.0f}")
+        names = NAMES + [f"project {n}" for n in ["A", "B", "C", "D", "counts"]] + [
+            f"regulation {n}" for n in ["P", "A", "B", "C", "serial"]] + ["#pairs>cap", "#items>cap"]
+        for k in np.argsort(-(wp[slow].mean(0) - wp[mid].mean(0)))[:14]:
+            print(f"  {names[k]:16s} slow {wp[slow, k].mean():9.0f}  median {wp[mid, k].mean():9.0f}")
+        if wp[:, 29].any():
+            print(f"waves taking the serial regulation fallback: {(wp[:, 29] > 2000).sum()} of {nw}")
 
 
 if __name__ == "__main__":

@@ -319,11 +319,10 @@ __device__ __forceinline__ bool reachable(const LaneT<T>& L, T vl, T px, T py) {
   return fabs(r) <= T(2) * L.w && T(0) <= s && s < L.len + vl;
 }
 
-// ControlledVehicle.steering_control controller.py:145-187
+// ControlledVehicle.steering_control controller.py:145-187, from the vehicle's local coordinates
+// (s, r) on its target lane L
 template <bool CV = true, typename T, typename PP>
-__device__ __forceinline__ T steering_control(const LaneT<T>& L, const PP& P, T x, T y, T h, T v) {
-  T s, r;
-  lane_local<CV>(L, x, y, s, r);
+__device__ __forceinline__ T steering_control_sr(const LaneT<T>& L, const PP& P, T s, T r, T h, T v) {
   const T lfh = heading_at<CV>(L, s + v * T(P.tau_pursuit));  // lane_future_heading
   const T lat_cmd = -T(P.kp_lateral) * r;
   const T hcmd = k_asin(clip(lat_cmd / not_zero(v), T(-1), T(1)));
@@ -334,6 +333,12 @@ __device__ __forceinline__ T steering_control(const LaneT<T>& L, const PP& P, T 
   const T c = clip(T(P.length) / T(2) / not_zero(v) * hrate, T(-1), T(1));
   const T st = k_atan(T(2) * (c / sqrt((T(1) - c) * (T(1) + c))));
   return clip(st, -T(P.max_steering), T(P.max_steering));
+}
+template <bool CV = true, typename T, typename PP>
+__device__ __forceinline__ T steering_control(const LaneT<T>& L, const PP& P, T x, T y, T h, T v) {
+  T s, r;
+  lane_local<CV>(L, x, y, s, r);
+  return steering_control_sr<CV>(L, P, s, r, h, v);
 }
 
 // MDPVehicle.speed_to_index controller.py:326-344 (np.round: half to even)
@@ -670,7 +675,9 @@ __host__ __device__ inline ViewLayout view_layout(int EPW, int NS, int n_lanes, 
     o.ynew = take(M, 4);
     o.rt = take(sizeof(RoadTab), 4);
     o.onm = take(sizeof(unsigned long long) * LMAX, 8);
-    o.pd = take(sizeof(T) * M, 16);
+    // a T, or project_items' float2 (y, bound) per vehicle, or the regulation's reach (float) and
+    // passing-pair queue (RQ_PAIRS bytes)
+    o.pd = take(8 * M > 4 * M + RQ_PAIRS ? 8 * M : 4 * M + RQ_PAIRS, 16);
     o.live = take(M, 4);
     o.lperm = take(LMAX, 4);
     o.pl = take(M, 4);
@@ -1149,20 +1156,31 @@ __device__ __forceinline__ void slot_nbrs(const View<T>& V, int le, int self, in
 // rebuilt at 4 waves, passes its intersection GPU tests and 40 finite steps, and so does this
 // source at 4 waves with round 3's item bounds checks silent (profiles/r03/netgraph_4wave/).  The
 // 2-wave budget of the road networks is a tuning choice, not a correctness one.)
+// Diagnostic timing slots: 20 phases, project_items' 5 steps (PJ), the regulation's 5 steps (RG)
+// and 2 event counts (RG_COUNT: enforcements past RQ_PAIRS pairs, past the item queue)
+constexpr int PH_SLOTS = 32;
 #ifdef TTRL_PHASE_TIMING
-// the phase accumulators of PH (below): 20 phases + project_items' 5 steps (PJ), one row per wave,
-// in LDS (namespace scope, so project_items reaches them)
-__shared__ unsigned ph_acc[4][25];
-#define PJ_INIT unsigned long long pj_t = __builtin_readcyclecounter();
-#define PJ(k)                                                                                     \
+// their accumulators, one row per wave, in LDS (namespace scope, so the helpers reach them)
+__shared__ unsigned ph_acc[4][PH_SLOTS];
+#define SUB_INIT(t) unsigned long long t = __builtin_readcyclecounter();
+#define SUB(t, k)                                                                                 \
   do {                                                                                            \
-    const unsigned long long pj_n = __builtin_readcyclecounter();                                 \
-    if ((threadIdx.x & 63) == 0) ph_acc[threadIdx.x >> 6][20 + (k)] += (unsigned)(pj_n - pj_t);   \
-    pj_t = pj_n;                                                                                  \
+    const unsigned long long sub_n = __builtin_readcyclecounter();                                \
+    if ((threadIdx.x & 63) == 0) ph_acc[threadIdx.x >> 6][k] += (unsigned)(sub_n - t);            \
+    t = sub_n;                                                                                    \
   } while (0)
 #else
-#define PJ_INIT
-#define PJ(k)
+#define SUB_INIT(t)
+#define SUB(t, k)
+#endif
+#define PJ_INIT SUB_INIT(pj_t)
+#define PJ(k) SUB(pj_t, 20 + (k))
+#define RG_INIT SUB_INIT(rg_t)
+#define RG(k) SUB(rg_t, 25 + (k))
+#ifdef TTRL_PHASE_TIMING
+#define RG_COUNT(k) do { if ((threadIdx.x & 63) == 0) ph_acc[threadIdx.x >> 6][30 + (k)] += 1u; } while (0)
+#else
+#define RG_COUNT(k)
 #endif
 #define TTRL_ITEMS_ATTR __forceinline__
 constexpr bool PROJ_PRUNE = true;
@@ -1217,7 +1235,12 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int 
         ub = fabs(r0) + a + b + T(1) * fabs(wrap_to_pi(V.h[tid] - heading_at<true>(L, s0)));
       }
     }
-    V.pd[tid] = ub;
+    // per vehicle, once: its float32 y and the box tests' bound (float32 rounding: 1e-3 m + 1e-6 of
+    // the coordinates); its float32 x is V.xf
+    const float fx = (float)V.x[tid], fy = (float)V.y[tid];
+    const float bound = fmaxf(onb, ub < T(3.0e38f) ? (float)ub * 1.000001f : INFINITY) + 1e-3f +
+                        1e-6f * (fabsf(fx) + fabsf(fy));
+    ((float2*)V.pd)[tid] = make_float2(fy, bound);
   }
   __syncthreads();
   int cl = 0;
@@ -1225,20 +1248,19 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int 
   if constexpr (PROJ_PRUNE) {
     // (A) box tests, (vehicle, lperm position) items in vehicle-major order
     const int nitems = total * nl;
+    const float rnl = 1.0f / (float)nl;  // k / nl as (k + 1/2) / nl in float32: exact for k < 2^16
     int nsv = 0;
     for (int k0 = 0; k0 < nitems; k0 += 64) {
       const int k = k0 + tid;
       bool keep = false;
       int q = 0, kk = 0, vv = 0;
       if (k < nitems) {
-        q = k / nl;
+        q = (int)(((float)k + 0.5f) * rnl);
         kk = k - q * nl;
         vv = V.live[q];
-        const float fx = (float)V.x[vv], fy = (float)V.y[vv];
-        const T ubv = V.pd[vv];
-        // the float32 rounding of the box test: 1e-3 m + 1e-6 of the coordinates
-        const float bound = fmaxf(onb, ubv < T(3.0e38f) ? (float)ubv * 1.000001f : INFINITY) + 1e-3f +
-                            1e-6f * (fabsf(fx) + fabsf(fy));
+        const float fx = V.xf[vv];
+        const float2 yb = ((const float2*)V.pd)[vv];
+        const float fy = yb.x, bound = yb.y;
         const float4 bx = lbox[V.lperm[kk]];
         const float ex = fmaxf(fmaxf(bx.x - fx, fx - bx.z), 0.0f), ey = fmaxf(fmaxf(bx.y - fy, fy - bx.w), 0.0f);
         keep = !(ex * ex + ey * ey > bound * bound);  // NaN positions are kept
@@ -1263,17 +1285,34 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int 
       for (int k = tid, u = 0; k < nsv; k += 64, ++u) {
         const int vv = psv[k] >> 5, l = V.lperm[psv[k] & 31];
         const LaneT<T> L = V.lanes[l];
-        T s, r;
-        lane_local<true>(L, V.x[vv], V.y[vv], s, r);
+        const T x = V.x[vv], y = V.y[vv];
+        T s = T(0), r;
+        bool full = true;  // s computed
+        if (L.type == TTRL_LANE_CIRCULAR) {
+          // CircularLane.local_coordinates (lane.py:327-334, as curved_local), the lateral part first:
+          // beyond the vehicle's bound (> its distance to its previous lane, >= the on-lane reach) the
+          // lane is neither on-lane nor the closest (d >= |r|), and its atan2 is skipped
+          const T dx = x - L.cx, dy = y - L.cy;
+          const T rr = sqrt(dx * dx + dy * dy);
+          r = L.dirn * (L.rad - rr);
+          full = !(fabs(r) > (T)((const float2*)V.pd)[vv].y);
+          if (full) {
+            T phi = atan2(dy, dx);
+            phi = L.sph + wrap_to_pi(phi - L.sph);
+            s = L.dirn * (phi - L.sph) * L.rad;
+          }
+        } else {
+          lane_local<true>(L, x, y, s, r);
+        }
 #pragma unroll
         for (int w = 0; w < SREG; ++w)
           if (u == w) sreg[w] = s;
-        if (fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl)  // AbstractLane.on_lane margin 1
+        if (full && fabs(r) <= L.w / T(2) + T(1) && -vl <= s && s < L.len + vl)  // AbstractLane.on_lane margin 1
           atomicOr(&V.onm[l], 1ull << vv);
         if (want_closest) {  // distance_with_heading lane.py:132-147
           T a = s - L.len; if (!(a > T(0))) a = T(0);
           T b = T(0) - s; if (!(b > T(0))) b = T(0);
-          pd_[k] = fabs(r) + a + b + T(1) * fabs(wrap_to_pi(V.h[vv] - heading_at<true>(L, s)));
+          pd_[k] = full ? fabs(r) + a + b + T(1) * fabs(wrap_to_pi(V.h[vv] - heading_at<true>(L, s))) : K<T>::inf();
           pl_[k] = (int8_t)l;
         }
       }
@@ -1706,10 +1745,10 @@ enum { FL_CRASHED = 1, FL_IMPACT = 2, FL_LC = 4, FL_YIELD = 8 };
 // wave's (start, end) shader clock with its HW_ID / XCC_ID, no LDS (tools/phases.py --waves).
 // The production kernel carries neither.
 #if defined(TTRL_PHASE_TIMING) || defined(TTRL_WAVE_TRACE)
-__device__ unsigned long long g_phase[25];  // 20 phases + project_items' 5 steps
+__device__ unsigned long long g_phase[PH_SLOTS];  // 20 phases, project_items' and the regulation's steps
 constexpr int WTRACE_MAX = 16384;
 __device__ unsigned long long g_wtrace[WTRACE_MAX][3];
-__device__ unsigned g_wphase[WTRACE_MAX][20];  // PHASE_TIMING: each wave's phase cycles of the last launch
+__device__ unsigned g_wphase[WTRACE_MAX][PH_SLOTS];  // PHASE_TIMING: each wave's phase cycles of the last launch
 #define WT_INIT const unsigned long long ph_t0 = __builtin_readcyclecounter();
 #define WT_FLUSH                                                       \
   {                                                                    \
@@ -1724,7 +1763,7 @@ __device__ unsigned g_wphase[WTRACE_MAX][20];  // PHASE_TIMING: each wave's phas
 #ifdef TTRL_PHASE_TIMING
 #define PH_INIT                                                        \
   WT_INIT                                                              \
-  if ((threadIdx.x & 63) < 25) ph_acc[threadIdx.x >> 6][threadIdx.x & 63] = 0; \
+  if ((threadIdx.x & 63) < PH_SLOTS) ph_acc[threadIdx.x >> 6][threadIdx.x & 63] = 0; \
   unsigned long long ph_t = ph_t0;
 #define PH(k)                                                          \
   do {                                                                 \
@@ -1733,10 +1772,10 @@ __device__ unsigned g_wphase[WTRACE_MAX][20];  // PHASE_TIMING: each wave's phas
     ph_t = ph_n;                                                       \
   } while (0)
 #define PH_FLUSH                                                       \
-  if ((threadIdx.x & 63) < 25) {                                       \
+  if ((threadIdx.x & 63) < PH_SLOTS) {                                 \
     atomicAdd(&g_phase[threadIdx.x & 63], (unsigned long long)ph_acc[threadIdx.x >> 6][threadIdx.x & 63]); \
     const unsigned ph_w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); \
-    if (ph_w < WTRACE_MAX && (threadIdx.x & 63) < 20) g_wphase[ph_w][threadIdx.x & 63] = ph_acc[threadIdx.x >> 6][threadIdx.x & 63]; \
+    if (ph_w < WTRACE_MAX) g_wphase[ph_w][threadIdx.x & 63] = ph_acc[threadIdx.x >> 6][threadIdx.x & 63]; \
   }                                                                    \
   WT_FLUSH
 #elif defined(TTRL_WAVE_TRACE)
@@ -2286,8 +2325,24 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
       // steering + IDM longitudinal (behavior.py:109-135); ego: ControlledVehicle.act (controller.py:126-133)
       const bool mdp = present && kind == TTRL_MDP;
       if (idm || mdp) {  // one steering pass for both kinds (the ego steers to its own target)
-        my_steer = (idm && (ablate & A_NO_STEER)) ? T(0)
-                                                 : steering_control<CV>(V.lanes[idm ? tgt_new : tgt], P, x, y, V.h[me], v);
+        const int sl = idm ? tgt_new : tgt;
+        const LaneT<T>& SL = V.lanes[sl];
+        T s, r;
+        bool turn = false;
+        if constexpr (!SO && CV) turn = SL.type == TTRL_LANE_CIRCULAR;
+        if (turn) {
+          if constexpr (!SO && CV) {
+            // a turn: s from the lane's candidate list (the projection stored lane_local's s for this
+            // position; lane_s recomputes it off the list), the lateral part as curved_local has it
+            s = lane_s<T, NS, EPW, LC>(V, sl, le, i, x, y);
+            const T dx = x - SL.cx, dy = y - SL.cy;
+            r = SL.dirn * (SL.rad - sqrt(dx * dx + dy * dy));
+          }
+        } else {
+          lane_local<CV>(SL, x, y, s, r);
+        }
+        // one steering evaluation for both branches (a divergent wave would run it twice)
+        my_steer = (idm && (ablate & A_NO_STEER)) ? T(0) : steering_control_sr<CV>(SL, P, s, r, V.h[me], v);
       }
       if (idm) {
         const T a_free = V.afree[me];
@@ -2353,6 +2408,7 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
             }
             __syncthreads();
             PH(18);
+            RG_INIT
             // is_conflict_possible (regulation.py:80-103) then respect_priorities (:62-77) for the pair
             // (a < b) of the env at LDS base ebp; a yield only ever sets ynew, so pairs commute
             auto reg_pair = [&](int ebp, int a, int b) {
@@ -2415,80 +2471,141 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
                 a = V.live[e * NS + kk - rb * (rb - 1) / 2];
                 b = V.live[e * NS + rb];
               };
-              bool flat = false;
-              if (tot <= RQ_PAIRS && V.rq_cap > 0) {
-                // Flattened: is_conflict_possible is an OR over the 11 time steps, so (pair, step) items
-                // are independent.  (A) the float32 distance prefilter over all items, survivors queued
-                // (ballot slots); (B) the exact float64 test of the survivors, one per lane (a close pair
-                // no longer walks its steps serially on one lane); (C) respect_priorities of the pairs
-                // that conflict.  Queue overflow: the serial per-pair loop below.
-                for (int k = tid; k < tot; k += 64) V.rqf[k] = 0;
-                const float thr_len = float(P.length) + 1e-3f;
-                int nq = 0;
-                for (int k0 = 0; k0 < tot * PRED_T; k0 += 64) {
-                  const int k = k0 + tid;
-                  bool pass = false;
-                  int pid = 0, t = 0;
-                  if (k < tot * PRED_T) {
-                    pid = k / PRED_T;
-                    t = k - pid * PRED_T;
-                    int e, a, b;
-                    decode(pid, e, a, b);
-                    const int pa = (e * NS + a) * PRED_T + t, pb = (e * NS + b) * PRED_T + t;
-                    const float fxa = V.px[pa], fya = V.py[pa], fxb = V.px[pb], fyb = V.py[pb];
-                    const float fdx = fxb - fxa, fdy = fyb - fya;
-                    const float thr = thr_len + 4e-7f * (fabsf(fxa) + fabsf(fxb) + fabsf(fya) + fabsf(fyb));
-                    pass = !(fdx * fdx + fdy * fdy > thr * thr);  // as reg_pair's prefilter (NaN passes)
-                  }
-                  const unsigned long long bal = __ballot(pass);
-                  const int pos = nq + __popcll(bal & ((1ull << tid) - 1));
-                  if (pass && pos < V.rq_cap) V.rq[pos] = pid << 4 | t;
-                  nq += __popcll(bal);
+              // Flattened: is_conflict_possible is an OR over the 11 time steps, so (pair, step) items
+              // are independent.  (P) a pair test: each vehicle's 11 predicted positions lie within its
+              // reach of the middle one, so a pair whose middle positions are farther apart than both
+              // reaches + the prefilter's threshold has no step that passes the prefilter (the triangle
+              // inequality, with a rounding slack); the passing pairs are queued.  (A) the float32
+              // distance prefilter over their (pair, step) items, survivors queued (ballot slots);
+              // (B) the exact float64 test of the survivors, one per lane (a close pair no longer walks
+              // its steps serially on one lane); (C) respect_priorities of the pairs that conflict.
+              // The pairs run in chunks of RQ_PAIRS (a yield only sets ynew: chunks commute); an item
+              // queue overflow takes the serial per-pair loop for its chunk.
+              const float thr_len = float(P.length) + 1e-3f;
+              float* reach = (float*)V.pd;  // [M], free until the projection; then the pair queue
+              uint8_t* pq2 = (uint8_t*)V.pd + sizeof(float) * EPW * NS;  // [RQ_PAIRS] a chunk's passing pairs
+              if (V.rq_cap > 0 && doreg && present) {
+                const float* qx = V.px + me * PRED_T;
+                const float* qy = V.py + me * PRED_T;
+                const float cx = qx[PRED_T / 2], cy = qy[PRED_T / 2];
+                float d2 = 0.0f;
+                bool bad = false;  // a NaN position: the reach is unbounded
+#pragma unroll
+                for (int t = 0; t < PRED_T; ++t) {
+                  const float dx = qx[t] - cx, dy = qy[t] - cy, dd = dx * dx + dy * dy;
+                  bad |= dd != dd;
+                  d2 = fmaxf(d2, dd);
                 }
-                if (nq <= V.rq_cap) {
-                  flat = true;
-                  __syncthreads();
-                  for (int k = tid; k < nq; k += 64) {
-                    const int pid = V.rq[k] >> 4, t = V.rq[k] & 15;
-                    int e, a, b;
-                    decode(pid, e, a, b);
-                    const int ka = e * NS + a, kb = e * NS + b;
-                    T xa, ya, ha, xb, yb, hb;
-                    pose_at(V.lanes, *V.rt, (int)V.lane[ka], V.ps0[ka], V.v[ka], V.rroad + ka * TTRL_ROUTE_MAX,
-                            V.rlane + ka * TTRL_ROUTE_MAX, (int)V.rn[ka], t, xa, ya, &ha);
-                    pose_at(V.lanes, *V.rt, (int)V.lane[kb], V.ps0[kb], V.v[kb], V.rroad + kb * TTRL_ROUTE_MAX,
-                            V.rlane + kb * TTRL_ROUTE_MAX, (int)V.rn[kb], t, xb, yb, &hb);
-                    const T dx = xb - xa, dy = yb - ya;
-                    if (!(sqrt(dx * dx + dy * dy) > T(P.length)) &&
-                        rects_intersect(xa, ya, ha, xb, yb, hb, T(1.5) * T(P.length), T(0.9) * T(P.width)))
-                      V.rqf[pid] = 1;
-                  }
-                  __syncthreads();
-                  for (int k = tid; k < tot; k += 64) {
-                    if (!V.rqf[k]) continue;
-                    int e, a, b;
-                    decode(k, e, a, b);
-                    const int ebp = e * NS;
-                    const int qa = V.lanes[V.lane[ebp + a]].prio, qb = V.lanes[V.lane[ebp + b]].prio;
-                    int yv;
-                    if (qa > qb) yv = b;
-                    else if (qa < qb) yv = a;
-                    else {
-                      const int ka = ebp + a, kb = ebp + b;
-                      const T fab = V.ch[ka] * (V.x[kb] - V.x[ka]) + V.sh[ka] * (V.y[kb] - V.y[ka]);
-                      const T fba = V.ch[kb] * (V.x[ka] - V.x[kb]) + V.sh[kb] * (V.y[ka] - V.y[kb]);
-                      yv = fab > fba ? a : b;
-                    }
-                    if (V.kind[ebp + yv] == TTRL_IDM) V.ynew[ebp + yv] = 1;  // ControlledVehicle, not MDPVehicle
-                  }
-                }
+                reach[me] = bad ? INFINITY : sqrtf(d2);
               }
-              if (!flat)
-                for (int k = tid; k < tot; k += 64) {
-                  int e, a, b;
-                  decode(k, e, a, b);
-                  reg_pair(e * NS, a, b);
+              if (tot > RQ_PAIRS) RG_COUNT(0);
+              for (int c0 = 0; c0 < tot; c0 += RQ_PAIRS) {
+                const int cn = tot - c0 < RQ_PAIRS ? tot - c0 : RQ_PAIRS;  // pairs c0 .. c0 + cn, ids k - c0
+                bool flat = false;
+                if (V.rq_cap > 0) {
+                  for (int k = tid; k < cn; k += 64) V.rqf[k] = 0;
+                  __syncthreads();
+                  int np2 = 0;
+                  for (int k0 = 0; k0 < cn; k0 += 64) {
+                    const int k = k0 + tid;
+                    bool pass = false;
+                    if (k < cn) {
+                      int e, a, b;
+                      decode(c0 + k, e, a, b);
+                      const int ka = e * NS + a, kb = e * NS + b;
+                      const float cxa = V.px[ka * PRED_T + PRED_T / 2], cya = V.py[ka * PRED_T + PRED_T / 2];
+                      const float cxb = V.px[kb * PRED_T + PRED_T / 2], cyb = V.py[kb * PRED_T + PRED_T / 2];
+                      const float ra = reach[ka], rb = reach[kb];
+                      const float dx = cxb - cxa, dy = cyb - cya;
+                      // the prefilter's threshold at any step is at most thr_len + 4e-7 of the
+                      // coordinates' magnitudes, each within its reach of the middle position; 1e-5
+                      // relative + 1 cm cover the float32 rounding of this test, of the reaches and of
+                      // the prefilter
+                      const float thr =
+                          thr_len + 4e-7f * (fabsf(cxa) + fabsf(cxb) + fabsf(cya) + fabsf(cyb) + 2.0f * (ra + rb));
+                      const float bound = (ra + rb + thr) * 1.00001f + 1e-2f;
+                      pass = !(dx * dx + dy * dy > bound * bound);  // NaN / inf pass
+                    }
+                    const unsigned long long bal = __ballot(pass);
+                    if (pass) pq2[np2 + __popcll(bal & ((1ull << tid) - 1))] = (uint8_t)k;
+                    np2 += __popcll(bal);
+                  }
+                  __syncthreads();
+                  RG(0);
+                  int nq = 0;
+                  for (int k0 = 0; k0 < np2 * PRED_T; k0 += 64) {
+                    const int k = k0 + tid;
+                    bool pass = false;
+                    int pid = 0, t = 0;
+                    if (k < np2 * PRED_T) {
+                      const int q = k / PRED_T;
+                      t = k - q * PRED_T;
+                      pid = pq2[q];
+                      int e, a, b;
+                      decode(c0 + pid, e, a, b);
+                      const int ka = e * NS + a, kb = e * NS + b;
+                      const int pa = ka * PRED_T + t, pb = kb * PRED_T + t;
+                      const float fxa = V.px[pa], fya = V.py[pa], fxb = V.px[pb], fyb = V.py[pb];
+                      const float fdx = fxb - fxa, fdy = fyb - fya;
+                      const float thr = thr_len + 4e-7f * (fabsf(fxa) + fabsf(fxb) + fabsf(fya) + fabsf(fyb));
+                      pass = !(fdx * fdx + fdy * fdy > thr * thr);  // as reg_pair's prefilter (NaN passes)
+                    }
+                    const unsigned long long bal = __ballot(pass);
+                    const int pos = nq + __popcll(bal & ((1ull << tid) - 1));
+                    if (pass && pos < V.rq_cap) V.rq[pos] = pid << 4 | t;
+                    nq += __popcll(bal);
+                  }
+                  RG(1);
+                  if (nq > V.rq_cap) RG_COUNT(1);
+                  if (nq <= V.rq_cap) {
+                    flat = true;
+                    __syncthreads();
+                    for (int k = tid; k < nq; k += 64) {
+                      const int pid = V.rq[k] >> 4, t = V.rq[k] & 15;
+                      int e, a, b;
+                      decode(c0 + pid, e, a, b);
+                      const int ka = e * NS + a, kb = e * NS + b;
+                      T xa, ya, ha, xb, yb, hb;
+                      pose_at(V.lanes, *V.rt, (int)V.lane[ka], V.ps0[ka], V.v[ka], V.rroad + ka * TTRL_ROUTE_MAX,
+                              V.rlane + ka * TTRL_ROUTE_MAX, (int)V.rn[ka], t, xa, ya, &ha);
+                      pose_at(V.lanes, *V.rt, (int)V.lane[kb], V.ps0[kb], V.v[kb], V.rroad + kb * TTRL_ROUTE_MAX,
+                              V.rlane + kb * TTRL_ROUTE_MAX, (int)V.rn[kb], t, xb, yb, &hb);
+                      const T dx = xb - xa, dy = yb - ya;
+                      if (!(sqrt(dx * dx + dy * dy) > T(P.length)) &&
+                          rects_intersect(xa, ya, ha, xb, yb, hb, T(1.5) * T(P.length), T(0.9) * T(P.width)))
+                        V.rqf[pid] = 1;
+                    }
+                    __syncthreads();
+                    RG(2);
+                    for (int k = tid; k < cn; k += 64) {
+                      if (!V.rqf[k]) continue;
+                      int e, a, b;
+                      decode(c0 + k, e, a, b);
+                      const int ebp = e * NS;
+                      const int qa = V.lanes[V.lane[ebp + a]].prio, qb = V.lanes[V.lane[ebp + b]].prio;
+                      int yv;
+                      if (qa > qb) yv = b;
+                      else if (qa < qb) yv = a;
+                      else {
+                        const int ka = ebp + a, kb = ebp + b;
+                        const T fab = V.ch[ka] * (V.x[kb] - V.x[ka]) + V.sh[ka] * (V.y[kb] - V.y[ka]);
+                        const T fba = V.ch[kb] * (V.x[ka] - V.x[kb]) + V.sh[kb] * (V.y[ka] - V.y[kb]);
+                        yv = fab > fba ? a : b;
+                      }
+                      if (V.kind[ebp + yv] == TTRL_IDM) V.ynew[ebp + yv] = 1;  // ControlledVehicle, not MDPVehicle
+                    }
+                  }
                 }
+                RG(3);
+                if (!flat)
+                  for (int k = tid; k < cn; k += 64) {
+                    int e, a, b;
+                    decode(c0 + k, e, a, b);
+                    reg_pair(e * NS, a, b);
+                  }
+                RG(4);
+                __syncthreads();  // the chunk's flags and queues read before the next chunk rewrites them
+              }
             } else if (doreg) {  // every pair (a < b) once: thread i takes (i, i + d mod NS), d = 1 .. NS/2
               for (int d = 1; d <= NS / 2; ++d) {
                 if (d == NS / 2 && i >= NS / 2) break;
@@ -2651,23 +2768,59 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
         }
         const unsigned long long seg = NS == 64 ? ~0ull : ((1ull << NS) - 1) << ((tid & 63) / NS * NS);
         const unsigned long long below = (1ull << (tid & 63)) - 1;
+        // The pairs within the threshold are queued first (cheap rounds, as many as the busiest
+        // vehicle has pairs), then the separating-axis proofs run one pair per lane in a single
+        // round, so a pile-up's vehicle with many close partners no longer serializes the proofs.
+        const unsigned long long m0 = m;
         int base = 0;  // pairs of this env queued so far
         while (__any(m != 0)) {
-          bool push = false;
+          const bool has = m != 0;
           int j = 0;
-          if (m) {
+          if (has) {
             j = __ffsll((long long)m) - 1;
             m &= m - 1;
-            // pairs the SAT provably separates contribute nothing
-            push = !sat_separated(P, xi, yi, V.ch[me], V.sh[me], vi, V.x[eb + j], V.y[eb + j], V.ch[eb + j],
-                                  V.sh[eb + j], V.v[eb + j], dt);
           }
-          const unsigned long long bal = __ballot(push) & seg;
-          if (push) {
+          const unsigned long long bal = __ballot(has) & seg;
+          if (has) {
             const int q = base + __popcll(bal & below);
             if (q < NS) V.pq_ij[le * NS + q] = pair_pack(i, j, 0);
           }
           base += __popcll(bal);
+        }
+        if (base <= NS) {
+          // the proofs, entry i on lane i; the survivors compacted in place (every lane reads its
+          // entry before any lane writes)
+          bool keep = false;
+          int ij = 0;
+          if (i < base) {
+            ij = V.pq_ij[le * NS + i];
+            const int a = eb + (ij & 0xff), b = eb + ((ij >> 8) & 0xff);
+            // pairs the SAT provably separates contribute nothing
+            keep = !sat_separated(P, V.x[a], V.y[a], V.ch[a], V.sh[a], V.v[a], V.x[b], V.y[b], V.ch[b], V.sh[b],
+                                  V.v[b], dt);
+          }
+          const unsigned long long bal = __ballot(keep) & seg;
+          if (keep) V.pq_ij[le * NS + __popcll(bal & below)] = ij;
+          base = __popcll(bal);
+        } else {  // more close pairs than queue slots: the proofs per vehicle, pushing the survivors
+          m = m0;
+          base = 0;
+          while (__any(m != 0)) {
+            bool push = false;
+            int j = 0;
+            if (m) {
+              j = __ffsll((long long)m) - 1;
+              m &= m - 1;
+              push = !sat_separated(P, xi, yi, V.ch[me], V.sh[me], vi, V.x[eb + j], V.y[eb + j], V.ch[eb + j],
+                                    V.sh[eb + j], V.v[eb + j], dt);
+            }
+            const unsigned long long bal = __ballot(push) & seg;
+            if (push) {
+              const int q = base + __popcll(bal & below);
+              if (q < NS) V.pq_ij[le * NS + q] = pair_pack(i, j, 0);
+            }
+            base += __popcll(bal);
+          }
         }
         if (i == 0) V.pq_n[le] = base;
       } else if (present && do_coll) {
@@ -4892,16 +5045,17 @@ int ttrl_diag_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road, con
 }
 
 #if defined(TTRL_PHASE_TIMING) || defined(TTRL_WAVE_TRACE)
-// Diagnostic build only: read and clear the per-phase cycle sums (25 u64: 20 phases, project_items' 5 steps).
+// Diagnostic build only: read and clear the per-phase cycle sums (PH_SLOTS u64: 20 phases,
+// project_items' 5 steps, the regulation's 5 steps and 2 event counts).
 int ttrl_diag_phase_read(unsigned long long* out) {
-  unsigned long long z[25] = {};
+  unsigned long long z[PH_SLOTS] = {};
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(z)) != hipSuccess) return TTRL_E_LAUNCH;
   return hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) == hipSuccess ? TTRL_OK : TTRL_E_LAUNCH;
 }
-// ... each wave's phase cycles of the last launch (PHASE_TIMING builds): n x 20 u32
+// ... each wave's phase cycles of the last launch (PHASE_TIMING builds): n x 30 u32
 int ttrl_diag_wave_phases(unsigned* out, int n) {
   if (n > WTRACE_MAX) n = WTRACE_MAX;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wphase), sizeof(unsigned) * 20 * n) == hipSuccess ? TTRL_OK
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wphase), sizeof(unsigned) * PH_SLOTS * n) == hipSuccess ? TTRL_OK
                                                                                                   : TTRL_E_LAUNCH;
 }
 // ... and the per-wave trace of the last launch: n x (start, end, hw_id | xcc_id << 32)
