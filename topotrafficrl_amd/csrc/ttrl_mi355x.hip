@@ -2771,7 +2771,7 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
         // The pairs within the threshold are queued first (cheap rounds, as many as the busiest
         // vehicle has pairs), then the separating-axis proofs run one pair per lane in a single
         // round, so a pile-up's vehicle with many close partners no longer serializes the proofs.
-        const unsigned long long m0 = m;
+        // More close pairs than queue slots: pq_n > NS sends the env to pass 3's per-vehicle sweep.
         int base = 0;  // pairs of this env queued so far
         while (__any(m != 0)) {
           const bool has = m != 0;
@@ -2802,25 +2802,6 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
           const unsigned long long bal = __ballot(keep) & seg;
           if (keep) V.pq_ij[le * NS + __popcll(bal & below)] = ij;
           base = __popcll(bal);
-        } else {  // more close pairs than queue slots: the proofs per vehicle, pushing the survivors
-          m = m0;
-          base = 0;
-          while (__any(m != 0)) {
-            bool push = false;
-            int j = 0;
-            if (m) {
-              j = __ffsll((long long)m) - 1;
-              m &= m - 1;
-              push = !sat_separated(P, xi, yi, V.ch[me], V.sh[me], vi, V.x[eb + j], V.y[eb + j], V.ch[eb + j],
-                                    V.sh[eb + j], V.v[eb + j], dt);
-            }
-            const unsigned long long bal = __ballot(push) & seg;
-            if (push) {
-              const int q = base + __popcll(bal & below);
-              if (q < NS) V.pq_ij[le * NS + q] = pair_pack(i, j, 0);
-            }
-            base += __popcll(bal);
-          }
         }
         if (i == 0) V.pq_n[le] = base;
       } else if (present && do_coll) {
@@ -3012,16 +2993,29 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
             if (d2 > (thr + T(1)) * (thr + T(1))) continue;
             if (sqrt(d2) > thr) continue;
             const T ci = V.ch[me], si = V.sh[me], cj = V.ch[eb + j], sj = V.sh[eb + j];
-            // the pair as the reference orders it: a = the lower index
-            const T ax = lo ? xi : xj, ay = lo ? yi : yj, ac = lo ? ci : cj, as = lo ? si : sj, av = lo ? vi : vj;
-            const T bx = lo ? xj : xi, by = lo ? yj : yi, bc = lo ? cj : ci, bs = lo ? sj : si, bv = lo ? vj : vi;
-            if (sat_separated(P, ax, ay, ac, as, av, bx, by, bc, bs, bv, dt)) continue;
-            const SatRes<T> sr = sat_pair_v(P, ax, ay, ac, as, av, bx, by, bc, bs, bv, dt);
-            if (sr.flags & 2) {
-              if (lo) { best_gt = j; gx = sr.tx / T(2); gy = sr.ty / T(2); }
-              else { best_lt = j; lx = -sr.tx / T(2); ly = -sr.ty / T(2); }
+            bool inter, will;
+            T tx, ty;
+            if constexpr (GR) {
+              // the pair as the reference orders it (a = the lower index), one out-of-line call
+              // returning by value: the road-network instance keeps it a call, and out-parameters
+              // of a call would live in scratch
+              const T ax = lo ? xi : xj, ay = lo ? yi : yj, ac = lo ? ci : cj, as = lo ? si : sj, av = lo ? vi : vj;
+              const T bx = lo ? xj : xi, by = lo ? yj : yi, bc = lo ? cj : ci, bs = lo ? sj : si, bv = lo ? vj : vi;
+              if (sat_separated(P, ax, ay, ac, as, av, bx, by, bc, bs, bv, dt)) continue;
+              const SatRes<T> sr = sat_pair_v(P, ax, ay, ac, as, av, bx, by, bc, bs, bv, dt);
+              inter = (sr.flags & 1) != 0; will = (sr.flags & 2) != 0; tx = sr.tx; ty = sr.ty;
+            } else {  // inlined in both orders (the selected operands cost the straight instance a spill)
+              if (lo ? sat_separated(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt)
+                     : sat_separated(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt))
+                continue;
+              if (lo) sat_pair(P, xi, yi, ci, si, vi, xj, yj, cj, sj, vj, dt, inter, will, tx, ty);
+              else sat_pair(P, xj, yj, cj, sj, vj, xi, yi, ci, si, vi, dt, inter, will, tx, ty);
             }
-            if (sr.flags & 1) crash = true;
+            if (will) {
+              if (lo) { best_gt = j; gx = tx / T(2); gy = ty / T(2); }
+              else { best_lt = j; lx = -tx / T(2); ly = -ty / T(2); }
+            }
+            if (inter) crash = true;
           }
         }
         int fl = V.flags[me];
