@@ -144,6 +144,11 @@ def reference_equiv(vehicles: int, seconds_target: float = 10.0, processes: int 
                       f"is not timed: ~2 % of the reference's step), {r['wall_s']:.1f} s wall"}
 
 
+# live vehicle-steps/s of cpu_baseline_ix over the reference IntersectionEnv's own loop, one core each
+# (oracle/time_reference_ix.py, 160 s in alternating rounds; profiles/r06/reference_ix_calibration.txt)
+REFERENCE_RATIO_IX = 371.1
+
+
 def cpu_baseline_ix(seconds_target: float = 10.0) -> dict:
     """The intersection episodes on the float64 C restatement (oracle/), OpenMP over envs: env.step
     = fused frames + shuffled Kinematics + rewards + clear/spawn, with resets (and their 45
@@ -549,9 +554,18 @@ def main():
                                cpu_baseline(N, C["obs"] if C["obs"]["type"] == "Kinematics" else GRID7,
                                             args.cpu_seconds, envs=E, threads=1 if E == 1 else None))
         # beside the C port: the reference's own per-object loop structure (straight highways only;
-        # the intersection's network lanes are not in oracle/objsim.py)
+        # the intersection's network lanes are not in oracle/objsim.py) ...
         out["cpu_baseline"]["reference_equiv"] = (
             None if ix else reference_equiv(N, args.cpu_seconds, processes=1 if E == 1 else None))
+        if ix:  # ... and for the intersection, the port's speed over its calibrated ratio to the reference
+            cb = out["cpu_baseline"]
+            cb["reference_estimate"] = cb["value"] / REFERENCE_RATIO_IX
+            cb["reference_calibration"] = {
+                "ratio_port_to_reference": REFERENCE_RATIO_IX, "cores": cb["cores"],
+                "source": "oracle/time_reference_ix.py, profiles/r06/reference_ix_calibration.txt: the unmodified "
+                          "reference IntersectionEnv (reset + step, shuffled Kinematics) against cpu_baseline_ix, "
+                          "one core each in the build container; the estimate assumes the reference's per-env "
+                          "loop would scale over these cores as the port's OpenMP envs do (one process per core)"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -37,6 +37,10 @@ def test_device_reset_matches_reference_scenes(hip_device):
 
 
 def test_device_episodes_match_reference(hip_device):
+    from test_ix_env_oracle import standstill_links
+    # the ix goldens are the reference env's episodes of seeds 0-5 bit for bit
+    # (test_ix_goldens_equal_the_reference_env): their standstill links come from those fixtures
+    links = [standstill_links(load_golden(golden_files(f"envref_ix_s{e}.npz")[0])) for e in range(len(GOLD))]
     env = VecIntersectionEnv({**ENV_JSON, "num_envs": len(GOLD), "device": hip_device})
     env.reset(seed=0)
     steps = int(GOLD[0]["meta"][1])
@@ -50,7 +54,7 @@ def test_device_episodes_match_reference(hip_device):
             assert abs(float(rew[e]) - d["reward"][p]) <= reward_tol(end, EPISODE_TOL), (e, p)
             assert bool(term[e]) == bool(d["terminated"][p]) and bool(trunc[e]) == bool(d["truncated"][p]), (e, p)
             same_state(env_view(st, e), HostState.from_ix(d, "post", p, pad_to=32), EPISODE_TOL, f"env {e} step {p}",
-                       "device ix episodes from seed")
+                       "device ix episodes from seed", links=links[e][p][1])
         # IntersectionEnv._info (intersection_env.py:120-128): the terms rebuild the reward
         terms = np.stack([info["rewards"][n].cpu().numpy() for n in env.REWARD_TERMS], 1)
         for e in range(len(GOLD)):
@@ -423,8 +427,9 @@ def test_device_episodes_match_the_reference_env(hip_device):
     env.json steps, crashes, arrivals and rejected spawns among them) replayed in one batch from
     their seeds: observation, reward, flags, the info dict, the state after clear / spawn, and
     each env's np_random state word for word after every step."""
-    from test_ix_env_oracle import ENVREF, INFO_TERMS
+    from test_ix_env_oracle import ENVREF, INFO_TERMS, standstill_links
     refs = [load_golden(p) for p in ENVREF]
+    links = [standstill_links(d) for d in refs]  # the vehicles the standstill chaos reaches (CPU)
     E = len(refs)
     env = VecIntersectionEnv({**ENV_JSON, "num_envs": E, "device": hip_device})
     obs, info = env.reset(seed=[int(d["meta"][0]) for d in refs])
@@ -453,7 +458,7 @@ def test_device_episodes_match_the_reference_env(hip_device):
             assert abs(terms[e, 1] - want[3]) <= tol and abs(float(ar[e]) - want[6]) <= tol, (e, p)
             assert bool(at[e]) == bool(want[7]), (e, p)
             same_state(env_view(st, e), HostState.from_ix(d, "post", p, pad_to=32), EPISODE_TOL, f"env {e} step {p}",
-                       "device envref episodes from seed")
+                       "device envref episodes from seed", links=links[e][p][1])
             assert np.array_equal(st["rng"][e], d["rng"][p]), (e, p, "np_random state")
 
 

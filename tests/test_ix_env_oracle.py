@@ -40,6 +40,9 @@ CFG = VecIntersectionEnv.default_config()
 EPISODE_TOL = 1e-4
 STANDSTILL = 0.1
 STANDSTILL_TOL = 1e-2
+# A moving vehicle linked to no such vehicle (standstill_links: none slow so far, no IDM front chain
+# to one) carries only the 1-ulp roundings themselves, compounded over the episode's frames.
+UNLINKED_TOL = 1e-4
 REW = _abi.reward_cfg(-5, 1, [7.0, 9.0], False, False, 13, arrived_reward=1)
 # one step (15 frames) from the reference's own state: the float64 oracle against the reference
 # (the largest differences seen: pose 2.7e-11, steer 8.1e-9 relative on a 0.15 m/s vehicle in
@@ -48,27 +51,43 @@ STEP_TOL = {"x": 1e-9, "y": 1e-9, "heading": 1e-9, "speed": 1e-9, "target_speed"
             "steer": 1e-7, "acc": 1e-9, "delta": 0.0}
 
 
-def same_state(h: HostState, g: HostState, tol, what: str, check: str | None = None, standstill: bool = True):
+def same_state(h: HostState, g: HostState, tol, what: str, check: str | None = None, standstill: bool = True,
+               links: np.ndarray | None = None):
     """Every live vehicle of env 0: discrete fields exact, continuous ones within ``tol`` (a float,
     or a per-field dict) relative; with ``standstill``, a vehicle slower than STANDSTILL is allowed
     STANDSTILL_TOL more on its pose and its steering / acceleration commands are not compared
     (multi-step episodes; one step from the reference's state holds every vehicle alike).
-    ``check`` names the parity_log entry the worst errors go to."""
+    ``links`` (bool per slot of ``g``, standstill_links): the moving vehicles it marks keep ``tol``,
+    every other moving vehicle is held to UNLINKED_TOL.  ``check`` names the parity_log entry the
+    worst errors go to (the linked moving vehicles' under "(linked)", with the slot in ``where``)."""
     n = int((g["kind"] > 0).sum())
     assert int((h["kind"] > 0).sum()) == n, (what, "vehicle count", int((h["kind"] > 0).sum()), n)
     moving = np.abs(g["speed"][:, :n]) >= (STANDSTILL if standstill else 0.0)
+    linked = np.ones_like(moving) if links is None else np.broadcast_to(links[:n], moving.shape)
     if check:
         parity_log.count(check, "slow vehicles", int((~moving).sum()))
+        if links is not None:
+            parity_log.count(check, "linked moving vehicles", int((moving & linked).sum()))
     for k in CONT + ["delta"]:
         err = np.abs(h[k][:, :n] - g[k][:, :n]) / (1 + np.abs(g[k][:, :n]))
         t = tol[k] if isinstance(tol, dict) else tol
-        if k in ("steer", "acc"):
-            err = err[moving]
-        else:
+        if k not in ("steer", "acc"):
             if check:
                 parity_log.note(check + " (slow vehicles)", k, err[~moving], what)
             err = np.where(moving, err, np.maximum(err - STANDSTILL_TOL, 0.0))
-        if check:
+        if links is not None:
+            un = moving & ~linked
+            e_un = np.where(un, err, 0.0)
+            e_ln = np.where(moving & linked, err, 0.0)
+            if check:
+                parity_log.note(check + " (linked)", k, e_ln, f"{what} slot {int(np.argmax(e_ln.max(0)))}")
+                parity_log.note(check, k, e_un, f"{what} slot {int(np.argmax(e_un.max(0)))}")
+            assert np.max(e_un, initial=0.0) <= min(t, UNLINKED_TOL), (what, k, "unlinked", np.max(e_un))
+            if k in ("steer", "acc"):
+                err = np.where(moving, err, 0.0)
+        elif k in ("steer", "acc"):
+            err = err[moving]
+        if check and links is None:
             parity_log.note(check, k, err, what)
         assert np.max(err, initial=0.0) <= t, (what, k, np.max(err, initial=0.0))
     for k in DISC:
@@ -157,16 +176,19 @@ def test_ix_episode_from_seed(path):
     same_state(h, HostState.from_ix(d, "pre", 0, pad_to=32), 1e-9, "reset")
     obs, _ = o.observe_kinematics(h, KIN)
     assert np.max(np.abs(obs[0] - d["obs0"])) <= 1e-6
+    # the reference env's episode of the same seed (test_ix_goldens_equal_the_reference_env)
+    links = standstill_links(load_golden(golden_files(f"envref_ix_s{seed}.npz")[0]))
     for p in range(steps):
         o.simulate(h, [LONGI[int(d["actions"][p])]], 15, 1 / 15)
         end = HostState.from_ix(d, "frame", (p, 14), pad_to=32)
-        same_state(h, end, EPISODE_TOL, f"frames {p}", "oracle ix episode from seed")
+        same_state(h, end, EPISODE_TOL, f"frames {p}", "oracle ix episode from seed", links=links[p][0])
         obs, _ = o.observe_kinematics(h, KIN)
         check_obs(obs[0], d["obs"][p], end, EPISODE_TOL, f"step {p}", "oracle ix episode from seed")
         rew, term, trunc = o.rewards(h, REW, float(p + 1))
         assert abs(rew[0] - d["reward"][p]) <= reward_tol(end, EPISODE_TOL) and term[0] == d["terminated"][p] and trunc[0] == d["truncated"][p]
         o.ix_clear_spawn(h, cfg)
-        same_state(h, HostState.from_ix(d, "post", p, pad_to=32), EPISODE_TOL, f"post {p}", "oracle ix episode from seed")
+        same_state(h, HostState.from_ix(d, "post", p, pad_to=32), EPISODE_TOL, f"post {p}", "oracle ix episode from seed",
+                   links=links[p][1])
 
 
 def test_ix_batch_and_mask():
@@ -292,10 +314,11 @@ def test_reference_env_episode_from_seed(path):
     want = d["info0"]
     got = _info_of(h, comp)
     assert np.allclose(got[[0, 2, 3, 4, 5]], want[[0, 2, 3, 4, 5]], rtol=0, atol=1e-6) and got[1] == want[1]
+    links = standstill_links(d)
     for p in range(steps):
         o.simulate(h, [LONGI[int(d["actions"][p])]], 15, 1 / 15)
         end = HostState.from_ix(d, "end", p, pad_to=32)
-        same_state(h, end, EPISODE_TOL, f"frames {p}", "oracle envref episode from seed")
+        same_state(h, end, EPISODE_TOL, f"frames {p}", "oracle envref episode from seed", links=links[p][0])
         obs, _ = o.observe_kinematics(h, KIN)
         check_obs(obs[0], d["obs"][p], end, EPISODE_TOL, f"step {p}", "oracle envref episode from seed")
         tol = reward_tol(end, EPISODE_TOL)  # the reward and the info terms follow the ego alone
@@ -308,8 +331,60 @@ def test_reference_env_episode_from_seed(path):
         assert abs(got[3] - want[3]) <= tol and got[2] == want[2] and abs(got[6] - want[6]) <= tol, (p, got, want)
         o.ix_clear_spawn(h, cfg)
         same_state(h, HostState.from_ix(d, "post", p, pad_to=32), EPISODE_TOL, f"post {p}",
-                   "oracle envref episode from seed")
+                   "oracle envref episode from seed", links=links[p][1])
         assert np.array_equal(h["rng"][0], d["rng"][p]), (p, "np_random state")
+
+
+def standstill_links(d: dict) -> list:
+    """Per step p of a reference episode, (end, post): the vehicles of its ``end`` state (the frames'
+    result) and of its ``post`` state (after clear / spawn), bool [32] each, whose state
+    may carry the standstill chaos (EPISODE_TOL's comment): a vehicle slower than STANDSTILL at
+    any frame so far, and every vehicle whose IDM front -- Road.neighbour_vehicles on its lane and,
+    while changing lane, on its target lane (behavior.py:110-131, road.py:480-513) -- carries it
+    at some frame: its acceleration reads that front's position and speed continuously (the
+    interaction term of acceleration, behavior.py:183-190), and a follower's follower in turn.
+    Each step is replayed on the float64 oracle frame by frame from the reference's own ``pre``
+    state (within STEP_TOL of the reference), so the links are the reference's; clears keep list
+    order and spawns append untainted vehicles."""
+    net = intersection_network()
+    o = Oracle(net.table, P_IX)
+    cfg = ix_cfg(net, CFG, P_IX)
+    taint = np.zeros(32, dtype=bool)  # slots of the state entering the step
+    out = []
+    for p in range(int(d["meta"][1])):
+        h = ref_step_input(d, p)
+        n = int((h["kind"][0] > 0).sum())
+
+        def spread():
+            live = h["kind"][0] > 0
+            taint[:] |= live & (np.abs(h["speed"][0]) < STANDSTILL)
+            fr, _ = o.neighbours(h)
+            ft, _ = o.neighbours(h, h["target_lane"])
+            fr, ft = fr[0], ft[0]
+            for _ in range(n):
+                t2 = taint | (live & (fr >= 0) & taint[np.maximum(fr, 0)]) | \
+                    (live & (h["lane"][0] != h["target_lane"][0]) & (ft >= 0) & taint[np.maximum(ft, 0)])
+                if np.array_equal(t2, taint):
+                    break
+                taint[:] = t2
+
+        spread()
+        for f in range(15):
+            o.simulate(h, [LONGI[int(d["actions"][p])]] if f == 0 else None, 1, 1 / 15)
+            spread()
+        at_end = taint.copy()
+        end_xy = np.stack([h["x"][0, :n], h["y"][0, :n]], 1)
+        o.observe_kinematics(h, KIN)  # the shuffle's draws precede the spawn's
+        o.ix_clear_spawn(h, cfg)
+        post = HostState.from_ix(d, "post", p, pad_to=32)
+        m = int((post["kind"][0] > 0).sum())
+        nxt = np.zeros(32, dtype=bool)
+        for j in range(m):  # a kept vehicle has not moved; a spawned one matches nothing
+            hit = np.flatnonzero((end_xy[:, 0] == post["x"][0, j]) & (end_xy[:, 1] == post["y"][0, j]))
+            nxt[j] = bool(hit.size) and bool(taint[hit[0]])
+        taint = nxt
+        out.append((at_end, taint.copy()))
+    return out
 
 
 def ref_step_input(d: dict, p: int, pad_to: int = 32) -> HostState:

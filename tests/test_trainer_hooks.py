@@ -1,6 +1,7 @@
 """BatchedEvaluation keeps the reference trainer's hook names and call order
 (Evaluation.step evaluation.py:163-194, reset :372-376, run_episodes :139-161).
 A recording fake env/agent (CPU, duck-typed) captures the trace."""
+import pytest
 import torch
 
 from topotrafficrl_amd.agent import EgoAttentionNetwork
@@ -105,3 +106,22 @@ def test_evaluation_keys_exploration_on_the_env_shard():
     assert agent.policy.env_id_offset == 0
     BatchedEvaluation(ShardEnv(), agent, num_episodes=1, sim_seed=0)
     assert agent.policy.env_id_offset == 8192
+
+
+def test_evaluation_keeps_an_explicit_agent_offset():
+    """An offset given to the agent explicitly survives an env left at offset 0 (with a warning),
+    and a different non-zero env offset is an error rather than a silent override."""
+    from topotrafficrl_amd.trainer import BatchedDQNAgent
+
+    class Env:
+        def __init__(self, off):
+            self.config = {"env_id_offset": off}
+
+    agent = BatchedDQNAgent("cpu", n_actions=3, env_id_offset=4096)
+    with pytest.warns(UserWarning):
+        BatchedEvaluation(Env(0), agent, num_episodes=1, sim_seed=0)
+    assert agent.policy.env_id_offset == 4096
+    BatchedEvaluation(Env(4096), agent, num_episodes=1, sim_seed=0)
+    assert agent.policy.env_id_offset == 4096
+    with pytest.raises(ValueError):
+        BatchedEvaluation(Env(8192), agent, num_episodes=1, sim_seed=0)

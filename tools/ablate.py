@@ -18,7 +18,7 @@ VARIANTS = {"full": 0, "no_coll": 1, "no_mobil": 2, "no_abort": 4, "no_scan": 8,
 
 def main(E=4096, N=64, rounds=5):
     # the ablation bits are compiled in only with -DTTRL_DIAG_ABLATE (tools/variants.py build)
-    lib = _lib.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_variants", "lib_ablate.so"))
+    lib = _lib.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_ab", "lib_ablate.so"))
     fn = lib.ttrl_diag_simulate
     fn.argtypes = [C.c_void_p] * 4 + [C.c_int32, C.c_double, C.c_int32, C.c_void_p]
     fn.restype = C.c_int

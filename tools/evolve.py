@@ -18,7 +18,7 @@ def main(dtype="f64", steps=40):
     env.reset(seed=12345)
     g = torch.Generator(device=dev).manual_seed(1000)
     # the ablation bits are compiled in only with -DTTRL_DIAG_ABLATE (tools/variants.py build)
-    lib = _lib.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_variants", "lib_ablate.so"))
+    lib = _lib.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_ab", "lib_ablate.so"))
     fn = lib.ttrl_diag_simulate
     fn.argtypes = [C.c_void_p] * 4 + [C.c_int32, C.c_double, C.c_int32, C.c_void_p]
     stream = torch.cuda.current_stream(dev).cuda_stream

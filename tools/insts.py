@@ -5,7 +5,7 @@ One-frame launches from the same mid-episode 4096 x 64 state, each with one phas
 full launch's is that phase's share of the frame (within one frame the ablation barely changes the
 work of the later phases: vehicles already changing lane keep changing, and so on).
 
-  python3 tools/variants.py build    # here: tools/_variants/lib_ablate.so (-DTTRL_DIAG_ABLATE)
+  python3 tools/variants.py build    # here: tools/_ab/lib_ablate.so (-DTTRL_DIAG_ABLATE)
   rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv \
       -d gpurun_out/insts -o insts -- python3 tools/insts.py
   python3 tools/insts.py --report gpurun_out/insts/insts_counter_collection.csv
@@ -30,7 +30,7 @@ def run(E=4096, N=64, frames=1):
     from topotrafficrl_amd.road import RoadNetwork
     from topotrafficrl_amd.state import BatchState
     # the ablation bits are compiled in only with -DTTRL_DIAG_ABLATE (tools/variants.py build)
-    lib = _lib.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_variants", "lib_ablate.so"))
+    lib = _lib.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_ab", "lib_ablate.so"))
     fn = lib.ttrl_diag_simulate
     fn.argtypes = [C.c_void_p] * 4 + [C.c_int32, C.c_double, C.c_int32, C.c_void_p]
     dev = torch.device("cuda:0")

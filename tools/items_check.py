@@ -1,4 +1,4 @@
-"""Debug: run ONE fused simulate launch of a variant library (tools/_variants/lib_<name>.so) on an
+"""Debug: run ONE fused simulate launch of a variant library (tools/_ab/lib_<name>.so) on an
 intersection batch reset by the default library; its device printf reports any mismatch."""
 import ctypes as C
 import os
@@ -14,7 +14,7 @@ from topotrafficrl_amd.intersection import VecIntersectionEnv  # noqa: E402
 
 
 def main(name, frames):
-    lib = _lib.load(os.path.join(ROOT, "tools", "_variants", f"lib_{name}.so"))
+    lib = _lib.load(os.path.join(ROOT, "tools", "_ab", f"lib_{name}.so"))
     lib.ttrl_simulate.argtypes = [C.c_void_p] * 4 + [C.c_int32, C.c_double, C.c_void_p]
     for dtype in ("f64", "f32"):
         env = VecIntersectionEnv({"num_envs": 256, "device": "cuda:0", "dtype": dtype, "auto_reset": False})

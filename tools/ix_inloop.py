@@ -5,7 +5,7 @@ then, on snapshots of the in-loop state with no side-stream work pending, times
   * the fused simulate launch alone (ttrl_simulate, 15 frames),
   * the env.step launch (simulate + shuffled Kinematics observation + step tail; ttrl_env_step),
   * a fresh-reset scene's simulate launch (the 0.36 ms of profiles/r03/r03n),
-and, with the phase-timing build (tools/_variants/lib_timing.so, -DTTRL_PHASE_TIMING), the per-phase
+and, with the phase-timing build (tools/_ab/lib_timing.so, -DTTRL_PHASE_TIMING), the per-phase
 cycles per wave of the in-loop simulate launch, plus the live-vehicle count distribution.
 
   python tools/ix_inloop.py [steps]
@@ -77,7 +77,7 @@ def main(steps=30):
     t_step = float(np.median(reps[1:]))
     print(f"simulate launch: in-loop {t_in:.3f} ms, fresh reset {t_fresh:.3f} ms; env_step launch (obs + tail) "
           f"in-loop {t_step:.3f} ms", flush=True)
-    lib_path = os.path.join(ROOT, "tools", "_variants", "lib_timing.so")
+    lib_path = os.path.join(ROOT, "tools", "_ab", "lib_timing.so")
     if not os.path.exists(lib_path):
         return
     lib = _lib.load(lib_path)

@@ -42,9 +42,9 @@ def main():
 
 if __name__ == "__main__":
     if len(sys.argv) > 1:  # a variant build (tools/variants.py)
-        lib = _lib.load(os.path.join(ROOT, "tools", "_variants", f"lib_{sys.argv[1]}.so"))
+        lib = _lib.load(os.path.join(ROOT, "tools", "_ab", f"lib_{sys.argv[1]}.so"))
         if len(sys.argv) > 2 and sys.argv[2] == "step-only":
-            _lib._lib = _lib.load(os.path.join(ROOT, "tools", "_variants", "lib_head.so"))
+            _lib._lib = _lib.load(os.path.join(ROOT, "tools", "_ab", "lib_head.so"))
             STEP_LIB = lib
         else:
             _lib._lib = lib

@@ -76,7 +76,7 @@ def main(steps=30):
     sink = torch.zeros(max(n_occ, 1), dtype=torch.int32, device=dev)
     if n_occ:
         import ctypes
-        occ_lib = ctypes.CDLL(os.path.join(ROOT, "tools", "_variants", "occupy.so"))
+        occ_lib = ctypes.CDLL(os.path.join(ROOT, "tools", "_ab", "occupy.so"))
         occ_lib.occupy.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p]
         print(f"instead: {n_occ} idle one-wave workgroups on the side stream")
 

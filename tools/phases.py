@@ -28,7 +28,7 @@ def main(dtype="f64", steps=30, frames=15, ix=False, E=4096):
     env.reset(seed=12345)
     n_act = env.action_space.n
     g = torch.Generator(device=dev).manual_seed(1000)
-    lib = _lib.load(os.path.join(ROOT, "tools", "_variants", os.environ.get("TIMING_LIB", "lib_timing.so")))
+    lib = _lib.load(os.path.join(ROOT, "tools", "_ab", os.environ.get("TIMING_LIB", "lib_timing.so")))
     sim = lib.ttrl_simulate
     sim.argtypes = [C.c_void_p] * 4 + [C.c_int32, C.c_double, C.c_void_p]
     rd = lib.ttrl_diag_phase_read

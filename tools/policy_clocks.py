@@ -1,6 +1,6 @@
 """Per-phase shader clocks of the fused EgoAttention kernel (diagnostic).
 
-  python3 tools/policy_clocks.py --build      # here: tools/_variants/lib_polclk.so (-DTTRL_POL_CLOCKS)
+  python3 tools/policy_clocks.py --build      # here: tools/_ab/lib_polclk.so (-DTTRL_POL_CLOCKS)
   python3 tools/policy_clocks.py [B]          # GPU box: one launch at batch B, phase medians / p95
 """
 import ctypes as C
@@ -10,7 +10,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-LIB = os.path.join(ROOT, "tools", "_variants", "lib_polclk.so")
+LIB = os.path.join(ROOT, "tools", "_ab", "lib_polclk.so")
 PHASES = ["obs staging", "ego embedding", "query", "qk_h", "entity-loop weights", "entities", "Wv + Wc",
           "output MLP"]
 

@@ -1,4 +1,4 @@
-"""Phase clocks of reset_wave_kernel (build: -DTTRL_RESET_TRACE into tools/_variants/lib_rtrace.so,
+"""Phase clocks of reset_wave_kernel (build: -DTTRL_RESET_TRACE into tools/_ab/lib_rtrace.so,
 then copy it over lib/libttrl_mi355x.so on the GPU box): one full reset of 4096 x 64 envs, then a
 masked one of every 8th env."""
 import os

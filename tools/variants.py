@@ -1,6 +1,6 @@
 """Build (here) and time (on the GPU) compile-time variants of the fused kernel, interleaved in one process.
 
-  python tools/variants.py build          # cross-compile variants into tools/_variants/
+  python tools/variants.py build          # cross-compile variants into tools/_ab/
   python tools/variants.py run [f64 f32]  # on the GPU box
 """
 import ctypes as C
@@ -10,7 +10,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-OUT = os.path.join(ROOT, "tools", "_variants")
+OUT = os.path.join(ROOT, "tools", "_ab")  # scratch: git-ignored, travels to the box; remove after use
 VARIANTS = {"head": [], "cur": []}  # committed kernel vs working tree, tuned defaults
 # built, not timed: tools/phases.py (timing, wtrace); tools/ablate.py, insts.py, evolve.py (ablate: the
 # phase-ablation bits of ttrl_diag_simulate exist only in -DTTRL_DIAG_ABLATE builds)

@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "ttrl_mi355x.h"
 #include "ttrl_math.h"
 
@@ -1435,9 +1437,11 @@ __device__ TTRL_ITEMS_ATTR int project_items(const View<T>& V, const PP& P, int 
   }
   }  // !pruned
   PJ(3);
-  // the list lengths, one thread per (lane, env)
-  if (tid < nl * EPW) {
-    const int l = tid / EPW, e = tid - l * EPW;
+  // the list lengths, one (lane, env) item per thread and round: nl * EPW may exceed the wavefront
+  // (the deleted 16-slot, four-envs-per-wave instance at 20 lanes had 80 items, and a single
+  // `tid < nl * EPW` round left lanes 16-19 with the previous frame's counts: DESIGN §3, r05e)
+  for (int t = tid; t < nl * EPW; t += 64) {
+    const int l = t / EPW, e = t - l * EPW;
     const int c = __popcll((V.onm[l] >> (e * NS)) & SEG);
     V.cnt[e * (LMAX + 1) + l] = c;
     atomicMax(&V.cnt[e * (LMAX + 1) + LMAX], c);
@@ -4828,15 +4832,24 @@ bool tail_fits(const ViewLayout& o, int EPW, int NS) {
   return o.afree + need <= o.item + sizeof(short) * 2 * M;
 }
 
-// SIMDs of the current device (4 per CU on CDNA), cached per device id.
-int simds_of_current_device() {
-  static int cache[16] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 1024;
-  if (dev < 16 && cache[dev]) return cache[dev];
+// SIMDs (4 per CU on CDNA) of the device the launch stream belongs to (the null stream: the
+// current device), cached per device id; the cache is atomic, so host threads driving different
+// devices may launch concurrently.
+int simds_of_stream_device(hipStream_t stream) {
+  static std::atomic<int> cache[16];
+  int dev = -1;
+  if (stream) {
+    hipDevice_t d = -1;
+    if (hipStreamGetDevice(stream, &d) == hipSuccess) dev = d;
+  }
+  if (dev < 0 && (hipGetDevice(&dev) != hipSuccess || dev < 0)) return 1024;
+  if (dev < 16) {
+    const int c = cache[dev].load(std::memory_order_relaxed);
+    if (c) return c;
+  }
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  if (dev < 16) cache[dev] = 4 * cus;
+  if (dev < 16) cache[dev].store(4 * cus, std::memory_order_relaxed);
   return 4 * cus;
 }
 
@@ -4863,7 +4876,7 @@ int launch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_par
   const ParamsT<T> PT = params_for<T>(P);
   if constexpr (NS == 32 && EPW == 2) {
     // every wave resident at 2 per SIMD: the 2-wave register budget (no spills) costs no occupancy
-    if (!graph && !curved && blocks <= 2 * simds_of_current_device()) {
+    if (!graph && !curved && blocks <= 2 * simds_of_stream_device(stream)) {
       hipLaunchKernelGGL((simulate_kernel<T, NS, EPW, NET_STRAIGHT, 2>), dim3(blocks), dim3(NS * EPW), lds, stream,
                          s, R, PT, actions, mask, frames, dt, mode, ablate, ob);
       return launch_status();

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import logging
 import time
+import warnings
 from pathlib import Path
 
 import numpy as np
@@ -110,8 +111,17 @@ class BatchedEvaluation:
         if hasattr(agent, "set_writer"):
             agent.set_writer(writer)
         if isinstance(getattr(agent, "policy", None), EgoAttentionPolicy) and hasattr(env, "config"):
-            # the env's global ids (a data-parallel rank's shard): exploration keyed on them
-            agent.policy.env_id_offset = int(env.config.get("env_id_offset", 0))
+            # the env's global ids (a data-parallel rank's shard): exploration keyed on them.  An
+            # offset given to the agent explicitly is kept: an env left at offset 0 does not reset it,
+            # and a different non-zero env offset is a conflict, not a silent override
+            env_off = int(env.config.get("env_id_offset", 0) or 0)
+            agent_off = int(agent.policy.env_id_offset)
+            if agent_off == 0:
+                agent.policy.env_id_offset = env_off
+            elif env_off not in (0, agent_off):
+                raise ValueError(f"the agent's env_id_offset {agent_off} conflicts with the env's {env_off}")
+            elif env_off == 0:
+                warnings.warn(f"keeping the agent's env_id_offset {agent_off} (the env's config has 0)")
         agent.evaluation = self
 
     # evaluation.py:115-121
