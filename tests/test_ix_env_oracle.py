@@ -41,8 +41,12 @@ EPISODE_TOL = 1e-4
 STANDSTILL = 0.1
 STANDSTILL_TOL = 1e-2
 # A moving vehicle linked to no such vehicle (standstill_links: none slow so far, no IDM front chain
-# to one) carries only the 1-ulp roundings themselves, compounded over the episode's frames.
-UNLINKED_TOL = 1e-4
+# to one) carries only the 1-ulp roundings themselves, compounded over the episode's frames: on the
+# MI355X (and the oracle alike) at most 2.2e-6 (y), 1.1e-6 (acc) over the 18 reference episodes
+# (profiles/r06/r06a_parity.json), so 10x that.  The linked moving vehicles keep EPISODE_TOL: the
+# worst is 5.0e-5 (acc, envref_ix_s12 step 11, slot 7, whose IDM front chain reaches a vehicle at
+# 0.006 m/s).
+UNLINKED_TOL = 2e-5
 REW = _abi.reward_cfg(-5, 1, [7.0, 9.0], False, False, 13, arrived_reward=1)
 # one step (15 frames) from the reference's own state: the float64 oracle against the reference
 # (the largest differences seen: pose 2.7e-11, steer 8.1e-9 relative on a 0.15 m/s vehicle in
