@@ -363,7 +363,9 @@ def main():
     if ix:
         from topotrafficrl_amd.intersection import VecIntersectionEnv
         env = VecIntersectionEnv({"num_envs": E, "vehicle_slots": N, "observation": C["obs"], "device": str(dev),
-                                  "dtype": args.dtype, "env_id_offset": offset, "auto_reset": True})
+                                  "dtype": args.dtype, "env_id_offset": offset, "auto_reset": True,
+                                  # A/B only: TTRL_IX_FUSE_TAIL=0 runs the two-launch step (same results)
+                                  "fuse_tail": os.environ.get("TTRL_IX_FUSE_TAIL", "1") != "0"})
     else:
         env = VecHighwayEnv({"num_envs": E, "vehicles_count": N, "observation": C["obs"], "device": str(dev),
                              "dtype": args.dtype, "env_id_offset": offset, "auto_reset": bool(args.auto_reset)})

@@ -276,6 +276,45 @@ def test_overlapped_resets_equal_in_place_resets(duration, dtype, streams, slots
     assert bool((w[:-1] >= w[1:]).all()), w
 
 
+@pytest.mark.parametrize("duration,dtype,init,slots", [(1, "f64", 10, 32), (3, "f64", 10, 32), (4, "f64", 16, 32),
+                                                      (4, "f32", 16, 32), (3, "f64", 10, 64), (5, "f64", 16, 20)])
+def test_fused_tail_equals_the_separate_tail(duration, dtype, init, slots, hip_device):
+    """fuse_tail (ttrl_ix_env_step: the envs that go on run _clear_vehicles / _spawn_vehicle inside
+    the step launch, from its LDS rows; ix_step_tail_(cleared=True) swaps in the finished envs'
+    spare scenes) against the two-launch step (ttrl_env_step, then ix_step_tail_'s clear / spawn):
+    observations, rewards, flags, the info terms, the final observation, every state field, every
+    np_random, the live-vehicle counter and the next dispatch order, bit for bit, step by step
+    (duration 1: every env finishes every step; 20 slots: rows narrower than the 32 lanes of
+    their half-wave; 64: one env per wavefront; init 16: dense scenes, full rows)."""
+    cfg = {**ENV_JSON, "num_envs": 40, "device": hip_device, "auto_reset": True, "duration": duration,
+           "dtype": dtype, "vehicle_slots": slots, "initial_vehicle_count": init}
+    a = VecIntersectionEnv({**cfg, "fuse_tail": True})
+    b = VecIntersectionEnv({**cfg, "fuse_tail": False})
+    for e in (a, b):
+        e.live_counter = torch.zeros((), dtype=torch.int64, device=hip_device)
+    oa, _ = a.reset(seed=31)
+    ob, _ = b.reset(seed=31)
+    assert torch.equal(oa, ob)
+    g = torch.Generator(device=hip_device).manual_seed(4)
+    spawned = 0
+    for t in range(10):
+        act = torch.randint(0, 3, (40,), device=hip_device, generator=g)
+        before = int((b.state["kind"] != 0).sum())
+        ra, rb = a.step(act), b.step(act)
+        for x, y in zip(ra[:4], rb[:4]):
+            assert torch.equal(x, y), t
+        for k in ("final_observation", "final_mask", "speed", "crashed"):
+            assert torch.equal(ra[4][k], rb[4][k]), (t, k)
+        for k in ra[4]["rewards"]:
+            assert torch.equal(ra[4]["rewards"][k], rb[4]["rewards"][k]), (t, k)
+        for k in a.state.t:
+            assert torch.equal(a.state[k], b.state[k]), (t, k)
+        assert torch.equal(a._order[:40], b._order[:40]), t
+        assert int(a.live_counter) == int(b.live_counter), t
+        spawned += int((b.state["kind"] != 0).sum()) - before
+    assert spawned != 0
+
+
 @pytest.mark.parametrize("E", [64, 63])
 def test_dispatch_order_leaves_results_unchanged(E, hip_device):
     """The step launch's dispatch order (workgroup slot -> env) changes only which workgroup runs an

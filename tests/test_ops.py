@@ -15,7 +15,7 @@ LANES = ops.struct_tensor(_abi.straight_lane_table(4))
 PARAMS = ops.struct_tensor(_abi.default_params())
 MUTATES = {"simulate_", "road_act_", "road_step_", "meta_action_", "env_step_", "kinematics_obs",
            "kinematics_obs_masked_", "reset_highway_", "reset_highway_seeded_", "auto_reset_highway_", "ix_reset_",
-           "ix_reset_parts_", "ix_clear_spawn_", "ix_step_tail_", "copy_envs_"}
+           "ix_reset_parts_", "ix_clear_spawn_", "ix_step_tail_", "ix_env_step_", "copy_envs_"}
 
 
 def test_every_device_entry_point_is_an_operator():
@@ -29,6 +29,7 @@ def test_every_device_entry_point_is_an_operator():
                           "auto_reset_highway_": "auto_reset_highway", "ix_reset_": "ix_reset",
                           "ix_reset_parts_": "ix_reset_parts",
                           "ix_clear_spawn_": "ix_clear_spawn", "ix_step_tail_": "ix_step_tail",
+                          "ix_env_step_": "ix_env_step",
                           "copy_envs_": "copy_envs", "rewards": "rewards",
                           "rewards_ex": "rewards_ex", "rewards_step_": "rewards_step",
                           "ego_attention_q": "ego_attention_q", "ego_attention_act": "ego_attention_act"}[o]
@@ -47,7 +48,7 @@ def test_schemas_declare_mutation(name):
 
 
 def test_time_is_mutated_by_the_step_ops():
-    for name in ("env_step_", "rewards_step_", "auto_reset_highway_", "ix_step_tail_"):
+    for name in ("env_step_", "rewards_step_", "auto_reset_highway_", "ix_step_tail_", "ix_env_step_"):
         s = getattr(torch.ops.ttrl, name).default._schema
         t = [a for a in s.arguments if a.name == "time"][0]
         assert t.alias_info is not None and t.alias_info.is_write
@@ -332,6 +333,67 @@ def test_intersection_ops_equal_the_c_abi(hip_device):
     torch.cuda.synchronize()
     _equal(e, f)
     assert lib.ttrl_ix_reset_parts(_c(f), R, P, IX, 8, None, 0, None, None, 0, None, _stream()) == -1
+
+
+@pytest.mark.gpu
+def test_ix_env_step_op_equals_the_c_abi(hip_device):
+    """ttrl::ix_env_step_ and ttrl::ix_step_tail_(cleared=True) against direct ctypes calls of
+    ttrl_ix_env_step and ttrl_ix_step_tail(cleared = 1), on copies of in-loop intersection scenes
+    whose clocks put some envs at their last step (terminated / truncated ones swap in spares)."""
+    from topotrafficrl_amd.intersection import VecIntersectionEnv
+    env = VecIntersectionEnv({"num_envs": 32, "device": hip_device, "auto_reset": True, "duration": 3})
+    env.reset(seed=3)
+    g = torch.Generator(device=hip_device).manual_seed(1)
+    for _ in range(2):
+        env.step(torch.randint(0, 3, (32,), device=hip_device, generator=g))
+    env._join_sides()
+    torch.cuda.synchronize()
+    lib = _lib.load()
+    lanes, params, cfg = ops.st(env.network.table), ops.st(env.params), ops.st(env.ix)
+    R, P, IX = C.byref(env.network.table), C.byref(env.params), C.byref(env.ix)
+    kin = env.observation_type.fused_cfg()
+    rc = env.reward_cfg
+    act = torch.randint(0, 3, (32,), device=hip_device, generator=g, dtype=torch.int32)
+    a, b = env.state.clone(), env.state.clone()
+    sa, sb = env._spare.clone(), env._spare.clone()
+    ta, tb = env.time.clone(), env.time.clone()
+    oa, ob = env._order.clone(), env._order.clone()
+    la, lb = torch.zeros((), dtype=torch.int64, device=hip_device), torch.zeros((), dtype=torch.int64, device=hip_device)
+    pa, pb = env._spare_par.clone(), env._spare_par.clone()
+    ea, eb = env._entropy.clone(), env._entropy.clone()
+    fa, fb = env._spare_ent.clone(), env._spare_ent.clone()
+    codes = env.action_type._codes(act).to(torch.int32)
+    outs = torch.ops.ttrl.ix_env_step_(a.tensors(), lanes, params, cfg, codes, 15, 1 / 15, ops.kin_cfg_tensor(kin),
+                                       ops.st(rc), ta, 1.0, oa, None, la)
+    tail = torch.ops.ttrl.ix_step_tail_(a.tensors(), lanes, params, cfg, sa.tensors(), outs[3], outs[4], pa, ea, fa, ta,
+                                        ops.kin_cfg_tensor(kin), outs[8], outs[9], la, oa, cleared=True)
+    E, V, F = 32, kin.vehicles_count, kin.n_features
+    o = [torch.empty(E, V, F, device=hip_device), torch.empty(E, V - 1, dtype=torch.int32, device=hip_device),
+         torch.empty(E, device=hip_device), torch.empty(E, dtype=torch.bool, device=hip_device),
+         torch.empty(E, dtype=torch.bool, device=hip_device), torch.empty(E, 4, device=hip_device),
+         torch.empty(E, dtype=torch.float64, device=hip_device), torch.empty(E, dtype=torch.bool, device=hip_device),
+         torch.empty(E, V, F, device=hip_device), torch.empty(E, V - 1, dtype=torch.int32, device=hip_device)]
+    KC = kin
+    assert lib.ttrl_ix_env_step(_c(b), R, P, IX, codes.data_ptr(), 15, 1 / 15, C.byref(KC), o[0].data_ptr(),
+                                o[1].data_ptr(), o[8].data_ptr(), o[9].data_ptr(), C.byref(rc), tb.data_ptr(), 1.0,
+                                o[2].data_ptr(), o[3].data_ptr(), o[4].data_ptr(), o[5].data_ptr(), o[6].data_ptr(),
+                                o[7].data_ptr(), ob.data_ptr(), None, 0, lb.data_ptr(), _stream()) == 0
+    done = torch.empty(E, dtype=torch.bool, device=hip_device)
+    smask = torch.empty(sb.n_envs, dtype=torch.uint8, device=hip_device)
+    assert lib.ttrl_ix_step_tail(_c(b), R, P, IX, _c(sb), o[3].data_ptr(), o[4].data_ptr(), pb.data_ptr(),
+                                 eb.data_ptr(), fb.data_ptr(), eb.shape[1], tb.data_ptr(), done.data_ptr(),
+                                 smask.data_ptr(), C.byref(KC), None, o[8].data_ptr(), None, o[9].data_ptr(),
+                                 lb.data_ptr(), ob.data_ptr(), 1, _stream()) == 0
+    torch.cuda.synchronize()
+    for x, y in zip(outs, o):
+        assert torch.equal(x, y)
+    assert torch.equal(tail[0], done) and torch.equal(tail[1], smask)
+    assert tail[2].data_ptr() == outs[8].data_ptr()  # written in place
+    _equal(a, b)
+    _equal(sa, sb)
+    for x, y in ((ta, tb), (oa, ob), (la, lb), (pa, pb), (ea, eb), (fa, fb)):
+        assert torch.equal(x, y)
+    assert bool(done.any())  # truncations at time 3 (and any crashes): spares swapped in
 
 
 @pytest.mark.gpu

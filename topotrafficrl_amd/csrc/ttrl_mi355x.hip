@@ -1797,7 +1797,8 @@ __device__ __forceinline__ void kin_observe(const ttrl_state_t& st, const LaneT<
                                             const ttrl_kin_cfg_t& cfg, bool env_ok, int env, T x, T y, T h, T v,
                                             T hc, T hs, int lane, bool present, bool mdp, EgoFn ego_of, T* s_key,
                                             int* s_cnt, int* s_ego, int (*s_perm)[64], int (*s_p)[64],
-                                            float* __restrict__ out, int32_t* __restrict__ ids);
+                                            float* __restrict__ out, int32_t* __restrict__ ids,
+                                            float* __restrict__ out2 = nullptr, int32_t* __restrict__ ids2 = nullptr);
 template <typename T>
 __device__ __forceinline__ void step_tail(const ttrl_lane_table_t& R, const LaneT<T>* L, const ttrl_reward_cfg_t& cfg,
                                           int env, bool has_ego, T x, T y, T v, int l, bool crashed, T v0,
@@ -1852,17 +1853,36 @@ template <bool L, typename T> struct Own {
   }
 };
 
+// ttrl_ix_env_step: IntersectionEnv.step's tail (_clear_vehicles, _spawn_vehicle;
+// intersection_env.py:135-139, 320-362) fused into the step launch for the envs that go on
+// (neither terminated nor truncated), on their LDS rows after the step tail (ix_epilogue).  The
+// finished envs are left to ttrl_ix_step_tail (cleared = 1), which swaps in their spare scenes.
+struct IxEpi {
+  ttrl_ix_cfg_t C;
+  double lane_change_delay;  // ttrl_params_t's, float64 as in the scene kernels (a spawn's IDM timer)
+  float* obs2;               // [E, V, F]: an env that goes on keeps the step's observation as its next
+  int32_t* ids2;             // [E, V - 1] (or null)
+  unsigned long long* live;  // optional: += the vehicles present after the tail
+  int32_t* live_env;         // optional [E]: each env's vehicles present after the tail (ix_order_kernel)
+};
+
+template <typename T, int NS, int EPW>
+__device__ __forceinline__ void ix_epilogue(const View<T>& V, const ttrl_state_t& st, const ttrl_lane_table_t& R,
+                                            const ParamsT<T>& P, const StepOut& so, const IxEpi& ie, int le, int i,
+                                            int env, bool env_on, bool slot, size_t k, int me, int eb, int reg,
+                                            T& timer, T& steer, T& acc, T& ix, T& iy, int& sidx);
+
 // Fused frame loop.  EPW envs per workgroup, NS slots per env, blockDim = EPW*NS.  The whole
 // vehicle state of the workgroup's envs is resident in LDS for the launch (HBM is read once
 // and written once); each phase loads the few fields it needs into registers, so no state is
 // live across phases and the kernel runs at high occupancy without spilling.  The workgroup
 // takes the envs of slots [q0, q0 + EPW) (below qend) of the dispatch order (simulate_kernel:
-// q0 = blockIdx.x * EPW, qend = n_envs).
-template <typename T, int NS, int EPW, int NET>
+// q0 = blockIdx.x * EPW, qend = n_envs).  IX: the epilogue is ix_epilogue (ie).
+template <typename T, int NS, int EPW, int NET, bool IX = false>
 __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state_t& st, const ttrl_lane_table_t& R,
                                               const ParamsT<T>& P, const int32_t* __restrict__ actions,
                                               const uint8_t* __restrict__ env_mask, int frames, double dt_d, int mode,
-                                              int ablate_arg, const StepOut& so);
+                                              int ablate_arg, const StepOut& so, const IxEpi* ie = nullptr);
 
 template <typename T, int NS, int EPW, int NET, int WB = 0>
 // Waves per SIMD the register budget is sized for: 4 on the straight highway (its compile-time
@@ -1882,11 +1902,20 @@ simulate_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_
                                  ablate_arg, so);
 }
 
-template <typename T, int NS, int EPW, int NET>
+// ttrl_ix_env_step: the road-network instance with IntersectionEnv.step's tail fused (IxEpi)
+template <typename T, int NS, int EPW>
+__global__ void __launch_bounds__(NS* EPW, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES : 2)
+simulate_ix_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_t* __restrict__ actions,
+                   int frames, double dt_d, StepOut so, IxEpi ie) {
+  simulate_body<T, NS, EPW, NET_GRAPH, true>((int)blockIdx.x * EPW, st.n_envs, st, R, P, actions, nullptr, frames,
+                                             dt_d, MODE_META | MODE_ACT | MODE_STEP, 0, so, &ie);
+}
+
+template <typename T, int NS, int EPW, int NET, bool IX>
 __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state_t& st, const ttrl_lane_table_t& R,
                                               const ParamsT<T>& P, const int32_t* __restrict__ actions,
                                               const uint8_t* __restrict__ env_mask, int frames, double dt_d, int mode,
-                                              int ablate_arg, const StepOut& so) {
+                                              int ablate_arg, const StepOut& so, const IxEpi* ie) {
   // The diagnostic phase ablations (ttrl_diag_simulate) exist only in -DTTRL_DIAG_ABLATE builds: as a
   // run-time argument their ~20 tests held SGPR masks for the whole launch (spilled to VGPR lanes),
   // and the product passes 0 anyway.
@@ -3047,6 +3076,10 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
   const int eb = le * NS;
   const int kind = V.kind[me];  // the view holds ABSENT for absent and out-of-range slots
   const bool present = kind != TTRL_ABSENT;
+  if constexpr (IX) {
+    ix_epilogue<T, NS, EPW>(V, st, R, P, so, *ie, le, i, env, env_on, slot, k, me, eb, reg, my_timer, my_steer.r,
+                            my_acc.r, my_ix.r, my_iy.r, my_sidx);
+  } else {
   if (slot) {  // LDS -> HBM, once per launch
     Veh<T> a;
     a.x = V.x[me]; a.y = V.y[me]; a.h = V.h[me]; a.v = V.v[me]; a.ts = V.ts[me]; a.timer = my_timer;
@@ -3106,6 +3139,7 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
       }
     }
   }
+  }  // !IX
   }
   PH_FLUSH
 }
@@ -3240,7 +3274,7 @@ __device__ __forceinline__ unsigned pcg_interval(Pcg& g, unsigned max) {
 #define TTRL_ZIG_QUAL __constant__
 #include "ttrl_ziggurat.h"
 // random_standard_normal: the 256-entry ziggurat of numpy (tables from gen_ziggurat.py)
-__device__ __noinline__ double pcg_normal(Pcg& g) {
+__device__ __forceinline__ double pcg_normal_body(Pcg& g) {
   for (;;) {
     unsigned long long r = pcg_next64(g);
     const int idx = (int)(r & 0xff);
@@ -3261,6 +3295,10 @@ __device__ __noinline__ double pcg_normal(Pcg& g) {
     }
   }
 }
+// out of line in the scene kernels (one wavefront per env, many call sites); the simulate launch's
+// fused spawn (ttrl_ix_env_step) inlines the body: a call there would give the road-network
+// instance a stack
+__device__ __noinline__ double pcg_normal(Pcg& g) { return pcg_normal_body(g); }
 // Generator.choice(pop, size, replace=False), small population: Floyd's algorithm, then
 // _shuffle_int (random_bounded_uint64 = buffered Lemire draws)
 __device__ __forceinline__ void pcg_choice_noreplace(Pcg& g, int pop, int size, int* out) {
@@ -3302,7 +3340,8 @@ __device__ __forceinline__ void kin_observe(const ttrl_state_t& st, const LaneT<
                                             const ttrl_kin_cfg_t& cfg, bool env_ok, int env, T x, T y, T h, T v,
                                             T hc, T hs, int lane, bool present, bool mdp, EgoFn ego_of, T* s_key,
                                             int* s_cnt, int* s_ego, int (*s_perm)[64], int (*s_p)[64],
-                                            float* __restrict__ out, int32_t* __restrict__ ids) {
+                                            float* __restrict__ out, int32_t* __restrict__ ids,
+                                            float* __restrict__ out2, int32_t* __restrict__ ids2) {
   const int tid = threadIdx.x, le = tid / NS, i = tid % NS;
   const int N = st.n_veh;
   const bool slot = env_ok && i < N;
@@ -3372,7 +3411,18 @@ __device__ __forceinline__ void kin_observe(const ttrl_state_t& st, const LaneT<
     __syncthreads();
   }
   if (!env_ok) return;
+  // out2 / ids2 (this thread's env; ttrl_ix_env_step: an env that goes on keeps this observation as
+  // the next step's): every row is written to both
   float* ob = out + (size_t)env * V * F;
+  float* ob2 = out2 ? out2 + (size_t)env * V * F : nullptr;
+  auto put = [&](int q, float val) {
+    ob[q] = val;
+    if (ob2) ob2[q] = val;
+  };
+  auto put_id = [&](int q, int32_t val) {
+    if (ids) ids[(size_t)env * (V - 1) + q] = val;
+    if (ids2) ids2[(size_t)env * (V - 1) + q] = val;
+  };
   auto slot_of = [&](int q) { return shuf ? 1 + s_perm[le][q] : 1 + q; };
   auto emit = [&](int row, T px, T py, T phd, T pv, T c, T s, int pl, bool rel) {
     for (int cidx = 0; cidx < F; ++cidx) {
@@ -3384,21 +3434,21 @@ __device__ __forceinline__ void kin_observe(const ttrl_state_t& st, const LaneT<
         val = lmap(val, T(cfg.range_lo[f]), T(cfg.range_hi[f]), T(-1), T(1));
         if (cfg.clip) val = clip(val, T(-1), T(1));
       }
-      ob[row * F + cidx] = (float)val;
+      put(row * F + cidx, (float)val);
     }
   };
   if (i == 0) {
     if (has_ego) emit(0, ex, ey, eh, ev, ec, es, elane, false);
-    else for (int cidx = 0; cidx < F; ++cidx) ob[cidx] = 0.f;  // no controlled vehicle: zeros
+    else for (int cidx = 0; cidx < F; ++cidx) put(cidx, 0.f);  // no controlled vehicle: zeros
   }
   if (cand && rank < nc) {
     emit(slot_of(rank), x, y, h, v, hc, hs, lane, true);
-    if (ids) ids[(size_t)env * (V - 1) + rank] = i;
+    put_id(rank, i);
   }
   for (int q = nc + i; q < V - 1; q += NS) {  // zero rows
     const int row = slot_of(q);
-    for (int cidx = 0; cidx < F; ++cidx) ob[row * F + cidx] = 0.f;
-    if (ids) ids[(size_t)env * (V - 1) + q] = -1;
+    for (int cidx = 0; cidx < F; ++cidx) put(row * F + cidx, 0.f);
+    put_id(q, -1);
   }
 }
 
@@ -4576,6 +4626,228 @@ __device__ void ix_clear_spawn_env(const ttrl_state_t& st, const ttrl_lane_table
   if (lane == 0) rng_store(g, w);
 }
 
+// Position of the n-th (0-based) set bit of m (n < popcount(m)).
+__device__ __forceinline__ int nth_set_bit(unsigned long long m, int n) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const int c = __popcll(m & ((1ull << w) - 1ull));
+    if (n >= c) { n -= c; m >>= w; pos += w; }
+  }
+  return pos;
+}
+
+// wave_closest_lane over the NS-lane segment of one env (NS <= 64, a power of two; the result is
+// uniform on the segment): the same float64 distances and first-minimum rule.
+template <int NS>
+__device__ int seg_closest_lane(const ttrl_lane_table_t& R, double x, double y, double h, int i) {
+  double best = K<double>::inf();
+  int bl = 0x7fffffff;
+  for (int l = i; l < R.n_lanes; l += NS) {
+    const LaneT<double> L = make_lane<double>(R, l);
+    double s, r;
+    lane_local(L, x, y, s, r);
+    const double ang = fabs(wrap_to_pi(h - heading_at(L, s)));
+    double a = s - R.length[l]; if (!(a > 0)) a = 0;
+    double c = 0 - s; if (!(c > 0)) c = 0;
+    const double d = fabs(r) + a + c + 1.0 * ang;
+    if (d < best || (d == best && l < bl)) { best = d; bl = l; }
+  }
+#pragma unroll
+  for (int off = NS / 2; off >= 1; off >>= 1) {
+    const double od = __shfl_xor(best, off);
+    const int ol = __shfl_xor(bl, off);
+    if (od < best || (od == best && ol < bl)) { best = od; bl = ol; }
+  }
+  return bl == 0x7fffffff ? 0 : bl;
+}
+
+// The simulate launch's epilogue under ttrl_ix_env_step (one wavefront per workgroup, an env's
+// vehicles on NS lanes of it), from the final LDS state:
+//  (a) the step tail (step_tail: time, reward, terminated, truncated, info terms), as ttrl_env_step;
+//  (b) the Kinematics observation of the final state (kin_observe, np_random's shuffle), written to
+//      so.obs and, for an env that goes on, to ie.obs2 as well (its next observation);
+//  (c) an env that goes on: _clear_vehicles (intersection_env.py:350-362) -- the IDM vehicles on an
+//      exit lane within leave_margin of its end or without a route are dropped, the others keep
+//      list order (each lane takes the row of the i-th kept slot: register fields by lane
+//      shuffles, the LDS ones by the lane that owns the destination) -- then _spawn_vehicle
+//      (:320-348) with every lane of the env replaying its np_random (wave_spawn's draws, 15 m test
+//      by a segment ballot, closest lane by segment shuffles);
+//  (d) the rows to HBM: a finished env's as ttrl_env_step stores them (ttrl_ix_step_tail then
+//      swaps in its spare scene), an env that goes on every field of every slot (absent ones as
+//      row_absent, as wave_compact leaves them);
+//  (e) the live counts of the envs that go on (live, live_env).
+// Bit for bit the separate launches: ttrl_env_step, then ix_step_tail_kernel's clear / spawn
+// (test_fused_tail_equals_the_separate_tail, test_overlapped_resets_equal_in_place_resets).
+template <typename T, int NS, int EPW>
+__device__ __forceinline__ void ix_epilogue(const View<T>& V, const ttrl_state_t& st, const ttrl_lane_table_t& R,
+                                            const ParamsT<T>& P, const StepOut& so, const IxEpi& ie, int le, int i,
+                                            int env, bool env_on, bool slot, size_t k, int me, int eb, int reg,
+                                            T& timer, T& steer, T& acc, T& ix, T& iy, int& sidx) {
+  static_assert(NS * EPW == 64, "the fused tail runs on the one-wavefront road-network instance");
+  constexpr unsigned long long SEG = NS == 64 ? ~0ull : ((1ull << NS) - 1);
+  constexpr int M = EPW * NS;
+  const int N = st.n_veh;
+  const int kind = V.kind[me];
+  const bool present = kind != TTRL_ABSENT;
+  char* scr = (char*)V.afree;
+  T* s_key = (T*)scr;
+  int(*s_perm)[64] = (int(*)[64])(scr + ((sizeof(T) * M + 15) & ~(size_t)15));
+  int(*s_p)[64] = s_perm + EPW;
+  int* s_cnt = (int*)(s_p + EPW);
+  int* s_ego = s_cnt + EPW;
+  if (i == 0 && env_on) st.reg_steps[env] = reg;
+  // (a) the step tail; V.nitem[le] (dead since the last act phase): 1 = the env goes on
+  if (i == 0) s_ego[le] = N;
+  __syncthreads();
+  if (present && kind == TTRL_MDP) atomicMin(&s_ego[le], i);
+  __syncthreads();
+  if (i == 0) {
+    bool go = false;
+    if (env_on) {
+      const int ego = s_ego[le];
+      step_tail<T>(R, V.lanes + (ego < N ? (int)V.lane[eb + ego] : 0), so.rcfg, env, ego < N, V.x[eb + ego % N],
+                   V.y[eb + ego % N], V.v[eb + ego % N], (int)V.lane[eb + ego % N],
+                   (V.flags[eb + ego % N] & FL_CRASHED) != 0, V.v[eb], (V.flags[eb] & FL_CRASHED) != 0, so.time,
+                   so.time_inc, so.reward, so.term, so.trunc, so.comp, (T*)so.ego_speed, so.ego_crashed);
+      go = !so.term[env] && !so.trunc[env];
+    }
+    V.nitem[le] = go ? 1 : 0;
+  }
+  __syncthreads();
+  const bool go_on = V.nitem[le] != 0;
+  // (b) the observation of the final state
+  {
+    auto ego_of = [&](int ego, T& ex, T& ey, T& eh, T& ev, T& ec, T& es, int& elane) {
+      ex = V.x[eb + ego]; ey = V.y[eb + ego]; eh = V.h[eb + ego]; ev = V.v[eb + ego]; elane = V.lane[eb + ego];
+      ec = V.ch[eb + ego]; es = V.sh[eb + ego];
+    };
+    kin_observe<T, NS, EPW>(st, V.lanes, P, so.kcfg, env_on, env, V.x[me], V.y[me], V.h[me], V.v[me], V.ch[me],
+                            V.sh[me], (int)V.lane[me], present, present && kind == TTRL_MDP, ego_of, s_key, s_cnt,
+                            s_ego, s_perm, s_p, so.obs, so.ids, go_on ? ie.obs2 : nullptr,
+                            go_on ? ie.ids2 : nullptr);
+  }
+  __syncthreads();  // the shuffle's np_random words (lane 0 of the env) before the spawn reads them
+  // (c) _clear_vehicles: the kept slots of an env that goes on
+  bool keep = present;
+  if (go_on && present && kind == TTRL_IDM) {
+    const int l = V.lane[me];
+    T s, r;
+    lane_local(V.lanes[l], V.x[me], V.y[me], s, r);
+    const bool leaving = R.exit_lane[l] && s >= T(R.length[l]) - T(ie.C.leave_margin);
+    keep = !(leaving || V.rn[me] < 0);
+  }
+  const unsigned long long kb = (__ballot(keep) >> eb) & SEG;
+  const int cnt = __popcll(kb);
+  // lane i takes the row of the i-th kept slot (i >= cnt: absent); the other envs keep their rows
+  const int src = go_on ? (i < cnt ? nth_set_bit(kb, i) : -1) : i;
+  const int sl = eb + (src < 0 ? i : src);
+  {
+    const T nx = __shfl(V.x[me], sl), ny = __shfl(V.y[me], sl), nv = __shfl(V.v[me], sl);
+    const T nts = __shfl(V.ts[me], sl), nh = __shfl(V.h[me], sl), nd = __shfl(V.delta[me], sl);
+    const int nb = __shfl((int)((unsigned)V.kind[me] | (unsigned)V.flags[me] << 8 | (unsigned)(uint8_t)V.lane[me] << 16 |
+                                (unsigned)(uint8_t)V.tgt[me] << 24), sl);
+    const int nrr = __shfl(((const int32_t*)V.rroad)[me], sl), nrl = __shfl(((const int32_t*)V.rlane)[me], sl);
+    const int nrn = __shfl((int)V.rn[me], sl);
+    const T nti = __shfl(timer, sl), nst = __shfl(steer, sl), nac = __shfl(acc, sl);
+    const T nix = __shfl(ix, sl), niy = __shfl(iy, sl);
+    const int nsi = __shfl(sidx, sl);
+    if (go_on) {
+      if (src >= 0) {
+        V.x[me] = nx; V.y[me] = ny; V.v[me] = nv; V.ts[me] = nts; V.h[me] = nh; V.delta[me] = nd;
+        V.kind[me] = (uint8_t)(nb & 0xff); V.flags[me] = (uint8_t)((nb >> 8) & 0xff);
+        V.lane[me] = (int8_t)((nb >> 16) & 0xff); V.tgt[me] = (int8_t)((nb >> 24) & 0xff);
+        ((int32_t*)V.rroad)[me] = nrr; ((int32_t*)V.rlane)[me] = nrl; V.rn[me] = (int8_t)nrn;
+        timer = nti; steer = nst; acc = nac; ix = nix; iy = niy; sidx = nsi;
+      } else {
+        V.kind[me] = TTRL_ABSENT;
+      }
+    }
+  }
+  __syncthreads();
+  // (d) _spawn_vehicle (wave_spawn's draws, in order), every lane of an env that goes on alike
+  int n_live = cnt;
+  if (go_on) {
+    uint64_t* w = st.rng + (size_t)env * TTRL_RNG_WORDS;
+    Pcg g = rng_load(w);
+    if (!(pcg_double(g) > ie.C.spawn_probability)) {
+      int route[2];
+      pcg_choice_noreplace(g, 4, 2, route);
+      const int l = ie.C.entry_lane[route[0]];
+      const double lon = 0.0 + ie.C.spawn_offset + pcg_normal_body(g) * 1.0;
+      const double sp = ie.C.spawn_speed + pcg_normal_body(g) * 1.0;
+      const LaneT<double> L = make_lane<double>(R, l);
+      double px, py;
+      lane_position(L, lon, 0.0, px, py);
+      const double ph = heading_at(L, lon);
+      bool near = false;
+      if (i < cnt) {
+        const double dx = (double)V.x[me] - px, dy = (double)V.y[me] - py;
+        near = sqrt(dx * dx + dy * dy) < ie.C.spawn_clear_distance;
+      }
+      if (((__ballot(near) >> eb) & SEG) == 0) {
+        const double delta = ie.C.delta_lo + (ie.C.delta_hi - ie.C.delta_lo) * pcg_double(g);  // drawn even with no slot left
+        if (cnt < N) {
+          const int cl = seg_closest_lane<NS>(R, px, py, ph, i);
+          if (i == cnt) {
+            int32_t rr, rl;
+            int8_t rn;
+            plan_route(R, ie.C, cl, route[1], rr, rl, rn);
+            V.x[me] = T(px); V.y[me] = T(py); V.h[me] = T(ph); V.v[me] = T(sp); V.ts[me] = T(sp);
+            V.delta[me] = T(delta);
+            V.kind[me] = TTRL_IDM; V.flags[me] = FL_LC;
+            V.lane[me] = (int8_t)cl; V.tgt[me] = (int8_t)cl;
+            ((int32_t*)V.rroad)[me] = rr; ((int32_t*)V.rlane)[me] = rl; V.rn[me] = rn;
+            timer = T(pymod((px + py) * 3.141592653589793, ie.lane_change_delay));
+            steer = acc = ix = iy = T(0);
+            sidx = -1;
+          }
+          n_live = cnt + 1;
+        }
+      }
+    }
+    if (i == 0) rng_store(g, w);
+  }
+  // (e) the rows, LDS -> HBM
+  if (slot) {
+    const int kd = V.kind[me];
+    const int fl = V.flags[me];
+    if (go_on) {  // every field of every slot (compaction moved them)
+      Row<T> r = row_absent<T>();
+      if (kd != TTRL_ABSENT) {
+        r.f[0] = V.x[me]; r.f[1] = V.y[me]; r.f[2] = V.h[me]; r.f[3] = V.v[me]; r.f[4] = V.ts[me];
+        r.f[5] = timer; r.f[6] = V.delta[me]; r.f[7] = steer; r.f[8] = acc; r.f[9] = ix; r.f[10] = iy;
+        r.lane = V.lane[me]; r.tgt = V.tgt[me]; r.sidx = sidx;
+        r.route_road = ((const int32_t*)V.rroad)[me]; r.route_lane = ((const int32_t*)V.rlane)[me];
+        r.kind = (uint8_t)kd; r.crashed = (fl & FL_CRASHED) ? 1 : 0; r.has_impact = (fl & FL_IMPACT) ? 1 : 0;
+        r.lane_change = (fl & FL_LC) ? 1 : 0; r.yielding = (fl & FL_YIELD) ? 1 : 0; r.route_n = V.rn[me];
+      }
+      row_store<T>(st, k, r);
+    } else {  // as ttrl_env_step stores them
+      Veh<T> a;
+      a.x = V.x[me]; a.y = V.y[me]; a.h = V.h[me]; a.v = V.v[me]; a.ts = V.ts[me]; a.timer = timer;
+      a.steer = steer; a.acc = acc; a.ix = ix; a.iy = iy;
+      a.lane = V.lane[me]; a.tgt = V.tgt[me]; a.sidx = sidx;
+      a.crashed = (fl & FL_CRASHED) != 0; a.hasimp = (fl & FL_IMPACT) != 0;
+      if (kd == TTRL_ABSENT) {  // absent rows pass through untouched
+        a.x = ((const T*)st.x)[k]; a.lane = st.lane[k]; a.tgt = st.target_lane[k];
+      }
+      store_veh(a, st, k);
+      for (int q = 0; q < TTRL_ROUTE_MAX; ++q) {
+        st.route_road[k * TTRL_ROUTE_MAX + q] = V.rroad[me * TTRL_ROUTE_MAX + q];
+        st.route_lane[k * TTRL_ROUTE_MAX + q] = V.rlane[me * TTRL_ROUTE_MAX + q];
+      }
+      st.route_n[k] = V.rn[me];
+      st.yielding[k] = (fl & FL_YIELD) ? 1 : 0;
+    }
+  }
+  // (f) the live counts of an env that goes on (a finished env's: ttrl_ix_step_tail)
+  if (go_on && i == 0) {
+    if (ie.live_env) ie.live_env[env] = n_live;
+    if (ie.live) atomicAdd(ie.live, (unsigned long long)n_live);
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(64) ix_clear_spawn_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P,
                                                             ttrl_ix_cfg_t C, const uint8_t* __restrict__ mask) {
@@ -4641,6 +4913,9 @@ struct IxTail {
   int32_t* ids_out;
   unsigned long long* live;  // optional: += the vehicles present after the tail (the next step's)
   int32_t* live_env;         // optional [E]: each env's vehicles present after the tail
+  // the envs that go on were cleared / spawned, observed and counted by ttrl_ix_env_step's launch:
+  // only the finished ones are handled here (obs_out / ids_out: that launch's next observation)
+  bool cleared;
 };
 
 // The env's present vehicles after the tail: added to *t.live (one atomic per env) and / or
@@ -4719,6 +4994,7 @@ __global__ void __launch_bounds__(64) ix_step_tail_kernel(ttrl_state_t st, ttrl_
       t.done[env] = 0;
       for (int q = 0; q < t.K; ++q) t.spare_mask[q * E + env] = 0;
     }
+    if (t.cleared) return;
     if (t.obs) {  // the row observed by the fused launch stays this step's observation
       for (int q = lane; q < V * F; q += 64) t.obs_out[(size_t)env * V * F + q] = t.obs_in[(size_t)env * V * F + q];
       if (t.ids_out)
@@ -4904,6 +5180,19 @@ int dispatch_sim(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_p
     case 128: return launch_sim<T, 128, 1>(s, R, P, actions, mask, frames, dt, mode, ablate, stream, ob);
     default: return launch_sim<T, 256, 1>(s, R, P, actions, mask, frames, dt, mode, ablate, stream, ob);
   }
+}
+
+// ttrl_ix_env_step's launch: the one-wavefront road-network instance with the fused tail (IxEpi)
+template <typename T, int NS, int EPW>
+int launch_sim_ix(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const int32_t* actions,
+                  int frames, double dt, hipStream_t stream, const StepOut& ob, const IxEpi& ie) {
+  const int blocks = (s.n_envs + EPW - 1) / EPW;
+  if (blocks == 0) return TTRL_OK;
+  const ViewLayout o = view_layout<T>(EPW, NS, R.n_lanes, true, false);
+  if (!tail_fits<T>(o, EPW, NS)) return TTRL_E_UNSUPPORTED;
+  hipLaunchKernelGGL((simulate_ix_kernel<T, NS, EPW>), dim3(blocks), dim3(NS * EPW), o.total, stream, s, R,
+                     params_for<T>(P), actions, frames, dt, ob, ie);
+  return launch_status();
 }
 
 int run_sim(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P, const int32_t* actions,
@@ -5329,7 +5618,7 @@ int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
                       const uint8_t* truncated, uint8_t* spare_parity, uint32_t* entropy, uint32_t* spare_entropy,
                       int32_t n_words, double* time, uint8_t* done, uint8_t* spare_mask,
                       const ttrl_kin_cfg_t* obs_cfg, const float* obs_in, float* obs_out, const int32_t* obs_ids_in,
-                      int32_t* obs_ids_out, int64_t* live_count, int32_t* order, void* stream) {
+                      int32_t* obs_ids_out, int64_t* live_count, int32_t* order, int32_t cleared, void* stream) {
   int rc = check_ix(s, road, p, cfg);
   if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!spare || !terminated || !truncated || !spare_parity || !entropy || !spare_entropy || n_words < 1 ||
@@ -5346,10 +5635,13 @@ int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
   for (const void* q : sp)
     if (!q) return TTRL_E_ARG;
   if (obs_cfg) {  // the re-observation puts one slot on each lane of the env's wavefront
-    if (check_kin_cfg(s, obs_cfg) || !obs_in || !obs_out || (!obs_ids_in) != (!obs_ids_out) || s->n_veh > 64)
+    if (check_kin_cfg(s, obs_cfg) || (!cleared && !obs_in) || !obs_out || (!cleared && (!obs_ids_in) != (!obs_ids_out)) ||
+        s->n_veh > 64)
       return obs_cfg && s->n_veh > 64 ? TTRL_E_UNSUPPORTED : TTRL_E_ARG;
   }
+  if (cleared && !obs_cfg) return TTRL_E_ARG;  // after ttrl_ix_env_step, whose observation is Kinematics
   IxTail t{};
+  t.cleared = cleared != 0;
   t.spare = *spare; t.K = K; t.term = terminated; t.trunc = truncated; t.par = spare_parity; t.ent = entropy;
   t.spare_ent = spare_entropy; t.nw = n_words; t.time = time; t.done = done; t.spare_mask = spare_mask;
   t.live = reinterpret_cast<unsigned long long*>(live_count);
@@ -5369,6 +5661,45 @@ int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
   if (ordered)
     hipLaunchKernelGGL(ix_order_kernel, dim3(1), dim3(1024), 0, st, order, s->n_envs, G, G * s->n_veh);
   return launch_status();
+}
+
+int ttrl_ix_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                     const ttrl_ix_cfg_t* cfg, const int32_t* actions, int32_t frames, double dt,
+                     const ttrl_kin_cfg_t* obs_cfg, float* obs, int32_t* obs_ids, float* obs_next, int32_t* ids_next,
+                     const ttrl_reward_cfg_t* reward_cfg, double* time, double time_inc, float* reward,
+                     uint8_t* terminated, uint8_t* truncated, float* components, void* ego_speed,
+                     uint8_t* ego_crashed, int32_t* order, const int32_t* action_lut, int32_t n_action_lut,
+                     int64_t* live_count, void* stream) {
+  int rc = check_ix(s, road, p, cfg);
+  if (rc) return rc < 0 ? rc : TTRL_OK;
+  if (!obs_cfg || !obs || !obs_next || check_kin_cfg(s, obs_cfg) || (!obs_ids) != (!ids_next)) return TTRL_E_ARG;
+  if (!reward_cfg || !time || !reward || !terminated || !truncated || (!ego_speed) != (!ego_crashed))
+    return TTRL_E_ARG;
+  if (n_action_lut < 0 || n_action_lut > 8 || (n_action_lut > 0 && !action_lut)) return TTRL_E_ARG;
+  if (slots_for(s->n_veh) > 64) return TTRL_E_UNSUPPORTED;  // the fused tail needs one wavefront per workgroup
+  StepOut so{};
+  for (int q = 0; q < n_action_lut; ++q) {
+    if (action_lut[q] < TTRL_LANE_LEFT || action_lut[q] > TTRL_SLOWER) return TTRL_E_ARG;
+    so.lut[q] = (int8_t)action_lut[q];
+  }
+  so.n_lut = n_action_lut;
+  so.kcfg = *obs_cfg; so.obs = obs; so.ids = obs_ids;
+  so.rcfg = *reward_cfg; so.time = time; so.time_inc = time_inc; so.reward = reward; so.term = terminated;
+  so.trunc = truncated; so.comp = components; so.ego_speed = ego_speed; so.ego_crashed = ego_crashed;
+  so.order = order;
+  IxEpi ie{};
+  ie.C = *cfg;
+  ie.lane_change_delay = p->lane_change_delay;
+  ie.obs2 = obs_next; ie.ids2 = ids_next;
+  ie.live = reinterpret_cast<unsigned long long*>(live_count);
+  const bool two = slots_for(s->n_veh) == 32;  // two envs per wavefront
+  if (order && s->n_envs % (two ? 2 : 1) == 0) ie.live_env = order + s->n_envs;  // ix_order_kernel's input
+  hipStream_t st = (hipStream_t)stream;
+  if (s->dtype == TTRL_F64)
+    return two ? launch_sim_ix<double, 32, 2>(*s, *road, *p, actions, frames, dt, st, so, ie)
+               : launch_sim_ix<double, 64, 1>(*s, *road, *p, actions, frames, dt, st, so, ie);
+  return two ? launch_sim_ix<float, 32, 2>(*s, *road, *p, actions, frames, dt, st, so, ie)
+             : launch_sim_ix<float, 64, 1>(*s, *road, *p, actions, frames, dt, st, so, ie);
 }
 
 int ttrl_rewards_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_reward_cfg_t* cfg,

@@ -284,6 +284,10 @@ class VecIntersectionEnv:
             # whole warm-up at once, on side streams in rotation
             "reset_chunk_frames": 15,
             "reset_streams": 2,  # side streams the whole-warm-up resets rotate over (chunks: one)
+            # the envs that go on run _clear_vehicles / _spawn_vehicle inside the step launch
+            # (ttrl_ix_env_step; Kinematics observations, <= 64 slots), the finished ones swap in
+            # their spare scenes in ix_step_tail_ -- bit for bit the two-launch step
+            "fuse_tail": True,
         }
 
     def configure(self, config: dict | None) -> None:
@@ -497,12 +501,14 @@ class VecIntersectionEnv:
         return obs, reward, terminated, truncated, info
 
     def _step_overlapped(self, action):
-        """The auto-reset step with overlapped resets in two launches: ttrl::env_step_ (the fused
-        frames, the observation of the final state and the step tail: time += 1 / policy_frequency,
-        rewards, dones, info) and ttrl::ix_step_tail_ (clear / spawn for the envs that go on; the
-        finished ones swap in their spare scene and are re-observed); then the consumed spare rows
-        are reset again on a side stream.  Bit for bit the in-place composition (simulate, observe,
-        rewards, clear / spawn, reset, masked observe; test_overlapped_resets_equal_in_place_resets)."""
+        """The auto-reset step with overlapped resets in two launches: ttrl::ix_env_step_ (the fused
+        frames, the observation of the final state, the step tail: time += 1 / policy_frequency,
+        rewards, dones, info -- and, for the envs that go on, clear / spawn) and ttrl::ix_step_tail_
+        (the finished envs swap in their spare scene and are re-observed); then the consumed spare
+        rows are reset again on a side stream.  (``fuse_tail`` False, or a non-Kinematics
+        observation: ttrl::env_step_, and the clear / spawn in ix_step_tail_.)  Bit for bit the
+        in-place composition (simulate, observe, rewards, clear / spawn, reset, masked observe;
+        test_overlapped_resets_equal_in_place_resets)."""
         ot = self.observation_type
         kin = isinstance(ot, BatchedKinematicObservation)
         frames = int(self.config["simulation_frequency"] // self.config["policy_frequency"])
@@ -510,9 +516,19 @@ class VecIntersectionEnv:
         if action is not None and not self.config["manual_control"]:
             idx, lut = self.action_type._indices(action)  # the launch maps them to meta-action codes
         self.steps += frames
-        obs, ids, *outs = self.road.env_step(idx, frames, 1 / self.config["simulation_frequency"],
-                                             ot.fused_cfg() if kin else None, self.reward_cfg, self.time,
-                                             1 / self.config["policy_frequency"], self._order, lut)
+        # the tail launch re-observes a new scene with one slot per lane of a wavefront: wider rows
+        # (vehicle_slots > 64) take the masked observation launch instead, which draws the same
+        # shuffles from the same generators (test_overlapped_resets_equal_in_place_resets[96])
+        fused_obs = kin and self.state.n_veh <= 64
+        fuse = fused_obs and bool(self.config["fuse_tail"])
+        dt, tinc = 1 / self.config["simulation_frequency"], 1 / self.config["policy_frequency"]
+        if fuse:  # the envs that go on are cleared / spawned inside the step launch
+            obs, ids, *outs, obs2, ids2 = self.road.ix_env_step(self.ix, idx, frames, dt, ot.fused_cfg(),
+                                                                self.reward_cfg, self.time, tinc, self._order, lut,
+                                                                self.live_counter)
+        else:
+            obs, ids, *outs = self.road.env_step(idx, frames, dt, ot.fused_cfg() if kin else None, self.reward_cfg,
+                                                 self.time, tinc, self._order, lut)
         reward, terminated, truncated = _keep_tail(self, outs)
         if not kin:
             obs = ot.observe()
@@ -521,15 +537,12 @@ class VecIntersectionEnv:
         # the slots this step's tail takes were prepared two steps back at the latest (waited for
         # here, after the step launch is queued: the side work gets the launch's time as slack)
         torch.cuda.current_stream(self.device).wait_event(self._wait_ev)
-        # the tail launch re-observes a new scene with one slot per lane of a wavefront: wider rows
-        # (vehicle_slots > 64) take the masked observation launch instead, which draws the same
-        # shuffles from the same generators (test_overlapped_resets_equal_in_place_resets[96])
-        fused_obs = kin and self.state.n_veh <= 64
         done, smask, obs2, ids2 = ops.T.ix_step_tail_(
             self.state.tensors(), ops.st(self.network.table), ops.st(self.params), ops.st(self.ix),
             self._spare.tensors(), terminated, truncated, self._spare_par, self._entropy, self._spare_ent, self.time,
-            ops.kin_cfg_tensor(ot.fused_cfg()) if fused_obs else None, obs if fused_obs else None,
-            ids if fused_obs else None, self.live_counter, self._order)
+            ops.kin_cfg_tensor(ot.fused_cfg()) if fused_obs else None,
+            (obs2 if fuse else obs) if fused_obs else None, (ids2 if fuse else ids) if fused_obs else None,
+            self.live_counter, self._order, cleared=fuse)
         self._prepare_spares(smask)
         info["final_observation"], info["final_mask"] = obs, done
         if fused_obs:

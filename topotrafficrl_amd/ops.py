@@ -25,7 +25,7 @@ from . import _lib
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libttrl_torch.so")
 OPS = ["simulate_", "road_act_", "road_step_", "meta_action_", "env_step_", "neighbours", "kinematics_obs",
        "kinematics_obs_masked_", "occupancy_grid", "observe_ttc", "observe_lidar", "reset_highway_",
-       "reset_highway_seeded_", "auto_reset_highway_", "ix_reset_", "ix_reset_parts_", "ix_clear_spawn_", "ix_step_tail_", "copy_envs_", "rewards", "rewards_ex",
+       "reset_highway_seeded_", "auto_reset_highway_", "ix_reset_", "ix_reset_parts_", "ix_clear_spawn_", "ix_step_tail_", "ix_env_step_", "copy_envs_", "rewards", "rewards_ex",
        "rewards_step_", "ego_attention_q", "ego_attention_act"]
 
 _loaded = False
