@@ -30,9 +30,9 @@
  *   ttrl_ix_clear_spawn      IntersectionEnv.step tail     ttrl_env/envs/intersection_env.py:135-139
  *                            (_clear_vehicles :350-362, _spawn_vehicle :320-348)
  *   ttrl_ix_step_tail        the step tail + auto-reset from spare scenes (AbstractEnv.reset abstract.py:188-214)
- *   ttrl_ix_env_step         IntersectionEnv.step (intersection_env.py:135-139 over abstract.py:224-250) in one
- *                            launch for the envs that go on: frames, observation, rewards, _clear_vehicles,
- *                            _spawn_vehicle
+ *   ttrl_ix_env_step         IntersectionEnv.step (intersection_env.py:135-139 over abstract.py:224-250) with
+ *                            the auto-reset from spare scenes, in one launch: frames, observation, rewards,
+ *                            _clear_vehicles / _spawn_vehicle, the reset's swap
  */
 #ifndef TTRL_MI355X_H
 #define TTRL_MI355X_H
@@ -426,34 +426,35 @@ int ttrl_ix_clear_spawn(const ttrl_state_t* s, const ttrl_lane_table_t* road, co
  * first n_envs initialised to any permutation of the envs): receives in [0, n_envs) the next
  * ttrl_env_step's dispatch order -- the envs grouped as that launch's workgroups hold them,
  * groups sorted by their live vehicles, heaviest first; [n_envs, 2 n_envs) is its scratch.
- * cleared != 0 (after ttrl_ix_env_step, ABI 7): the envs that go on were cleared, spawned, observed
- * into obs_out / obs_ids_out (that call's obs_next / ids_next) and counted by that launch; only
- * their done / spare_mask entries are written here, and obs_in / obs_ids_in are unused (may be NULL).
  * Reference: intersection_env.py:135-139, :350-362, :320-348; abstract.py:188-214. */
 int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                       const ttrl_ix_cfg_t* cfg, const ttrl_state_t* spare, const uint8_t* terminated,
                       const uint8_t* truncated, uint8_t* spare_parity, uint32_t* entropy, uint32_t* spare_entropy,
                       int32_t n_words, double* time, uint8_t* done, uint8_t* spare_mask,
                       const ttrl_kin_cfg_t* obs_cfg, const float* obs_in, float* obs_out, const int32_t* obs_ids_in,
-                      int32_t* obs_ids_out, int64_t* live_count, int32_t* order, int32_t cleared, void* stream);
-/* VecIntersectionEnv.step with overlapped resets, first half (ABI 7): ttrl_env_step's launch
- * (frames, the Kinematics observation obs_cfg -> obs / obs_ids, the step tail) on a road network of
- * <= 64 slots, and in the same launch, for every env that goes on (terminated | truncated == 0),
- * IntersectionEnv.step's tail as ttrl_ix_clear_spawn does it (_clear_vehicles, then
- * _spawn_vehicle drawing from state.rng after the observation's shuffle) and the copy of its
- * observation row into obs_next / ids_next (its next observation), its live vehicles added to
- * live_count (optional) and written to order[n_envs + e] (order given: the dispatch order of
- * this launch in [0, n_envs), ix_order_kernel's input in [n_envs, 2 n_envs)).  The finished envs'
- * rows are stored as ttrl_env_step stores them; ttrl_ix_step_tail(cleared = 1) then swaps in their
- * spare scenes and writes their rows of obs_next / ids_next.  Together bit for bit ttrl_env_step
- * followed by ttrl_ix_step_tail(cleared = 0).  Reference: intersection_env.py:135-139, :320-362. */
+                      int32_t* obs_ids_out, int64_t* live_count, int32_t* order, void* stream);
+/* VecIntersectionEnv.step with the auto-reset from spare scenes in one launch (ABI 7): ttrl_env_step
+ * followed by ttrl_ix_step_tail, fused, on a road network of <= 64 slots (one wavefront per
+ * workgroup).  From the on-chip final state: the Kinematics observation (obs_cfg -> obs / obs_ids)
+ * and the step tail (time += time_inc, reward, terminated, truncated, components, ego speed /
+ * crashed) as ttrl_env_step; then an env that goes on (terminated | truncated == 0) runs
+ * IntersectionEnv.step's tail as ttrl_ix_clear_spawn does (_clear_vehicles, then _spawn_vehicle
+ * drawing from state.rng after the observation's shuffle) and keeps its observation row as its
+ * next one (obs_next / ids_next), while a finished env takes its spare scene and counters and has
+ * its new first observation written to obs_next / ids_next -- spare, spare_parity, entropy,
+ * spare_entropy, n_words, done, spare_mask, live_count and order exactly as ttrl_ix_step_tail takes
+ * them (the next dispatch order is written after the launch).  The spare rows an env may take must
+ * be ready when the launch starts (VecIntersectionEnv keeps one more spare slot for that).  Bit for
+ * bit ttrl_env_step + ttrl_ix_step_tail.  Reference: intersection_env.py:135-139, :320-362;
+ * abstract.py:188-250. */
 int ttrl_ix_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                      const ttrl_ix_cfg_t* cfg, const int32_t* actions, int32_t frames, double dt,
                      const ttrl_kin_cfg_t* obs_cfg, float* obs, int32_t* obs_ids, float* obs_next, int32_t* ids_next,
                      const ttrl_reward_cfg_t* reward_cfg, double* time, double time_inc, float* reward,
                      uint8_t* terminated, uint8_t* truncated, float* components, void* ego_speed,
-                     uint8_t* ego_crashed, int32_t* order, const int32_t* action_lut, int32_t n_action_lut,
-                     int64_t* live_count, void* stream);
+                     uint8_t* ego_crashed, const ttrl_state_t* spare, uint8_t* spare_parity, uint32_t* entropy,
+                     uint32_t* spare_entropy, int32_t n_words, uint8_t* done, uint8_t* spare_mask, int32_t* order,
+                     const int32_t* action_lut, int32_t n_action_lut, int64_t* live_count, void* stream);
 /* Per-env reward [E] float32, terminated/truncated [E] uint8, given time [E] float64, for the
  * env's controlled vehicle (its first TTRL_MDP slot). */
 int ttrl_rewards(const ttrl_state_t* s, const ttrl_lane_table_t* road,

@@ -337,9 +337,8 @@ def test_intersection_ops_equal_the_c_abi(hip_device):
 
 @pytest.mark.gpu
 def test_ix_env_step_op_equals_the_c_abi(hip_device):
-    """ttrl::ix_env_step_ and ttrl::ix_step_tail_(cleared=True) against direct ctypes calls of
-    ttrl_ix_env_step and ttrl_ix_step_tail(cleared = 1), on copies of in-loop intersection scenes
-    whose clocks put some envs at their last step (terminated / truncated ones swap in spares)."""
+    """ttrl::ix_env_step_ against a direct ctypes call of ttrl_ix_env_step, on copies of in-loop
+    intersection scenes whose clocks put some envs at their last step (those swap in spares)."""
     from topotrafficrl_amd.intersection import VecIntersectionEnv
     env = VecIntersectionEnv({"num_envs": 32, "device": hip_device, "auto_reset": True, "duration": 3})
     env.reset(seed=3)
@@ -354,6 +353,7 @@ def test_ix_env_step_op_equals_the_c_abi(hip_device):
     kin = env.observation_type.fused_cfg()
     rc = env.reward_cfg
     act = torch.randint(0, 3, (32,), device=hip_device, generator=g, dtype=torch.int32)
+    codes = env.action_type._codes(act).to(torch.int32)
     a, b = env.state.clone(), env.state.clone()
     sa, sb = env._spare.clone(), env._spare.clone()
     ta, tb = env.time.clone(), env.time.clone()
@@ -362,38 +362,29 @@ def test_ix_env_step_op_equals_the_c_abi(hip_device):
     pa, pb = env._spare_par.clone(), env._spare_par.clone()
     ea, eb = env._entropy.clone(), env._entropy.clone()
     fa, fb = env._spare_ent.clone(), env._spare_ent.clone()
-    codes = env.action_type._codes(act).to(torch.int32)
     outs = torch.ops.ttrl.ix_env_step_(a.tensors(), lanes, params, cfg, codes, 15, 1 / 15, ops.kin_cfg_tensor(kin),
-                                       ops.st(rc), ta, 1.0, oa, None, la)
-    tail = torch.ops.ttrl.ix_step_tail_(a.tensors(), lanes, params, cfg, sa.tensors(), outs[3], outs[4], pa, ea, fa, ta,
-                                        ops.kin_cfg_tensor(kin), outs[8], outs[9], la, oa, cleared=True)
+                                       ops.st(rc), ta, 1.0, sa.tensors(), pa, ea, fa, oa, None, la)
     E, V, F = 32, kin.vehicles_count, kin.n_features
     o = [torch.empty(E, V, F, device=hip_device), torch.empty(E, V - 1, dtype=torch.int32, device=hip_device),
          torch.empty(E, device=hip_device), torch.empty(E, dtype=torch.bool, device=hip_device),
          torch.empty(E, dtype=torch.bool, device=hip_device), torch.empty(E, 4, device=hip_device),
          torch.empty(E, dtype=torch.float64, device=hip_device), torch.empty(E, dtype=torch.bool, device=hip_device),
+         torch.empty(E, dtype=torch.bool, device=hip_device), torch.empty(sb.n_envs, dtype=torch.uint8, device=hip_device),
          torch.empty(E, V, F, device=hip_device), torch.empty(E, V - 1, dtype=torch.int32, device=hip_device)]
-    KC = kin
-    assert lib.ttrl_ix_env_step(_c(b), R, P, IX, codes.data_ptr(), 15, 1 / 15, C.byref(KC), o[0].data_ptr(),
-                                o[1].data_ptr(), o[8].data_ptr(), o[9].data_ptr(), C.byref(rc), tb.data_ptr(), 1.0,
+    assert lib.ttrl_ix_env_step(_c(b), R, P, IX, codes.data_ptr(), 15, 1 / 15, C.byref(kin), o[0].data_ptr(),
+                                o[1].data_ptr(), o[10].data_ptr(), o[11].data_ptr(), C.byref(rc), tb.data_ptr(), 1.0,
                                 o[2].data_ptr(), o[3].data_ptr(), o[4].data_ptr(), o[5].data_ptr(), o[6].data_ptr(),
-                                o[7].data_ptr(), ob.data_ptr(), None, 0, lb.data_ptr(), _stream()) == 0
-    done = torch.empty(E, dtype=torch.bool, device=hip_device)
-    smask = torch.empty(sb.n_envs, dtype=torch.uint8, device=hip_device)
-    assert lib.ttrl_ix_step_tail(_c(b), R, P, IX, _c(sb), o[3].data_ptr(), o[4].data_ptr(), pb.data_ptr(),
-                                 eb.data_ptr(), fb.data_ptr(), eb.shape[1], tb.data_ptr(), done.data_ptr(),
-                                 smask.data_ptr(), C.byref(KC), None, o[8].data_ptr(), None, o[9].data_ptr(),
-                                 lb.data_ptr(), ob.data_ptr(), 1, _stream()) == 0
+                                o[7].data_ptr(), _c(sb), pb.data_ptr(), eb.data_ptr(), fb.data_ptr(), eb.shape[1],
+                                o[8].data_ptr(), o[9].data_ptr(), ob.data_ptr(), None, 0, lb.data_ptr(),
+                                _stream()) == 0
     torch.cuda.synchronize()
     for x, y in zip(outs, o):
         assert torch.equal(x, y)
-    assert torch.equal(tail[0], done) and torch.equal(tail[1], smask)
-    assert tail[2].data_ptr() == outs[8].data_ptr()  # written in place
     _equal(a, b)
     _equal(sa, sb)
     for x, y in ((ta, tb), (oa, ob), (la, lb), (pa, pb), (ea, eb), (fa, fb)):
         assert torch.equal(x, y)
-    assert bool(done.any())  # truncations at time 3 (and any crashes): spares swapped in
+    assert bool(o[8].any())  # truncations at time 3 (and any crashes): spares swapped in
 
 
 @pytest.mark.gpu

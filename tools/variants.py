@@ -27,6 +27,15 @@ SOURCE_EDITS = {
 for name in os.environ.get("EDIT_VARIANTS", "").split(","):
     if name.strip():
         VARIANTS[name.strip()] = []
+# variants built from an earlier commit's kernel source (its include/ and csrc/ as they were),
+# e.g. REV_VARIANTS="r04=ec952d4;r05=5e3157c": the same fused launch (ttrl_simulate, unchanged since
+# round 1) timed against that round's build in one process, on one box
+REV = {}
+for arg in os.environ.get("REV_VARIANTS", "").split(";"):
+    if arg.strip():
+        name, rev = arg.split("=", 1)
+        REV[name.strip()] = rev.strip()
+        VARIANTS[name.strip()] = []
 for arg in os.environ.get("EXTRA_VARIANTS", "").split(";"):
     if arg.strip():
         name, flags = arg.split("=", 1)
@@ -49,12 +58,21 @@ def build():
                 text = text.replace(old, new)
             with open(os.path.join(OUT, f"{name}.hip"), "w") as f:
                 f.write(text)
+    for name, rev in REV.items():  # that commit's sources, extracted whole
+        d = os.path.join(OUT, f"src_{name}")
+        os.makedirs(d, exist_ok=True)
+        tar = subprocess.run(["git", "-C", ROOT, "archive", rev, "include", "topotrafficrl_amd/csrc"], check=True,
+                             capture_output=True).stdout
+        subprocess.run(["tar", "-x", "-C", d], input=tar, check=True)
     only = os.environ.get("ONLY")  # build just these (comma-separated)
     for name, flags in {**VARIANTS, **TIMING}.items():
         if only and name not in only.split(","):
             continue
+        base = os.path.join(OUT, f"src_{name}") if name in REV else ROOT
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
-               "-shared", "-mllvm", "-disable-machine-licm", "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "topotrafficrl_amd", "csrc"), *flags, "-o", os.path.join(OUT, f"lib_{name}.so"),
+               "-shared", "-mllvm", "-disable-machine-licm", "-I", os.path.join(base, "include"), "-I",
+               os.path.join(base, "topotrafficrl_amd", "csrc"), *flags, "-o", os.path.join(OUT, f"lib_{name}.so"),
+               os.path.join(base, "topotrafficrl_amd", "csrc", "ttrl_mi355x.hip") if name in REV else
                head if name.startswith("head") else
                os.path.join(OUT, f"{name}.hip") if name in SOURCE_EDITS else src]
         procs.append(subprocess.Popen(cmd))
@@ -74,7 +92,10 @@ def run(dtypes, E=4096, N=64, rounds=7):
     P = _abi.default_params()
     libs = {}
     for name in VARIANTS:
-        lib = _lib.load(os.path.join(OUT, f"lib_{name}.so"))
+        if not os.path.exists(os.path.join(OUT, f"lib_{name}.so")):
+            print(f"  (variant {name} not built: skipped)")
+            continue
+        lib = _lib.load(os.path.join(OUT, f"lib_{name}.so"), check_abi=name not in REV)
         lib.ttrl_simulate.argtypes = [C.c_void_p] * 4 + [C.c_int32, C.c_double, C.c_void_p]
         libs[name] = lib
     ix = os.environ.get("IX") == "1"  # the intersection scenario (NET_GRAPH instance), 32 slots
@@ -104,7 +125,7 @@ def run(dtypes, E=4096, N=64, rounds=7):
         torch.cuda.synchronize()
         ref = None
         work = base.clone()
-        times = {k: [] for k in VARIANTS}
+        times = {k: [] for k in libs}
         for r in range(rounds):
             for name, lib in libs.items():
                 work.copy_(base)

@@ -42,10 +42,10 @@ _SIGS = {
     "ttrl_ix_reset_parts": ([_P, _P, _P, _P, C.c_int32, _P, C.c_int32, _P, _P, C.c_int32, _P, _P], C.c_int),
     "ttrl_ix_clear_spawn": ([_P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_ix_step_tail": ([_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, C.c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                           C.c_int32, _P],
+                           _P],
                           C.c_int),
     "ttrl_ix_env_step": ([_P, _P, _P, _P, _P, C.c_int32, C.c_double, _P, _P, _P, _P, _P, _P, _P, C.c_double, _P, _P,
-                          _P, _P, _P, _P, _P, _P, C.c_int32, _P, _P], C.c_int),
+                          _P, _P, _P, _P, _P, _P, _P, _P, C.c_int32, _P, _P, _P, _P, C.c_int32, _P, _P], C.c_int),
     "ttrl_copy_envs": ([_P, _P, _P, _P], C.c_int),
     "ttrl_ego_attention_sizes": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P], C.c_int64),
     "ttrl_ego_attention_q": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, C.c_int32, _P, _P, _P], C.c_int),
@@ -61,8 +61,10 @@ class TTRLError(RuntimeError):
     pass
 
 
-def load(path: str | None = None) -> C.CDLL:
-    """Load (once) and return the HIP library; raises if it is not built."""
+def load(path: str | None = None, check_abi: bool = True) -> C.CDLL:
+    """Load (once) and return the HIP library; raises if it is not built.  ``check_abi`` False:
+    an earlier round's build loaded by path for an A/B timing of entry points whose signature
+    did not change (tools/variants.py REV_VARIANTS; ttrl_simulate only)."""
     global _lib
     if _lib is not None and path is None:
         return _lib
@@ -80,7 +82,7 @@ def load(path: str | None = None) -> C.CDLL:
             continue  # an older build loaded for comparison (tools/variants.py)
         fn.argtypes = args
         fn.restype = res
-    if lib.ttrl_abi_version() != 7:  # include/ttrl_mi355x.h TTRL_ABI_VERSION
+    if (check_abi or path is None) and lib.ttrl_abi_version() != 7:  # include/ttrl_mi355x.h TTRL_ABI_VERSION
         raise ImportError("ABI version mismatch with include/ttrl_mi355x.h")
     if path is None:
         _lib = lib

@@ -1860,10 +1860,20 @@ template <bool L, typename T> struct Own {
 struct IxEpi {
   ttrl_ix_cfg_t C;
   double lane_change_delay;  // ttrl_params_t's, float64 as in the scene kernels (a spawn's IDM timer)
-  float* obs2;               // [E, V, F]: an env that goes on keeps the step's observation as its next
+  float* obs2;               // [E, V, F]: the next observation (an env that goes on keeps this step's)
   int32_t* ids2;             // [E, V - 1] (or null)
   unsigned long long* live;  // optional: += the vehicles present after the tail
   int32_t* live_env;         // optional [E]: each env's vehicles present after the tail (ix_order_kernel)
+  // the auto-reset from scenes reset ahead of time (ttrl_ix_step_tail's, see there): a finished env
+  // takes spare row par[e] * E + e
+  ttrl_state_t spare;        // K * E rows
+  int K;
+  uint8_t* par;              // [E]
+  uint32_t* ent;             // [E][nw], the episode counter last
+  uint32_t* spare_ent;       // [K * E][nw]
+  int nw;
+  uint8_t* done;             // [E] out
+  uint8_t* spare_mask;       // [K * E] out
 };
 
 template <typename T, int NS, int EPW>
@@ -4663,22 +4673,24 @@ __device__ int seg_closest_lane(const ttrl_lane_table_t& R, double x, double y, 
 }
 
 // The simulate launch's epilogue under ttrl_ix_env_step (one wavefront per workgroup, an env's
-// vehicles on NS lanes of it), from the final LDS state:
+// vehicles on NS lanes of it), from the final LDS state -- IntersectionEnv.step after the frames
+// (intersection_env.py:135-139 over abstract.py:224-250) and the auto-reset (abstract.py:188-214):
 //  (a) the step tail (step_tail: time, reward, terminated, truncated, info terms), as ttrl_env_step;
-//  (b) the Kinematics observation of the final state (kin_observe, np_random's shuffle), written to
-//      so.obs and, for an env that goes on, to ie.obs2 as well (its next observation);
-//  (c) an env that goes on: _clear_vehicles (intersection_env.py:350-362) -- the IDM vehicles on an
-//      exit lane within leave_margin of its end or without a route are dropped, the others keep
-//      list order (each lane takes the row of the i-th kept slot: register fields by lane
-//      shuffles, the LDS ones by the lane that owns the destination) -- then _spawn_vehicle
-//      (:320-348) with every lane of the env replaying its np_random (wave_spawn's draws, 15 m test
-//      by a segment ballot, closest lane by segment shuffles);
-//  (d) the rows to HBM: a finished env's as ttrl_env_step stores them (ttrl_ix_step_tail then
-//      swaps in its spare scene), an env that goes on every field of every slot (absent ones as
-//      row_absent, as wave_compact leaves them);
-//  (e) the live counts of the envs that go on (live, live_env).
-// Bit for bit the separate launches: ttrl_env_step, then ix_step_tail_kernel's clear / spawn
-// (test_fused_tail_equals_the_separate_tail, test_overlapped_resets_equal_in_place_resets).
+//  (b) the Kinematics observation of the final state (kin_observe, np_random's shuffle) into so.obs
+//      and, for an env that goes on, into ie.obs2 as well (its next observation);
+//  (c) an env that goes on: _clear_vehicles (:350-362) -- the IDM vehicles on an exit lane within
+//      leave_margin of its end or without a route are dropped, the others keep list order (each
+//      lane takes the row of the i-th kept slot by lane shuffles) -- then (d) _spawn_vehicle
+//      (:320-348), every lane of the env replaying its np_random (wave_spawn's draws; the 15 m test
+//      by a segment ballot, the closest lane by segment shuffles);
+//  (e) the rows to HBM: an env that goes on every field of every slot (absent ones as row_absent,
+//      as wave_compact leaves them); a finished env takes its spare scene instead, row par[e] * E + e
+//      (every field, the regulation and np_random words included; its final rows are discarded, as
+//      the reset discards them), and (f) the tail's counters (episode words, parity, time, masks);
+//  (g) a finished env's first observation of the new scene into ie.obs2 (kin_observe from HBM);
+//  (h) the live counts (live, live_env).
+// Bit for bit ttrl_env_step followed by ttrl_ix_step_tail (test_fused_tail_equals_the_separate_tail,
+// test_overlapped_resets_equal_in_place_resets).
 template <typename T, int NS, int EPW>
 __device__ __forceinline__ void ix_epilogue(const View<T>& V, const ttrl_state_t& st, const ttrl_lane_table_t& R,
                                             const ParamsT<T>& P, const StepOut& so, const IxEpi& ie, int le, int i,
@@ -4687,7 +4699,7 @@ __device__ __forceinline__ void ix_epilogue(const View<T>& V, const ttrl_state_t
   static_assert(NS * EPW == 64, "the fused tail runs on the one-wavefront road-network instance");
   constexpr unsigned long long SEG = NS == 64 ? ~0ull : ((1ull << NS) - 1);
   constexpr int M = EPW * NS;
-  const int N = st.n_veh;
+  const int N = st.n_veh, E = st.n_envs;
   const int kind = V.kind[me];
   const bool present = kind != TTRL_ABSENT;
   char* scr = (char*)V.afree;
@@ -4697,25 +4709,27 @@ __device__ __forceinline__ void ix_epilogue(const View<T>& V, const ttrl_state_t
   int* s_cnt = (int*)(s_p + EPW);
   int* s_ego = s_cnt + EPW;
   if (i == 0 && env_on) st.reg_steps[env] = reg;
-  // (a) the step tail; V.nitem[le] (dead since the last act phase): 1 = the env goes on
+  // (a) the step tail; V.nitem[le] (dead since the last act phase): -1 the env goes on, else the
+  // spare slot a finished env takes (-2: no env)
   if (i == 0) s_ego[le] = N;
   __syncthreads();
   if (present && kind == TTRL_MDP) atomicMin(&s_ego[le], i);
   __syncthreads();
   if (i == 0) {
-    bool go = false;
+    int st8 = -2;
     if (env_on) {
       const int ego = s_ego[le];
       step_tail<T>(R, V.lanes + (ego < N ? (int)V.lane[eb + ego] : 0), so.rcfg, env, ego < N, V.x[eb + ego % N],
                    V.y[eb + ego % N], V.v[eb + ego % N], (int)V.lane[eb + ego % N],
                    (V.flags[eb + ego % N] & FL_CRASHED) != 0, V.v[eb], (V.flags[eb] & FL_CRASHED) != 0, so.time,
                    so.time_inc, so.reward, so.term, so.trunc, so.comp, (T*)so.ego_speed, so.ego_crashed);
-      go = !so.term[env] && !so.trunc[env];
+      st8 = !so.term[env] && !so.trunc[env] ? -1 : (int)ie.par[env];
     }
-    V.nitem[le] = go ? 1 : 0;
+    V.nitem[le] = st8;
   }
   __syncthreads();
-  const bool go_on = V.nitem[le] != 0;
+  const int pslot = V.nitem[le];
+  const bool go_on = pslot == -1, fin = pslot >= 0;
   // (b) the observation of the final state
   {
     auto ego_of = [&](int ego, T& ex, T& ey, T& eh, T& ev, T& ec, T& es, int& elane) {
@@ -4808,41 +4822,66 @@ __device__ __forceinline__ void ix_epilogue(const View<T>& V, const ttrl_state_t
     }
     if (i == 0) rng_store(g, w);
   }
-  // (e) the rows, LDS -> HBM
-  if (slot) {
+  // (e) the rows to HBM
+  if (slot && go_on) {  // every field of every slot (compaction moved them)
     const int kd = V.kind[me];
     const int fl = V.flags[me];
-    if (go_on) {  // every field of every slot (compaction moved them)
-      Row<T> r = row_absent<T>();
-      if (kd != TTRL_ABSENT) {
-        r.f[0] = V.x[me]; r.f[1] = V.y[me]; r.f[2] = V.h[me]; r.f[3] = V.v[me]; r.f[4] = V.ts[me];
-        r.f[5] = timer; r.f[6] = V.delta[me]; r.f[7] = steer; r.f[8] = acc; r.f[9] = ix; r.f[10] = iy;
-        r.lane = V.lane[me]; r.tgt = V.tgt[me]; r.sidx = sidx;
-        r.route_road = ((const int32_t*)V.rroad)[me]; r.route_lane = ((const int32_t*)V.rlane)[me];
-        r.kind = (uint8_t)kd; r.crashed = (fl & FL_CRASHED) ? 1 : 0; r.has_impact = (fl & FL_IMPACT) ? 1 : 0;
-        r.lane_change = (fl & FL_LC) ? 1 : 0; r.yielding = (fl & FL_YIELD) ? 1 : 0; r.route_n = V.rn[me];
-      }
+    Row<T> r = row_absent<T>();
+    if (kd != TTRL_ABSENT) {
+      r.f[0] = V.x[me]; r.f[1] = V.y[me]; r.f[2] = V.h[me]; r.f[3] = V.v[me]; r.f[4] = V.ts[me];
+      r.f[5] = timer; r.f[6] = V.delta[me]; r.f[7] = steer; r.f[8] = acc; r.f[9] = ix; r.f[10] = iy;
+      r.lane = V.lane[me]; r.tgt = V.tgt[me]; r.sidx = sidx;
+      r.route_road = ((const int32_t*)V.rroad)[me]; r.route_lane = ((const int32_t*)V.rlane)[me];
+      r.kind = (uint8_t)kd; r.crashed = (fl & FL_CRASHED) ? 1 : 0; r.has_impact = (fl & FL_IMPACT) ? 1 : 0;
+      r.lane_change = (fl & FL_LC) ? 1 : 0; r.yielding = (fl & FL_YIELD) ? 1 : 0; r.route_n = V.rn[me];
+    }
+    row_store<T>(st, k, r);
+  }
+  if (fin) {  // the spare scene: every slot of row par * E + env (copy_env_rows' fields)
+    const int row = pslot * E + env;
+    Row<T> r = row_absent<T>();
+    if (i < N) {
+      r = row_load<T>(ie.spare, (size_t)row * N + i);
       row_store<T>(st, k, r);
-    } else {  // as ttrl_env_step stores them
-      Veh<T> a;
-      a.x = V.x[me]; a.y = V.y[me]; a.h = V.h[me]; a.v = V.v[me]; a.ts = V.ts[me]; a.timer = timer;
-      a.steer = steer; a.acc = acc; a.ix = ix; a.iy = iy;
-      a.lane = V.lane[me]; a.tgt = V.tgt[me]; a.sidx = sidx;
-      a.crashed = (fl & FL_CRASHED) != 0; a.hasimp = (fl & FL_IMPACT) != 0;
-      if (kd == TTRL_ABSENT) {  // absent rows pass through untouched
-        a.x = ((const T*)st.x)[k]; a.lane = st.lane[k]; a.tgt = st.target_lane[k];
-      }
-      store_veh(a, st, k);
-      for (int q = 0; q < TTRL_ROUTE_MAX; ++q) {
-        st.route_road[k * TTRL_ROUTE_MAX + q] = V.rroad[me * TTRL_ROUTE_MAX + q];
-        st.route_lane[k * TTRL_ROUTE_MAX + q] = V.rlane[me * TTRL_ROUTE_MAX + q];
-      }
-      st.route_n[k] = V.rn[me];
-      st.yielding[k] = (fl & FL_YIELD) ? 1 : 0;
+    }
+    if (i == 0) st.reg_steps[env] = ie.spare.reg_steps[row];
+    if (i < TTRL_RNG_WORDS) st.rng[(size_t)env * TTRL_RNG_WORDS + i] = ie.spare.rng[(size_t)row * TTRL_RNG_WORDS + i];
+    // the new scene into the env's (dead) view rows for its observation: the same values (g) would
+    // load back from HBM
+    V.x[me] = r.f[0]; V.y[me] = r.f[1]; V.h[me] = r.f[2]; V.v[me] = r.f[3];
+    V.lane[me] = (int8_t)(i < N ? r.lane : 0);
+    V.kind[me] = (uint8_t)(i < N ? r.kind : TTRL_ABSENT);
+    const SinCos<T> sc = k_sincos(r.f[2]);
+    V.ch[me] = sc.c; V.sh[me] = sc.s;
+  }
+  // (f) the tail's counters (ix_step_tail_kernel's)
+  if (i == 0 && env_on) {
+    ie.done[env] = fin ? 1 : 0;
+    for (int q = 0; q < ie.K; ++q) ie.spare_mask[(size_t)q * E + env] = fin && q == pslot;
+    if (fin) {
+      const int row = pslot * E + env;
+      ie.ent[(size_t)env * ie.nw + ie.nw - 1] += 1u;
+      ie.spare_ent[(size_t)row * ie.nw + ie.nw - 1] += (unsigned)ie.K;  // this slot's next episode
+      ie.par[env] = (uint8_t)(pslot + 1 == ie.K ? 0 : pslot + 1);
+      so.time[env] = 0.0;
     }
   }
-  // (f) the live counts of an env that goes on (a finished env's: ttrl_ix_step_tail)
-  if (go_on && i == 0) {
+  __syncthreads();  // the new scenes' view rows and np_random words
+  // (g) a finished env's first observation of its new scene (ix_step_tail_kernel's, from the view)
+  {
+    const int kd = V.kind[me];
+    const bool pr = fin && kd != TTRL_ABSENT;
+    if (fin) n_live = __popcll((__ballot(pr) >> eb) & SEG);
+    auto ego_of = [&](int ego, T& ex, T& ey, T& eh, T& ev, T& ec, T& es, int& elane) {
+      ex = V.x[eb + ego]; ey = V.y[eb + ego]; eh = V.h[eb + ego]; ev = V.v[eb + ego]; elane = V.lane[eb + ego];
+      ec = V.ch[eb + ego]; es = V.sh[eb + ego];
+    };
+    kin_observe<T, NS, EPW>(st, V.lanes, P, so.kcfg, fin, env, V.x[me], V.y[me], V.h[me], V.v[me], V.ch[me], V.sh[me],
+                            (int)V.lane[me], pr, pr && kd == TTRL_MDP, ego_of, s_key, s_cnt, s_ego, s_perm, s_p,
+                            ie.obs2, ie.ids2);
+  }
+  // (h) the live counts
+  if (env_on && i == 0) {
     if (ie.live_env) ie.live_env[env] = n_live;
     if (ie.live) atomicAdd(ie.live, (unsigned long long)n_live);
   }
@@ -4913,9 +4952,6 @@ struct IxTail {
   int32_t* ids_out;
   unsigned long long* live;  // optional: += the vehicles present after the tail (the next step's)
   int32_t* live_env;         // optional [E]: each env's vehicles present after the tail
-  // the envs that go on were cleared / spawned, observed and counted by ttrl_ix_env_step's launch:
-  // only the finished ones are handled here (obs_out / ids_out: that launch's next observation)
-  bool cleared;
 };
 
 // The env's present vehicles after the tail: added to *t.live (one atomic per env) and / or
@@ -4994,7 +5030,6 @@ __global__ void __launch_bounds__(64) ix_step_tail_kernel(ttrl_state_t st, ttrl_
       t.done[env] = 0;
       for (int q = 0; q < t.K; ++q) t.spare_mask[q * E + env] = 0;
     }
-    if (t.cleared) return;
     if (t.obs) {  // the row observed by the fused launch stays this step's observation
       for (int q = lane; q < V * F; q += 64) t.obs_out[(size_t)env * V * F + q] = t.obs_in[(size_t)env * V * F + q];
       if (t.ids_out)
@@ -5618,7 +5653,7 @@ int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
                       const uint8_t* truncated, uint8_t* spare_parity, uint32_t* entropy, uint32_t* spare_entropy,
                       int32_t n_words, double* time, uint8_t* done, uint8_t* spare_mask,
                       const ttrl_kin_cfg_t* obs_cfg, const float* obs_in, float* obs_out, const int32_t* obs_ids_in,
-                      int32_t* obs_ids_out, int64_t* live_count, int32_t* order, int32_t cleared, void* stream) {
+                      int32_t* obs_ids_out, int64_t* live_count, int32_t* order, void* stream) {
   int rc = check_ix(s, road, p, cfg);
   if (rc) return rc < 0 ? rc : TTRL_OK;
   if (!spare || !terminated || !truncated || !spare_parity || !entropy || !spare_entropy || n_words < 1 ||
@@ -5635,13 +5670,10 @@ int ttrl_ix_step_tail(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
   for (const void* q : sp)
     if (!q) return TTRL_E_ARG;
   if (obs_cfg) {  // the re-observation puts one slot on each lane of the env's wavefront
-    if (check_kin_cfg(s, obs_cfg) || (!cleared && !obs_in) || !obs_out || (!cleared && (!obs_ids_in) != (!obs_ids_out)) ||
-        s->n_veh > 64)
+    if (check_kin_cfg(s, obs_cfg) || !obs_in || !obs_out || (!obs_ids_in) != (!obs_ids_out) || s->n_veh > 64)
       return obs_cfg && s->n_veh > 64 ? TTRL_E_UNSUPPORTED : TTRL_E_ARG;
   }
-  if (cleared && !obs_cfg) return TTRL_E_ARG;  // after ttrl_ix_env_step, whose observation is Kinematics
   IxTail t{};
-  t.cleared = cleared != 0;
   t.spare = *spare; t.K = K; t.term = terminated; t.trunc = truncated; t.par = spare_parity; t.ent = entropy;
   t.spare_ent = spare_entropy; t.nw = n_words; t.time = time; t.done = done; t.spare_mask = spare_mask;
   t.live = reinterpret_cast<unsigned long long*>(live_count);
@@ -5668,10 +5700,25 @@ int ttrl_ix_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const
                      const ttrl_kin_cfg_t* obs_cfg, float* obs, int32_t* obs_ids, float* obs_next, int32_t* ids_next,
                      const ttrl_reward_cfg_t* reward_cfg, double* time, double time_inc, float* reward,
                      uint8_t* terminated, uint8_t* truncated, float* components, void* ego_speed,
-                     uint8_t* ego_crashed, int32_t* order, const int32_t* action_lut, int32_t n_action_lut,
-                     int64_t* live_count, void* stream) {
+                     uint8_t* ego_crashed, const ttrl_state_t* spare, uint8_t* spare_parity, uint32_t* entropy,
+                     uint32_t* spare_entropy, int32_t n_words, uint8_t* done, uint8_t* spare_mask, int32_t* order,
+                     const int32_t* action_lut, int32_t n_action_lut, int64_t* live_count, void* stream) {
   int rc = check_ix(s, road, p, cfg);
   if (rc) return rc < 0 ? rc : TTRL_OK;
+  if (!spare || !spare_parity || !entropy || !spare_entropy || n_words < 1 || n_words > 65 || !done || !spare_mask)
+    return TTRL_E_ARG;
+  const int K = spare->n_envs / s->n_envs;
+  if (K < 2 || K > 16 || spare->n_envs != K * s->n_envs || spare->n_veh != s->n_veh || spare->dtype != s->dtype ||
+      !spare->rng || !spare->reg_steps || !spare->route_road || !spare->route_lane || !spare->route_n || !spare->yielding)
+    return TTRL_E_ARG;
+  {
+    const void* sp[] = {spare->x, spare->y, spare->heading, spare->speed, spare->target_speed, spare->timer,
+                        spare->delta, spare->steer, spare->acc, spare->impact_x, spare->impact_y, spare->lane,
+                        spare->target_lane, spare->speed_index, spare->kind, spare->crashed, spare->has_impact,
+                        spare->lane_change};
+    for (const void* q : sp)
+      if (!q) return TTRL_E_ARG;
+  }
   if (!obs_cfg || !obs || !obs_next || check_kin_cfg(s, obs_cfg) || (!obs_ids) != (!ids_next)) return TTRL_E_ARG;
   if (!reward_cfg || !time || !reward || !terminated || !truncated || (!ego_speed) != (!ego_crashed))
     return TTRL_E_ARG;
@@ -5692,14 +5739,22 @@ int ttrl_ix_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const
   ie.lane_change_delay = p->lane_change_delay;
   ie.obs2 = obs_next; ie.ids2 = ids_next;
   ie.live = reinterpret_cast<unsigned long long*>(live_count);
-  const bool two = slots_for(s->n_veh) == 32;  // two envs per wavefront
-  if (order && s->n_envs % (two ? 2 : 1) == 0) ie.live_env = order + s->n_envs;  // ix_order_kernel's input
+  ie.spare = *spare; ie.K = K; ie.par = spare_parity; ie.ent = entropy; ie.spare_ent = spare_entropy;
+  ie.nw = n_words; ie.done = done; ie.spare_mask = spare_mask;
+  const int G = slots_for(s->n_veh) == 32 ? 2 : 1;  // envs per wavefront (the dispatch order's groups)
+  const bool ordered = order && s->n_envs % G == 0;
+  if (ordered) ie.live_env = order + s->n_envs;  // ix_order_kernel's input
   hipStream_t st = (hipStream_t)stream;
   if (s->dtype == TTRL_F64)
-    return two ? launch_sim_ix<double, 32, 2>(*s, *road, *p, actions, frames, dt, st, so, ie)
-               : launch_sim_ix<double, 64, 1>(*s, *road, *p, actions, frames, dt, st, so, ie);
-  return two ? launch_sim_ix<float, 32, 2>(*s, *road, *p, actions, frames, dt, st, so, ie)
-             : launch_sim_ix<float, 64, 1>(*s, *road, *p, actions, frames, dt, st, so, ie);
+    rc = G == 2 ? launch_sim_ix<double, 32, 2>(*s, *road, *p, actions, frames, dt, st, so, ie)
+                : launch_sim_ix<double, 64, 1>(*s, *road, *p, actions, frames, dt, st, so, ie);
+  else
+    rc = G == 2 ? launch_sim_ix<float, 32, 2>(*s, *road, *p, actions, frames, dt, st, so, ie)
+                : launch_sim_ix<float, 64, 1>(*s, *road, *p, actions, frames, dt, st, so, ie);
+  if (rc) return rc;
+  if (ordered)  // the next step's dispatch order, as ttrl_ix_step_tail writes it
+    hipLaunchKernelGGL(ix_order_kernel, dim3(1), dim3(1024), 0, st, order, s->n_envs, G, G * s->n_veh);
+  return launch_status();
 }
 
 int ttrl_rewards_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_reward_cfg_t* cfg,

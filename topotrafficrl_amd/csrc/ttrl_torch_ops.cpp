@@ -403,7 +403,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ix_step_tail_(
     const at::Tensor& entropy, const at::Tensor& spare_entropy, const at::Tensor& time,
     const c10::optional<at::Tensor>& kin_cfg, const c10::optional<at::Tensor>& obs,
     const c10::optional<at::Tensor>& ids, const c10::optional<at::Tensor>& live_count,
-    const c10::optional<at::Tensor>& order, bool cleared) {
+    const c10::optional<at::Tensor>& order) {
   check_hip(state[0]);
   ttrl_state_t s = state_of(state), sp = state_of(spare);
   const auto& x = state[0];
@@ -430,17 +430,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ix_step_tail_(
   check_time(time, s, x);
   const ttrl_kin_cfg_t* kc = kin_cfg && kin_cfg->defined() ? as_struct<ttrl_kin_cfg_t>(*kin_cfg, "kin_cfg") : nullptr;
   at::Tensor obs_out, ids_out, oin, iin;
-  TORCH_CHECK(!cleared || kc, "ttrl: cleared (after ix_env_step_) needs its kin_cfg");
-  if (kc && cleared) {  // ix_env_step_'s obs_next / ids_next: the finished envs' rows are written in place
-    TORCH_CHECK(obs && obs->defined() && ids && ids->defined() && obs->is_contiguous() && ids->is_contiguous(),
-                "ttrl: cleared needs ix_env_step_'s contiguous obs_next and ids_next");
-    std::tie(obs_out, ids_out) = kin_outputs(x, kc);
-    TORCH_CHECK(obs->device() == x.device() && obs->scalar_type() == at::kFloat && obs->sizes() == obs_out.sizes() &&
-                    ids->device() == x.device() && ids->scalar_type() == at::kInt && ids->sizes() == ids_out.sizes(),
-                "ttrl: obs / ids must be ix_env_step_'s float32 [E, V, F] / int32 [E, V-1] next observation");
-    obs_out = *obs;
-    ids_out = *ids;
-  } else if (kc) {
+  if (kc) {
     TORCH_CHECK(obs && obs->defined() && ids && ids->defined(), "ttrl: a kin_cfg needs the step's obs and ids");
     std::tie(obs_out, ids_out) = kin_outputs(x, kc);
     oin = obs->contiguous();
@@ -471,31 +461,46 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ix_step_tail_(
                        static_cast<uint8_t*>(spare_parity.data_ptr()), reinterpret_cast<uint32_t*>(entropy.data_ptr()),
                        reinterpret_cast<uint32_t*>(spare_entropy.data_ptr()), static_cast<int32_t>(entropy.size(1)),
                        time.data_ptr<double>(), static_cast<uint8_t*>(done.data_ptr()),
-                       static_cast<uint8_t*>(smask.data_ptr()), kc,
-                       kc && !cleared ? oin.data_ptr<float>() : nullptr, kc ? obs_out.data_ptr<float>() : nullptr,
-                       kc && !cleared ? iin.data_ptr<int32_t>() : nullptr, kc ? ids_out.data_ptr<int32_t>() : nullptr,
-                       lc ? live_count->data_ptr<int64_t>() : nullptr, od ? order->data_ptr<int32_t>() : nullptr,
-                       cleared ? 1 : 0, stream_of(x)),
+                       static_cast<uint8_t*>(smask.data_ptr()), kc, kc ? oin.data_ptr<float>() : nullptr,
+                       kc ? obs_out.data_ptr<float>() : nullptr, kc ? iin.data_ptr<int32_t>() : nullptr,
+                       kc ? ids_out.data_ptr<int32_t>() : nullptr, lc ? live_count->data_ptr<int64_t>() : nullptr,
+                       od ? order->data_ptr<int32_t>() : nullptr, stream_of(x)),
      "ttrl_ix_step_tail");
   return {done, smask, obs_out, ids_out};
 }
 
-// IntersectionEnv.step for the envs that go on, in one launch (ttrl_ix_env_step): env_step_'s eight
-// outputs, then obs_next / ids_next (the envs that go on keep this step's observation as their next;
-// the finished ones' rows are written by ix_step_tail_(..., cleared=True)).  live_count / order as
-// ix_step_tail_ takes them.
+// VecIntersectionEnv.step with the auto-reset from spare scenes, in one launch (ttrl_ix_env_step):
+// env_step_'s eight outputs, then done [E] bool, spare_mask [K * E] uint8 and the next observation
+// obs_next / ids_next -- ix_step_tail_'s outputs -- with the same spare / parity / entropy / time /
+// live_count / order arguments as env_step_ followed by ix_step_tail_.
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor,
-           at::Tensor>
+           at::Tensor, at::Tensor, at::Tensor>
 ix_env_step_(at::TensorList state, const at::Tensor& lanes, const at::Tensor& params, const at::Tensor& cfg,
              const c10::optional<at::Tensor>& actions, int64_t frames, double dt, const at::Tensor& kin_cfg,
-             const at::Tensor& reward_cfg, const at::Tensor& time, double time_inc,
+             const at::Tensor& reward_cfg, const at::Tensor& time, double time_inc, at::TensorList spare,
+             const at::Tensor& spare_parity, const at::Tensor& entropy, const at::Tensor& spare_entropy,
              const c10::optional<at::Tensor>& order, at::OptionalIntArrayRef action_lut,
              const c10::optional<at::Tensor>& live_count) {
   check_hip(state[0]);
-  ttrl_state_t s = state_of(state);
+  ttrl_state_t s = state_of(state), sp = state_of(spare);
   const auto& x = state[0];
   const auto* kc = as_struct<ttrl_kin_cfg_t>(kin_cfg, "kin_cfg");
   check_time(time, s, x);
+  const int64_t K = s.n_envs > 0 ? sp.n_envs / s.n_envs : 0;
+  TORCH_CHECK(spare[0].device() == x.device() && K >= 2 && K <= 16 && sp.n_envs == K * s.n_envs &&
+                  sp.n_veh == s.n_veh && sp.dtype == s.dtype,
+              "ttrl: spare must be a state of K * n_envs rows (K in [2, 16]) of the same width and dtype on the "
+              "state's device");
+  TORCH_CHECK(spare_parity.device() == x.device() && spare_parity.scalar_type() == at::kByte &&
+                  spare_parity.is_contiguous() && spare_parity.numel() == s.n_envs,
+              "ttrl: spare_parity must be a contiguous uint8 [n_envs] tensor on the state's device");
+  TORCH_CHECK(entropy.dim() == 2 && entropy.size(0) == s.n_envs && entropy.scalar_type() == at::kInt &&
+                  entropy.is_contiguous() && entropy.device() == x.device(),
+              "ttrl: entropy must be a contiguous int32 [n_envs, n_words] tensor on the state's device");
+  TORCH_CHECK(spare_entropy.dim() == 2 && spare_entropy.size(0) == sp.n_envs &&
+                  spare_entropy.size(1) == entropy.size(1) && spare_entropy.scalar_type() == at::kInt &&
+                  spare_entropy.is_contiguous() && spare_entropy.device() == x.device(),
+              "ttrl: spare_entropy must be a contiguous int32 [K * n_envs, n_words] tensor on the state's device");
   at::Tensor a = dev_i32(actions, s.n_envs, x, "actions");
   const bool od = order && order->defined();
   if (od)
@@ -512,6 +517,8 @@ ix_env_step_(at::TensorList state, const at::Tensor& lanes, const at::Tensor& pa
     for (int64_t c : *action_lut) lut.push_back(static_cast<int32_t>(c));
   auto [obs, ids, rew, term, trunc, comp, speed, crashed] = env_step_outputs(x, kc);
   auto [obs2, ids2] = kin_outputs(x, kc);
+  at::Tensor done = at::empty({s.n_envs}, opts(x, at::kBool));
+  at::Tensor smask = at::empty({sp.n_envs}, opts(x, at::kByte));
   ok(ttrl_ix_env_step(&s, as_struct<ttrl_lane_table_t>(lanes, "lanes"), as_struct<ttrl_params_t>(params, "params"),
                       as_struct<ttrl_ix_cfg_t>(cfg, "cfg"), static_cast<const int32_t*>(ptr(a)),
                       static_cast<int32_t>(frames), dt, kc, obs.data_ptr<float>(), ids.data_ptr<int32_t>(),
@@ -519,11 +526,14 @@ ix_env_step_(at::TensorList state, const at::Tensor& lanes, const at::Tensor& pa
                       as_struct<ttrl_reward_cfg_t>(reward_cfg, "reward_cfg"), time.data_ptr<double>(), time_inc,
                       rew.data_ptr<float>(), static_cast<uint8_t*>(term.data_ptr()),
                       static_cast<uint8_t*>(trunc.data_ptr()), comp.data_ptr<float>(), speed.data_ptr(),
-                      static_cast<uint8_t*>(crashed.data_ptr()), od ? order->data_ptr<int32_t>() : nullptr,
-                      lut.empty() ? nullptr : lut.data(), static_cast<int32_t>(lut.size()),
-                      lc ? live_count->data_ptr<int64_t>() : nullptr, stream_of(x)),
+                      static_cast<uint8_t*>(crashed.data_ptr()), &sp, static_cast<uint8_t*>(spare_parity.data_ptr()),
+                      reinterpret_cast<uint32_t*>(entropy.data_ptr()),
+                      reinterpret_cast<uint32_t*>(spare_entropy.data_ptr()), static_cast<int32_t>(entropy.size(1)),
+                      static_cast<uint8_t*>(done.data_ptr()), static_cast<uint8_t*>(smask.data_ptr()),
+                      od ? order->data_ptr<int32_t>() : nullptr, lut.empty() ? nullptr : lut.data(),
+                      static_cast<int32_t>(lut.size()), lc ? live_count->data_ptr<int64_t>() : nullptr, stream_of(x)),
      "ttrl_ix_env_step");
-  return {obs, ids, rew, term, trunc, comp, speed, crashed, obs2, ids2};
+  return {obs, ids, rew, term, trunc, comp, speed, crashed, done, smask, obs2, ids2};
 }
 
 void copy_envs_(at::TensorList dst, at::TensorList src, const at::Tensor& mask) {
@@ -713,7 +723,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> meta_ix_step_tail(
     at::TensorList state, const at::Tensor&, const at::Tensor&, const at::Tensor&, at::TensorList, const at::Tensor&,
     const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&,
     const c10::optional<at::Tensor>& kin_cfg, const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&,
-    const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&, bool) {
+    const c10::optional<at::Tensor>&, const c10::optional<at::Tensor>&) {
   const auto& x = meta_x(state);
   const int64_t E = x.size(0);
   at::Tensor o = at::empty({0}, opts(x, at::kFloat)), i = at::empty({0}, opts(x, at::kInt));
@@ -721,16 +731,18 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> meta_ix_step_tail(
   return {at::empty({E}, opts(x, at::kBool)), at::empty({2 * E}, opts(x, at::kByte)), o, i};
 }
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor,
-           at::Tensor>
+           at::Tensor, at::Tensor, at::Tensor>
 meta_ix_env_step(at::TensorList state, const at::Tensor&, const at::Tensor&, const at::Tensor&,
                  const c10::optional<at::Tensor>&, int64_t, double, const at::Tensor& kin_cfg, const at::Tensor&,
-                 const at::Tensor&, double, const c10::optional<at::Tensor>&, at::OptionalIntArrayRef,
+                 const at::Tensor&, double, at::TensorList spare, const at::Tensor&, const at::Tensor&,
+                 const at::Tensor&, const c10::optional<at::Tensor>&, at::OptionalIntArrayRef,
                  const c10::optional<at::Tensor>&) {
   const auto& x = meta_x(state);
   const auto* kc = as_struct<ttrl_kin_cfg_t>(kin_cfg, "kin_cfg");
   auto [obs, ids, rew, term, trunc, comp, speed, crashed] = env_step_outputs(x, kc);
   auto [obs2, ids2] = kin_outputs(x, kc);
-  return {obs, ids, rew, term, trunc, comp, speed, crashed, obs2, ids2};
+  return {obs, ids, rew, term, trunc, comp, speed, crashed, at::empty({x.size(0)}, opts(x, at::kBool)),
+          at::empty({meta_x(spare).size(0)}, opts(x, at::kByte)), obs2, ids2};
 }
 at::Tensor meta_auto_reset(at::TensorList state, const at::Tensor&, const at::Tensor&, const at::Tensor&,
                            const at::Tensor&, int64_t, const at::Tensor&, const at::Tensor&, const at::Tensor&) {
@@ -803,13 +815,14 @@ TORCH_LIBRARY(ttrl, m) {
   m.def("copy_envs_(Tensor(a!)[] dst, Tensor[] src, Tensor mask) -> ()");
   m.def("ix_step_tail_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor[] spare, "
         "Tensor terminated, Tensor truncated, Tensor(b!) spare_parity, Tensor(c!) entropy, Tensor(d!) spare_entropy, "
-        "Tensor(e!) time, Tensor? kin_cfg, Tensor(h!)? obs, Tensor(i!)? ids, Tensor(f!)? live_count=None, "
-        "Tensor(g!)? order=None, bool cleared=False) -> (Tensor done, Tensor spare_mask, Tensor obs, Tensor ids)");
+        "Tensor(e!) time, Tensor? kin_cfg, Tensor? obs, Tensor? ids, Tensor(f!)? live_count=None, "
+        "Tensor(g!)? order=None) -> (Tensor done, Tensor spare_mask, Tensor obs, Tensor ids)");
   m.def("ix_env_step_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor cfg, Tensor? actions, int frames, "
-        "float dt, Tensor kin_cfg, Tensor reward_cfg, Tensor(b!) time, float time_inc, Tensor(c!)? order=None, "
+        "float dt, Tensor kin_cfg, Tensor reward_cfg, Tensor(b!) time, float time_inc, Tensor[] spare, "
+        "Tensor(e!) spare_parity, Tensor(f!) entropy, Tensor(g!) spare_entropy, Tensor(c!)? order=None, "
         "int[]? action_lut=None, Tensor(d!)? live_count=None) -> (Tensor obs, Tensor ids, Tensor reward, "
         "Tensor terminated, Tensor truncated, Tensor components, Tensor ego_speed, Tensor ego_crashed, "
-        "Tensor obs_next, Tensor ids_next)");
+        "Tensor done, Tensor spare_mask, Tensor obs_next, Tensor ids_next)");
   m.def("rewards(Tensor[] state, Tensor lanes, Tensor cfg, Tensor time) -> (Tensor reward, Tensor terminated, "
         "Tensor truncated)");
   m.def("rewards_ex(Tensor[] state, Tensor lanes, Tensor cfg, Tensor time) -> (Tensor reward, Tensor terminated, "

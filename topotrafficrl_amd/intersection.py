@@ -344,9 +344,16 @@ class VecIntersectionEnv:
             E = self.num_envs
             chunk, wf = int(c["reset_chunk_frames"]), int(self.ix.warmup_frames)
             # chunks must divide the warm-up, and the tail kernel rotates over at most 16 slots
-            self._chunk = chunk if 0 < chunk < wf and wf % chunk == 0 and wf // chunk + 1 <= 16 else 0
+            self._chunk = chunk if 0 < chunk < wf and wf % chunk == 0 and wf // chunk + 2 <= 16 else 0
             self._n_chunks = wf // self._chunk if self._chunk else 1
-            self._slots = self._n_chunks + 1 if self._chunk else 2  # spare scenes per env
+            # fuse_tail (ttrl_ix_env_step): the step launch itself takes the finished envs' spare
+            # scenes, so a chunked reset must be finished one step earlier than the two-launch step
+            # needs it (the launch waits for the finishes of two steps back, not the previous step's,
+            # which run beside it): one more spare scene per env.  The whole-warm-up rotation already
+            # waits for two steps back.
+            self._fuse = (bool(c["fuse_tail"]) and c["observation"].get("type", "Kinematics") == "Kinematics"
+                          and int(c["vehicle_slots"]) <= 64)
+            self._slots = self._n_chunks + (2 if self._fuse else 1) if self._chunk else 2  # spare scenes per env
             self._cohorts = []  # the consumed-row masks of the resets still warming up, oldest first
             self._spare = BatchState(self._slots * E, int(c["vehicle_slots"]), device=self.device, dtype=c["dtype"])
             self._spare_par = torch.zeros(E, dtype=torch.uint8, device=self.device)
@@ -358,6 +365,7 @@ class VecIntersectionEnv:
             self._sides = tuple(torch.cuda.Stream(self.device) for _ in range(n_sides))
             self._side_i = 0
             self._spare_ready = self._spare_prev = self._wait_ev = self._warm_ev = torch.cuda.Event()
+            self._fin_evs = [self._wait_ev, self._wait_ev]  # chunked: side stream B after each of the last two steps
             self._to_finish = None  # chunked: the cohort whose last chunk ran in the previous step
             # [slots * E, words + 1]: each spare scene's seed words and episode counter (the last
             # word); ix_step_tail_ advances the counter of a consumed row by the number of slots
@@ -415,6 +423,7 @@ class VecIntersectionEnv:
             self._pinned = []  # the side streams the current spare buffers are recorded on
             self._prepare_spares(None)
             self._spare_prev = self._wait_ev = self._warm_ev = self._spare_ready
+            self._fin_evs = [self._spare_ready, self._spare_ready]
         obs = self.observation_type.observe()
         self._rewards_and_dones()  # abstract.py:211 reset's _info evaluates _rewards too
         return obs, self._info(obs, None)
@@ -453,6 +462,9 @@ class VecIntersectionEnv:
                     self._wait_ev = torch.cuda.Event()
                     self._wait_ev.record(B)
                 self._to_finish = None
+            ev = torch.cuda.Event()  # B's position after this step's finishes (if any)
+            ev.record(B)
+            self._fin_evs = [self._fin_evs[-1], ev]
             A.wait_stream(main)  # A: begin this step's resets, warm every reset in flight one chunk
             self._cohorts.append(mask)
             for m in self._cohorts:  # read on A (a fork's cohorts were cloned on the main stream)
@@ -501,14 +513,14 @@ class VecIntersectionEnv:
         return obs, reward, terminated, truncated, info
 
     def _step_overlapped(self, action):
-        """The auto-reset step with overlapped resets in two launches: ttrl::ix_env_step_ (the fused
-        frames, the observation of the final state, the step tail: time += 1 / policy_frequency,
-        rewards, dones, info -- and, for the envs that go on, clear / spawn) and ttrl::ix_step_tail_
-        (the finished envs swap in their spare scene and are re-observed); then the consumed spare
-        rows are reset again on a side stream.  (``fuse_tail`` False, or a non-Kinematics
-        observation: ttrl::env_step_, and the clear / spawn in ix_step_tail_.)  Bit for bit the
-        in-place composition (simulate, observe, rewards, clear / spawn, reset, masked observe;
-        test_overlapped_resets_equal_in_place_resets)."""
+        """The auto-reset step with overlapped resets.  fuse_tail (Kinematics, <= 64 slots): one launch,
+        ttrl::ix_env_step_ (the fused frames, the observation of the final state, the step tail:
+        time += 1 / policy_frequency, rewards, dones, info; clear / spawn for the envs that go on;
+        the finished envs swap in their spare scenes and are observed), then the next dispatch order.
+        Otherwise two launches: ttrl::env_step_, then ttrl::ix_step_tail_ (clear / spawn, the swap).
+        Then the consumed spare rows are reset again on a side stream.  Bit for bit the in-place
+        composition (simulate, observe, rewards, clear / spawn, reset, masked observe;
+        test_overlapped_resets_equal_in_place_resets, test_fused_tail_equals_the_separate_tail)."""
         ot = self.observation_type
         kin = isinstance(ot, BatchedKinematicObservation)
         frames = int(self.config["simulation_frequency"] // self.config["policy_frequency"])
@@ -520,29 +532,33 @@ class VecIntersectionEnv:
         # (vehicle_slots > 64) take the masked observation launch instead, which draws the same
         # shuffles from the same generators (test_overlapped_resets_equal_in_place_resets[96])
         fused_obs = kin and self.state.n_veh <= 64
-        fuse = fused_obs and bool(self.config["fuse_tail"])
         dt, tinc = 1 / self.config["simulation_frequency"], 1 / self.config["policy_frequency"]
-        if fuse:  # the envs that go on are cleared / spawned inside the step launch
-            obs, ids, *outs, obs2, ids2 = self.road.ix_env_step(self.ix, idx, frames, dt, ot.fused_cfg(),
-                                                                self.reward_cfg, self.time, tinc, self._order, lut,
-                                                                self.live_counter)
+        main = torch.cuda.current_stream(self.device)
+        if self._fuse:
+            # one launch: the frames, the observation, the step tail, clear / spawn for the envs that go
+            # on, the spare scenes of the finished ones (ready: prepared two steps back at the latest)
+            main.wait_event(self._fin_evs[0] if self._chunk else self._wait_ev)
+            obs, ids, *outs, done, smask, obs2, ids2 = self.road.ix_env_step(
+                self.ix, idx, frames, dt, ot.fused_cfg(), self.reward_cfg, self.time, tinc, self._spare,
+                self._spare_par, self._entropy, self._spare_ent, self._order, lut, self.live_counter)
+            reward, terminated, truncated = _keep_tail(self, outs)
+            info = self._info(obs, action)
         else:
             obs, ids, *outs = self.road.env_step(idx, frames, dt, ot.fused_cfg() if kin else None, self.reward_cfg,
                                                  self.time, tinc, self._order, lut)
-        reward, terminated, truncated = _keep_tail(self, outs)
-        if not kin:
-            obs = ot.observe()
-        info = self._info(obs, action)
-        _device_only(self.state)
-        # the slots this step's tail takes were prepared two steps back at the latest (waited for
-        # here, after the step launch is queued: the side work gets the launch's time as slack)
-        torch.cuda.current_stream(self.device).wait_event(self._wait_ev)
-        done, smask, obs2, ids2 = ops.T.ix_step_tail_(
-            self.state.tensors(), ops.st(self.network.table), ops.st(self.params), ops.st(self.ix),
-            self._spare.tensors(), terminated, truncated, self._spare_par, self._entropy, self._spare_ent, self.time,
-            ops.kin_cfg_tensor(ot.fused_cfg()) if fused_obs else None,
-            (obs2 if fuse else obs) if fused_obs else None, (ids2 if fuse else ids) if fused_obs else None,
-            self.live_counter, self._order, cleared=fuse)
+            reward, terminated, truncated = _keep_tail(self, outs)
+            if not kin:
+                obs = ot.observe()
+            info = self._info(obs, action)
+            _device_only(self.state)
+            # the slots this step's tail takes were prepared two steps back at the latest (waited for
+            # here, after the step launch is queued: the side work gets the launch's time as slack)
+            main.wait_event(self._wait_ev)
+            done, smask, obs2, ids2 = ops.T.ix_step_tail_(
+                self.state.tensors(), ops.st(self.network.table), ops.st(self.params), ops.st(self.ix),
+                self._spare.tensors(), terminated, truncated, self._spare_par, self._entropy, self._spare_ent,
+                self.time, ops.kin_cfg_tensor(ot.fused_cfg()) if fused_obs else None, obs if fused_obs else None,
+                ids if fused_obs else None, self.live_counter, self._order)
         self._prepare_spares(smask)
         info["final_observation"], info["final_mask"] = obs, done
         if fused_obs:
@@ -636,5 +652,6 @@ class VecIntersectionEnv:
             new._spare_ready = torch.cuda.Event()
             new._spare_ready.record(torch.cuda.current_stream(self.device))
             new._spare_prev = new._wait_ev = new._warm_ev = new._spare_ready
+            new._fin_evs = [new._spare_ready, new._spare_ready]
         new.define_spaces()
         return new

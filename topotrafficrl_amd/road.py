@@ -119,18 +119,19 @@ class BatchedRoad:
 
     def ix_env_step(self, cfg: _abi.IxCfg, actions: torch.Tensor | None, frames: int, dt: float,
                     kin_cfg: _abi.KinCfg, reward_cfg: _abi.RewardCfg, time: torch.Tensor, time_inc: float,
-                    order: torch.Tensor | None = None, action_lut: list[int] | None = None,
-                    live_count: torch.Tensor | None = None):
-        """IntersectionEnv.step (intersection_env.py:135-139) in one launch for the envs that go on
-        (ttrl_ix_env_step): env_step's launch, and for every env neither terminated nor truncated its
-        _clear_vehicles / _spawn_vehicle (:320-362) from the final LDS rows.  Returns env_step's 8
-        tensors, then obs_next / ids_next: this step's observation for the envs that go on (their
-        next one); ix_step_tail_(..., cleared=True) writes the finished envs' rows after swapping in
-        their spare scenes.  ``order`` ([2 E], ix_step_tail_'s buffer) also receives the live counts
-        of the envs that go on; ``live_count`` (int64 scalar) += them."""
+                    spare: BatchState, spare_parity: torch.Tensor, entropy: torch.Tensor,
+                    spare_entropy: torch.Tensor, order: torch.Tensor | None = None,
+                    action_lut: list[int] | None = None, live_count: torch.Tensor | None = None):
+        """IntersectionEnv.step (intersection_env.py:135-139 over abstract.py:224-250) with the
+        auto-reset from spare scenes, in one launch (ttrl_ix_env_step): env_step's launch, then for
+        every env that goes on its _clear_vehicles / _spawn_vehicle (:320-362), and for every finished
+        env its spare scene and first observation.  Returns env_step's 8 tensors, then done,
+        spare_mask, obs_next, ids_next (ix_step_tail_'s outputs; spare / spare_parity / entropy /
+        spare_entropy / order / live_count as ix_step_tail_ takes them)."""
         a = None if actions is None else self._actions(actions)
         return ops.T.ix_env_step_(*self._args(), ops.st(cfg), a, int(frames), float(dt), ops.kin_cfg_tensor(kin_cfg),
-                                  ops.st(reward_cfg), time, float(time_inc), order, action_lut, live_count)
+                                  ops.st(reward_cfg), time, float(time_inc), spare.tensors(), spare_parity, entropy,
+                                  spare_entropy, order, action_lut, live_count)
 
     def neighbour_vehicles(self, query_lane: torch.Tensor | None = None):
         """Road.neighbour_vehicles (road.py:480-513) for every vehicle: (front, rear) slot ids, -1 = None."""
