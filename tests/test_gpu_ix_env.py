@@ -361,6 +361,42 @@ def test_deepcopy_forks_an_independent_env(hip_device):
     assert torch.equal(env.state["x"], fork.state["x"]) and env.state["x"].data_ptr() != fork.state["x"].data_ptr()
 
 
+def test_regulation_chunks_with_yields_vs_oracle(hip_device):
+    """RegulatedRoad.enforce_road_rules (regulation.py:34-103) with more live pairs in a wavefront
+    than one chunk of RQ_PAIRS (256) holds, on crossing routes: two dense envs share the wave (16
+    initial vehicles, a spawn every step), env 0's pairs first, env 1's after them, past the first
+    chunk; reset and fourteen steps equal the oracle, the yielding flags and every other discrete
+    field exact, and at steps with more than 256 pairs both envs yield (chunks that
+    contain conflicting pairs, yields decided in different chunks)."""
+    E = 2
+    cfg = {**ENV_JSON, "num_envs": E, "device": hip_device, "initial_vehicle_count": 16, "spawn_probability": 1.0,
+           "duration": 100}
+    env = VecIntersectionEnv(cfg)
+    env.reset(seed=11)
+    net = intersection_network()
+    o = Oracle(net.table, P_IX)
+    icfg = ix_cfg(net, {**VecIntersectionEnv.default_config(), **cfg}, P_IX)
+    h = HostState(E, 32)
+    o.ix_reset(h, icfg, [11 + e for e in range(E)])
+    o.observe_kinematics(h, KIN)
+    from test_ix_oracle import LONGI
+    acts = np.random.default_rng(3).integers(0, 3, size=(14, E))
+    chunked = 0  # steps with more than RQ_PAIRS live pairs in the wave and yields in both envs
+    for p in range(14):
+        live = (h["kind"] > 0).sum(1)
+        tot = int(sum(n * (n - 1) // 2 for n in live))
+        a = torch.from_numpy(acts[p]).to(hip_device)
+        env.step(a)
+        o.simulate(h, [LONGI[int(x)] for x in acts[p]], 15, 1 / 15)
+        chunked += tot > 256 and all(bool(h["yielding"][e].any()) for e in range(E))
+        o.observe_kinematics(h, KIN)
+        o.ix_clear_spawn(h, icfg)
+        st = env.state.to_numpy()
+        for e in range(E):
+            same_state(env_view(st, e), {k: v[e:e + 1] for k, v in h.a.items()}, EPISODE_TOL, f"dense {e} {p}")
+    assert chunked >= 2, chunked
+
+
 @pytest.mark.parametrize("slots", [16, 96])
 def test_slot_classes_match_the_oracle(slots, hip_device):
     """Other slot widths: 16 (tight: spawns beyond the last slot are dropped after their draws)
