@@ -66,14 +66,15 @@ def state_bytes(dtype: str) -> tuple[int, int]:
     return 11 * r + 3 * 4 + 4, 10 * r + 3 * 4 + 2
 
 
-def launch_bytes(E: int, N: int, dtype: str, obs_cfg: dict | None, graph: bool) -> int:
+def launch_bytes(E: int, N: int, dtype: str, obs_cfg: dict | None, graph: bool, grid_cells: int = 0) -> int:
     """Algorithmic HBM bytes of one env.step launch (ttrl_env_step): every slot's state read and
     written once (state_bytes); on a road network also its route rows (road, lane: 4 + 4 int8),
     route length and yield flag, read and written; per env the step tail (time read + written,
     reward, terminated, truncated, the 4 reward terms, the info's ego speed / crashed), the action
     read, and on a road network the regulation counter and np_random's 5 words (the shuffled
     observation draws from it), read and written, and the dispatch order read; the Kinematics
-    observation and its ids written once."""
+    observation and its ids written once; an OccupancyGrid written by the launch (ttrl_env_step_grid):
+    its ``grid_cells`` float32 cells per env written once."""
     rd, wr = state_bytes(dtype)
     r = 8 if dtype == "f64" else 4
     per_slot = rd + wr + (2 * (4 + 4 + 1 + 1) if graph else 0)
@@ -82,6 +83,7 @@ def launch_bytes(E: int, N: int, dtype: str, obs_cfg: dict | None, graph: bool) 
         V = obs_cfg.get("vehicles_count", 5)
         F = len(obs_cfg.get("features", ["presence", "x", "y", "vx", "vy"]))
         per_env += V * F * 4 + (V - 1) * 4
+    per_env += 4 * grid_cells
     return E * (N * per_slot + per_env)
 
 
@@ -368,7 +370,9 @@ def main():
                                   "fuse_tail": os.environ.get("TTRL_IX_FUSE_TAIL", "1") != "0"})
     else:
         env = VecHighwayEnv({"num_envs": E, "vehicles_count": N, "observation": C["obs"], "device": str(dev),
-                             "dtype": args.dtype, "env_id_offset": offset, "auto_reset": bool(args.auto_reset)})
+                             "dtype": args.dtype, "env_id_offset": offset, "auto_reset": bool(args.auto_reset),
+                             # A/B only: TTRL_FUSE_GRID=0 writes config 3's grid with its own kernel
+                             "fuse_grid": os.environ.get("TTRL_FUSE_GRID", "1") != "0"})
     policy = None
     if args.config == 5:
         from topotrafficrl_amd.agent import EgoAttentionPolicy
@@ -483,10 +487,16 @@ def main():
     value = veh_steps / elapsed
     rd, wr = state_bytes(args.dtype)
     # per env.step launch: the state, the step tail and (Kinematics) the observation (launch_bytes)
-    alg_bytes = launch_bytes(E, N, args.dtype, C["obs"], graph=ix)
+    # config 3: the launch writes the OccupancyGrid too (ttrl_env_step_grid) unless the A/B switch
+    # TTRL_FUSE_GRID=0 left it to the grid kernel (roofline_obs)
+    fused_grid = C["obs"]["type"] == "OccupancyGrid" and not grid_launches
+    cells = int(np.prod(env.observation_space.shape)) if fused_grid else 0
+    alg_bytes = launch_bytes(E, N, args.dtype, C["obs"], graph=ix, grid_cells=cells)
     kernel = "simulate_kernel (fused 15-frame Road.act+Road.step + step tail)"
     if C["obs"]["type"] == "Kinematics":  # the launch also writes the observation (ttrl_env_step)
         kernel = "simulate_kernel (fused 15-frame Road.act+Road.step + Kinematics observation + step tail)"
+    if fused_grid:
+        kernel = "simulate_grid_kernel (fused 15-frame Road.act+Road.step + OccupancyGrid + step tail)"
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     pmc, pmc_source = read_pmc(args.dtype, args.config)
     hbm = {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

@@ -20,6 +20,7 @@
  *   ttrl_observe_kinematics  KinematicObservation.observe  ttrl_env/envs/common/observation.py:233-275
  *                            (Road.close_objects_to road.py:418-447, Vehicle.to_dict kinematics.py:237-261)
  *   ttrl_observe_grid        OccupancyGridObservation.observe observation.py:353-483
+ *   ttrl_env_step_grid       AbstractEnv.step with that observation (abstract.py:224-250), one launch
  *   ttrl_reset_highway       scene init: Vehicle.create_random kinematics.py:50-104,
  *                            IDMVehicle.__init__/randomize_behavior behavior.py:48-69
  *   ttrl_rewards             reward/termination template  ttrl_env/envs/intersection_env.py:78-119
@@ -43,7 +44,7 @@
 extern "C" {
 #endif
 
-#define TTRL_ABI_VERSION 7
+#define TTRL_ABI_VERSION 8
 #define TTRL_MAX_LANES 32
 #define TTRL_MAX_ROADS 32
 #define TTRL_MAX_NODES 32
@@ -305,6 +306,17 @@ int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const tt
                   float* reward, uint8_t* terminated, uint8_t* truncated, float* components,
                   void* ego_speed, uint8_t* ego_crashed, const int32_t* order, const int32_t* action_lut,
                   int32_t n_action_lut, void* stream);
+/* ttrl_env_step with an OccupancyGridObservation (observation.py:353-483) of the final state
+ * instead of the Kinematics one: grid [E][F][shape_x][shape_y] float32, as ttrl_observe_grid
+ * writes it after ttrl_env_step.  On a straight road of 64 / 128 vehicle slots the step's own
+ * launch writes it from its LDS view (one launch); elsewhere the two launches run in turn. */
+int ttrl_env_step_grid(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                       const int32_t* actions, int32_t frames, double dt,
+                       const ttrl_grid_cfg_t* grid_cfg, float* grid,
+                       const ttrl_reward_cfg_t* reward_cfg, double* time, double time_inc,
+                       float* reward, uint8_t* terminated, uint8_t* truncated, float* components,
+                       void* ego_speed, uint8_t* ego_crashed, const int32_t* action_lut,
+                       int32_t n_action_lut, void* stream);
 /* Road.neighbour_vehicles(v, lane) for every vehicle; query_lane [E*N] int32
  * (-1 = the vehicle's own lane).  front/rear [E*N] int32 vehicle index or -1. */
 int ttrl_neighbours(const ttrl_state_t* s, const ttrl_lane_table_t* road,

@@ -21,7 +21,7 @@ def declared():
 
 def test_library_loads_and_exports_every_declared_symbol():
     lib = _lib.load()
-    assert lib.ttrl_abi_version() == 7
+    assert lib.ttrl_abi_version() == 8
     names = declared()
     assert len(names) >= 10
     for n in names:

@@ -302,13 +302,21 @@ GRID = {"type": "OccupancyGrid", "features": ["presence", "x", "y", "vx", "vy", 
         "grid_size": [[-32, 32], [-32, 32]], "grid_step": [2, 2]}
 
 
-@pytest.mark.parametrize("obs_cfg,N,dtype", [(GRID, 128, "f64"), (GRID, 128, "f32"), (GRID, 48, "f64"),
-                                             ({"type": "TimeToCollision", "horizon": 10}, 64, "f64")])
-def test_fused_step_tail_without_kinematics(obs_cfg, N, dtype, hip_device):
+GRID_ROAD = {"type": "OccupancyGrid", "features": ["presence", "vx", "vy", "on_road"]}  # the reference default
+
+
+@pytest.mark.parametrize("obs_cfg,N,dtype,road", [(GRID, 128, "f64", "straight"), (GRID, 128, "f32", "straight"),
+                                                  (GRID, 48, "f64", "straight"), (GRID_ROAD, 64, "f64", "straight"),
+                                                  (GRID_ROAD, 100, "f32", "straight"), (GRID, 64, "f64", "sine"),
+                                                  ({"type": "TimeToCollision", "horizon": 10}, 64, "f64", "straight")])
+def test_fused_step_tail_without_kinematics(obs_cfg, N, dtype, road, hip_device):
     """With a non-Kinematics observation env.step runs the simulate launch with the reward-only step
-    tail (the ego found and read from the on-chip final state) and the observer separately; it must
-    equal ttrl_simulate followed by ttrl_rewards_step bit for bit (rewards, dones, terms, info, time)."""
-    a, b = make(16, N, obs=obs_cfg, dtype=dtype), make(16, N, obs=obs_cfg, dtype=dtype)
+    tail (the ego found and read from the on-chip final state); an OccupancyGrid is written by the
+    same launch (ttrl_env_step_grid, straight roads of 64 / 128 slots; the sine road takes its two
+    launches), another observer runs separately.  It must equal ttrl_simulate, the observer and
+    ttrl_rewards_step bit for bit (observation, rewards, dones, terms, info, time)."""
+    kw = dict(road=road, lanes_count=4 if road == "straight" else 3)
+    a, b = make(16, N, obs=obs_cfg, dtype=dtype, **kw), make(16, N, obs=obs_cfg, dtype=dtype, **kw)
     a.reset(seed=8)
     b.reset(seed=8)
     rng = np.random.default_rng(6)

@@ -34,6 +34,7 @@ def test_every_device_entry_point_is_an_operator():
                           "rewards_ex": "rewards_ex", "rewards_step_": "rewards_step",
                           "ego_attention_q": "ego_attention_q", "ego_attention_act": "ego_attention_act"}[o]
                for o in ops.OPS}
+    covered.add("ttrl_env_step_grid")  # env_step_ with a grid_cfg
     assert covered == abi
     for o in ops.OPS:
         assert hasattr(torch.ops.ttrl, o), o
@@ -69,6 +70,9 @@ def test_meta_shapes():
                                     ops.struct_tensor(_abi.reward_cfg()), t, 1.0)
     assert [tuple(o.shape) for o in outs] == [(6, 15, 7), (6, 14), (6,), (6,), (6,), (6, 4), (6,), (6,)]
     assert outs[6].dtype == torch.float64 and outs[3].dtype == torch.bool
+    outs = torch.ops.ttrl.env_step_(st.tensors(), LANES, PARAMS, None, 15, 1 / 15, None,
+                                    ops.struct_tensor(_abi.reward_cfg()), t, 1.0, grid_cfg=ops.struct_tensor(grid))
+    assert [tuple(o.shape) for o in outs] == [(6, 2, 32, 32), (0,), (6,), (6,), (6,), (6, 4), (6,), (6,)]
     o, i = torch.ops.ttrl.kinematics_obs(st.tensors(), LANES, PARAMS, ops.struct_tensor(kin))
     assert o.shape == (6, 15, 7) and i.shape == (6, 14)
     ttc = torch.ops.ttrl.observe_ttc(st.tensors(), LANES, PARAMS, ops.struct_tensor(_abi.ttc_cfg()))
@@ -213,6 +217,48 @@ def test_env_step_and_rewards_ops_equal_the_c_abi(hip_device):
     r4, te4, tr4 = torch.ops.ttrl.rewards(other.tensors(), lanes, rc, t2)
     torch.cuda.synchronize()
     assert torch.equal(rew, r3) and torch.equal(comp, c3) and torch.equal(r3, r4) and torch.equal(te3, te4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [100, 40, 20])
+def test_env_step_grid_op_equals_the_c_abi(N, hip_device):
+    """ttrl::env_step_ with a grid_cfg against a direct ctypes call of ttrl_env_step_grid (100 and 40
+    vehicles: the 128- and 64-slot fused launches; 20: the two-launch path of the 32-slot instance),
+    and both against ttrl_env_step followed by ttrl_observe_grid."""
+    env, other = _pair(hip_device, N=N)
+    third = env.state.clone()
+    st = env.state
+    lib = _lib.load()
+    lanes, params, rc = ops.st(env.network.table), ops.st(env.params), ops.st(env.reward_cfg)
+    R, P, RC = C.byref(env.network.table), C.byref(env.params), C.byref(env.reward_cfg)
+    grid = _abi.grid_cfg(["presence", "x", "y", "vx", "vy", "on_road", "cos_h"], [[-32, 32], [-32, 32]], [2, 2],
+                         {"x": [-100, 100], "y": [-100, 100], "vx": [-20, 20], "vy": [-20, 20]})
+    E = 64
+    a = torch.randint(0, 5, (E,), device=hip_device, dtype=torch.int32,
+                      generator=torch.Generator(device=hip_device).manual_seed(5))
+    t1 = torch.full((E,), 2.0, dtype=torch.float64, device=hip_device)
+    t2, t3 = t1.clone(), t1.clone()
+    g1 = torch.empty((E, 7, 32, 32), device=hip_device)
+    rew, comp = torch.empty(E, device=hip_device), torch.empty((E, 4), device=hip_device)
+    te, tr, cr = (torch.empty(E, dtype=torch.uint8, device=hip_device) for _ in range(3))
+    sp = torch.empty(E, dtype=torch.float64, device=hip_device)
+    assert lib.ttrl_env_step_grid(_c(st), R, P, a.data_ptr(), 15, 1 / 15, C.byref(grid), g1.data_ptr(), RC,
+                                  t1.data_ptr(), 1.0, rew.data_ptr(), te.data_ptr(), tr.data_ptr(), comp.data_ptr(),
+                                  sp.data_ptr(), cr.data_ptr(), None, 0, _stream()) == 0
+    outs = torch.ops.ttrl.env_step_(other.tensors(), lanes, params, a, 15, 1 / 15, None, rc, t2, 1.0,
+                                    grid_cfg=ops.struct_tensor(grid))
+    sep = torch.ops.ttrl.env_step_(third.tensors(), lanes, params, a, 15, 1 / 15, None, rc, t3, 1.0)
+    g3 = torch.ops.ttrl.occupancy_grid(third.tensors(), lanes, params, ops.struct_tensor(grid))
+    torch.cuda.synchronize()
+    _equal(st, other)
+    _equal(st, third)
+    assert torch.equal(t1, t2) and torch.equal(t1, t3)
+    assert torch.equal(g1, outs[0]) and torch.equal(g1, g3)
+    assert float(g1[:, 5].sum()) > 0  # the on_road layer is drawn
+    for x, y, z in zip((rew, te, tr, comp, sp, cr), outs[2:], sep[2:]):
+        y = y.view(torch.uint8) if y.dtype == torch.bool else y
+        z = z.view(torch.uint8) if z.dtype == torch.bool else z
+        assert torch.equal(x, y) and torch.equal(x, z)
 
 
 @pytest.mark.gpu

@@ -25,6 +25,8 @@ _SIGS = {
     "ttrl_simulate": ([_P, _P, _P, _P, C.c_int32, C.c_double, _P], C.c_int),
     "ttrl_env_step": ([_P, _P, _P, _P, C.c_int32, C.c_double, _P, _P, _P, _P, _P, C.c_double, _P, _P, _P, _P, _P,
                        _P, _P, _P, C.c_int32, _P], C.c_int),
+    "ttrl_env_step_grid": ([_P, _P, _P, _P, C.c_int32, C.c_double, _P, _P, _P, _P, C.c_double, _P, _P, _P, _P, _P, _P,
+                            _P, C.c_int32, _P], C.c_int),
     "ttrl_neighbours": ([_P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_observe_kinematics": ([_P, _P, _P, _P, _P, _P, _P], C.c_int),
     "ttrl_observe_kinematics_masked": ([_P, _P, _P, _P, _P, _P, _P, _P], C.c_int),
@@ -82,7 +84,7 @@ def load(path: str | None = None, check_abi: bool = True) -> C.CDLL:
             continue  # an older build loaded for comparison (tools/variants.py)
         fn.argtypes = args
         fn.restype = res
-    if (check_abi or path is None) and lib.ttrl_abi_version() != 7:  # include/ttrl_mi355x.h TTRL_ABI_VERSION
+    if (check_abi or path is None) and lib.ttrl_abi_version() != 8:  # include/ttrl_mi355x.h TTRL_ABI_VERSION
         raise ImportError("ABI version mismatch with include/ttrl_mi355x.h")
     if path is None:
         _lib = lib

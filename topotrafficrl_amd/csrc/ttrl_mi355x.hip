@@ -1026,7 +1026,7 @@ __device__ __forceinline__ void sort_order(const View<T>& V, int nl, int tid, in
 // the wave boundary -- the bitonic j = 64 stage of a launch's first order, the odd-even pair
 // (63, 64), the sortedness and tie checks -- go through LDS (the act phase's scratch, dead here).
 template <typename T>
-__device__ void sort_order128(const View<T>& V, int nl, int tid, bool init, int& my_slot) {
+__device__ __forceinline__ void sort_order128(const View<T>& V, int nl, int tid, bool init, int& my_slot) {
   constexpr int NS = 128;
   T* xk = V.afree;          // [128] keys for the cross-wave exchanges
   int* xp = (int*)V.mob;    // [128] payloads
@@ -1810,6 +1810,56 @@ __device__ __forceinline__ void step_tail(const ttrl_lane_table_t& R, const Lane
 // What ttrl_env_step adds after the last frame (null pointers: nothing): the Kinematics observation
 // of the final state and the step tail of ttrl_rewards_step (time, reward, terminated, truncated,
 // reward components, the info's ego speed / crashed), both from the on-chip view.
+// Scratch of grid_observe (LDS): per-cell winners, the on_road bitmap, the clipped feature values
+// per vehicle, and the observer passed through LDS.
+template <typename T> struct GridScr {
+  int* win;         // [C] winner vehicle index
+  unsigned* road;   // [ceil(C/32)] on_road bitmap
+  float* val;       // [F][N] clipped feature values
+  int* ego;         // [1] the observer's slot
+  T* e;             // [6] its x, y, heading, speed, cos, sin
+  int* elane;       // [1] its lane
+};
+__host__ __device__ inline size_t grid_scratch_bytes(const ttrl_grid_cfg_t& cfg, int N, size_t real) {
+  const size_t C = (size_t)cfg.shape_x * cfg.shape_y;
+  return ((4 * C + 4 * ((C + 31) / 32) + 15) & ~(size_t)15) + ((4 * (size_t)cfg.n_features * N + 15) & ~(size_t)15) +
+         6 * real + 16;
+}
+template <typename T>
+__device__ __forceinline__ GridScr<T> grid_scratch(char* base, const ttrl_grid_cfg_t& cfg, int N) {
+  const int C = cfg.shape_x * cfg.shape_y;
+  GridScr<T> g;
+  g.win = (int*)base;
+  g.road = (unsigned*)(g.win + C);
+  g.val = (float*)(base + ((4 * (size_t)C + 4 * (size_t)((C + 31) / 32) + 15) & ~(size_t)15));
+  g.e = (T*)((char*)g.val + ((4 * (size_t)cfg.n_features * N + 15) & ~(size_t)15));
+  g.ego = (int*)(g.e + 6);
+  g.elane = g.ego + 1;
+  return g;
+}
+
+template <typename T, typename KindOf, typename VehOf>
+__device__ __forceinline__ void grid_observe(const ttrl_lane_table_t& R, const ttrl_grid_cfg_t& cfg, int N, int tid,
+                                             int nt, int kd, T x, T y, T h, T v, T hc, T hs, int ln, KindOf kind_of,
+                                             VehOf veh_of, const GridScr<T>& g, float* __restrict__ ob,
+                                             bool nt_stores = true);
+
+// The fused launch's grid write-out: nontemporal stores (1: 0.580 against 0.583 ms per config-3
+// step with plain ones, profiles/r06/r06i_*)
+#ifndef TTRL_GRID_NT_STORES
+#define TTRL_GRID_NT_STORES 1
+#endif
+// ttrl_env_step_grid's epilogue: the OccupancyGrid of the final state, with grid_observe's scratch
+// at byte `scr` of the view's LDS block (over the blocks dead after the last frame)
+struct GridEpi {
+  ttrl_grid_cfg_t cfg;
+  float* out;
+  uint32_t scr;
+};
+// simulate_body's epilogues: the state store + ttrl_env_step's tail; + the OccupancyGrid; the
+// intersection's (ix_epilogue)
+constexpr int EPI_STEP = 0, EPI_GRID = 1, EPI_IX = 2;
+
 struct StepOut {
   ttrl_kin_cfg_t kcfg;
   float* obs;
@@ -1887,12 +1937,14 @@ __device__ __forceinline__ void ix_epilogue(const View<T>& V, const ttrl_state_t
 // and written once); each phase loads the few fields it needs into registers, so no state is
 // live across phases and the kernel runs at high occupancy without spilling.  The workgroup
 // takes the envs of slots [q0, q0 + EPW) (below qend) of the dispatch order (simulate_kernel:
-// q0 = blockIdx.x * EPW, qend = n_envs).  IX: the epilogue is ix_epilogue (ie).
-template <typename T, int NS, int EPW, int NET, bool IX = false>
+// q0 = blockIdx.x * EPW, qend = n_envs).  EPI: the epilogue (EPI_GRID: + the OccupancyGrid, ge;
+// EPI_IX: ix_epilogue, ie).
+template <typename T, int NS, int EPW, int NET, int EPI = EPI_STEP>
 __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state_t& st, const ttrl_lane_table_t& R,
                                               const ParamsT<T>& P, const int32_t* __restrict__ actions,
                                               const uint8_t* __restrict__ env_mask, int frames, double dt_d, int mode,
-                                              int ablate_arg, const StepOut& so, const IxEpi* ie = nullptr);
+                                              int ablate_arg, const StepOut& so, const IxEpi* ie = nullptr,
+                                              const GridEpi* ge = nullptr);
 
 template <typename T, int NS, int EPW, int NET, int WB = 0>
 // Waves per SIMD the register budget is sized for: 4 on the straight highway (its compile-time
@@ -1917,15 +1969,25 @@ template <typename T, int NS, int EPW>
 __global__ void __launch_bounds__(NS* EPW, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES : 2)
 simulate_ix_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_t* __restrict__ actions,
                    int frames, double dt_d, StepOut so, IxEpi ie) {
-  simulate_body<T, NS, EPW, NET_GRAPH, true>((int)blockIdx.x * EPW, st.n_envs, st, R, P, actions, nullptr, frames,
-                                             dt_d, MODE_META | MODE_ACT | MODE_STEP, 0, so, &ie);
+  simulate_body<T, NS, EPW, NET_GRAPH, EPI_IX>((int)blockIdx.x * EPW, st.n_envs, st, R, P, actions, nullptr, frames,
+                                               dt_d, MODE_META | MODE_ACT | MODE_STEP, 0, so, &ie);
 }
 
-template <typename T, int NS, int EPW, int NET, bool IX>
+// ttrl_env_step_grid: the straight one-env-per-workgroup instance (sorted view) with the
+// OccupancyGrid of the final state written by the launch (GridEpi)
+template <typename T, int NS>
+__global__ void __launch_bounds__(NS, TTRL_SIM_WAVES > 0 ? TTRL_SIM_WAVES : 4)
+simulate_grid_kernel(ttrl_state_t st, ttrl_lane_table_t R, ParamsT<T> P, const int32_t* __restrict__ actions,
+                     int frames, double dt_d, StepOut so, GridEpi ge) {
+  simulate_body<T, NS, 1, NET_STRAIGHT, EPI_GRID>((int)blockIdx.x, st.n_envs, st, R, P, actions, nullptr, frames, dt_d,
+                                                  MODE_META | MODE_ACT | MODE_STEP, 0, so, nullptr, &ge);
+}
+
+template <typename T, int NS, int EPW, int NET, int EPI>
 __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state_t& st, const ttrl_lane_table_t& R,
                                               const ParamsT<T>& P, const int32_t* __restrict__ actions,
                                               const uint8_t* __restrict__ env_mask, int frames, double dt_d, int mode,
-                                              int ablate_arg, const StepOut& so, const IxEpi* ie) {
+                                              int ablate_arg, const StepOut& so, const IxEpi* ie, const GridEpi* ge) {
   // The diagnostic phase ablations (ttrl_diag_simulate) exist only in -DTTRL_DIAG_ABLATE builds: as a
   // run-time argument their ~20 tests held SGPR masks for the whole launch (spilled to VGPR lanes),
   // and the product passes 0 anyway.
@@ -2041,7 +2103,9 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
   for (int frame = 0; frame < frames; ++frame) {
     // ---------------- ego meta-action (DiscreteMetaAction.act, action.py:259-260) ----
     if ((mode & MODE_META) && frame == 0 && actions && present && kind == TTRL_MDP) {
-      int act = actions[env];
+      int envl = env;  // NS = 128: laundered, so the action's address is not hoisted and spilled
+      if constexpr (NS > 64) asm volatile("" : "+v"(envl));
+      int act = actions[envl];
       if (so.n_lut > 0) {  // the env's action index -> its meta-action code (a select chain)
         int c = -1;
 #pragma unroll
@@ -2928,20 +2992,24 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
               }
           }
         } else {
+          // NS = 128: the slot index laundered, so the chunks' j > i masks and addresses are made
+          // here (this is the rare tie path) rather than hoisted out of the frame loop and spilled
+          int il = i, ebl = eb;
+          if constexpr (NS > 64) asm volatile("" : "+v"(il), "+v"(ebl));
 #pragma unroll
           for (int c0 = 0; c0 < NS; c0 += CH) {
-            if (c0 + CH <= i + 1) continue;  // only partners j > i
+            if (c0 + CH <= il + 1) continue;  // only partners j > i
             unsigned long long m = 0;
 #pragma unroll
             for (int j1 = 0; j1 < CH; j1 += 8) {
               float xs[8];
 #pragma unroll
-              for (int u = 0; u < 8; ++u) xs[u] = V.xf[eb + c0 + j1 + u];
+              for (int u = 0; u < 8; ++u) xs[u] = V.xf[ebl + c0 + j1 + u];
 #pragma unroll
               for (int u = 0; u < 8; ++u)
                 if (!(fabsf(xs[u] - xfi) > Rwf)) m |= 1ull << (j1 + u);
             }
-            if (i >= c0) m &= ~((2ull << (i - c0)) - 1);  // keep j > i
+            if (il >= c0) m &= ~((2ull << (il - c0)) - 1);  // keep j > i
             if (ablate & A_NO_PREF) m = 0;
             while (m) {
               const int j = c0 + __ffsll((long long)m) - 1;
@@ -3086,7 +3154,7 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
   const int eb = le * NS;
   const int kind = V.kind[me];  // the view holds ABSENT for absent and out-of-range slots
   const bool present = kind != TTRL_ABSENT;
-  if constexpr (IX) {
+  if constexpr (EPI == EPI_IX) {
     ix_epilogue<T, NS, EPW>(V, st, R, P, so, *ie, le, i, env, env_on, slot, k, me, eb, reg, my_timer, my_steer.r,
                             my_acc.r, my_ix.r, my_iy.r, my_sidx);
   } else {
@@ -3149,7 +3217,32 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
       }
     }
   }
-  }  // !IX
+  if constexpr (EPI == EPI_GRID) {  // the OccupancyGrid of the final state, from the view (EPW == 1)
+    __syncthreads();  // its scratch overlays the tail's
+    auto kind_of = [&](int j) { return (int)V.kind[eb + j]; };
+    auto veh_of = [&](int j, T& vx, T& vy, T& vh, T& vv, T& vc, T& vs, int& vl) {
+      vx = V.x[eb + j]; vy = V.y[eb + j]; vh = V.h[eb + j]; vv = V.v[eb + j]; vc = V.ch[eb + j]; vs = V.sh[eb + j];
+      vl = V.lane[eb + j];
+    };
+    // the cfg is staged in LDS (word copies at constant offsets): indexed by feature in the loops,
+    // the kernel argument itself would be copied to scratch
+    constexpr int CW = sizeof(ttrl_grid_cfg_t) / 4;
+    uint32_t* cw = (uint32_t*)(smem + ge->scr);
+    if (i == 0) {
+      const uint32_t* src = (const uint32_t*)&ge->cfg;
+#pragma unroll
+      for (int w = 0; w < CW; ++w) cw[w] = src[w];
+    }
+    __syncthreads();
+    const ttrl_grid_cfg_t& gc = *(const ttrl_grid_cfg_t*)cw;
+    if (env_on)
+      grid_observe<T>(R, gc, N, i, NS, kind, V.x[me], V.y[me], V.h[me], V.v[me], V.ch[me], V.sh[me],
+                      (int)V.lane[me], kind_of, veh_of,
+                      grid_scratch<T>(smem + ge->scr + ((sizeof(ttrl_grid_cfg_t) + 15) & ~(size_t)15), gc, N),
+                      ge->out + (size_t)env * ge->cfg.n_features * ge->cfg.shape_x * ge->cfg.shape_y,
+                      TTRL_GRID_NT_STORES != 0);
+  }
+  }  // EPI != EPI_IX
   }
   PH_FLUSH
 }
@@ -3500,77 +3593,51 @@ kinematics_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttr
 }
 
 // OccupancyGridObservation.observe (observation.py:353-434) + fill_road_layer_by_lanes
-// (:453-483).  One workgroup per env, one thread per slot; the grid is assembled in LDS as
-// per-cell winner vehicle indices (lowest list index wins = the reference's reverse-order
-// overwrite) and streamed to HBM with 16-byte nontemporal stores.
-template <typename T>
-__global__ void __launch_bounds__(256)
-grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid_cfg_t cfg, float* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int env = blockIdx.x;
-  const int N = st.n_veh;
+// (:453-483) of one env over the nt threads of a workgroup (grid_obs_kernel, and the fused
+// env.step's epilogue, ttrl_env_step_grid).  The grid is assembled in LDS as per-cell winner
+// vehicle indices (lowest list index wins = the reference's reverse-order overwrite) and streamed
+// to HBM with 16-byte nontemporal stores.  Thread tid brings slot tid's vehicle in registers (kd
+// TTRL_ABSENT if it has none); kind_of(j) / veh_of(j, x, y, h, v, cos, sin, lane) give any slot's.
+template <typename T, typename KindOf, typename VehOf>
+__device__ __forceinline__ void grid_observe(const ttrl_lane_table_t& R, const ttrl_grid_cfg_t& cfg, int N, int tid,
+                                             int nt, int kd, T x, T y, T h, T v, T hc, T hs, int ln, KindOf kind_of,
+                                             VehOf veh_of, const GridScr<T>& g, float* __restrict__ ob,
+                                             bool nt_stores) {
   const int W = cfg.shape_x, H = cfg.shape_y, C = W * H, F = cfg.n_features;
-  int* s_win = (int*)smem;                         // [C] winner vehicle index
-  unsigned* s_road = (unsigned*)(s_win + C);       // [ceil(C/32)] on_road bitmap
-  float* s_val = (float*)(s_road + ((C + 31) / 32));  // [F][N] clipped feature values
-  const size_t k0 = (size_t)env * N;
-  const int nt = (int)blockDim.x;
-  // the observer (AbstractEnv.vehicle: the env's first MDP slot) and its state, passed through LDS
-  __shared__ int s_ego;
-  __shared__ T s_e[6];  // x, y, heading, speed, cos, sin
-  __shared__ int s_elane;
-  if (tid == 0) s_ego = N;
-  for (int c = tid; c < C; c += nt) s_win[c] = 0x7fffffff;
-  for (int c = tid; c < (C + 31) / 32; c += nt) s_road[c] = 0u;
-  // this thread's vehicle (slot tid; the block is sized so that normally every slot has one)
-  // is loaded once, before the observer is known, so the block makes one HBM round trip
-  const bool mine = tid < N;
-  const size_t km = k0 + (mine ? tid : 0);
-  const int kd = mine ? (int)st.kind[km] : TTRL_ABSENT;
-  const T x = ((const T*)st.x)[km], y = ((const T*)st.y)[km], h = ((const T*)st.heading)[km];
-  const T v = ((const T*)st.speed)[km];
-  const int ln = st.lane[km];
-  const SinCos<T> sc = t_sincos(h);
+  if (tid == 0) *g.ego = N;
+  for (int c = tid; c < C; c += nt) g.win[c] = 0x7fffffff;
+  for (int c = tid; c < (C + 31) / 32; c += nt) g.road[c] = 0u;
   __syncthreads();
   for (int j = tid; j < N; j += nt)
-    if ((j == tid ? kd : (int)st.kind[k0 + j]) == TTRL_MDP) atomicMin(&s_ego, j);
+    if ((j == tid ? kd : kind_of(j)) == TTRL_MDP) atomicMin(g.ego, j);
   __syncthreads();
-  float* ob = out + (size_t)env * F * C;
-  const int ego = s_ego;
+  // the observer: AbstractEnv.vehicle, the env's first MDP slot
+  const int ego = *g.ego;
   if (ego >= N) {  // no controlled vehicle: an all-zero grid
     for (int q = tid; q < F * C; q += nt) __builtin_nontemporal_store(0.f, ob + q);
     return;
   }
   if (tid == ego % nt) {
-    if (ego == tid) {
-      s_e[0] = x; s_e[1] = y; s_e[2] = h; s_e[3] = v; s_e[4] = sc.c; s_e[5] = sc.s; s_elane = ln;
-    } else {
-      const size_t ke = k0 + ego;
-      const T eh = ((const T*)st.heading)[ke];
-      const SinCos<T> esc = t_sincos(eh);
-      s_e[0] = ((const T*)st.x)[ke]; s_e[1] = ((const T*)st.y)[ke]; s_e[2] = eh; s_e[3] = ((const T*)st.speed)[ke];
-      s_e[4] = esc.c; s_e[5] = esc.s; s_elane = st.lane[ke];
-    }
+    T ex, ey, eh, ev, ec, es;
+    int el;
+    if (ego == tid) { ex = x; ey = y; eh = h; ev = v; ec = hc; es = hs; el = ln; }
+    else veh_of(ego, ex, ey, eh, ev, ec, es, el);
+    g.e[0] = ex; g.e[1] = ey; g.e[2] = eh; g.e[3] = ev; g.e[4] = ec; g.e[5] = es; *g.elane = el;
   }
   __syncthreads();
-  const T ex = s_e[0], ey = s_e[1], eh = s_e[2], ev = s_e[3], ec = s_e[4], es = s_e[5];
-  const int elane = s_elane;
+  const T ex = g.e[0], ey = g.e[1], eh = g.e[2], ev = g.e[3], ec = g.e[4], es = g.e[5];
+  const int elane = *g.elane;
   bool has_road = false;
   for (int c = 0; c < F; ++c) has_road |= cfg.features[c] == TTRL_F_ON_ROAD;
   const T rx0 = T(cfg.range_lo[TTRL_F_X]), rx1 = T(cfg.range_hi[TTRL_F_X]);
   const T ry0 = T(cfg.range_lo[TTRL_F_Y]), ry1 = T(cfg.range_hi[TTRL_F_Y]);
   const LaneT<T> EL = make_lane<T>(R, elane);
   for (int j = tid; j < N; j += nt) {
-    T vx = x, vy = y, vh = h, vv = v, vc = sc.c, vs = sc.s;
+    T vx = x, vy = y, vh = h, vv = v, vc = hc, vs = hs;
     int vl = ln;
-    if (j != tid) {  // slots beyond the block (N > blockDim)
-      const size_t k = k0 + j;
-      if (st.kind[k] == TTRL_ABSENT) continue;
-      vx = ((const T*)st.x)[k]; vy = ((const T*)st.y)[k]; vh = ((const T*)st.heading)[k]; vv = ((const T*)st.speed)[k];
-      vl = st.lane[k];
-      const SinCos<T> q = t_sincos(vh);
-      vc = q.c; vs = q.s;
+    if (j != tid) {  // slots beyond the block (N > nt)
+      if (kind_of(j) == TTRL_ABSENT) continue;
+      veh_of(j, vx, vy, vh, vv, vc, vs, vl);
     } else if (kd == TTRL_ABSENT) {
       continue;
     }
@@ -3583,13 +3650,13 @@ grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid
         val -= feature(EL, f, ex, ey, eh, ev, ec, es);
       if (cfg.has_range[f]) val = lmap(val, T(cfg.range_lo[f]), T(cfg.range_hi[f]), T(-1), T(1));
       if (cfg.clip) val = clip(val, T(-1), T(1));
-      s_val[ci * N + j] = (float)val;
+      g.val[ci * N + j] = (float)val;
     }
     if (cfg.has_range[TTRL_F_X]) rx = lmap(lmap(rx, rx0, rx1, T(-1), T(1)), T(-1), T(1), rx0, rx1);
     if (cfg.has_range[TTRL_F_Y]) ry = lmap(lmap(ry, ry0, ry1, T(-1), T(1)), T(-1), T(1), ry0, ry1);
     const T fx = floor((rx - T(cfg.grid_min_x)) / T(cfg.step_x));
     const T fy = floor((ry - T(cfg.grid_min_y)) / T(cfg.step_y));
-    if (T(0) <= fx && fx < T(W) && T(0) <= fy && fy < T(H)) atomicMin(&s_win[(int)fx * H + (int)fy], j);
+    if (T(0) <= fx && fx < T(W) && T(0) <= fy && fy < T(H)) atomicMin(&g.win[(int)fx * H + (int)fy], j);
   }
   if (has_road) {  // fill_road_layer_by_lanes observation.py:453-483, (lane, waypoint) items over the block
     const T spacing = T(cfg.step_x) < T(cfg.step_y) ? T(cfg.step_x) : T(cfg.step_y);
@@ -3616,7 +3683,7 @@ grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid
         const T fy = floor((py - T(cfg.grid_min_y)) / T(cfg.step_y));
         if (T(0) <= fx && fx < T(W) && T(0) <= fy && fy < T(H)) {
           const int c = (int)fx * H + (int)fy;
-          atomicOr(&s_road[c >> 5], 1u << (c & 31));
+          atomicOr(&g.road[c >> 5], 1u << (c & 31));
         }
       }
       base += n;
@@ -3624,14 +3691,15 @@ grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid
   }
   __syncthreads();
   // the grid streams out once: 16-byte nontemporal stores (no reuse in L2); each thread owns
-  // 4-cell groups and looks their winners up once for all feature layers
+  // 4-cell groups and looks their winners up once for all feature layers.  !nt_stores: plain
+  // stores (the fused launch's write-out, A/B)
   if ((C & 3) == 0) {
     typedef float f4 __attribute__((ext_vector_type(4)));
     for (int c4 = tid; c4 < C / 4; c4 += nt) {
       int w[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) w[u] = s_win[c4 * 4 + u];
-      const unsigned rb = (s_road[c4 >> 3] >> ((c4 & 7) * 4)) & 0xfu;  // the 4 cells' on_road bits
+      for (int u = 0; u < 4; ++u) w[u] = g.win[c4 * 4 + u];
+      const unsigned rb = (g.road[c4 >> 3] >> ((c4 & 7) * 4)) & 0xfu;  // the 4 cells' on_road bits
       for (int ci = 0; ci < F; ++ci) {
         float r[4];
         if (cfg.features[ci] == TTRL_F_ON_ROAD) {
@@ -3639,9 +3707,11 @@ grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid
           for (int u = 0; u < 4; ++u) r[u] = ((rb >> u) & 1u) ? 1.f : 0.f;
         } else {
 #pragma unroll
-          for (int u = 0; u < 4; ++u) r[u] = w[u] == 0x7fffffff ? 0.f : s_val[ci * N + w[u]];
+          for (int u = 0; u < 4; ++u) r[u] = w[u] == 0x7fffffff ? 0.f : g.val[ci * N + w[u]];
         }
-        __builtin_nontemporal_store((f4){r[0], r[1], r[2], r[3]}, reinterpret_cast<f4*>(ob + (size_t)ci * C + c4 * 4));
+        f4* dst = reinterpret_cast<f4*>(ob + (size_t)ci * C + c4 * 4);
+        if (nt_stores) __builtin_nontemporal_store((f4){r[0], r[1], r[2], r[3]}, dst);
+        else *dst = (f4){r[0], r[1], r[2], r[3]};
       }
     }
   } else {
@@ -3649,12 +3719,42 @@ grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid
       const bool road = cfg.features[ci] == TTRL_F_ON_ROAD;
       for (int c = tid; c < C; c += nt) {
         float r;
-        if (road) r = ((s_road[c >> 5] >> (c & 31)) & 1u) ? 1.f : 0.f;
-        else { const int w = s_win[c]; r = w == 0x7fffffff ? 0.f : s_val[ci * N + w]; }
+        if (road) r = ((g.road[c >> 5] >> (c & 31)) & 1u) ? 1.f : 0.f;
+        else { const int w = g.win[c]; r = w == 0x7fffffff ? 0.f : g.val[ci * N + w]; }
         __builtin_nontemporal_store(r, ob + (size_t)ci * C + c);
       }
     }
   }
+}
+
+// One workgroup per env, one thread per slot (vehicles of slots beyond the block from HBM).
+template <typename T>
+__global__ void __launch_bounds__(256)
+grid_obs_kernel(ttrl_state_t st, ttrl_lane_table_t R, ttrl_params_t P, ttrl_grid_cfg_t cfg, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int env = blockIdx.x;
+  const int N = st.n_veh;
+  const size_t k0 = (size_t)env * N;
+  // this thread's vehicle (slot tid; the block is sized so that normally every slot has one) is
+  // loaded once, before the observer is known, so the block makes one HBM round trip
+  const bool mine = tid < N;
+  const size_t km = k0 + (mine ? tid : 0);
+  const int kd = mine ? (int)st.kind[km] : TTRL_ABSENT;
+  const T x = ((const T*)st.x)[km], y = ((const T*)st.y)[km], h = ((const T*)st.heading)[km];
+  const T v = ((const T*)st.speed)[km];
+  const int ln = st.lane[km];
+  const SinCos<T> sc = t_sincos(h);
+  auto kind_of = [&](int j) { return (int)st.kind[k0 + j]; };
+  auto veh_of = [&](int j, T& vx, T& vy, T& vh, T& vv, T& vc, T& vs, int& vl) {
+    const size_t k = k0 + j;
+    vx = ((const T*)st.x)[k]; vy = ((const T*)st.y)[k]; vh = ((const T*)st.heading)[k]; vv = ((const T*)st.speed)[k];
+    vl = st.lane[k];
+    const SinCos<T> q = t_sincos(vh);
+    vc = q.c; vs = q.s;
+  };
+  grid_observe<T>(R, cfg, N, tid, (int)blockDim.x, kd, x, y, h, v, sc.c, sc.s, ln, kind_of, veh_of,
+                  grid_scratch<T>(smem, cfg, N), out + (size_t)env * cfg.n_features * cfg.shape_x * cfg.shape_y);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -5230,6 +5330,36 @@ int launch_sim_ix(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_
   return launch_status();
 }
 
+// ttrl_env_step_grid's launch: the straight one-env instance (sorted view) with the OccupancyGrid
+// epilogue, its scratch over the view's blocks dead after the last frame (the own-state and the
+// frame-transient blocks: 8.8 KB per float64 128-slot env for the 8 KB a 7 x 32 x 32 grid and its
+// cfg need; the block grows if a grid needs more)
+template <typename T, int NS>
+int launch_sim_grid(const ttrl_state_t& s, const ttrl_lane_table_t& R, const ttrl_params_t& P, const int32_t* actions,
+                    int frames, double dt, hipStream_t stream, const StepOut& ob, GridEpi ge) {
+  if (s.n_envs == 0) return TTRL_OK;
+  const ViewLayout o = view_layout<T>(1, NS, STRAIGHT_LANE_CAP, false, true);
+  if (!tail_fits<T>(o, 1, NS)) return TTRL_E_UNSUPPORTED;
+  ge.scr = (uint32_t)o.own;
+  const size_t need =
+      o.own + ((sizeof(ttrl_grid_cfg_t) + 15) & ~(size_t)15) + grid_scratch_bytes(ge.cfg, s.n_veh, sizeof(T));
+  const size_t lds = need > o.total ? (need + 15) & ~(size_t)15 : o.total;
+  if (lds > 64 * 1024) return TTRL_E_UNSUPPORTED;
+  hipLaunchKernelGGL((simulate_grid_kernel<T, NS>), dim3(s.n_envs), dim3(NS), lds, stream, s, R, params_for<T>(P),
+                     actions, frames, dt, ob, ge);
+  return launch_status();
+}
+
+// The road and slot count run the straight one-env-per-workgroup instance with a sorted view
+// (launch_sim's choice for 64 and 128 slots on <= STRAIGHT_LANE_CAP straight lanes along +x).
+bool grid_fusable(const ttrl_state_t& s, const ttrl_lane_table_t& R) {
+  if (is_graph(R) || R.n_lanes > STRAIGHT_LANE_CAP) return false;
+  for (int l = 0; l < R.n_lanes; ++l)
+    if (R.type[l] != TTRL_LANE_STRAIGHT || R.dir_x[l] != 1.0 || R.dir_y[l] != 0.0) return false;
+  const int ns = slots_for(s.n_veh);
+  return ns == 64 || ns == 128;
+}
+
 int run_sim(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params_t* P, const int32_t* actions,
             int frames, double dt, int mode, void* stream, int ablate = 0, const uint8_t* mask = nullptr,
             const StepOut* ob = nullptr) {
@@ -5241,6 +5371,15 @@ int run_sim(const ttrl_state_t* s, const ttrl_lane_table_t* R, const ttrl_params
   const StepOut& o = ob ? *ob : none;
   return s->dtype == TTRL_F64 ? dispatch_sim<double>(*s, *R, *P, actions, mask, frames, dt, mode, ablate, st, o)
                               : dispatch_sim<float>(*s, *R, *P, actions, mask, frames, dt, mode, ablate, st, o);
+}
+
+int check_grid_cfg(const ttrl_grid_cfg_t* cfg, const float* out) {
+  if (!cfg || !out || cfg->n_features < 1 || cfg->n_features > TTRL_N_FEATURES || cfg->shape_x < 1 ||
+      cfg->shape_y < 1 || cfg->step_x <= 0 || cfg->step_y <= 0)
+    return TTRL_E_ARG;
+  for (int c = 0; c < cfg->n_features; ++c)
+    if (cfg->features[c] < 0 || cfg->features[c] >= TTRL_N_FEATURES) return TTRL_E_ARG;
+  return TTRL_OK;
 }
 
 int check_kin_cfg(const ttrl_state_t* s, const ttrl_kin_cfg_t* cfg) {
@@ -5326,6 +5465,46 @@ int ttrl_road_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const t
 int ttrl_simulate(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
                   const int32_t* actions, int32_t frames, double dt, void* stream) {
   return run_sim(s, road, p, actions, frames, dt, MODE_META | MODE_ACT | MODE_STEP, stream);
+}
+
+int ttrl_env_step_grid(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p,
+                       const int32_t* actions, int32_t frames, double dt, const ttrl_grid_cfg_t* grid_cfg, float* grid,
+                       const ttrl_reward_cfg_t* reward_cfg, double* time, double time_inc, float* reward,
+                       uint8_t* terminated, uint8_t* truncated, float* components, void* ego_speed,
+                       uint8_t* ego_crashed, const int32_t* action_lut, int32_t n_action_lut, void* stream) {
+  int rc = check_state(s, road);
+  if (rc) return rc < 0 ? rc : TTRL_OK;
+  if (check_grid_cfg(grid_cfg, grid)) return TTRL_E_ARG;
+  if (!grid_fusable(*s, *road)) {  // two launches: the step, then grid_obs_kernel
+    rc = ttrl_env_step(s, road, p, actions, frames, dt, nullptr, nullptr, nullptr, reward_cfg, time, time_inc, reward,
+                       terminated, truncated, components, ego_speed, ego_crashed, nullptr, action_lut, n_action_lut,
+                       stream);
+    return rc ? rc : ttrl_observe_grid(s, road, p, grid_cfg, grid, stream);
+  }
+  if (!p || frames < 0 || p->n_target_speeds < 1 || p->n_target_speeds > 8) return TTRL_E_ARG;
+  if (reward_cfg && (!time || !reward || !terminated || !truncated || (!ego_speed) != (!ego_crashed)))
+    return TTRL_E_ARG;
+  if (n_action_lut < 0 || n_action_lut > 8 || (n_action_lut > 0 && !action_lut)) return TTRL_E_ARG;
+  StepOut so{};
+  for (int q = 0; q < n_action_lut; ++q) {
+    if (action_lut[q] < TTRL_LANE_LEFT || action_lut[q] > TTRL_SLOWER) return TTRL_E_ARG;
+    so.lut[q] = (int8_t)action_lut[q];
+  }
+  so.n_lut = n_action_lut;
+  if (reward_cfg) {
+    so.rcfg = *reward_cfg; so.time = time; so.time_inc = time_inc; so.reward = reward; so.term = terminated;
+    so.trunc = truncated; so.comp = components; so.ego_speed = ego_speed; so.ego_crashed = ego_crashed;
+  }
+  GridEpi ge{};
+  ge.cfg = *grid_cfg;
+  ge.out = grid;
+  hipStream_t st = (hipStream_t)stream;
+  const bool wide = slots_for(s->n_veh) == 128;
+  if (s->dtype == TTRL_F64)
+    return wide ? launch_sim_grid<double, 128>(*s, *road, *p, actions, frames, dt, st, so, ge)
+                : launch_sim_grid<double, 64>(*s, *road, *p, actions, frames, dt, st, so, ge);
+  return wide ? launch_sim_grid<float, 128>(*s, *road, *p, actions, frames, dt, st, so, ge)
+              : launch_sim_grid<float, 64>(*s, *road, *p, actions, frames, dt, st, so, ge);
 }
 
 int ttrl_env_step(const ttrl_state_t* s, const ttrl_lane_table_t* road, const ttrl_params_t* p, const int32_t* actions,
@@ -5429,13 +5608,8 @@ int ttrl_observe_grid(const ttrl_state_t* s, const ttrl_lane_table_t* road, cons
                       const ttrl_grid_cfg_t* cfg, float* out, void* stream) {
   int rc = check_state(s, road);
   if (rc) return rc < 0 ? rc : TTRL_OK;
-  if (!p || !cfg || !out || cfg->n_features < 1 || cfg->n_features > TTRL_N_FEATURES || cfg->shape_x < 1 ||
-      cfg->shape_y < 1 || cfg->step_x <= 0 || cfg->step_y <= 0)
-    return TTRL_E_ARG;
-  for (int c = 0; c < cfg->n_features; ++c)
-    if (cfg->features[c] < 0 || cfg->features[c] >= TTRL_N_FEATURES) return TTRL_E_ARG;
-  const int C = cfg->shape_x * cfg->shape_y;
-  const size_t lds = sizeof(int) * C + sizeof(unsigned) * ((C + 31) / 32) + sizeof(float) * cfg->n_features * s->n_veh;
+  if (!p || check_grid_cfg(cfg, out)) return TTRL_E_ARG;
+  const size_t lds = grid_scratch_bytes(*cfg, s->n_veh, s->dtype == TTRL_F64 ? 8 : 4);
   if (lds > 160 * 1024) return TTRL_E_UNSUPPORTED;
   if (s->n_envs == 0) return TTRL_OK;
   hipStream_t st = (hipStream_t)stream;

@@ -137,10 +137,13 @@ void meta_action_(at::TensorList state, const at::Tensor& lanes, const at::Tenso
 // Kinematics observation of the final state (kin_cfg given; else obs / ids are empty) and the step
 // tail (time += time_inc, reward, terminated, truncated, components, the info's ego speed / crashed).
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor>
-env_step_outputs(const at::Tensor& x, const ttrl_kin_cfg_t* kc) {
+env_step_outputs(const at::Tensor& x, const ttrl_kin_cfg_t* kc, const ttrl_grid_cfg_t* gc = nullptr) {
   const int64_t E = x.size(0);
   at::Tensor obs, ids;
-  if (kc) {
+  if (gc) {
+    obs = at::empty({E, gc->n_features, gc->shape_x, gc->shape_y}, opts(x, at::kFloat));
+    ids = at::empty({0}, opts(x, at::kInt));
+  } else if (kc) {
     obs = at::empty({E, kc->vehicles_count, kc->n_features}, opts(x, at::kFloat));
     ids = at::empty({E, std::max<int64_t>(kc->vehicles_count - 1, 1)}, opts(x, at::kInt));
   } else {
@@ -156,10 +159,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
     at::TensorList state, const at::Tensor& lanes, const at::Tensor& params, const c10::optional<at::Tensor>& actions,
     int64_t frames, double dt, const c10::optional<at::Tensor>& kin_cfg, const at::Tensor& reward_cfg,
     const at::Tensor& time, double time_inc, const c10::optional<at::Tensor>& order,
-    at::OptionalIntArrayRef action_lut) {
+    at::OptionalIntArrayRef action_lut, const c10::optional<at::Tensor>& grid_cfg) {
   check_hip(state[0]);
   ttrl_state_t s = state_of(state);
   const ttrl_kin_cfg_t* kc = kin_cfg && kin_cfg->defined() ? as_struct<ttrl_kin_cfg_t>(*kin_cfg, "kin_cfg") : nullptr;
+  const ttrl_grid_cfg_t* gc =
+      grid_cfg && grid_cfg->defined() ? as_struct<ttrl_grid_cfg_t>(*grid_cfg, "grid_cfg") : nullptr;
+  TORCH_CHECK(!(kc && gc), "ttrl: env_step_ takes a kin_cfg or a grid_cfg, not both");
   TORCH_CHECK(time.device() == state[0].device() && time.scalar_type() == at::kDouble && time.is_contiguous() &&
                   time.numel() == s.n_envs,
               "ttrl: time must be a contiguous float64 [n_envs] tensor on the state's device");
@@ -172,8 +178,20 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
   std::vector<int32_t> lut;  // the action index -> meta-action code table (host; ttrl_env_step copies it)
   if (action_lut.has_value())
     for (int64_t c : *action_lut) lut.push_back(static_cast<int32_t>(c));
-  auto out = env_step_outputs(state[0], kc);
+  auto out = env_step_outputs(state[0], kc, gc);
   auto& [obs, ids, rew, term, trunc, comp, speed, crashed] = out;
+  if (gc) {  // the OccupancyGrid of the final state (the step's own launch where it fuses)
+    TORCH_CHECK(!od, "ttrl: env_step_ with a grid_cfg takes no dispatch order (straight roads)");
+    ok(ttrl_env_step_grid(&s, as_struct<ttrl_lane_table_t>(lanes, "lanes"), as_struct<ttrl_params_t>(params, "params"),
+                          static_cast<const int32_t*>(ptr(a)), static_cast<int32_t>(frames), dt, gc,
+                          obs.data_ptr<float>(), as_struct<ttrl_reward_cfg_t>(reward_cfg, "reward_cfg"),
+                          time.data_ptr<double>(), time_inc, rew.data_ptr<float>(),
+                          static_cast<uint8_t*>(term.data_ptr()), static_cast<uint8_t*>(trunc.data_ptr()),
+                          comp.data_ptr<float>(), speed.data_ptr(), static_cast<uint8_t*>(crashed.data_ptr()),
+                          lut.empty() ? nullptr : lut.data(), static_cast<int32_t>(lut.size()), stream_of(state[0])),
+       "ttrl_env_step_grid");
+    return out;
+  }
   ok(ttrl_env_step(&s, as_struct<ttrl_lane_table_t>(lanes, "lanes"), as_struct<ttrl_params_t>(params, "params"),
                    static_cast<const int32_t*>(ptr(a)), static_cast<int32_t>(frames), dt, kc,
                    kc ? obs.data_ptr<float>() : nullptr, kc ? ids.data_ptr<int32_t>() : nullptr,
@@ -675,9 +693,11 @@ void meta_none_meta(at::TensorList, const at::Tensor&, const at::Tensor&, const 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor>
 meta_env_step(at::TensorList state, const at::Tensor&, const at::Tensor&, const c10::optional<at::Tensor>&, int64_t,
               double, const c10::optional<at::Tensor>& kin_cfg, const at::Tensor&, const at::Tensor&, double,
-              const c10::optional<at::Tensor>&, at::OptionalIntArrayRef) {
+              const c10::optional<at::Tensor>&, at::OptionalIntArrayRef, const c10::optional<at::Tensor>& grid_cfg) {
   const ttrl_kin_cfg_t* kc = kin_cfg && kin_cfg->defined() ? as_struct<ttrl_kin_cfg_t>(*kin_cfg, "kin_cfg") : nullptr;
-  return env_step_outputs(meta_x(state), kc);
+  const ttrl_grid_cfg_t* gc =
+      grid_cfg && grid_cfg->defined() ? as_struct<ttrl_grid_cfg_t>(*grid_cfg, "grid_cfg") : nullptr;
+  return env_step_outputs(meta_x(state), kc, gc);
 }
 
 std::tuple<at::Tensor, at::Tensor> meta_neighbours(at::TensorList state, const at::Tensor& lanes,
@@ -793,7 +813,7 @@ TORCH_LIBRARY(ttrl, m) {
   m.def("meta_action_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor actions) -> ()");
   m.def("env_step_(Tensor(a!)[] state, Tensor lanes, Tensor params, Tensor? actions, int frames, float dt, "
         "Tensor? kin_cfg, Tensor reward_cfg, Tensor(b!) time, float time_inc, Tensor? order=None, "
-        "int[]? action_lut=None) -> (Tensor obs, Tensor ids, "
+        "int[]? action_lut=None, Tensor? grid_cfg=None) -> (Tensor obs, Tensor ids, "
         "Tensor reward, Tensor terminated, Tensor truncated, Tensor components, Tensor ego_speed, Tensor ego_crashed)");
   m.def("neighbours(Tensor[] state, Tensor lanes, Tensor? query_lane) -> (Tensor front, Tensor rear)");
   // the np_random-shuffled observation (order_shuffled 2) advances state.rng: the state is mutated

@@ -17,7 +17,7 @@ import torch
 
 from . import _abi, ops
 from .action import action_factory
-from .observation import BatchedKinematicObservation, observation_factory
+from .observation import BatchedKinematicObservation, BatchedOccupancyGridObservation, observation_factory
 from .road import BatchedRoad, RoadNetwork
 from .state import BatchState
 
@@ -136,6 +136,9 @@ class VecHighwayEnv:
             "device": "cuda",
             "dtype": "f64",
             "auto_reset": False,
+            # an OccupancyGrid observation is written by the env.step launch (ttrl_env_step_grid);
+            # False: the grid kernel runs after the step (A/B timing only, the same bits)
+            "fuse_grid": True,
         }
 
     def configure(self, config: dict | None) -> None:
@@ -229,8 +232,9 @@ class VecHighwayEnv:
         """abstract.py:224-250: (obs, reward[E], terminated[E], truncated[E], info)."""
         if self.road is None:
             raise NotImplementedError("The road and vehicle must be initialized in the environment implementation")
-        # one launch: _simulate, the Kinematics observation of the final state and the step tail
-        # (time += 1 / policy_frequency, abstract.py:239; rewards, dones, info), ttrl_env_step
+        # one launch: _simulate, the Kinematics observation (or OccupancyGrid) of the final state and
+        # the step tail (time += 1 / policy_frequency, abstract.py:239; rewards, dones, info),
+        # ttrl_env_step / ttrl_env_step_grid
         obs, (reward, terminated, truncated) = self._simulate(action, tail=True)
         if obs is None:
             obs = self.observation_type.observe()
@@ -262,12 +266,16 @@ class VecHighwayEnv:
         # action indices: the launch maps them to meta-action codes (no lookup launch)
         idx, lut = self.action_type._indices(action) if act else (None, None)
         kin = isinstance(self.observation_type, BatchedKinematicObservation)
+        grid = isinstance(self.observation_type, BatchedOccupancyGridObservation) and self.config["fuse_grid"]
         kc = self.observation_type.fused_cfg() if kin else None
+        gc = self.observation_type.cfg if grid else None
         obs, ids, *outs = self.road.env_step(idx, frames, dt, kc, self.reward_cfg, self.time,
-                                             1 / self.config["policy_frequency"], None, lut)
+                                             1 / self.config["policy_frequency"], None, lut, gc)
         if kin:
             self.observation_type.fused_result(obs, ids)
-        return (obs if kin else None), _keep_tail(self, outs)
+        elif grid:
+            self.observation_type._out = obs
+        return (obs if kin or grid else None), _keep_tail(self, outs)
 
     REWARD_TERMS = ["collision_reward", "high_speed_reward", "arrived_reward", "on_road_reward"]
 

@@ -102,9 +102,10 @@ class BatchedRoad:
 
     def env_step(self, actions: torch.Tensor | None, frames: int, dt: float, kin_cfg: _abi.KinCfg | None,
                  reward_cfg: _abi.RewardCfg, time: torch.Tensor, time_inc: float, order: torch.Tensor | None = None,
-                 action_lut: list[int] | None = None):
+                 action_lut: list[int] | None = None, grid_cfg: _abi.GridCfg | None = None):
         """AbstractEnv.step (abstract.py:224-250) in one launch (ttrl_env_step): the fused frames, the
-        Kinematics observation of the final state (``kin_cfg``; else obs / ids are empty) and the step
+        Kinematics observation of the final state (``kin_cfg``; else obs / ids are empty; ``grid_cfg``
+        instead: obs is the OccupancyGrid [E, F, W, H] of ttrl_env_step_grid, ids empty) and the step
         tail (time += time_inc, reward, terminated, truncated, components, the info's ego speed /
         crashed).  Returns those 8 tensors.  ``order``: an optional dispatch order of the envs (int32
         permutation, ix_step_tail_ writes it; road networks only, results unchanged).  It must be a
@@ -114,8 +115,9 @@ class BatchedRoad:
         the launch (DiscreteMetaAction._indices)."""
         a = None if actions is None else self._actions(actions)
         kc = None if kin_cfg is None else ops.kin_cfg_tensor(kin_cfg)
+        gc = None if grid_cfg is None else ops.st(grid_cfg)
         return ops.T.env_step_(*self._args(), a, int(frames), float(dt), kc, ops.st(reward_cfg), time,
-                               float(time_inc), order, action_lut)
+                               float(time_inc), order, action_lut, gc)
 
     def ix_env_step(self, cfg: _abi.IxCfg, actions: torch.Tensor | None, frames: int, dt: float,
                     kin_cfg: _abi.KinCfg, reward_cfg: _abi.RewardCfg, time: torch.Tensor, time_inc: float,
