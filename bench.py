@@ -430,7 +430,7 @@ def main():
     # env.step BatchedRoad.env_step) on the stream it is enqueued on; a step's simulate time is the
     # span from its first launch's start to its last one's end
     from topotrafficrl_amd.road import BatchedRoad
-    orig_sim, orig_env_step = BatchedRoad.simulate, BatchedRoad.env_step
+    orig_sim, orig_env_step, orig_ix_step = BatchedRoad.simulate, BatchedRoad.env_step, BatchedRoad.ix_env_step
     launches = []
 
     def timed(fn):
@@ -445,6 +445,7 @@ def main():
         return wrapper
 
     BatchedRoad.simulate, BatchedRoad.env_step = timed(orig_sim), timed(orig_env_step)
+    BatchedRoad.ix_env_step = timed(orig_ix_step)
     # config 3: the OccupancyGrid launch (the path's HBM-bound kernel) timed the same way
     from topotrafficrl_amd.observation import BatchedOccupancyGridObservation
     orig_grid = BatchedOccupancyGridObservation.observe
@@ -471,7 +472,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if ix:  # the counter holds the tails of the timed steps: the last one counts the step after them
         live_steps = live0 + int(live.item()) - int((env.state["kind"] != 0).sum())
-    BatchedRoad.simulate, BatchedRoad.env_step = orig_sim, orig_env_step
+    BatchedRoad.simulate, BatchedRoad.env_step, BatchedRoad.ix_env_step = orig_sim, orig_env_step, orig_ix_step
     BatchedOccupancyGridObservation.observe = orig_grid
 
     def span(recs):
@@ -497,6 +498,9 @@ def main():
         kernel = "simulate_kernel (fused 15-frame Road.act+Road.step + Kinematics observation + step tail)"
     if fused_grid:
         kernel = "simulate_grid_kernel (fused 15-frame Road.act+Road.step + OccupancyGrid + step tail)"
+    if ix and getattr(env, "_fuse", False):  # ttrl_ix_env_step: + _clear_vehicles / _spawn_vehicle, the swap
+        kernel = ("simulate_ix_kernel (fused 15-frame Road.act+Road.step + Kinematics observation + step tail "
+                  "+ _clear_vehicles / _spawn_vehicle + the finished envs' spare scenes)")
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     pmc, pmc_source = read_pmc(args.dtype, args.config)
     hbm = {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
