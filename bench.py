@@ -381,7 +381,9 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
     n_act = env.action_space.n
-    acts = torch.randint(0, n_act, (args.warmup + args.steps, E), device=dev, generator=g, dtype=torch.int32)
+    # the timed steps run bare; the launches' HIP-event timing runs on the steps after them (n_ev)
+    n_ev = min(args.steps, 20)
+    acts = torch.randint(0, n_act, (args.warmup + args.steps + n_ev, E), device=dev, generator=g, dtype=torch.int32)
     # config 6 counts live vehicles, not slots: every step's tail launch (ttrl_ix_step_tail) adds the
     # vehicles present after it -- the next step's live vehicles -- to this counter, so the timed
     # steps' count is (live at the first timed step) + counter - (live after the last one)
@@ -425,10 +427,23 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream(dev)
-    # HIP events bracket every fused simulate launch (BatchedRoad.simulate, or the one-launch
-    # env.step BatchedRoad.env_step) on the stream it is enqueued on; a step's simulate time is the
-    # span from its first launch's start to its last one's end
+    t0 = time.perf_counter()
+    for t in range(args.warmup, args.warmup + args.steps):
+        one_step(t)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if ix:  # the counter holds the tails of the timed steps: the last one counts the step after them
+        live_steps = live0 + int(live.item()) - int((env.state["kind"] != 0).sum())
+
+    # The launch time for the roofline, on the n_ev steps that follow the timed ones (untimed): HIP
+    # events bracket every fused simulate launch (BatchedRoad.simulate, or the one-launch env.step
+    # BatchedRoad.env_step / ix_env_step) on the stream it is enqueued on; a step's simulate time is
+    # the span from its first launch's start to its last one's end.  The events stay out of the timed
+    # loop: two timing markers around each launch cost ~8 us per step between back-to-back launches
+    # (tools/gap_ab.py, profiles/r06/r06l_event_markers.txt).
     from topotrafficrl_amd.road import BatchedRoad
     orig_sim, orig_env_step, orig_ix_step = BatchedRoad.simulate, BatchedRoad.env_step, BatchedRoad.ix_env_step
     launches = []
@@ -461,17 +476,11 @@ def main():
         return r
 
     BatchedOccupancyGridObservation.observe = timed_grid
-    t0 = time.perf_counter()
-    for t in range(args.warmup, args.warmup + args.steps):
-        launches.append([])
-        one_step(t)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if ix:  # the counter holds the tails of the timed steps: the last one counts the step after them
-        live_steps = live0 + int(live.item()) - int((env.state["kind"] != 0).sum())
+    if sg is None:
+        for t in range(args.warmup + args.steps, args.warmup + args.steps + n_ev):
+            launches.append([])
+            one_step(t)
+        torch.cuda.synchronize()
     BatchedRoad.simulate, BatchedRoad.env_step, BatchedRoad.ix_env_step = orig_sim, orig_env_step, orig_ix_step
     BatchedOccupancyGridObservation.observe = orig_grid
 

@@ -39,6 +39,11 @@ def step_dispatches(rows, id_key="Dispatch_Id", name_key="Kernel_Name"):
     """Dispatch ids of the step's simulate launches: every simulate dispatch except those directly
     after an ix_begin dispatch (the resets' warm-ups)."""
     order = sorted({(int(r[id_key]), short(r[name_key])) for r in rows})
+    # round 6: config 6's step is simulate_ix_kernel (the warm-ups stay simulate_kernel) and config 3's
+    # simulate_grid_kernel; when a trace holds one of them, it is the step launch
+    for fused in ("simulate_ix_kernel", "simulate_grid_kernel"):
+        if any(fused in k for _, k in order):
+            return {did for did, k in order if fused in k}
     keep, prev = set(), ""
     for did, k in order:
         if SIM in k and "ix_begin_kernel" not in prev:
