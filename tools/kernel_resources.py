@@ -38,7 +38,14 @@ def main():
     print(f"{'instance (T, NS, EPW, net, wave budget)':44s} {'VGPRs':>5s} {'scratch B/lane':>14s} {'waves/SIMD':>10s}")
     for r in rows:
         m = re.search(r"simulate_kernelI([df])Li(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", r["name"])
-        if not m:
+        if not m:  # the fused step instances: config 3's grid epilogue, config 6's intersection tail
+            g = re.search(r"simulate_(grid|ix)_kernelI([df])Li(\d+)E(?:Li(\d+)E)?", r["name"])
+            if g:
+                kind, t, ns, epw = g.groups()
+                name = (f"{'double' if t == 'd' else 'float'}, {ns}, {epw or 1}, "
+                        f"{'straight + grid' if kind == 'grid' else 'graph + ix tail'}, default")
+                print(f"{name:44s} {r.get('VGPRs', '?'):>5s} {r.get('ScratchSize [bytes/lane]', '?'):>14s} "
+                      f"{r.get('Occupancy [waves/SIMD]', '?'):>10s}")
             continue
         t, ns, epw, nt, wb = m.groups()
         name = f"{'double' if t == 'd' else 'float'}, {ns}, {epw}, {net[nt]}, {wb if wb != '0' else 'default'}"

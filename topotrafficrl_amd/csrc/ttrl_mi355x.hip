@@ -797,7 +797,9 @@ __device__ __forceinline__ void load_veh(Veh<T>& a, const ttrl_state_t& s, size_
   a.lc = s.lane_change[k] != 0;
 }
 
-template <typename T>
+// SIDX = false: the speed index is left as it is in HBM (the simulate launch writes a changed one
+// where it changes it, in the meta-action)
+template <bool SIDX = true, typename T>
 __device__ __forceinline__ void store_veh(const Veh<T>& a, const ttrl_state_t& s, size_t k) {
   ((T*)s.x)[k] = a.x;
   ((T*)s.y)[k] = a.y;
@@ -811,7 +813,7 @@ __device__ __forceinline__ void store_veh(const Veh<T>& a, const ttrl_state_t& s
   ((T*)s.impact_y)[k] = a.iy;
   s.lane[k] = a.lane;
   s.target_lane[k] = a.tgt;
-  s.speed_index[k] = a.sidx;
+  if (SIDX) s.speed_index[k] = a.sidx;
   s.crashed[k] = a.crashed ? 1 : 0;
   s.has_impact[k] = a.hasimp ? 1 : 0;
 }
@@ -2099,47 +2101,62 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
   }
   const int kind = V.kind[me];
 
+  // ---------------- ego meta-action (DiscreteMetaAction.act, action.py:259-260) ----
+  // PEEL (the 128 / 256-slot straight instances, road networks): the first frame's meta-action runs
+  // before the frame loop (nothing of frame 0 runs before it), so the env index and the action's
+  // address die there instead of living through the loop (at NS = 128 they were spilled to scratch),
+  // and the ego's speed index is written to HBM where it changes (store_veh<false> at the end), not
+  // held in a register to the end.  The 32 / 64-slot straight instances keep it inside the loop:
+  // peeled, their launches measured ~1 % slower (profiles/r06/r06n).
+  constexpr bool PEEL = NS > 64 || GR;
+  auto meta_action = [&](int envl) {
+    int act = actions[envl];
+    if (so.n_lut > 0) {  // the env's action index -> its meta-action code (a select chain)
+      int c = -1;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (q < so.n_lut && act == q) c = so.lut[q];
+      act = c;
+    }
+    const T x = V.x[me], y = V.y[me], h = V.h[me], v = V.v[me];
+    T ts = V.ts[me];
+    int tgt = V.tgt[me];
+    if constexpr (GR)  // ControlledVehicle.act starts with follow_road (controller.py:98)
+      tgt = follow_road(V.lanes, *V.rt, T(P.lane_vehicle_length), tgt, x, y, V.rroad + me * TTRL_ROUTE_MAX,
+                        V.rlane + me * TTRL_ROUTE_MAX, V.rn + me, lane_s<T, NS, EPW, LC>(V, tgt, le, i, x, y));
+    if (act == TTRL_FASTER || act == TTRL_SLOWER) {  // MDPVehicle.act controller.py:304-315
+      int si = speed_to_index(P, v) + (act == TTRL_FASTER ? 1 : -1);
+      si = si < 0 ? 0 : (si > P.n_target_speeds - 1 ? P.n_target_speeds - 1 : si);
+      my_sidx = si;
+      // the launch's own state write-back leaves the speed index alone (store_veh<false>): a
+      // register held to the end for one ego per env was spilled to scratch (NS = 128)
+      if constexpr (PEEL && EPI != EPI_IX) st.speed_index[k] = si;
+      ts = T(P.target_speeds[si]);
+    } else if (act == TTRL_LANE_LEFT || act == TTRL_LANE_RIGHT) {  // controller.py:103-124
+      int id, lo = 0, hi = nl - 1;
+      if constexpr (GR) {  // clip within the target's road
+        const LaneT<T>& TL = V.lanes[tgt];
+        lo = TL.rfirst; hi = TL.rfirst + TL.rn - 1;
+      }
+      id = tgt + (act == TTRL_LANE_RIGHT ? 1 : -1);
+      id = id < lo ? lo : (id > hi ? hi : id);
+      if (reachable<CV>(V.lanes[id], T(P.lane_vehicle_length), x, y)) tgt = id;
+    }
+    // ControlledVehicle.act low-level control (controller.py:126-133); Road.act recomputes
+    // the same values this frame, the standalone ttrl_meta_action returns them.
+    my_steer = steering_control<CV>(V.lanes[tgt], P, x, y, h, v);
+    my_acc = T(P.kp_a) * (ts - v);
+    V.ts[me] = ts;
+    V.tgt[me] = (int8_t)tgt;
+  };
+  if constexpr (PEEL) {
+    if ((mode & MODE_META) && frames > 0 && actions && present && kind == TTRL_MDP) meta_action(env);
+  }
+
   PH(11);
   for (int frame = 0; frame < frames; ++frame) {
-    // ---------------- ego meta-action (DiscreteMetaAction.act, action.py:259-260) ----
-    if ((mode & MODE_META) && frame == 0 && actions && present && kind == TTRL_MDP) {
-      int envl = env;  // NS = 128: laundered, so the action's address is not hoisted and spilled
-      if constexpr (NS > 64) asm volatile("" : "+v"(envl));
-      int act = actions[envl];
-      if (so.n_lut > 0) {  // the env's action index -> its meta-action code (a select chain)
-        int c = -1;
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (q < so.n_lut && act == q) c = so.lut[q];
-        act = c;
-      }
-      const T x = V.x[me], y = V.y[me], h = V.h[me], v = V.v[me];
-      T ts = V.ts[me];
-      int tgt = V.tgt[me];
-      if constexpr (GR)  // ControlledVehicle.act starts with follow_road (controller.py:98)
-        tgt = follow_road(V.lanes, *V.rt, T(P.lane_vehicle_length), tgt, x, y, V.rroad + me * TTRL_ROUTE_MAX,
-                          V.rlane + me * TTRL_ROUTE_MAX, V.rn + me, lane_s<T, NS, EPW, LC>(V, tgt, le, i, x, y));
-      if (act == TTRL_FASTER || act == TTRL_SLOWER) {  // MDPVehicle.act controller.py:304-315
-        int si = speed_to_index(P, v) + (act == TTRL_FASTER ? 1 : -1);
-        si = si < 0 ? 0 : (si > P.n_target_speeds - 1 ? P.n_target_speeds - 1 : si);
-        my_sidx = si;
-        ts = T(P.target_speeds[si]);
-      } else if (act == TTRL_LANE_LEFT || act == TTRL_LANE_RIGHT) {  // controller.py:103-124
-        int id, lo = 0, hi = nl - 1;
-        if constexpr (GR) {  // clip within the target's road
-          const LaneT<T>& TL = V.lanes[tgt];
-          lo = TL.rfirst; hi = TL.rfirst + TL.rn - 1;
-        }
-        id = tgt + (act == TTRL_LANE_RIGHT ? 1 : -1);
-        id = id < lo ? lo : (id > hi ? hi : id);
-        if (reachable<CV>(V.lanes[id], T(P.lane_vehicle_length), x, y)) tgt = id;
-      }
-      // ControlledVehicle.act low-level control (controller.py:126-133); Road.act recomputes
-      // the same values this frame, the standalone ttrl_meta_action returns them.
-      my_steer = steering_control<CV>(V.lanes[tgt], P, x, y, h, v);
-      my_acc = T(P.kp_a) * (ts - v);
-      V.ts[me] = ts;
-      V.tgt[me] = (int8_t)tgt;
+    if constexpr (!PEEL) {
+      if ((mode & MODE_META) && frame == 0 && actions && present && kind == TTRL_MDP) meta_action(env);
     }
     __syncthreads();
     PH(0);
@@ -3028,8 +3045,10 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
         // the lane group); translation = the first strict minimum of |distance| (min over the
         // group, ties to the lower axis), so the result equals sat_pair's.  Groups of 8 lanes
         // never straddle a wave or an env, and are either fully active or fully idle.
+        int il = i;  // NS = 128: laundered, so the queue row's LDS address is not hoisted out of the
+        if constexpr (NS > 64) asm volatile("" : "+v"(il));  // frame loop (and spilled to scratch)
         for (int t0 = 0; t0 < npairs * 8; t0 += NS) {
-          const int t = t0 + i;
+          const int t = t0 + il;
           if (t < npairs * 8) {
             const int q = t >> 3, kx = t & 7;
             const int ij = V.pq_ij[le * NS + q];
@@ -3162,13 +3181,13 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
     Veh<T> a;
     a.x = V.x[me]; a.y = V.y[me]; a.h = V.h[me]; a.v = V.v[me]; a.ts = V.ts[me]; a.timer = my_timer;
     a.steer = my_steer; a.acc = my_acc; a.ix = my_ix; a.iy = my_iy;
-    a.lane = V.lane[me]; a.tgt = V.tgt[me]; a.sidx = my_sidx;
+    a.lane = V.lane[me]; a.tgt = V.tgt[me]; a.sidx = PEEL ? 0 : my_sidx;  // PEEL: not stored, see the meta-action
     const int fl = V.flags[me];
     a.crashed = (fl & FL_CRASHED) != 0; a.hasimp = (fl & FL_IMPACT) != 0;
     if (!present) {  // absent rows pass through untouched
       a.x = ((const T*)st.x)[k]; a.lane = st.lane[k]; a.tgt = st.target_lane[k];
     }
-    store_veh(a, st, k);
+    store_veh<!PEEL>(a, st, k);
     if constexpr (GR) {
       for (int q = 0; q < TTRL_ROUTE_MAX; ++q) {
         st.route_road[k * TTRL_ROUTE_MAX + q] = V.rroad[me * TTRL_ROUTE_MAX + q];
@@ -3192,7 +3211,10 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
     int(*s_p)[64] = s_perm + EPW;
     int* s_cnt = (int*)(s_p + EPW);
     int* s_ego = s_cnt + EPW;
-    if (so.obs) {  // the Kinematics observation of the final state
+    // the Kinematics observation of the final state (the 128-slot grid instance writes its grid
+    // instead: compiled out there, its LDS row indices were spilled to scratch; at 64 slots the
+    // register allocation came out worse without it, 0 -> 20 B per lane)
+    if ((EPI != EPI_GRID || NS <= 64) && so.obs) {
       __syncthreads();
       auto ego_of = [&](int ego, T& ex, T& ey, T& eh, T& ev, T& ec, T& es, int& elane) {
         ex = V.x[eb + ego]; ey = V.y[eb + ego]; eh = V.h[eb + ego]; ev = V.v[eb + ego]; elane = V.lane[eb + ego];
