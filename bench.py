@@ -66,7 +66,8 @@ def state_bytes(dtype: str) -> tuple[int, int]:
     return 11 * r + 3 * 4 + 4, 10 * r + 3 * 4 + 2
 
 
-def launch_bytes(E: int, N: int, dtype: str, obs_cfg: dict | None, graph: bool, grid_cells: int = 0) -> int:
+def launch_bytes(E: int, N: int, dtype: str, obs_cfg: dict | None, graph: bool, grid_cells: int = 0,
+                 ix_tail: bool = False) -> int:
     """Algorithmic HBM bytes of one env.step launch (ttrl_env_step): every slot's state read and
     written once (state_bytes); on a road network also its route rows (road, lane: 4 + 4 int8),
     route length and yield flag, read and written; per env the step tail (time read + written,
@@ -74,7 +75,10 @@ def launch_bytes(E: int, N: int, dtype: str, obs_cfg: dict | None, graph: bool, 
     read, and on a road network the regulation counter and np_random's 5 words (the shuffled
     observation draws from it), read and written, and the dispatch order read; the Kinematics
     observation and its ids written once; an OccupancyGrid written by the launch (ttrl_env_step_grid):
-    its ``grid_cells`` float32 cells per env written once."""
+    its ``grid_cells`` float32 cells per env written once.  ``ix_tail`` (ttrl_ix_env_step, round 6):
+    also the next step's observation and ids (a second copy), the done flag, the two spare-mask
+    bytes and the live count per env; the spare rows the finished envs swap in (~8 % of the envs
+    per step at config 6) are data-dependent and not counted."""
     rd, wr = state_bytes(dtype)
     r = 8 if dtype == "f64" else 4
     per_slot = rd + wr + (2 * (4 + 4 + 1 + 1) if graph else 0)
@@ -82,7 +86,9 @@ def launch_bytes(E: int, N: int, dtype: str, obs_cfg: dict | None, graph: bool, 
     if obs_cfg is not None and obs_cfg["type"] == "Kinematics":
         V = obs_cfg.get("vehicles_count", 5)
         F = len(obs_cfg.get("features", ["presence", "x", "y", "vx", "vy"]))
-        per_env += V * F * 4 + (V - 1) * 4
+        per_env += (2 if ix_tail else 1) * (V * F * 4 + (V - 1) * 4)
+    if ix_tail:
+        per_env += 1 + 2 + 4
     per_env += 4 * grid_cells
     return E * (N * per_slot + per_env)
 
@@ -511,7 +517,8 @@ def main():
     # TTRL_FUSE_GRID=0 left it to the grid kernel (roofline_obs)
     fused_grid = C["obs"]["type"] == "OccupancyGrid" and not grid_launches
     cells = int(np.prod(env.observation_space.shape)) if fused_grid else 0
-    alg_bytes = launch_bytes(E, N, args.dtype, C["obs"], graph=ix, grid_cells=cells)
+    alg_bytes = launch_bytes(E, N, args.dtype, C["obs"], graph=ix, grid_cells=cells,
+                             ix_tail=ix and getattr(env, "_fuse", False))
     kernel = "simulate_kernel (fused 15-frame Road.act+Road.step + step tail)"
     if C["obs"]["type"] == "Kinematics":  # the launch also writes the observation (ttrl_env_step)
         kernel = "simulate_kernel (fused 15-frame Road.act+Road.step + Kinematics observation + step tail)"

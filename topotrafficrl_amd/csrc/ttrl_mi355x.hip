@@ -2153,8 +2153,30 @@ __device__ __forceinline__ void simulate_body(int q0, int qend, const ttrl_state
     if ((mode & MODE_META) && frames > 0 && actions && present && kind == TTRL_MDP) meta_action(env);
   }
 
+  // Fair issue among a SIMD's waves.  The SIMD's arbiter issues the oldest ready wave first, so the
+  // first-dispatched of its waves ran ahead and the last one finished alone: on the headline launch
+  // the four waves of a SIMD took 295 k / 348 k / 423 k / 511 k cycles by dispatch rank, the last
+  // ~90 k of them one wave with no latency hiding (tools/placement.py, profiles/r06/
+  // r06l_wave_placement.txt).  A wave's priority now falls with its progress, 3 in the first
+  // quarter of the frames ... 0 in the last: a wave that is ahead yields to the ones behind it, so
+  // the SIMD's waves stay together and finish close together (385 k / 408 k / 430 k / 451 k;
+  // profiles/r06/r06r).  The straight instances with <= 64 slots only: the 128-slot one (two rounds
+  // of two-wave workgroups) measured 5 % slower with it, and the road-network step launch 0.494 ms
+  // per step with it and without (profiles/r06/r06s).  Masked launches (the intersection's
+  // spare-reset warm-ups) keep the default priority.
+  constexpr bool FAIR = NS <= 64 && !GR;
+  const bool fair = FAIR && !env_mask && frames >= 4;
+  if (fair) __builtin_amdgcn_s_setprio(3);
   PH(11);
   for (int frame = 0; frame < frames; ++frame) {
+    if (fair && frame > 0) {
+      const int q = frame * 4 / frames, qp = (frame - 1) * 4 / frames;
+      if (q != qp) {
+        if (q == 1) __builtin_amdgcn_s_setprio(2);
+        else if (q == 2) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
+    }
     if constexpr (!PEEL) {
       if ((mode & MODE_META) && frame == 0 && actions && present && kind == TTRL_MDP) meta_action(env);
     }
