@@ -1,8 +1,8 @@
 """Where the hardware puts a launch's waves (diagnostic; the -DTTRL_WAVE_TRACE build, tools/variants.py
 'wtrace'): for the headline's simulate launch (4096 x 64, one env per wave) and the intersection's
 (4096 envs, two per wave), every wave's start / end shader clock with its HW_ID and XCC_ID, saved raw
-(gpurun_out/placement_*.npy) and summarised per XCD, shader engine, CU and SIMD: how many waves each
-got, how many started late (a second-round wave waits for a slot on its CU), and what that costs.
+(gpurun_out/placement_*.npy) and summarised per CU and SIMD: how many waves each got, and the
+durations of a SIMD's waves by their dispatch rank (the SIMD's arbiter issues the oldest first).
 
   python tools/placement.py [out_dir]
 """
@@ -28,34 +28,29 @@ def decode(tr):
 
 
 def summary(tag, tr):
+    """Per wave: duration (start / end read on one CU's clock: the clocks of different CUs are not
+    aligned, so only same-CU differences mean anything).  Per SIMD: its waves by dispatch rank (the
+    order of their block ids) and the SIMD's span (first start to last end)."""
     d = decode(tr)
-    t0, t1 = d["t0"].copy(), d["t1"].copy()
-    for x in np.unique(d["xcc"]):  # each XCD has its own clock: relative to its first wave's start
-        m = d["xcc"] == x
-        b = t0[m].min()
-        t0[m] -= b
-        t1[m] -= b
+    t0, t1 = d["t0"], d["t1"]
     dur = t1 - t0
     cu_key = ((d["xcc"] * 8 + d["se"]) * 2 + d["sh"]) * 16 + d["cu"]
     simd_key = cu_key * 4 + d["simd"]
-    late = t0 > 20000  # started well after the launch's first wave on its XCD
-    print(f"[{tag}] waves {len(t0)}: duration mean {dur.mean():.0f} p50 {np.median(dur):.0f} max {dur.max()}; "
-          f"launch end per XCD (cycles) {[int(t1[d['xcc'] == x].max()) for x in np.unique(d['xcc'])]}")
-    print(f"  late-start waves (> 20k cycles after the XCD's first): {late.sum()}, start mean {t0[late].mean() if late.any() else 0:.0f}")
     _, cu_cnt = np.unique(cu_key, return_counts=True)
-    _, simd_cnt = np.unique(simd_key, return_counts=True)
-    print(f"  CUs {len(cu_cnt)}: waves per CU {dict(zip(*[a.tolist() for a in np.unique(cu_cnt, return_counts=True)]))}")
-    print(f"  SIMDs {len(simd_cnt)}: waves per SIMD {dict(zip(*[a.tolist() for a in np.unique(simd_cnt, return_counts=True)]))}")
-    se_key = d["xcc"] * 8 + d["se"]
-    for x in np.unique(d["xcc"])[:2]:
-        row = []
-        for s in np.unique(d["se"][d["xcc"] == x]):
-            m = se_key == x * 8 + s
-            row.append(f"SE{s}: {m.sum()} waves on {len(np.unique(cu_key[m]))} CUs, {late[m].sum()} late, "
-                       f"end {t1[m].max()}")
-        print(f"  XCD {x}: " + "; ".join(row))
-    # the launch without its late waves: when would the last first-round wave have ended?
-    print(f"  end of the first-round waves {t1[~late].max()}, of all {t1.max()}")
+    keys, inv, simd_cnt = np.unique(simd_key, return_inverse=True, return_counts=True)
+    print(f"[{tag}] waves {len(t0)}: duration mean {dur.mean():.0f} p50 {np.median(dur):.0f} "
+          f"p90 {np.percentile(dur, 90):.0f} max {dur.max()}")
+    print(f"  CUs {len(cu_cnt)}: waves per CU {dict(zip(*[a.tolist() for a in np.unique(cu_cnt, return_counts=True)]))}; "
+          f"SIMDs {len(simd_cnt)}: waves per SIMD {dict(zip(*[a.tolist() for a in np.unique(simd_cnt, return_counts=True)]))}")
+    per = int(simd_cnt.max())
+    ranks = np.full((len(keys), per), np.nan)
+    span = np.zeros(len(keys))
+    for s_ in range(len(keys)):
+        bs = np.sort(np.nonzero(inv == s_)[0])  # block ids = dispatch order
+        ranks[s_, :len(bs)] = dur[bs]
+        span[s_] = t1[bs].max() - t0[bs].min()
+    print(f"  mean duration by dispatch rank on its SIMD {np.nanmean(ranks, 0).astype(int).tolist()}; "
+          f"SIMD span mean {span.mean():.0f} max {span.max():.0f}")
 
 
 def main(out):
@@ -79,10 +74,7 @@ def main(out):
         for t in range(8):
             a_idx = torch.randint(0, env.action_space.n, (4096,), device=dev, generator=g)
             work = env.state.clone()
-            if tag == "ix":
-                env.step(a_idx)
-            else:
-                env.step(a_idx)
+            env.step(a_idx)
             torch.cuda.synchronize()
             a = env.action_type._codes(a_idx)
             assert sim(C.byref(work.struct()), C.byref(env.network.table), C.byref(env.params), a.data_ptr(), 15,
